@@ -1,0 +1,200 @@
+/*
+ * ska_sdp_hip.h -- C ABI of the MI355X-native predict/invert + calibration
+ * hot path (libska_sdp_hip.so, hand-written HIP for gfx950).
+ *
+ * Every entry point takes DEVICE pointers (plain pointers + sizes + strides,
+ * no torch types), an optional hipStream_t passed as void*, and an error
+ * buffer.  It returns SDP_HIP_OK or one of the error codes below, which the
+ * Python layer maps back onto the reference's exception types
+ * (AssertionError / ValueError / RuntimeError).
+ *
+ * Outputs are always caller-allocated (the ska-sdp-func convention of
+ * dft_point_v00, reference src/ska_sdp_func_python/imaging/dft.py:169-178);
+ * the library never returns memory it allocated.  Internal scratch
+ * (visibility records, w-plane grids, FFT plans) lives in a per-device cache
+ * that grows on demand and is released by sdp_hip_release_workspace().
+ */
+#ifndef SKA_SDP_HIP_H
+#define SKA_SDP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define SDP_HIP_OK 0
+#define SDP_HIP_ERR_INVALID_ARG 1 /* -> ValueError   */
+#define SDP_HIP_ERR_RUNTIME 2     /* -> RuntimeError */
+#define SDP_HIP_ERR_NO_DEVICE 3   /* -> RuntimeError */
+#define SDP_HIP_ERR_MEMORY 4      /* -> MemoryError  */
+
+/* ---- dtype codes ------------------------------------------------------- */
+#define SDP_HIP_F32 1
+#define SDP_HIP_F64 2
+#define SDP_HIP_C64 3
+#define SDP_HIP_C128 4
+
+/* ---- flags for the NUFFT pair ------------------------------------------ */
+#define SDP_HIP_FLIP_UW 1u    /* negate u and w on the fly (RASCIL, ng.py:210-213) */
+#define SDP_HIP_ACCUMULATE 2u /* add into the output instead of overwriting      */
+
+/* Diagnostics filled by the NUFFT entry points (may be NULL). */
+typedef struct sdp_hip_wgrid_info {
+    int support;          /* ES kernel support W                            */
+    double beta;          /* ES kernel shape                                */
+    int ngrid_x, ngrid_y; /* oversampled grid (sigma = 2)                   */
+    int nplanes;          /* w planes (1 when do_wstacking == 0)            */
+    double w0, dw;        /* plane 0 position and spacing (wavelengths)     */
+    int64_t nvis_used;    /* visibilities with non-zero weight              */
+    int64_t nitems;       /* gridding work items launched                   */
+    int plane_chunk;      /* planes resident per pass                       */
+    float ms_prep, ms_grid, ms_fft, ms_screen; /* stage times if timing on  */
+} sdp_hip_wgrid_info;
+
+/* Library/ABI version and a device probe. */
+int sdp_hip_version(void);
+int sdp_hip_device_count(int *count, char *errbuf, size_t errbuf_len);
+int sdp_hip_release_workspace(char *errbuf, size_t errbuf_len);
+/* When non-zero, the NUFFT entry points time their stages with HIP events
+ * (adds stream synchronisations; off by default). */
+int sdp_hip_set_stage_timing(int enable);
+
+/*
+ * sdp_hip_ms2dirty -- replaces ducc0.wgridder.ms2dirty as called by
+ * invert_ng (reference src/ska_sdp_func_python/imaging/ng.py:240-256 MFS,
+ * :271-287 per channel; double_precision_accumulation=True).
+ *
+ * dirty[x,y] = sum_{row,chan} wgt * Re{vis * exp(2 pi i (u l_x + v m_y - w (n-1)))} [/n]
+ * (ducc0 convention, l_x = (x - nx/2) pixsize_x).
+ *
+ * uvw      [nrow, 3] f64 metres, row stride uvw_row_stride (elements)
+ * freq     [nchan] f64 Hz
+ * vis      [nrow, nchan] c64 (vis_dtype SDP_HIP_C64) with element strides;
+ *          NULL means unit visibilities (PSF, ng.py:231-233)
+ * wgt      [nrow, nchan] f32 with element strides; NULL means unit weights
+ * dirty    f64, element (x, y) at dirty[x*dirty_stride_x + y*dirty_stride_y]
+ *          (pass strides (1, nx) to receive RASCIL's transposed image)
+ * epsilon  requested accuracy; clamped to the fp32 floor 1e-7 (W <= 8)
+ */
+int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride,
+                     const double *freq, int nchan, int64_t nrow,
+                     const void *vis, int vis_dtype, int64_t vis_row_stride,
+                     int64_t vis_chan_stride, const float *wgt,
+                     int64_t wgt_row_stride, int64_t wgt_chan_stride,
+                     int npix_x, int npix_y, double pixsize_x,
+                     double pixsize_y, double epsilon, int do_wstacking,
+                     unsigned flags, double *dirty, int64_t dirty_stride_x,
+                     int64_t dirty_stride_y, void *stream,
+                     sdp_hip_wgrid_info *info, char *errbuf,
+                     size_t errbuf_len);
+
+/*
+ * sdp_hip_dirty2ms -- replaces ducc0.wgridder.dirty2ms as called by
+ * predict_ng (reference src/ska_sdp_func_python/imaging/ng.py:99-112 MFS,
+ * :117-129 per channel).  Exact adjoint of sdp_hip_ms2dirty:
+ * vis = wgt * sum_{x,y} dirty[x,y] exp(-2 pi i (u l_x + v m_y - w (n-1))) [/n]
+ */
+int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride,
+                     const double *freq, int nchan, int64_t nrow,
+                     const double *dirty, int64_t dirty_stride_x,
+                     int64_t dirty_stride_y, int npix_x, int npix_y,
+                     double pixsize_x, double pixsize_y, const float *wgt,
+                     int64_t wgt_row_stride, int64_t wgt_chan_stride,
+                     double epsilon, int do_wstacking, unsigned flags,
+                     void *vis, int vis_dtype, int64_t vis_row_stride,
+                     int64_t vis_chan_stride, void *stream,
+                     sdp_hip_wgrid_info *info, char *errbuf,
+                     size_t errbuf_len);
+
+/*
+ * sdp_hip_dft_point_v00 -- replaces ska_sdp_func.visibility.dft_point_v00
+ * (reference src/ska_sdp_func_python/imaging/dft.py:173-178) and the cupy
+ * dft_kernel (:185-262, :288-337).  Caller-allocated output, replaced (not
+ * accumulated), all arrays C-contiguous:
+ *   direction_cosines [ncomp, 3] f64 (l, m, n-1)
+ *   fluxes            [ncomp, flux_nchan, npol] c128; flux_nchan == nchan
+ *                     or 1 (broadcast over channels, as numpy does in
+ *                     dft_cpu_looped, dft.py:284)
+ *   uvw_lambda        [ntimes*nbaselines, nchan, 3] f64 wavelengths
+ *   vis               [ntimes*nbaselines, nchan, npol] c64 or c128
+ * vis = sum_c flux[c] * exp(-2 pi i (u l + v m + w (n-1)))   (no 1/n)
+ */
+int sdp_hip_dft_point_v00(int ncomp, const double *direction_cosines,
+                          const void *fluxes, int flux_nchan, int npol,
+                          int64_t nrow, int nchan, const double *uvw_lambda,
+                          void *vis, int vis_dtype, void *stream,
+                          char *errbuf, size_t errbuf_len);
+
+/* Same contraction with uvw in metres [nrow, 3] + freq [nchan]: the lambda
+ * scaling (reference visibility/base.py:54-56) is fused into the kernel so
+ * the [nrow, nchan, 3] uvw_lambda array is never materialised. */
+int sdp_hip_dft_point_metres(int ncomp, const double *direction_cosines,
+                             const void *fluxes, int flux_nchan, int npol,
+                             int64_t nrow, int nchan, const double *uvw,
+                             const double *freq, void *vis, int vis_dtype,
+                             void *stream, char *errbuf, size_t errbuf_len);
+
+/*
+ * Convolution-function (AW-projection) gridder/degridder, replacing the
+ * Python triple loops of grid_visibility_to_griddata /
+ * degrid_visibility_from_griddata (reference
+ * src/ska_sdp_func_python/grid_data/gridding.py:160-255, :502-590).
+ * The Python layer evaluates the reference's WCS mappings
+ * (spatial_mapping, gridding.py:60-157) into integer indices; the kernels do
+ * the per-visibility slice add / einsum, including the edge-skip rule
+ * (gridding.py:230-237).
+ *   pu,pv,pwc,pdu,pdv [nchan_vis, nrowvis] int32 (per channel mappings)
+ *   vis,wt            [nrowvis, nchan_vis, npol] c128 / f64 (flagged)
+ *   cf                [cf_nchan, npol, nw, ndv, ndu, gv, gu] c128
+ *   grid              [g_nchan, npol, ny, nx] c128 (accumulated)
+ *   vis_to_im         [nchan_vis] int32
+ *   sumwt             [g_nchan, npol] f64 (accumulated)
+ *   nskipped          [1] int64 (accumulated count of edge-skipped rows)
+ */
+int sdp_hip_grid_cf(int64_t nrowvis, int nchan_vis, int npol,
+                    const int32_t *pu, const int32_t *pv, const int32_t *pwc,
+                    const int32_t *pdu, const int32_t *pdv,
+                    const int32_t *vis_to_im, const void *vis,
+                    const double *wt, const void *cf, int cf_nchan, int nw,
+                    int ndv, int ndu, int gv, int gu, void *grid,
+                    int g_nchan, int ny, int nx, double *sumwt,
+                    int64_t *nskipped, void *stream, char *errbuf,
+                    size_t errbuf_len);
+int sdp_hip_degrid_cf(int64_t nrowvis, int nchan_vis, int npol,
+                      const int32_t *pu, const int32_t *pv,
+                      const int32_t *pwc, const int32_t *pdu,
+                      const int32_t *pdv, const int32_t *vis_to_im,
+                      const void *grid, int g_nchan, int ny, int nx,
+                      const void *cf, int cf_nchan, int nw, int ndv, int ndu,
+                      int gv, int gu, void *vis_out, int64_t *nskipped,
+                      void *stream, char *errbuf, size_t errbuf_len);
+
+/*
+ * Batched iterative-substitution gain solver, replacing
+ * _solve_antenna_gains_itsubs_scalar / _matrix / _nocrossdata
+ * (reference src/ska_sdp_func_python/calibration/solvers.py:217-539).
+ * One solve = one gain-table row: all of its channels iterate together and
+ * stop on max|g - g_last| over ants AND channels (solvers.py:268, :427).
+ *   x, xwt   [nsolve, nants, nants, nchan, npol] c128 / f64 (dense, the
+ *            layout _solve_with_mask hands over, already normalised)
+ *   gain     [nsolve, nants, nchan, nrec, nrec] c128  (in: start, out)
+ *   gwt      [nsolve, nants, nchan, nrec, nrec] f64   (out)
+ *   residual [nsolve, nchan, nrec, nrec] f64          (out)
+ *   niter_out[nsolve] int32 iterations used (niter+1 = not converged)
+ * mode: 0 scalar (npol 1), 1 matrix (npol 4, crosspol), 2 nocrossdata
+ * (npol 2 or npol 4 without crosspol).
+ */
+int sdp_hip_solve_gains(int nsolve, int nants, int nchan, int npol, int mode,
+                        const void *x, const double *xwt, void *gain,
+                        double *gwt, double *residual, int32_t *niter_out,
+                        int niter, double tol, int phase_only, int refant,
+                        double damping, void *stream, char *errbuf,
+                        size_t errbuf_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKA_SDP_HIP_H */

@@ -1,0 +1,1212 @@
+// w-stacking / w-gridding NUFFT pair for gfx950 (MI355X): sdp_hip_ms2dirty
+// and sdp_hip_dirty2ms, the drop-in for ducc0.wgridder.ms2dirty/dirty2ms as
+// called by the reference's invert_ng / predict_ng
+// (src/ska_sdp_func_python/imaging/ng.py:99-129, :240-289).
+//
+// Pipeline (one stream, two host syncs per call):
+//   k_bounds       fp64 w range / uv extent over the rows
+//   k_bucket<0>    per-visibility fp64 grid coordinates -> bucket key
+//                  (first w plane p0, 16x16 uv tile), wave-level run-length
+//                  histogram (one atomic per run of equal keys)
+//   scan           hipcub exclusive sum over buckets
+//   k_bucket<1>    32-byte visibility records in bucket order
+//   k_items_*      work items = one bucket, split into <= kChunk records
+//   per plane chunk (all planes resident when they fit the budget):
+//     k_grid       one wave per item; the wave owns an LDS tile of W planes
+//                  x (16+W-1)^2 complex cells; per record one lane per (u,v)
+//                  tap does a plain ds_read_b64/ds_write_b64 update of all W
+//                  planes; the tile is flushed with global float atomics
+//     hipFFT       batched in-place c2c over the planes
+//     k_screen_fwd w-screen phase, real part, fp64 accumulate, grid correction
+//   dirty2ms runs the stages in adjoint order (k_screen_adj, FFT, k_degrid).
+//
+// Numerics: coordinates, plane positions and phases in fp64; kernel taps and
+// grid values in fp32; image accumulation and corrections in fp64.  ES kernel
+// exp(beta (sqrt(1 - x^2) - 1)), beta = 2.30 W, oversampling 2 (FINUFFT
+// parameter rule); the grid correction is its Fourier transform (128-point
+// Gauss-Legendre quadrature on host), tabulated and interpolated on device.
+#include <hipcub/hipcub.hpp>
+#include <hipfft/hipfft.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <tuple>
+#include <type_traits>
+#include <vector>
+
+#include "sdp_common.h"
+
+namespace sdp {
+namespace wstack {
+
+constexpr double kCLight = 299792458.0;
+constexpr int kTile = 16;      // uv tile edge in grid cells
+constexpr int kChunk = 2048;   // max records per work item
+constexpr int kPitch = 24;     // LDS row pitch in complex values (b64 conflict-free)
+constexpr int kMaxW = 8;
+constexpr int kPhiTab = 8193;  // Phi(xi) table on xi in [0, 0.5]
+
+struct Geo {
+    int W;
+    float beta, inv_half_w, beta_l2e;
+    int nx, ny, ngx, ngy;
+    double px, py;
+    int do_w, nplanes, nps;  // nps = number of distinct first planes
+    double w0, dw, s0;
+    int nty, ntiles;
+    double su;  // sign applied to u and w (-1 with SDP_HIP_FLIP_UW)
+    int nchan;
+    int64_t nrow;
+};
+
+struct __attribute__((aligned(32))) VisRec {
+    float cre, cim;    // gridding: vis*wgt*exp(2 pi i w s0); degridding: wgt*exp(-2 pi i w s0)
+    float fu, fv, fw;  // offset of the first tap from the exact position (cells/planes)
+    uint32_t ij;       // footprint start in the centred grid: ic0 | jc0 << 16
+    uint32_t p0;       // first w plane
+    uint32_t idx;      // row * nchan + chan
+};
+static_assert(sizeof(VisRec) == 32, "record layout");
+
+struct Item {
+    uint32_t b, e, tile, p0;
+};
+
+// ------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long ord_enc(double d) {
+    long long i = __double_as_longlong(d);
+    return i < 0 ? ~(unsigned long long)i : ((unsigned long long)i | 0x8000000000000000ull);
+}
+
+// ES kernel exp(beta (sqrt(1 - x^2) - 1)), x = 2t/W; `beta_l2e` = beta*log2(e)
+// so the raw v_exp_f32 (2^x) and v_sqrt_f32 are used directly.
+__device__ __forceinline__ float es_kernel(float t, float inv_half_w, float beta_l2e) {
+    const float x = t * inv_half_w;
+    const float y = 1.0f - x * x;
+    const float e =
+        __builtin_amdgcn_exp2f(beta_l2e * (__builtin_amdgcn_sqrtf(fmaxf(y, 0.0f)) - 1.0f));
+    return y > 0.0f ? e : 0.0f;
+}
+
+// 4-point Lagrange interpolation of the tabulated Phi on [0, 0.5].
+__device__ __forceinline__ double phi_lookup(const double *__restrict__ tab, double xi) {
+    xi = fabs(xi);
+    const double t = xi * (2.0 * (kPhiTab - 1));
+    int k = (int)t;
+    k = min(max(k, 1), kPhiTab - 3);
+    const double f = t - k;
+    const double p0 = tab[k - 1], p1 = tab[k], p2 = tab[k + 1], p3 = tab[k + 2];
+    const double fm1 = f + 1.0, f1 = f - 1.0, f2 = f - 2.0;
+    return -p0 * f * f1 * f2 / 6.0 + p1 * fm1 * f1 * f2 / 2.0 - p2 * fm1 * f * f2 / 2.0 +
+           p3 * fm1 * f * f1 / 6.0;
+}
+
+struct Coord {
+    int ic0, jc0, p0;
+    float fu, fv, fw;
+    double w;  // w in wavelengths (sign applied)
+    bool ok;
+};
+
+__device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restrict__ uvw,
+                                           int64_t rs, int64_t row, double f) {
+    Coord c;
+    const double s = f / kCLight;
+    const double u = g.su * uvw[row * rs] * s;
+    const double v = uvw[row * rs + 1] * s;
+    c.w = g.su * uvw[row * rs + 2] * s;
+    const double a = u * g.px * g.ngx;
+    const double b = v * g.py * g.ngy;
+    c.ok = fabs(a) < (double)g.ngx && fabs(b) < (double)g.ngy;
+    if (!c.ok) return c;
+    const double fa = floor(a - 0.5 * g.W), fb = floor(b - 0.5 * g.W);
+    c.fu = (float)(fa + 1.0 - a);
+    c.fv = (float)(fb + 1.0 - b);
+    const int ic = ((int)fa + 1 + g.ngx / 2) % g.ngx;
+    const int jc = ((int)fb + 1 + g.ngy / 2) % g.ngy;
+    c.ic0 = ic < 0 ? ic + g.ngx : ic;
+    c.jc0 = jc < 0 ? jc + g.ngy : jc;
+    if (g.do_w) {
+        const double pw = (c.w - g.w0) / g.dw;
+        const double fp = floor(pw - 0.5 * g.W);
+        c.fw = (float)(fp + 1.0 - pw);
+        c.p0 = min(max((int)fp + 1, 0), g.nps - 1);
+    } else {
+        c.p0 = 0;
+        c.fw = 0.0f;
+    }
+    return c;
+}
+
+// p0-major bucket keys: the items of a range of first planes are contiguous.
+__device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c) {
+    const int tile = (c.ic0 / kTile) * g.nty + (c.jc0 / kTile);
+    return (unsigned)c.p0 * (unsigned)g.ntiles + (unsigned)tile;
+}
+
+// ------------------------------------------------------------------------
+// kernels: geometry and bucketing
+// ------------------------------------------------------------------------
+__global__ void k_init_bounds(unsigned long long *out) {
+    out[0] = ~0ull;
+    out[1] = 0ull;
+    out[2] = 0ull;
+    out[3] = 0ull;
+}
+
+__global__ void k_bounds(const double *__restrict__ uvw, int64_t rs, int64_t nrow, double su,
+                         double slo, double shi, unsigned long long *out) {
+    double wmn = 1e300, wmx = -1e300, umx = 0.0, vmx = 0.0;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrow;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const double u = uvw[r * rs], v = uvw[r * rs + 1], w = su * uvw[r * rs + 2];
+        const double w1 = w * slo, w2 = w * shi;
+        wmn = fmin(wmn, fmin(w1, w2));
+        wmx = fmax(wmx, fmax(w1, w2));
+        umx = fmax(umx, fabs(u) * shi);
+        vmx = fmax(vmx, fabs(v) * shi);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        wmn = fmin(wmn, __shfl_xor(wmn, o));
+        wmx = fmax(wmx, __shfl_xor(wmx, o));
+        umx = fmax(umx, __shfl_xor(umx, o));
+        vmx = fmax(vmx, __shfl_xor(vmx, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&out[0], ord_enc(wmn));
+        atomicMax(&out[1], ord_enc(wmx));
+        atomicMax(&out[2], ord_enc(umx));
+        atomicMax(&out[3], ord_enc(vmx));
+    }
+}
+
+// Wave-level run-length aggregation: consecutive lanes with equal keys share
+// one atomic on counter[key]; with kScatter each lane gets its slot.
+template <bool kScatter>
+__device__ __forceinline__ unsigned run_reserve(unsigned key, bool valid, unsigned *counter) {
+    const int lane = threadIdx.x & 63;
+    const unsigned prev = __shfl_up(key, 1);
+    const bool start = (lane == 0) || (prev != key);
+    const unsigned long long B = __ballot(start);
+    const unsigned long long above = (lane == 63) ? 0ull : (B & ~((2ull << lane) - 1ull));
+    const int end = above ? (__ffsll((long long)above) - 1) : 64;
+    unsigned base = 0;
+    if (valid && start) base = atomicAdd(&counter[key], (unsigned)(end - lane));
+    if (!kScatter) return 0;
+    const unsigned long long upto = (lane == 63) ? B : (B & ((2ull << lane) - 1ull));
+    const int head = 63 - __clzll((long long)upto);
+    const unsigned hb = __shfl(base, head);
+    return hb + (unsigned)(lane - head);
+}
+
+__device__ __forceinline__ float2 load_vis(const float2 *p) { return *p; }
+__device__ __forceinline__ float2 load_vis(const double2 *p) {
+    const double2 v = *p;
+    return make_float2((float)v.x, (float)v.y);
+}
+
+template <class VT, bool kScatter, bool kGrid>
+__global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
+                         const double *__restrict__ freq, const VT *__restrict__ vis,
+                         int64_t vrs, int64_t vcs, const float *__restrict__ wgt, int64_t wrs,
+                         int64_t wcs, unsigned *counter, VisRec *__restrict__ recs,
+                         unsigned long long *nbad) {
+    const int64_t nvis = g.nrow * (int64_t)g.nchan;
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    bool valid = v < nvis;
+    int64_t row = 0;
+    int chan = 0;
+    float wt = 1.0f;
+    Coord c;
+    c.ok = false;
+    if (valid) {
+        row = v / g.nchan;
+        chan = (int)(v - row * g.nchan);
+        if (wgt) wt = wgt[row * wrs + chan * wcs];
+        valid = (wt != 0.0f);
+        if (valid) {
+            c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
+            if (!c.ok) {
+                valid = false;
+                if (!kScatter) atomicAdd(nbad, 1ull);
+            }
+        }
+    }
+    const unsigned key = valid ? coord_key(g, c) : 0xffffffffu;
+    const unsigned pos = run_reserve<kScatter>(key, valid, counter);
+    if (!kScatter || !valid) return;
+    float cr = wt, ci = 0.0f;
+    if (kGrid) {
+        const float2 x = vis ? load_vis(vis + row * vrs + chan * vcs) : make_float2(1.0f, 0.0f);
+        cr = x.x * wt;
+        ci = x.y * wt;
+    }
+    if (g.do_w) {
+        double ph = c.w * g.s0;
+        ph -= rint(ph);
+        float sn, cs;
+        sincospif((float)(2.0 * ph), &sn, &cs);
+        if (!kGrid) sn = -sn;
+        const float r_ = cr * cs - ci * sn, i_ = cr * sn + ci * cs;
+        cr = r_;
+        ci = i_;
+    }
+    VisRec rec;
+    rec.cre = cr;
+    rec.cim = ci;
+    rec.fu = c.fu;
+    rec.fv = c.fv;
+    rec.fw = c.fw;
+    rec.ij = (uint32_t)c.ic0 | ((uint32_t)c.jc0 << 16);
+    rec.p0 = (uint32_t)c.p0;
+    rec.idx = (uint32_t)v;
+    recs[pos] = rec;
+}
+
+__global__ void k_items_count(int64_t nkeys, const unsigned *__restrict__ offs, unsigned *nch) {
+    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (k >= nkeys) return;
+    const unsigned n = offs[k + 1] - offs[k];
+    nch[k] = (n + kChunk - 1) / kChunk;
+}
+
+__global__ void k_items_fill(int64_t nkeys, int ntiles, const unsigned *__restrict__ offs,
+                             const unsigned *__restrict__ ioffs, Item *items) {
+    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (k >= nkeys) return;
+    const unsigned b = offs[k], e = offs[k + 1];
+    unsigned o = ioffs[k];
+    const uint32_t p0 = (uint32_t)(k / ntiles);
+    const uint32_t tile = (uint32_t)(k - (int64_t)p0 * ntiles);
+    for (unsigned s = b; s < e; s += kChunk) {
+        Item x;
+        x.b = s;
+        x.e = min(e, s + (unsigned)kChunk);
+        x.tile = tile;
+        x.p0 = p0;
+        items[o++] = x;
+    }
+}
+
+__global__ void k_gather_p0_offsets(const unsigned *__restrict__ ioffs, int ntiles, int nps,
+                                    unsigned *out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k <= nps) out[k] = ioffs[(size_t)k * ntiles];
+}
+
+// ------------------------------------------------------------------------
+// kernels: gridding / degridding (the hot loops)
+// ------------------------------------------------------------------------
+template <int W>
+struct TileShape {
+    static constexpr int R = kTile + W - 1;   // tile + halo rows/cols
+    static constexpr int PLANE = R * kPitch;  // complex values per plane in LDS
+};
+
+__device__ __forceinline__ Item load_item(const Item *__restrict__ items) {
+    const Item raw = items[blockIdx.x];
+    Item it;
+    it.b = __builtin_amdgcn_readfirstlane(raw.b);
+    it.e = __builtin_amdgcn_readfirstlane(raw.e);
+    it.tile = __builtin_amdgcn_readfirstlane(raw.tile);
+    it.p0 = __builtin_amdgcn_readfirstlane(raw.p0);
+    return it;
+}
+
+__device__ __forceinline__ float lane_readf(float v, int src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
+// Records are fetched 64 at a time, one per lane (coalesced 2 KiB), and
+// broadcast to the wave with v_readlane.
+struct RecRegs {
+    float cre, cim, fu, fv, fw;
+    uint32_t ij;
+};
+
+__device__ __forceinline__ RecRegs rec_at(const VisRec &my, int k) {
+    RecRegs r;
+    r.cre = lane_readf(my.cre, k);
+    r.cim = lane_readf(my.cim, k);
+    r.fu = lane_readf(my.fu, k);
+    r.fv = lane_readf(my.fv, k);
+    r.fw = lane_readf(my.fw, k);
+    r.ij = (uint32_t)__builtin_amdgcn_readlane((int)my.ij, k);
+    return r;
+}
+
+// Per-lane roles inside a wave for support W: lane = kx*W + ky is the (u,v)
+// tap it accumulates; lanes [0,W) / [W,2W) / [2W,3W) evaluate the u / v / w
+// 1-D taps of the current record (one ES evaluation per lane).
+template <int W>
+struct LaneRole {
+    int kx, ky;
+    bool act;
+    float m0, m1, m2, toff;
+    __device__ __forceinline__ explicit LaneRole(int lane) {
+        kx = lane / W;
+        ky = lane - kx * W;
+        act = lane < W * W;
+        const int set = lane / W;
+        toff = (float)(lane - set * W);
+        // arithmetic 0/1 selectors: a ternary chain here is lowered to scratch
+        m0 = set == 0 ? 1.0f : 0.0f;
+        m1 = set == 1 ? 1.0f : 0.0f;
+        m2 = set == 2 ? 1.0f : 0.0f;
+    }
+    __device__ __forceinline__ float taps(const RecRegs &rc, float ihw, float bl) const {
+        const float base = fmaf(m0, rc.fu, fmaf(m1, rc.fv, m2 * rc.fw));
+        return es_kernel(base + toff, ihw, bl);
+    }
+};
+
+// One wave per work item (= one (p0, tile) bucket chunk).  The wave owns its
+// LDS tile of W planes, so accumulation is a plain ds_read_b64/ds_write_b64
+// read-modify-write: no LDS float atomics (gfx950 runs ds_add_f32 at ~0.3
+// lanes/clk/CU), exact fp32 sums, and in-order LDS execution
+// inside the wave orders the updates of consecutive records.
+template <int W, bool WS>
+__global__ __launch_bounds__(64) void k_grid(Geo g, const VisRec *__restrict__ recs,
+                                             const Item *__restrict__ items,
+                                             float *__restrict__ grid, int p_lo, int p_hi) {
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    constexpr int R = TileShape<W>::R;
+    constexpr int PS = TileShape<W>::PLANE;
+    constexpr int NQ = WS ? W : 1;
+    const Item it = load_item(items);
+    const int lane = threadIdx.x;
+    for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
+
+    const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
+    const LaneRole<W> role(lane);
+    const float ihw = g.inv_half_w, bl = g.beta_l2e;
+    const int lane_off = role.kx * kPitch + role.ky - (tx * kTile) * kPitch - ty * kTile;
+
+    for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+        const int n = (int)min(64u, it.e - b0);
+        const VisRec my = recs[b0 + min(lane, n - 1)];
+        for (int k = 0; k < n; ++k) {
+            const RecRegs rc = rec_at(my, k);
+            const float kval = role.taps(rc, ihw, bl);
+            const float ku = __shfl(kval, role.kx);
+            const float kv = __shfl(kval, W + role.ky);
+            const float kk = ku * kv;
+            const float vr = rc.cre * kk, vi = rc.cim * kk;
+            const int off = lane_off + (int)(rc.ij & 0xffffu) * kPitch + (int)(rc.ij >> 16);
+            float kw[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(kval, 2 * W + q) : 1.0f;
+            if (role.act) {
+                float2 a[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) a[q] = tile[q * PS + off];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    a[q].x = fmaf(vr, kw[q], a[q].x);
+                    a[q].y = fmaf(vi, kw[q], a[q].y);
+                    tile[q * PS + off] = a[q];
+                }
+            }
+        }
+    }
+
+    // flush: float atomics into the resident planes (the halo overlaps the
+    // neighbouring tiles); zero cells are skipped.
+    const int cells = R * R;
+    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+    for (int c = lane; c < NQ * cells; c += 64) {
+        const int q = c / cells;
+        const int p = (int)it.p0 + q;
+        if (p < p_lo || p >= p_hi) continue;
+        const int rem = c - q * cells;
+        const int xl = rem / R, yl = rem - (rem / R) * R;
+        const float2 val = tile[q * PS + xl * kPitch + yl];
+        if (val.x != 0.0f || val.y != 0.0f) {
+            int gx = tx * kTile + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = ty * kTile + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            float *dst =
+                grid + ((int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy) * 2;
+            atomicAdd(dst, val.x);
+            atomicAdd(dst + 1, val.y);
+        }
+    }
+}
+
+template <int W, bool WS>
+__global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__ recs,
+                                               const Item *__restrict__ items,
+                                               const float2 *__restrict__ grid, int p_lo,
+                                               int p_hi, float2 *acc) {
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    constexpr int R = TileShape<W>::R;
+    constexpr int PS = TileShape<W>::PLANE;
+    constexpr int NQ = WS ? W : 1;
+    const Item it = load_item(items);
+    const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
+    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < NQ * R * R; i += 64) {
+        const int q = i / (R * R);
+        const int p = (int)it.p0 + q;
+        const int rem = i - q * R * R;
+        const int xl = rem / R, yl = rem - (rem / R) * R;
+        int gx = tx * kTile + xl;
+        if (gx >= g.ngx) gx -= g.ngx;
+        int gy = ty * kTile + yl;
+        if (gy >= g.ngy) gy -= g.ngy;
+        tile[q * PS + xl * kPitch + yl] =
+            (p >= p_lo && p < p_hi)
+                ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
+                : make_float2(0.0f, 0.0f);
+    }
+
+    const LaneRole<W> role(lane);
+    const float ihw = g.inv_half_w, bl = g.beta_l2e;
+    const int lane_off = role.kx * kPitch + role.ky - (tx * kTile) * kPitch - ty * kTile;
+    for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+        const int n = (int)min(64u, it.e - b0);
+        const VisRec my = recs[b0 + min(lane, n - 1)];
+        float mine_r = 0.0f, mine_i = 0.0f;
+        for (int k = 0; k < n; ++k) {
+            const RecRegs rc = rec_at(my, k);
+            const float kval = role.taps(rc, ihw, bl);
+            const float ku = __shfl(kval, role.kx);
+            const float kv = __shfl(kval, W + role.ky);
+            const int off = lane_off + (int)(rc.ij & 0xffffu) * kPitch + (int)(rc.ij >> 16);
+            float kw[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(kval, 2 * W + q) : 1.0f;
+            float sr = 0.0f, si = 0.0f;
+            if (role.act) {
+                float2 a[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) a[q] = tile[q * PS + off];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    sr = fmaf(kw[q], a[q].x, sr);
+                    si = fmaf(kw[q], a[q].y, si);
+                }
+            }
+            const float kk = role.act ? ku * kv : 0.0f;
+            sr *= kk;
+            si *= kk;
+            for (int o = 32; o > 0; o >>= 1) {
+                sr += __shfl_xor(sr, o);
+                si += __shfl_xor(si, o);
+            }
+            if (k == lane) {
+                mine_r = sr;
+                mine_i = si;
+            }
+        }
+        if (lane < n) {
+            atomicAdd(&acc[b0 + lane].x, mine_r);
+            atomicAdd(&acc[b0 + lane].y, mine_i);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// kernels: image-domain w screens and grid correction
+// ------------------------------------------------------------------------
+struct PixelGeom {
+    int gx, gy;
+    double corr, s;
+    bool inside;
+};
+
+__device__ __forceinline__ PixelGeom pixel_geom(const Geo &g, int ix, int iy,
+                                                const double *__restrict__ tab) {
+    PixelGeom p;
+    const int X = ix - g.nx / 2, Y = iy - g.ny / 2;
+    p.gx = X < 0 ? X + g.ngx : X;
+    p.gy = Y < 0 ? Y + g.ngy : Y;
+    const double l = X * g.px, m = Y * g.py;
+    const double r2 = l * l + m * m;
+    p.inside = !g.do_w || r2 < 1.0;
+    p.corr = 1.0 / (phi_lookup(tab, (double)X / g.ngx) * phi_lookup(tab, (double)Y / g.ngy));
+    p.s = 0.0;
+    if (g.do_w && p.inside) {
+        const double nm1 = -r2 / (sqrt(1.0 - r2) + 1.0);
+        p.s = -nm1 - g.s0;
+        p.corr /= phi_lookup(tab, g.dw * p.s) * (nm1 + 1.0);
+    }
+    if ((X + Y) & 1) p.corr = -p.corr;  // centred-grid storage
+    return p;
+}
+
+__global__ void k_screen_fwd(Geo g, const float2 *__restrict__ grid, int p_begin, int np,
+                             double *dirty, int64_t sx, int64_t sy, int accumulate,
+                             const double *__restrict__ tab) {
+    const int iy = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ix = blockIdx.y;
+    if (iy >= g.ny) return;
+    const PixelGeom p = pixel_geom(g, ix, iy, tab);
+    double res = 0.0;
+    if (p.inside) {
+        const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+        const float2 *src = grid + (int64_t)p.gx * g.ngy + p.gy;
+        if (g.do_w) {
+            double acc = 0.0;
+            for (int q = 0; q < np; ++q) {
+                const float2 h = src[q * plane_elems];
+                double ph = (g.w0 + (p_begin + q) * g.dw) * p.s;
+                ph -= rint(ph);
+                float sn, cs;
+                sincospif((float)(2.0 * ph), &sn, &cs);
+                acc += (double)h.x * cs - (double)h.y * sn;
+            }
+            res = acc * p.corr;
+        } else {
+            res = (double)src[0].x * p.corr;
+        }
+    }
+    double *o = dirty + ix * sx + iy * sy;
+    *o = accumulate ? *o + res : res;
+}
+
+__global__ void k_screen_adj(Geo g, const double *__restrict__ dirty, int64_t sx, int64_t sy,
+                             int p_begin, int np, float2 *grid, const double *__restrict__ tab) {
+    const int iy = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ix = blockIdx.y;
+    if (iy >= g.ny) return;
+    const PixelGeom p = pixel_geom(g, ix, iy, tab);
+    const double val = p.inside ? dirty[ix * sx + iy * sy] * p.corr : 0.0;
+    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+    float2 *dst = grid + (int64_t)p.gx * g.ngy + p.gy;
+    if (g.do_w) {
+        for (int q = 0; q < np; ++q) {
+            double ph = (g.w0 + (p_begin + q) * g.dw) * p.s;
+            ph -= rint(ph);
+            float sn, cs;
+            sincospif((float)(2.0 * ph), &sn, &cs);
+            dst[q * plane_elems] = make_float2((float)(val * cs), (float)(-val * sn));
+        }
+    } else {
+        dst[0] = make_float2((float)val, 0.0f);
+    }
+}
+
+__device__ __forceinline__ void store_vis(float2 *p, float2 v, int accumulate) {
+    if (accumulate) {
+        const float2 o = *p;
+        v.x += o.x;
+        v.y += o.y;
+    }
+    *p = v;
+}
+__device__ __forceinline__ void store_vis(double2 *p, float2 v, int accumulate) {
+    double2 w = make_double2(v.x, v.y);
+    if (accumulate) {
+        const double2 o = *p;
+        w.x += o.x;
+        w.y += o.y;
+    }
+    *p = w;
+}
+
+template <class VT>
+__global__ void k_zero_vis(int64_t nrow, int nchan, VT *vis, int64_t vrs, int64_t vcs) {
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v >= nrow * nchan) return;
+    const int64_t row = v / nchan;
+    const int chan = (int)(v - row * nchan);
+    VT z;
+    z.x = 0;
+    z.y = 0;
+    vis[row * vrs + chan * vcs] = z;
+}
+
+template <class VT>
+__global__ void k_finalize(int64_t nrec, int nchan, const VisRec *__restrict__ recs,
+                           const float2 *__restrict__ acc, VT *vis, int64_t vrs, int64_t vcs,
+                           int accumulate) {
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const VisRec rc = recs[r];
+    const float2 a = acc[r];
+    const float2 v = make_float2(rc.cre * a.x - rc.cim * a.y, rc.cre * a.y + rc.cim * a.x);
+    const int64_t row = rc.idx / (uint32_t)nchan;
+    const int chan = (int)(rc.idx - row * nchan);
+    store_vis(vis + row * vrs + chan * vcs, v, accumulate);
+}
+
+// ------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------
+static double es_kernel_host(double t, int W, double beta) {
+    const double x = 2.0 * t / W;
+    const double y = 1.0 - x * x;
+    return y > 0.0 ? std::exp(beta * (std::sqrt(y) - 1.0)) : 0.0;
+}
+
+static void gauss_legendre(int n, std::vector<double> &x, std::vector<double> &w) {
+    x.resize(n);
+    w.resize(n);
+    for (int i = 0; i < n; ++i) {
+        double z = std::cos(M_PI * (i + 0.75) / (n + 0.5));
+        double dp = 1.0;
+        for (int it = 0; it < 100; ++it) {
+            double p0 = 1.0, p1 = 0.0;
+            for (int k = 1; k <= n; ++k) {
+                const double p2 = p1;
+                p1 = p0;
+                p0 = ((2.0 * k - 1.0) * z * p1 - (k - 1.0) * p2) / k;
+            }
+            dp = n * (z * p0 - p1) / (z * z - 1.0);
+            const double dz = p0 / dp;
+            z -= dz;
+            if (std::fabs(dz) < 1e-16) break;
+        }
+        x[i] = z;
+        w[i] = 2.0 / ((1.0 - z * z) * dp * dp);
+    }
+}
+
+// Phi(xi) = int_{-W/2}^{W/2} phi(t) cos(2 pi t xi) dt on xi in [0, 0.5].
+static const double *phi_table(int W, double beta, hipStream_t stream) {
+    static std::mutex mu;
+    static std::map<int, std::vector<double>> cache;
+    const std::vector<double> *tab;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        std::vector<double> &t = cache[W];
+        if (t.empty()) {
+            std::vector<double> z, wq;
+            gauss_legendre(128, z, wq);
+            t.resize(kPhiTab);
+            for (int k = 0; k < kPhiTab; ++k) {
+                const double xi = 0.5 * k / (kPhiTab - 1);
+                double s = 0.0;
+                for (int i = 0; i < 128; ++i) {
+                    const double tt = 0.25 * W * (z[i] + 1.0);
+                    s += 0.25 * W * wq[i] * es_kernel_host(tt, W, beta) *
+                         std::cos(2.0 * M_PI * tt * xi);
+                }
+                t[k] = 2.0 * s;
+            }
+        }
+        tab = &t;
+    }
+    double *d = scratch<double>("phi_tab_W" + std::to_string(W), kPhiTab);
+    SDP_HIP_CHECK(hipMemcpyAsync(d, tab->data(), kPhiTab * sizeof(double),
+                                 hipMemcpyHostToDevice, stream));
+    return d;
+}
+
+static hipfftHandle fft_plan(int ngx, int ngy, int batch, hipStream_t stream) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int, int>, hipfftHandle> plans;
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple(dev, ngx, ngy, batch);
+    auto itp = plans.find(key);
+    hipfftHandle h;
+    if (itp == plans.end()) {
+        int n[2] = {ngx, ngy};
+        if (hipfftPlanMany(&h, 2, n, nullptr, 1, 0, nullptr, 1, 0, HIPFFT_C2C, batch) !=
+            HIPFFT_SUCCESS)
+            throw Error(SDP_HIP_ERR_RUNTIME, "hipfftPlanMany failed");
+        plans[key] = h;
+    } else {
+        h = itp->second;
+    }
+    if (hipfftSetStream(h, stream) != HIPFFT_SUCCESS)
+        throw Error(SDP_HIP_ERR_RUNTIME, "hipfftSetStream failed");
+    return h;
+}
+
+static double ord_dec(unsigned long long u) {
+    const long long i = (u & 0x8000000000000000ull) ? (long long)(u & 0x7fffffffffffffffull)
+                                                    : (long long)~u;
+    double d;
+    std::memcpy(&d, &i, sizeof(d));
+    return d;
+}
+
+static int kernel_support(double epsilon) {
+    const double eps = std::max(epsilon, 1.0e-7);
+    const int W = (int)std::ceil(-std::log10(eps / 10.0) - 1e-9);
+    return std::min(std::max(W, 2), kMaxW);
+}
+
+static bool g_stage_timing = false;
+
+struct StageTimer {
+    hipStream_t s;
+    bool on;
+    hipEvent_t ev[8];
+    int n = 0;
+    explicit StageTimer(hipStream_t st) : s(st), on(g_stage_timing) {
+        if (on)
+            for (auto &e : ev) SDP_HIP_CHECK(hipEventCreate(&e));
+    }
+    void mark() {
+        if (on && n < 8) SDP_HIP_CHECK(hipEventRecord(ev[n++], s));
+    }
+    float ms(int a, int b) {
+        if (!on || b >= n) return 0.0f;
+        float t = 0.0f;
+        SDP_HIP_CHECK(hipEventSynchronize(ev[b]));
+        SDP_HIP_CHECK(hipEventElapsedTime(&t, ev[a], ev[b]));
+        return t;
+    }
+    ~StageTimer() {
+        if (on)
+            for (auto &e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+struct Plan {
+    Geo g;
+    VisRec *recs = nullptr;
+    Item *items = nullptr;
+    int64_t nrec = 0;
+    int64_t nitems = 0;
+    std::vector<unsigned> p0_items;  // first item of every first-plane value
+    int chunk_planes = 1;            // planes resident per pass
+    float2 *grid = nullptr;
+};
+
+struct Inputs {
+    const double *uvw;
+    int64_t uvw_rs;
+    const double *freq;
+    int nchan;
+    int64_t nrow;
+    const void *vis;
+    int vis_dtype;
+    int64_t vrs, vcs;
+    const float *wgt;
+    int64_t wrs, wcs;
+    int nx, ny;
+    double px, py;
+    double eps;
+    int do_w;
+    unsigned flags;
+};
+
+static size_t grid_budget_bytes() {
+    const char *e = std::getenv("SDP_HIP_GRID_BUDGET_GB");
+    double gb = e ? std::atof(e) : 48.0;
+    if (!(gb > 0)) gb = 48.0;
+    return (size_t)(gb * 1073741824.0);
+}
+
+// Geometry, bucketing and work items shared by both directions.
+static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
+    SDP_REQUIRE(in.nx > 0 && in.ny > 0 && in.nx % 2 == 0 && in.ny % 2 == 0,
+                "npix_x and npix_y must be positive and even");
+    SDP_REQUIRE(in.px > 0 && in.py > 0, "pixel sizes must be positive");
+    SDP_REQUIRE(in.nchan > 0 && in.nrow >= 0, "nchan must be positive");
+    SDP_REQUIRE(in.nrow * (int64_t)in.nchan < (int64_t)0xffffffffll,
+                "more than 2^32 visibilities per call");
+    Plan P;
+    Geo &g = P.g;
+    g.W = kernel_support(in.eps);
+    g.beta = (float)(2.30 * g.W);
+    g.inv_half_w = 2.0f / (float)g.W;
+    g.beta_l2e = (float)(2.30 * g.W * 1.4426950408889634);
+    g.nx = in.nx;
+    g.ny = in.ny;
+    g.ngx = ((2 * in.nx + kTile - 1) / kTile) * kTile;
+    g.ngy = ((2 * in.ny + kTile - 1) / kTile) * kTile;
+    SDP_REQUIRE(g.ngx <= 65535 && g.ngy <= 65535, "image too large (padded grid > 65535)");
+    g.px = in.px;
+    g.py = in.py;
+    g.su = (in.flags & SDP_HIP_FLIP_UW) ? -1.0 : 1.0;
+    g.nchan = in.nchan;
+    g.nrow = in.nrow;
+    g.nty = g.ngy / kTile;
+    g.ntiles = (g.ngx / kTile) * g.nty;
+
+    // frequency extremes (host) and uvw bounds (device)
+    std::vector<double> f(in.nchan);
+    SDP_HIP_CHECK(hipMemcpyAsync(f.data(), in.freq, in.nchan * sizeof(double),
+                                 hipMemcpyDeviceToHost, st));
+    auto *bnd = scratch<unsigned long long>("bounds", 4);
+    k_init_bounds<<<1, 1, 0, st>>>(bnd);
+    SDP_HIP_CHECK(hipStreamSynchronize(st));
+    const double fmin_ = *std::min_element(f.begin(), f.end());
+    const double fmax_ = *std::max_element(f.begin(), f.end());
+    SDP_REQUIRE(fmin_ > 0, "frequencies must be positive");
+    unsigned long long hb[4] = {~0ull, 0, 0, 0};
+    if (in.nrow > 0) {
+        k_bounds<<<std::min<unsigned>(grid1d(in.nrow, 256), 2048), 256, 0, st>>>(
+            in.uvw, in.uvw_rs, in.nrow, g.su, fmin_ / kCLight, fmax_ / kCLight, bnd);
+        SDP_HIP_CHECK(hipMemcpyAsync(hb, bnd, sizeof(hb), hipMemcpyDeviceToHost, st));
+        SDP_HIP_CHECK(hipStreamSynchronize(st));
+    }
+    const double wmin = in.nrow > 0 ? ord_dec(hb[0]) : 0.0;
+    const double wmax = in.nrow > 0 ? ord_dec(hb[1]) : 0.0;
+    const double umax = in.nrow > 0 ? ord_dec(hb[2]) : 0.0;
+    const double vmax = in.nrow > 0 ? ord_dec(hb[3]) : 0.0;
+    SDP_REQUIRE(std::isfinite(wmin) && std::isfinite(wmax) && std::isfinite(umax) &&
+                    std::isfinite(vmax),
+                "non-finite uvw coordinates");
+    SDP_REQUIRE(umax * in.px < 0.5 && vmax * in.py < 0.5,
+                "some uvw coordinates exceed the image's Nyquist limit (|u|*pixsize >= 0.5)");
+
+    const double lmax = (in.nx / 2) * in.px, mmax = (in.ny / 2) * in.py;
+    const double r2 = std::min(lmax * lmax + mmax * mmax, 1.0);
+    const double tmax = 1.0 - std::sqrt(1.0 - r2);
+    g.do_w = (in.do_w && tmax > 0.0) ? 1 : 0;
+    if (g.do_w) {
+        g.s0 = 0.5 * tmax;
+        g.dw = 1.0 / (2.0 * tmax);
+        g.w0 = wmin - (0.5 * g.W - 0.5) * g.dw;
+        const double pwmax = (wmax - g.w0) / g.dw;
+        g.nplanes = (int)std::floor(pwmax - 0.5 * g.W) + 1 + g.W;
+        g.nps = g.nplanes - g.W + 1;
+    } else {
+        g.s0 = 0.0;
+        g.dw = 1.0;
+        g.w0 = 0.0;
+        g.nplanes = 1;
+        g.nps = 1;
+    }
+    SDP_REQUIRE((double)g.ntiles * g.nps < 4.0e9, "too many (plane, tile) buckets");
+
+    // ---- bucketing
+    const int64_t nvis = in.nrow * (int64_t)in.nchan;
+    const size_t nkeys = (size_t)g.ntiles * g.nps;
+    unsigned *hist = scratch<unsigned>("hist", nkeys + 1);
+    unsigned *offs = scratch<unsigned>("offs", nkeys + 1);
+    auto *nbad = scratch<unsigned long long>("nbad", 1);
+    SDP_HIP_CHECK(hipMemsetAsync(hist, 0, (nkeys + 1) * sizeof(unsigned), st));
+    SDP_HIP_CHECK(hipMemsetAsync(nbad, 0, sizeof(unsigned long long), st));
+
+    const unsigned nb = grid1d(nvis, 256);
+    auto launch_bucket = [&](auto scatter_tag, unsigned *counter, VisRec *recs) {
+        constexpr bool S = decltype(scatter_tag)::value;
+        if (in.vis_dtype == SDP_HIP_C128) {
+            if (grid_mode)
+                k_bucket<double2, S, true><<<nb, 256, 0, st>>>(
+                    g, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis, in.vrs, in.vcs,
+                    in.wgt, in.wrs, in.wcs, counter, recs, nbad);
+            else
+                k_bucket<double2, S, false><<<nb, 256, 0, st>>>(
+                    g, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs, in.wcs,
+                    counter, recs, nbad);
+        } else {
+            if (grid_mode)
+                k_bucket<float2, S, true><<<nb, 256, 0, st>>>(
+                    g, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis, in.vrs, in.vcs,
+                    in.wgt, in.wrs, in.wcs, counter, recs, nbad);
+            else
+                k_bucket<float2, S, false><<<nb, 256, 0, st>>>(
+                    g, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs, in.wcs,
+                    counter, recs, nbad);
+        }
+    };
+    if (nvis > 0) launch_bucket(std::false_type{}, hist, nullptr);
+
+    unsigned *nch = scratch<unsigned>("nch", nkeys + 1);
+    unsigned *ioffs = scratch<unsigned>("ioffs", nkeys + 1);
+    size_t tmp_bytes = 0;
+    SDP_HIP_CHECK(
+        hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, hist, offs, (int)(nkeys + 1), st));
+    void *tmp = scratch<char>("scan_tmp", tmp_bytes + 16);
+    size_t tb = tmp_bytes + 16;
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, offs, (int)(nkeys + 1), st));
+    // reuse hist as the scatter cursor
+    SDP_HIP_CHECK(hipMemcpyAsync(hist, offs, (nkeys + 1) * sizeof(unsigned),
+                                 hipMemcpyDeviceToDevice, st));
+    P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
+    if (nvis > 0) launch_bucket(std::true_type{}, hist, P.recs);
+
+    // ---- work items (p0-major, so a first-plane range is a contiguous item range)
+    SDP_HIP_CHECK(hipMemsetAsync(nch + nkeys, 0, sizeof(unsigned), st));
+    k_items_count<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, offs, nch);
+    tb = tmp_bytes + 16;
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nch, ioffs, (int)(nkeys + 1), st));
+    unsigned *pofs = scratch<unsigned>("p0_offs", g.nps + 1);
+    k_gather_p0_offsets<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(ioffs, g.ntiles, g.nps, pofs);
+    P.p0_items.resize(g.nps + 1);
+    unsigned long long nbad_h = 0;
+    unsigned nrec_h = 0;
+    SDP_HIP_CHECK(hipMemcpyAsync(P.p0_items.data(), pofs, (g.nps + 1) * sizeof(unsigned),
+                                 hipMemcpyDeviceToHost, st));
+    SDP_HIP_CHECK(hipMemcpyAsync(&nbad_h, nbad, sizeof(nbad_h), hipMemcpyDeviceToHost, st));
+    SDP_HIP_CHECK(
+        hipMemcpyAsync(&nrec_h, offs + nkeys, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    SDP_HIP_CHECK(hipStreamSynchronize(st));
+    SDP_REQUIRE(nbad_h == 0, "visibilities outside the padded grid");
+    P.nrec = nrec_h;
+    P.nitems = P.p0_items[g.nps];
+    P.items = scratch<Item>("items", std::max<int64_t>(P.nitems, 1));
+    k_items_fill<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, g.ntiles, offs, ioffs,
+                                                     P.items);
+
+    // ---- plane chunking against the grid memory budget
+    const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
+    const int cp = (int)std::max<size_t>(1, grid_budget_bytes() / plane_bytes);
+    P.chunk_planes = std::min(cp, g.nplanes);
+    P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy);
+    return P;
+}
+
+// Item range whose W-plane windows intersect planes [p_lo, p_hi).
+static std::pair<unsigned, unsigned> chunk_items(const Plan &P, int p_lo, int p_hi) {
+    const int a = std::max(0, p_lo - (P.g.do_w ? P.g.W : 1) + 1);
+    const int b = std::min(P.g.nps - 1, p_hi - 1);
+    if (a > b) return {0u, 0u};
+    return {P.p0_items[a], P.p0_items[b + 1]};
+}
+
+static void allow_lds(const void *fn, size_t bytes) {
+    if (bytes > 65536)
+        SDP_HIP_CHECK(
+            hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
+
+template <int W>
+static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
+    const auto r = chunk_items(P, p_lo, p_hi);
+    if (r.second <= r.first) return;
+    const size_t lds = (size_t)(P.g.do_w ? W : 1) * TileShape<W>::PLANE * sizeof(float2);
+    if (P.g.do_w) {
+        allow_lds((const void *)k_grid<W, true>, lds);
+        k_grid<W, true><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
+                                                            (float *)P.grid, p_lo, p_hi);
+    } else {
+        allow_lds((const void *)k_grid<W, false>, lds);
+        k_grid<W, false><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
+                                                             (float *)P.grid, p_lo, p_hi);
+    }
+}
+
+template <int W>
+static void launch_degrid(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
+    const auto r = chunk_items(P, p_lo, p_hi);
+    if (r.second <= r.first) return;
+    const size_t lds = (size_t)(P.g.do_w ? W : 1) * TileShape<W>::PLANE * sizeof(float2);
+    if (P.g.do_w) {
+        allow_lds((const void *)k_degrid<W, true>, lds);
+        k_degrid<W, true><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
+                                                              P.grid, p_lo, p_hi, acc);
+    } else {
+        allow_lds((const void *)k_degrid<W, false>, lds);
+        k_degrid<W, false><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
+                                                               P.grid, p_lo, p_hi, acc);
+    }
+}
+
+#define SDP_W_DISPATCH(W, CALL) \
+    switch (W) {                \
+        case 2: CALL(2); break; \
+        case 3: CALL(3); break; \
+        case 4: CALL(4); break; \
+        case 5: CALL(5); break; \
+        case 6: CALL(6); break; \
+        case 7: CALL(7); break; \
+        default: CALL(8); break; \
+    }
+
+static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
+    if (!info) return;
+    info->support = P.g.W;
+    info->beta = P.g.beta;
+    info->ngrid_x = P.g.ngx;
+    info->ngrid_y = P.g.ngy;
+    info->nplanes = P.g.nplanes;
+    info->w0 = P.g.w0;
+    info->dw = P.g.dw;
+    info->nvis_used = P.nrec;
+    info->nitems = P.nitems;
+    info->plane_chunk = P.chunk_planes;
+}
+
+static void fft_planes(const Plan &P, int np, int direction, hipStream_t st) {
+    hipfftHandle h = fft_plan(P.g.ngx, P.g.ngy, np, st);
+    if (hipfftExecC2C(h, (hipfftComplex *)P.grid, (hipfftComplex *)P.grid, direction) !=
+        HIPFFT_SUCCESS)
+        throw Error(SDP_HIP_ERR_RUNTIME, "hipfftExecC2C failed");
+}
+
+static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
+                     sdp_hip_wgrid_info *info, hipStream_t st) {
+    SDP_REQUIRE(in.vis == nullptr || in.vis_dtype == SDP_HIP_C64 ||
+                    in.vis_dtype == SDP_HIP_C128,
+                "vis must be complex64 or complex128");
+    StageTimer tm(st);
+    tm.mark();
+    Plan P = make_plan(in, true, st);
+    const Geo &g = P.g;
+    const double *tab = phi_table(g.W, g.beta, st);
+    tm.mark();
+    const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
+    const size_t plane_elems = (size_t)g.ngx * g.ngy;
+    float tgrid = 0, tfft = 0, tscr = 0;
+    for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
+        const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
+        const int np = p_hi - p_lo;
+        StageTimer t2(st);
+        t2.mark();
+        SDP_HIP_CHECK(hipMemsetAsync(P.grid, 0, (size_t)np * plane_elems * sizeof(float2), st));
+#define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, p_lo, p_hi, st)
+        SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
+#undef SDP_LAUNCH_GRID
+        SDP_HIP_CHECK(hipGetLastError());
+        t2.mark();
+        fft_planes(P, np, HIPFFT_BACKWARD, st);
+        t2.mark();
+        const dim3 grd(grid1d(g.ny, 256), g.nx);
+        k_screen_fwd<<<grd, 256, 0, st>>>(g, P.grid, p_lo, np, dirty, sx, sy,
+                                          (accumulate || p_lo > 0) ? 1 : 0, tab);
+        SDP_HIP_CHECK(hipGetLastError());
+        t2.mark();
+        tgrid += t2.ms(0, 1);
+        tfft += t2.ms(1, 2);
+        tscr += t2.ms(2, 3);
+    }
+    tm.mark();
+    fill_info(P, info);
+    if (info) {
+        info->ms_prep = tm.ms(0, 1);
+        info->ms_grid = tgrid;
+        info->ms_fft = tfft;
+        info->ms_screen = tscr;
+    }
+}
+
+static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t sy, void *vis,
+                     sdp_hip_wgrid_info *info, hipStream_t st) {
+    SDP_REQUIRE(in.vis_dtype == SDP_HIP_C64 || in.vis_dtype == SDP_HIP_C128,
+                "vis must be complex64 or complex128");
+    StageTimer tm(st);
+    tm.mark();
+    Plan P = make_plan(in, false, st);
+    const Geo &g = P.g;
+    const double *tab = phi_table(g.W, g.beta, st);
+    tm.mark();
+    const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
+    const int64_t nvis = in.nrow * (int64_t)in.nchan;
+    if (!accumulate && nvis > 0) {
+        if (in.vis_dtype == SDP_HIP_C128)
+            k_zero_vis<double2><<<grid1d(nvis, 256), 256, 0, st>>>(
+                in.nrow, in.nchan, (double2 *)vis, in.vrs, in.vcs);
+        else
+            k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, st>>>(
+                in.nrow, in.nchan, (float2 *)vis, in.vrs, in.vcs);
+    }
+    float2 *acc = scratch<float2>("degrid_acc", std::max<int64_t>(P.nrec, 1));
+    SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(P.nrec, 1) * sizeof(float2), st));
+    const size_t plane_elems = (size_t)g.ngx * g.ngy;
+    float tgrid = 0, tfft = 0, tscr = 0;
+    for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
+        const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
+        const int np = p_hi - p_lo;
+        StageTimer t2(st);
+        t2.mark();
+        SDP_HIP_CHECK(hipMemsetAsync(P.grid, 0, (size_t)np * plane_elems * sizeof(float2), st));
+        const dim3 grd(grid1d(g.ny, 256), g.nx);
+        k_screen_adj<<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_lo, np, P.grid, tab);
+        SDP_HIP_CHECK(hipGetLastError());
+        t2.mark();
+        fft_planes(P, np, HIPFFT_FORWARD, st);
+        t2.mark();
+#define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, acc, st)
+        SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
+#undef SDP_LAUNCH_DEGRID
+        SDP_HIP_CHECK(hipGetLastError());
+        t2.mark();
+        tscr += t2.ms(0, 1);
+        tfft += t2.ms(1, 2);
+        tgrid += t2.ms(2, 3);
+    }
+    if (P.nrec > 0) {
+        if (in.vis_dtype == SDP_HIP_C128)
+            k_finalize<double2><<<grid1d(P.nrec, 256), 256, 0, st>>>(
+                P.nrec, in.nchan, P.recs, acc, (double2 *)vis, in.vrs, in.vcs, accumulate);
+        else
+            k_finalize<float2><<<grid1d(P.nrec, 256), 256, 0, st>>>(
+                P.nrec, in.nchan, P.recs, acc, (float2 *)vis, in.vrs, in.vcs, accumulate);
+        SDP_HIP_CHECK(hipGetLastError());
+    }
+    tm.mark();
+    fill_info(P, info);
+    if (info) {
+        info->ms_prep = tm.ms(0, 1);
+        info->ms_grid = tgrid;
+        info->ms_fft = tfft;
+        info->ms_screen = tscr;
+    }
+}
+
+}  // namespace wstack
+}  // namespace sdp
+
+using namespace sdp;
+
+extern "C" {
+
+int sdp_hip_version(void) { return 1; }
+
+int sdp_hip_set_stage_timing(int enable) {
+    wstack::g_stage_timing = enable != 0;
+    return SDP_HIP_OK;
+}
+
+int sdp_hip_device_count(int *count, char *errbuf, size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) {
+            (void)hipGetLastError();
+            n = 0;
+        }
+        if (count) *count = n;
+    });
+}
+
+int sdp_hip_release_workspace(char *errbuf, size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] { Workspace::get().release(); });
+}
+
+int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride, const double *freq, int nchan,
+                     int64_t nrow, const void *vis, int vis_dtype, int64_t vis_row_stride,
+                     int64_t vis_chan_stride, const float *wgt, int64_t wgt_row_stride,
+                     int64_t wgt_chan_stride, int npix_x, int npix_y, double pixsize_x,
+                     double pixsize_y, double epsilon, int do_wstacking, unsigned flags,
+                     double *dirty, int64_t dirty_stride_x, int64_t dirty_stride_y, void *stream,
+                     sdp_hip_wgrid_info *info, char *errbuf, size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(dirty != nullptr && freq != nullptr && (uvw != nullptr || nrow == 0),
+                    "null pointer argument");
+        const wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                                nrow,        vis,             vis_dtype,      vis_row_stride,
+                                vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
+                                npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                                epsilon,     do_wstacking,    flags};
+        wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
+    });
+}
+
+int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride, const double *freq, int nchan,
+                     int64_t nrow, const double *dirty, int64_t dirty_stride_x,
+                     int64_t dirty_stride_y, int npix_x, int npix_y, double pixsize_x,
+                     double pixsize_y, const float *wgt, int64_t wgt_row_stride,
+                     int64_t wgt_chan_stride, double epsilon, int do_wstacking, unsigned flags,
+                     void *vis, int vis_dtype, int64_t vis_row_stride, int64_t vis_chan_stride,
+                     void *stream, sdp_hip_wgrid_info *info, char *errbuf, size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(dirty != nullptr && freq != nullptr && vis != nullptr &&
+                        (uvw != nullptr || nrow == 0),
+                    "null pointer argument");
+        const wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                                nrow,        nullptr,         vis_dtype,      vis_row_stride,
+                                vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
+                                npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                                epsilon,     do_wstacking,    flags};
+        wstack::dirty2ms(in, dirty, dirty_stride_x, dirty_stride_y, vis, info,
+                         as_stream(stream));
+    });
+}
+
+}  // extern "C"
