@@ -174,25 +174,29 @@ int sdp_hip_degrid_cf(int64_t nrowvis, int nchan_vis, int npol,
 
 /*
  * Batched iterative-substitution gain solver, replacing
- * _solve_antenna_gains_itsubs_scalar / _matrix / _nocrossdata
- * (reference src/ska_sdp_func_python/calibration/solvers.py:217-539).
- * One solve = one gain-table row: all of its channels iterate together and
- * stop on max|g - g_last| over ants AND channels (solvers.py:268, :427).
- *   x, xwt   [nsolve, nants, nants, nchan, npol] c128 / f64 (dense, the
- *            layout _solve_with_mask hands over, already normalised)
- *   gain     [nsolve, nants, nchan, nrec, nrec] c128  (in: start, out)
- *   gwt      [nsolve, nants, nchan, nrec, nrec] f64   (out)
- *   residual [nsolve, nchan, nrec, nrec] f64          (out)
- *   niter_out[nsolve] int32 iterations used (niter+1 = not converged)
- * mode: 0 scalar (npol 1), 1 matrix (npol 4, crosspol), 2 nocrossdata
- * (npol 2 or npol 4 without crosspol).
+ * _solve_with_mask + _solve_antenna_gains_itsubs_scalar / _matrix /
+ * _nocrossdata + the residual functions (reference
+ * src/ska_sdp_func_python/calibration/solvers.py:148-539).  One solve = one
+ * gain-table row; all of its channels (and 2x2 components) iterate together
+ * and stop on max|g - g_last| over antennas AND channels (solvers.py:268,
+ * :427), as in the reference.
+ *   baselines   canonical: a1 < a2, sorted by (a1, a2); row_start[nants+1]
+ *               is the CSR offset of each a1, ant2[nbl] the partner
+ *   xb, wb      [nsolve, nbl, nchan, npol] c128 / f64: the weighted sums
+ *               sum(V w) and sum(w) of solvers.py:99-107 (point-source vis)
+ *   gain        [nsolve, nants, nchan, nrec, nrec] c128 (in: start, out)
+ *   gwt         [nsolve, nants, nchan, nrec, nrec] f64   (out)
+ *   residual    [nsolve, nchan, nrec, nrec] f64          (out)
+ *   niter_out   [nsolve] int32 iterations used (niter + 1: not converged)
+ * mode: 0 scalar (npol 1), 1 matrix (npol 4, crosspol), 2 no cross data
+ * (npol 2, or npol 4 without crosspol).
  */
-int sdp_hip_solve_gains(int nsolve, int nants, int nchan, int npol, int mode,
-                        const void *x, const double *xwt, void *gain,
-                        double *gwt, double *residual, int32_t *niter_out,
-                        int niter, double tol, int phase_only, int refant,
-                        double damping, void *stream, char *errbuf,
-                        size_t errbuf_len);
+int sdp_hip_solve_gains(int nsolve, int nants, int nbl, const int32_t *row_start,
+                        const int32_t *ant2, int nchan, int npol, int mode,
+                        const void *xb, const double *wb, void *gain, double *gwt,
+                        double *residual, int32_t *niter_out, int niter, double tol,
+                        int phase_only, int refant, double damping, void *stream,
+                        char *errbuf, size_t errbuf_len);
 
 #ifdef __cplusplus
 }

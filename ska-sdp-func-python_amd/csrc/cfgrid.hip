@@ -1,0 +1,197 @@
+// Convolution-function (AW-projection) gridder / degridder for gfx950:
+// sdp_hip_grid_cf / sdp_hip_degrid_cf, replacing the pure-Python
+// chan x pol x row loops of the reference's grid_visibility_to_griddata and
+// degrid_visibility_from_griddata
+// (src/ska_sdp_func_python/grid_data/gridding.py:160-255, :502-590).
+//
+// The Python layer evaluates the reference's WCS mappings (spatial_mapping,
+// gridding.py:60-157) into integer grid / sub-sample / w-plane indices per
+// (channel, row).  Here one wave handles one (row, channel) with one lane per
+// CF tap:
+//   grid:   gd[c, p, pv-dv+iv, pu-du+iu] += conj(cf[c, p, w, dv_off, du_off, iv, iu]) * V * wt
+//           (fp64 global atomics; sumwt per block in LDS, one atomic per pol)
+//   degrid: V = sum_{iv,iu} gd[c, p, window] * cf[c, p, w, dv_off, du_off, iv, iu]
+// with the reference's edge-skip rule (gridding.py:230-237, :555-563): a row
+// whose window touches pv+dv >= ny or pu+du >= nx (or < 0) is skipped.
+#include "sdp_common.h"
+
+namespace sdp {
+namespace cfgrid {
+
+constexpr int kThreads = 256;
+constexpr int kMaxPol = 4;
+
+struct Shape {
+    int64_t nrow;
+    int nchan, npol, cf_nchan, nw, ndv, ndu, gv, gu, g_nchan, ny, nx;
+};
+
+__device__ __forceinline__ bool window_ok(const Shape &s, int pu, int pv) {
+    const int dv = s.gv / 2, du = s.gu / 2;
+    return !(pv - dv < 0 || pv + dv >= s.ny || pu - du < 0 || pu + du >= s.nx);
+}
+
+__device__ __forceinline__ size_t cf_index(const Shape &s, int c, int p, int w, int idv, int idu) {
+    return ((((size_t)c * s.npol + p) * s.nw + w) * s.ndv + idv) * s.ndu + idu;
+}
+
+__global__ __launch_bounds__(kThreads) void k_grid_cf(Shape s, const int32_t *__restrict__ pu,
+                                                      const int32_t *__restrict__ pv,
+                                                      const int32_t *__restrict__ pwc,
+                                                      const int32_t *__restrict__ pdu,
+                                                      const int32_t *__restrict__ pdv,
+                                                      const int32_t *__restrict__ vis_to_im,
+                                                      const double2 *__restrict__ vis,
+                                                      const double *__restrict__ wt,
+                                                      const double2 *__restrict__ cf,
+                                                      double2 *grid, double *sumwt,
+                                                      unsigned long long *nskipped) {
+    __shared__ double s_wt[kMaxPol];
+    __shared__ unsigned long long s_skip;
+    if (threadIdx.x < kMaxPol) s_wt[threadIdx.x] = 0.0;
+    if (threadIdx.x == 0) s_skip = 0;
+    __syncthreads();
+    const int chan = blockIdx.y;
+    const int imchan = vis_to_im[chan];
+    const int lane = threadIdx.x & 63;
+    const int taps = s.gv * s.gu;
+    const int dv = s.gv / 2, du = s.gu / 2;
+    const int64_t row = blockIdx.x * (int64_t)(kThreads / 64) + (threadIdx.x >> 6);
+    if (row < s.nrow) {
+        const size_t m = (size_t)chan * s.nrow + row;
+        const int u0 = pu[m], v0 = pv[m];
+        if (!window_ok(s, u0, v0)) {
+            if (lane == 0) atomicAdd(&s_skip, (unsigned long long)s.npol);
+        } else {
+            const int iw = pwc[m], idu = pdu[m], idv = pdv[m];
+            for (int p = 0; p < s.npol; ++p) {
+                const size_t vi = ((size_t)row * s.nchan + chan) * s.npol + p;
+                const double2 x = vis[vi];
+                const double w = wt[vi];
+                const double xr = x.x * w, xi = x.y * w;
+                const double2 *sub = cf + cf_index(s, imchan, p, iw, idv, idu) * taps;
+                double2 *g = grid + ((size_t)imchan * s.npol + p) * s.ny * s.nx;
+                for (int t = lane; t < taps; t += 64) {
+                    const int iv = t / s.gu, iu = t - (t / s.gu) * s.gu;
+                    const double2 c = sub[t];
+                    // conj(cf) * x
+                    const double re = c.x * xr + c.y * xi;
+                    const double im = c.x * xi - c.y * xr;
+                    double *dst = reinterpret_cast<double *>(
+                        g + (size_t)(v0 - dv + iv) * s.nx + (u0 - du + iu));
+                    if (re != 0.0) atomicAdd(dst, re);
+                    if (im != 0.0) atomicAdd(dst + 1, im);
+                }
+                if (lane == 0) atomicAdd(&s_wt[p], w);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < s.npol && sumwt) atomicAdd(&sumwt[(size_t)imchan * s.npol + threadIdx.x],
+                                                 s_wt[threadIdx.x]);
+    if (threadIdx.x == 0 && nskipped && s_skip) atomicAdd(nskipped, s_skip);
+}
+
+__global__ __launch_bounds__(kThreads) void k_degrid_cf(Shape s, const int32_t *__restrict__ pu,
+                                                        const int32_t *__restrict__ pv,
+                                                        const int32_t *__restrict__ pwc,
+                                                        const int32_t *__restrict__ pdu,
+                                                        const int32_t *__restrict__ pdv,
+                                                        const int32_t *__restrict__ vis_to_im,
+                                                        const double2 *__restrict__ grid,
+                                                        const double2 *__restrict__ cf,
+                                                        double2 *vis_out,
+                                                        unsigned long long *nskipped) {
+    const int chan = blockIdx.y;
+    const int imchan = vis_to_im[chan];
+    const int lane = threadIdx.x & 63;
+    const int taps = s.gv * s.gu;
+    const int dv = s.gv / 2, du = s.gu / 2;
+    const int64_t row = blockIdx.x * (int64_t)(kThreads / 64) + (threadIdx.x >> 6);
+    if (row >= s.nrow) return;
+    const size_t m = (size_t)chan * s.nrow + row;
+    const int u0 = pu[m], v0 = pv[m];
+    const bool ok = window_ok(s, u0, v0);
+    if (!ok && lane == 0 && nskipped) atomicAdd(nskipped, (unsigned long long)s.npol);
+    const int iw = pwc[m], idu = pdu[m], idv = pdv[m];
+    for (int p = 0; p < s.npol; ++p) {
+        double sr = 0.0, si = 0.0;
+        if (ok) {
+            const double2 *sub = cf + cf_index(s, imchan, p, iw, idv, idu) * taps;
+            const double2 *g = grid + ((size_t)imchan * s.npol + p) * s.ny * s.nx;
+            for (int t = lane; t < taps; t += 64) {
+                const int iv = t / s.gu, iu = t - (t / s.gu) * s.gu;
+                const double2 c = sub[t];
+                const double2 a = g[(size_t)(v0 - dv + iv) * s.nx + (u0 - du + iu)];
+                sr += a.x * c.x - a.y * c.y;
+                si += a.x * c.y + a.y * c.x;
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                sr += __shfl_xor(sr, o);
+                si += __shfl_xor(si, o);
+            }
+        }
+        if (lane == 0) vis_out[((size_t)row * s.nchan + chan) * s.npol + p] = make_double2(sr, si);
+    }
+}
+
+static Shape make_shape(int64_t nrow, int nchan, int npol, int cf_nchan, int nw, int ndv, int ndu,
+                        int gv, int gu, int g_nchan, int ny, int nx) {
+    SDP_REQUIRE(nrow >= 0 && nchan > 0 && npol > 0 && npol <= kMaxPol, "bad visibility shape");
+    SDP_REQUIRE(gv > 0 && gu > 0 && gv % 2 == 0 && gu % 2 == 0,
+                "convolution function support must be even (gridding.py:199-201)");
+    SDP_REQUIRE(cf_nchan >= g_nchan && nw > 0 && ndv > 0 && ndu > 0, "bad convolution function shape");
+    SDP_REQUIRE(ny > 0 && nx > 0 && g_nchan > 0, "bad grid shape");
+    return Shape{nrow, nchan, npol, cf_nchan, nw, ndv, ndu, gv, gu, g_nchan, ny, nx};
+}
+
+}  // namespace cfgrid
+}  // namespace sdp
+
+extern "C" {
+
+int sdp_hip_grid_cf(int64_t nrowvis, int nchan_vis, int npol, const int32_t *pu,
+                    const int32_t *pv, const int32_t *pwc, const int32_t *pdu,
+                    const int32_t *pdv, const int32_t *vis_to_im, const void *vis,
+                    const double *wt, const void *cf, int cf_nchan, int nw, int ndv, int ndu,
+                    int gv, int gu, void *grid, int g_nchan, int ny, int nx, double *sumwt,
+                    int64_t *nskipped, void *stream, char *errbuf, size_t errbuf_len) {
+    using namespace sdp;
+    return guarded(errbuf, errbuf_len, [&] {
+        const cfgrid::Shape s = cfgrid::make_shape(nrowvis, nchan_vis, npol, cf_nchan, nw, ndv,
+                                                   ndu, gv, gu, g_nchan, ny, nx);
+        if (nrowvis == 0) return;
+        SDP_REQUIRE(pu && pv && pwc && pdu && pdv && vis_to_im && vis && wt && cf && grid,
+                    "null pointer argument");
+        const dim3 blocks((unsigned)((nrowvis + 3) / 4), nchan_vis);
+        cfgrid::k_grid_cf<<<blocks, cfgrid::kThreads, 0, as_stream(stream)>>>(
+            s, pu, pv, pwc, pdu, pdv, vis_to_im, static_cast<const double2 *>(vis), wt,
+            static_cast<const double2 *>(cf), static_cast<double2 *>(grid), sumwt,
+            reinterpret_cast<unsigned long long *>(nskipped));
+        SDP_HIP_CHECK(hipGetLastError());
+    });
+}
+
+int sdp_hip_degrid_cf(int64_t nrowvis, int nchan_vis, int npol, const int32_t *pu,
+                      const int32_t *pv, const int32_t *pwc, const int32_t *pdu,
+                      const int32_t *pdv, const int32_t *vis_to_im, const void *grid,
+                      int g_nchan, int ny, int nx, const void *cf, int cf_nchan, int nw, int ndv,
+                      int ndu, int gv, int gu, void *vis_out, int64_t *nskipped, void *stream,
+                      char *errbuf, size_t errbuf_len) {
+    using namespace sdp;
+    return guarded(errbuf, errbuf_len, [&] {
+        const cfgrid::Shape s = cfgrid::make_shape(nrowvis, nchan_vis, npol, cf_nchan, nw, ndv,
+                                                   ndu, gv, gu, g_nchan, ny, nx);
+        if (nrowvis == 0) return;
+        SDP_REQUIRE(pu && pv && pwc && pdu && pdv && vis_to_im && grid && cf && vis_out,
+                    "null pointer argument");
+        const dim3 blocks((unsigned)((nrowvis + 3) / 4), nchan_vis);
+        cfgrid::k_degrid_cf<<<blocks, cfgrid::kThreads, 0, as_stream(stream)>>>(
+            s, pu, pv, pwc, pdu, pdv, vis_to_im, static_cast<const double2 *>(grid),
+            static_cast<const double2 *>(cf), static_cast<double2 *>(vis_out),
+            reinterpret_cast<unsigned long long *>(nskipped));
+        SDP_HIP_CHECK(hipGetLastError());
+    });
+}
+
+}  // extern "C"

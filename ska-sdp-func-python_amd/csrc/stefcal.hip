@@ -1,0 +1,454 @@
+// Batched antenna-gain solve by iterative substitution ("StefCal") for
+// gfx950: sdp_hip_solve_gains, replacing the numpy loops of the reference's
+// solve_gaintable inner solvers (src/ska_sdp_func_python/calibration/
+// solvers.py:148-539).
+//
+// A "solve" is one gain-table row; it holds nchan x ncomp independent
+// sub-problems (ncomp = 1 scalar, 4 for the 2x2 element-wise matrix forms)
+// that share one convergence test, exactly as the reference's
+// change = max|g - g_last| over antennas AND channels (solvers.py:268, :427).
+//
+// Device layout (fp32 storage, fp64 arithmetic):
+//   x, w   [solve][chan][comp][baseline]  normalised point-source vis/weight
+//   g, gw  [solve][chan][comp][antenna]   current gains / gain weights
+// Per iteration two launches: k_iter (one 256-thread workgroup per active
+// sub-problem: baselines streamed once, per-wave partial sums in LDS -- plain
+// read-modify-write, no LDS float atomics -- then the substitution, phase
+// normalisation, refant rotation, damping and the per-row max change) and
+// k_commit (row-level convergence).  The host polls the converged-row count
+// every few iterations.
+#include <cmath>
+#include <vector>
+
+#include "sdp_common.h"
+
+namespace sdp {
+namespace stefcal {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kMaxAnts = 1024;
+
+enum Mode { kScalar = 0, kMatrix = 1, kNoCross = 2 };
+
+struct Dims {
+    int nsolve, nants, nbl, nchan, npol, ncomp, nrec, mode;
+    int phase_only, refant;
+    double tol, damping;
+};
+
+__device__ __forceinline__ size_t sub_index(const Dims &d, int s, int chan, int comp) {
+    return ((size_t)s * d.nchan + chan) * d.ncomp + comp;
+}
+
+// input pol feeding component `comp`, or -1 (component has no data)
+__device__ __forceinline__ int comp_pol(const Dims &d, int comp) {
+    if (d.mode == kScalar) return 0;
+    if (d.mode == kMatrix) return comp;
+    if (comp == 1 || comp == 2) return -1;  // no cross-hand data
+    return d.npol == 2 ? (comp == 0 ? 0 : 1) : comp;
+}
+
+__device__ __forceinline__ unsigned long long dbits(double v) {
+    return (unsigned long long)__double_as_longlong(v);
+}
+
+// max over the row of wb (solvers.py:167: xwt / max(xwt))
+__global__ void k_rowmax(Dims d, const double *__restrict__ wb, unsigned long long *rowmax) {
+    const size_t per = (size_t)d.nbl * d.nchan * d.npol;
+    const int s = blockIdx.y;
+    double m = 0.0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < per;
+         i += (size_t)gridDim.x * blockDim.x)
+        m = fmax(m, fabs(wb[(size_t)s * per + i]));
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0 && m > 0.0) atomicMax(&rowmax[s], dbits(m));
+}
+
+// x = xb / wb, w = wb / max  (masked where wb <= 0), into [s][chan][comp][bl]
+__global__ void k_fill(Dims d, const double2 *__restrict__ xb, const double *__restrict__ wb,
+                       const unsigned long long *__restrict__ rowmax, float2 *x, float *w) {
+    const size_t nsub = (size_t)d.nsolve * d.nchan * d.ncomp;
+    const size_t total = nsub * d.nbl;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int b = (int)(i % d.nbl);
+        const size_t sub = i / d.nbl;
+        const int comp = (int)(sub % d.ncomp);
+        const int chan = (int)((sub / d.ncomp) % d.nchan);
+        const int s = (int)(sub / ((size_t)d.ncomp * d.nchan));
+        const int p = comp_pol(d, comp);
+        float2 xv = make_float2(0.0f, 0.0f);
+        float wv = 0.0f;
+        if (p >= 0) {
+            const size_t src = (((size_t)s * d.nbl + b) * d.nchan + chan) * d.npol + p;
+            const double ww = wb[src];
+            const double mx = __longlong_as_double((long long)rowmax[s]);
+            if (ww > 0.0 && mx > 0.0) {
+                const double2 xx = xb[src];
+                xv = make_float2((float)(xx.x / ww), (float)(xx.y / ww));
+                wv = (float)(ww / mx);
+            }
+        }
+        x[i] = xv;
+        w[i] = wv;
+    }
+}
+
+// gains [s][ant][chan][r1][r2] (c128) -> working [s][chan][comp][ant]
+__global__ void k_load_gains(Dims d, const double2 *__restrict__ gin,
+                             const double *__restrict__ gwin, double2 *g, double *gw) {
+    const size_t total = (size_t)d.nsolve * d.nchan * d.ncomp * d.nants;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int a = (int)(i % d.nants);
+        const size_t sub = i / d.nants;
+        const int comp = (int)(sub % d.ncomp);
+        const int chan = (int)((sub / d.ncomp) % d.nchan);
+        const int s = (int)(sub / ((size_t)d.ncomp * d.nchan));
+        const size_t src = (((size_t)s * d.nants + a) * d.nchan + chan) * d.ncomp + comp;
+        double2 v = gin[src];
+        if (d.mode != kScalar && (comp == 1 || comp == 2)) v = make_double2(0.0, 0.0);  // :418-419
+        g[i] = v;
+        gw[i] = gwin[src];  // returned unchanged when no iteration runs
+    }
+}
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+__global__ __launch_bounds__(kThreads) void k_iter(Dims d, const int32_t *__restrict__ row_start,
+                                                   const int32_t *__restrict__ ant2,
+                                                   const float2 *__restrict__ x,
+                                                   const float *__restrict__ w,
+                                                   const double2 *__restrict__ g, double2 *gnext,
+                                                   double *gwnext, const int32_t *__restrict__ done,
+                                                   unsigned long long *change) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int sub = blockIdx.x;
+    const int comp = sub % d.ncomp;
+    const int chan = (sub / d.ncomp) % d.nchan;
+    const int s = sub / (d.ncomp * d.nchan);
+    if (done[s]) return;
+    const int na = d.nants;
+    double2 *gl = reinterpret_cast<double2 *>(lds);  // [na]
+    double2 *top = gl + na;                          // [kWaves][na]
+    double *bot = reinterpret_cast<double *>(top + (size_t)kWaves * na);  // [kWaves][na]
+    const size_t gbase = (size_t)sub * na;
+    const size_t xbase = (size_t)sub * d.nbl;
+    for (int a = threadIdx.x; a < na; a += kThreads) {
+        gl[a] = g[gbase + a];
+        for (int k = 0; k < kWaves; ++k) {
+            top[k * na + a] = make_double2(0.0, 0.0);
+            bot[k * na + a] = 0.0;
+        }
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    double2 *tw = top + (size_t)wave * na;
+    double *bw = bot + (size_t)wave * na;
+    for (int a1 = wave; a1 < na; a1 += kWaves) {
+        const double2 g1 = gl[a1];
+        const double p1 = g1.x * g1.x + g1.y * g1.y;
+        double tr = 0.0, ti = 0.0, bs = 0.0;
+        const int b1 = row_start[a1 + 1];
+        for (int b = row_start[a1] + lane; b < b1; b += 64) {
+            const int a2 = ant2[b];
+            const float2 xv = x[xbase + b];
+            const double wv = w[xbase + b];
+            const double2 g2 = gl[a2];
+            // antenna a2 (i = a1): x[a1,a2] = conj(x_b)
+            const double2 c1 = cmul(g1, make_double2(xv.x * wv, -xv.y * wv));
+            double2 t = tw[a2];
+            t.x += c1.x;
+            t.y += c1.y;
+            tw[a2] = t;
+            bw[a2] += p1 * wv;
+            // antenna a1 (i = a2): x[a2,a1] = x_b
+            const double2 c2 = cmul(g2, make_double2(xv.x * wv, xv.y * wv));
+            tr += c2.x;
+            ti += c2.y;
+            bs += (g2.x * g2.x + g2.y * g2.y) * wv;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            tr += __shfl_xor(tr, o);
+            ti += __shfl_xor(ti, o);
+            bs += __shfl_xor(bs, o);
+        }
+        if (lane == 0) {
+            double2 t = tw[a1];
+            t.x += tr;
+            t.y += ti;
+            tw[a1] = t;
+            bw[a1] += bs;
+        }
+    }
+    __syncthreads();
+    // substitution (solvers.py:308-319 / :466-477), new gains into top[0]
+    for (int a = threadIdx.x; a < na; a += kThreads) {
+        double tx = 0.0, ty = 0.0, bb = 0.0;
+        for (int k = 0; k < kWaves; ++k) {
+            tx += top[k * na + a].x;
+            ty += top[k * na + a].y;
+            bb += bot[k * na + a];
+        }
+        double2 ng = bb > 0.0 ? make_double2(tx / bb, ty / bb) : make_double2(0.0, 0.0);
+        if (d.phase_only) {
+            const double m = sqrt(ng.x * ng.x + ng.y * ng.y);
+            if (m > 0.0) ng = make_double2(ng.x / m, ng.y / m);
+        }
+        top[a] = ng;
+        bot[a] = (d.mode == kScalar) ? (bb > 0.0 ? bb : 0.0) : bb;
+    }
+    __syncthreads();
+    // refant rotation (scalar only, :265-266): multiply by exp(-i angle(g_ref))
+    double2 rot = make_double2(1.0, 0.0);
+    if (d.mode == kScalar) {
+        const double2 gr = top[d.refant];
+        const double m = sqrt(gr.x * gr.x + gr.y * gr.y);
+        if (m > 0.0) rot = make_double2(gr.x / m, -gr.y / m);
+    }
+    double cmax = 0.0;
+    for (int a = threadIdx.x; a < na; a += kThreads) {
+        const double2 gold = gl[a];
+        double2 ng = cmul(top[a], rot);
+        double2 out;
+        double ch;
+        if (d.mode == kScalar) {  // damp, then change (:267-268)
+            out = make_double2((1.0 - d.damping) * ng.x + d.damping * gold.x,
+                               (1.0 - d.damping) * ng.y + d.damping * gold.y);
+            ch = hypot(out.x - gold.x, out.y - gold.y);
+        } else {  // change, then average (:427-428)
+            ch = hypot(ng.x - gold.x, ng.y - gold.y);
+            out = make_double2(0.5 * (ng.x + gold.x), 0.5 * (ng.y + gold.y));
+        }
+        cmax = fmax(cmax, ch);
+        gnext[gbase + a] = out;
+        gwnext[gbase + a] = bot[a];
+    }
+    for (int o = 32; o > 0; o >>= 1) cmax = fmax(cmax, __shfl_xor(cmax, o));
+    if (lane == 0) atomicMax(&change[s], dbits(cmax));
+}
+
+__global__ void k_commit(Dims d, int it, double2 *g, double *gw, const double2 *__restrict__ gnext,
+                         const double *__restrict__ gwnext, int32_t *done,
+                         const unsigned long long *__restrict__ change_cur,
+                         unsigned long long *change_next, int *ndone) {
+    const size_t per = (size_t)d.nchan * d.ncomp * d.nants;
+    const size_t total = (size_t)d.nsolve * per;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int s = (int)(i / per);
+        if (done[s]) continue;
+        const double ch = __longlong_as_double((long long)change_cur[s]);
+        double2 v = gnext[i];
+        const bool conv = ch < d.tol;
+        if (conv && d.mode == kScalar && d.phase_only) {  // :270-272
+            const double m = sqrt(v.x * v.x + v.y * v.y);
+            if (m > 0.0) v = make_double2(v.x / m, v.y / m);
+        }
+        g[i] = v;
+        gw[i] = gwnext[i];
+    }
+    // row bookkeeping: one thread per solve
+    for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < (size_t)d.nsolve;
+         s += (size_t)gridDim.x * blockDim.x) {
+        change_next[s] = 0ull;
+    }
+}
+
+__global__ void k_mark_done(Dims d, int it, int32_t *done, const unsigned long long *change_cur,
+                            int *ndone) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= d.nsolve || done[s]) return;
+    const double ch = __longlong_as_double((long long)change_cur[s]);
+    if (ch < d.tol) {
+        done[s] = it + 1;
+        atomicAdd(ndone, 1);
+    }
+}
+
+// rows that did not converge: phase-only normalisation (:280-282), niter+1
+__global__ void k_finish(Dims d, int niter, double2 *g, const int32_t *__restrict__ done,
+                         int32_t *niter_out) {
+    const size_t per = (size_t)d.nchan * d.ncomp * d.nants;
+    const size_t total = (size_t)d.nsolve * per;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int s = (int)(i / per);
+        if (done[s]) continue;
+        if (d.mode == kScalar && d.phase_only) {
+            double2 v = g[i];
+            const double m = sqrt(v.x * v.x + v.y * v.y);
+            if (m > 0.0) g[i] = make_double2(v.x / m, v.y / m);
+        }
+    }
+    for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < (size_t)d.nsolve;
+         s += (size_t)gridDim.x * blockDim.x)
+        niter_out[s] = done[s] ? done[s] : niter + 1;
+}
+
+// residual (solvers.py:481-539): sqrt(sum w |x - g_a1 conj(g_a2)|^2 / sum w)
+__global__ __launch_bounds__(kThreads) void k_residual(Dims d, const int32_t *__restrict__ row_start,
+                                                       const int32_t *__restrict__ ant2,
+                                                       const float2 *__restrict__ x,
+                                                       const float *__restrict__ w,
+                                                       const double2 *__restrict__ g,
+                                                       double *residual) {
+    __shared__ double red[2][kWaves];
+    const int sub = blockIdx.x;
+    const int na = d.nants;
+    const size_t gbase = (size_t)sub * na;
+    const size_t xbase = (size_t)sub * d.nbl;
+    double r = 0.0, sw = 0.0;
+    for (int a1 = threadIdx.x >> 6; a1 < na; a1 += kWaves) {
+        const double2 g1 = g[gbase + a1];
+        for (int b = row_start[a1] + (threadIdx.x & 63); b < row_start[a1 + 1]; b += 64) {
+            const double2 g2 = g[gbase + ant2[b]];
+            const double mr = g1.x * g2.x + g1.y * g2.y;   // g1 conj(g2)
+            const double mi = g1.y * g2.x - g1.x * g2.y;
+            const float2 xv = x[xbase + b];
+            const double wv = w[xbase + b];
+            const double er = xv.x - mr, ei = xv.y - mi;
+            r += wv * (er * er + ei * ei);
+            sw += wv;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        r += __shfl_xor(r, o);
+        sw += __shfl_xor(sw, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = r;
+        red[1][threadIdx.x >> 6] = sw;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double rr = 0.0, ss = 0.0;
+        for (int k = 0; k < kWaves; ++k) {
+            rr += red[0][k];
+            ss += red[1][k];
+        }
+        residual[sub] = ss > 0.0 ? sqrt(rr / ss) : 0.0;
+    }
+}
+
+// working [s][chan][comp][ant] -> outputs [s][ant][chan][comp]
+__global__ void k_store(Dims d, const double2 *__restrict__ g, const double *__restrict__ gw,
+                        double2 *gout, double *gwout) {
+    const size_t total = (size_t)d.nsolve * d.nchan * d.ncomp * d.nants;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const int a = (int)(i % d.nants);
+        const size_t sub = i / d.nants;
+        const int comp = (int)(sub % d.ncomp);
+        const int chan = (int)((sub / d.ncomp) % d.nchan);
+        const int s = (int)(sub / ((size_t)d.ncomp * d.nchan));
+        const size_t o = (((size_t)s * d.nants + a) * d.nchan + chan) * d.ncomp + comp;
+        gout[o] = g[i];
+        gwout[o] = gw[i];
+    }
+}
+
+static unsigned blocks_for(size_t n) {
+    size_t b = (n + 255) / 256;
+    return (unsigned)std::max<size_t>(1, std::min<size_t>(b, 65535));
+}
+
+static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, const void *xb,
+                  const double *wb, void *gain, double *gwt, double *residual,
+                  int32_t *niter_out, int niter, hipStream_t st) {
+    const size_t nsub = (size_t)d.nsolve * d.nchan * d.ncomp;
+    const size_t nx = nsub * d.nbl;
+    const size_t ng = nsub * d.nants;
+    float2 *x = scratch<float2>("sc_x", std::max<size_t>(nx, 1));
+    float *w = scratch<float>("sc_w", std::max<size_t>(nx, 1));
+    double2 *g = scratch<double2>("sc_g", ng);
+    double2 *gn = scratch<double2>("sc_gn", ng);
+    double *gw = scratch<double>("sc_gw", ng);
+    double *gwn = scratch<double>("sc_gwn", ng);
+    auto *rowmax = scratch<unsigned long long>("sc_rowmax", d.nsolve);
+    auto *change = scratch<unsigned long long>("sc_change", 2 * (size_t)d.nsolve);
+    int32_t *done = scratch<int32_t>("sc_done", d.nsolve);
+    int *ndone = scratch<int>("sc_ndone", 1);
+    SDP_HIP_CHECK(hipMemsetAsync(rowmax, 0, d.nsolve * sizeof(unsigned long long), st));
+    SDP_HIP_CHECK(hipMemsetAsync(change, 0, 2 * (size_t)d.nsolve * sizeof(unsigned long long), st));
+    SDP_HIP_CHECK(hipMemsetAsync(done, 0, d.nsolve * sizeof(int32_t), st));
+    SDP_HIP_CHECK(hipMemsetAsync(ndone, 0, sizeof(int), st));
+
+    const size_t per = (size_t)d.nbl * d.nchan * d.npol;
+    k_rowmax<<<dim3(std::max<unsigned>(1, std::min<unsigned>(64, (unsigned)((per + 255) / 256))),
+                    d.nsolve),
+               256, 0, st>>>(d, wb, rowmax);
+    k_fill<<<blocks_for(nx), 256, 0, st>>>(d, static_cast<const double2 *>(xb), wb, rowmax, x, w);
+    k_load_gains<<<blocks_for(ng), 256, 0, st>>>(d, static_cast<const double2 *>(gain), gwt, g,
+                                                  gw);
+    SDP_HIP_CHECK(hipGetLastError());
+
+    const size_t lds = (size_t)d.nants * (sizeof(double2) * (1 + kWaves) + sizeof(double) * kWaves);
+    if (lds > 65536)
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_iter,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int it = 0;
+    for (; it < niter; ++it) {
+        unsigned long long *cur = change + (size_t)(it & 1) * d.nsolve;
+        unsigned long long *nxt = change + (size_t)((it + 1) & 1) * d.nsolve;
+        k_iter<<<(unsigned)nsub, kThreads, lds, st>>>(d, row_start, ant2, x, w, g, gn, gwn, done,
+                                                     cur);
+        k_commit<<<blocks_for(ng), 256, 0, st>>>(d, it, g, gw, gn, gwn, done, cur, nxt, ndone);
+        k_mark_done<<<(d.nsolve + 255) / 256, 256, 0, st>>>(d, it, done, cur, ndone);
+        SDP_HIP_CHECK(hipGetLastError());
+        if ((it & 3) == 3 || it == niter - 1) {
+            int h = 0;
+            SDP_HIP_CHECK(hipMemcpyAsync(&h, ndone, sizeof(int), hipMemcpyDeviceToHost, st));
+            SDP_HIP_CHECK(hipStreamSynchronize(st));
+            if (h >= d.nsolve) break;
+        }
+    }
+    k_finish<<<blocks_for(ng), 256, 0, st>>>(d, niter, g, done, niter_out);
+    k_residual<<<(unsigned)nsub, kThreads, 0, st>>>(d, row_start, ant2, x, w, g, residual);
+    k_store<<<blocks_for(ng), 256, 0, st>>>(d, g, gw, static_cast<double2 *>(gain), gwt);
+    SDP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace stefcal
+}  // namespace sdp
+
+extern "C" int sdp_hip_solve_gains(int nsolve, int nants, int nbl, const int32_t *row_start,
+                                   const int32_t *ant2, int nchan, int npol, int mode,
+                                   const void *xb, const double *wb, void *gain, double *gwt,
+                                   double *residual, int32_t *niter_out, int niter, double tol,
+                                   int phase_only, int refant, double damping, void *stream,
+                                   char *errbuf, size_t errbuf_len) {
+    using namespace sdp;
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(nsolve >= 0 && nants > 0 && nbl >= 0 && nchan > 0, "bad sizes");
+        SDP_REQUIRE(nants <= stefcal::kMaxAnts, "at most 1024 antennas per solve");
+        SDP_REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (scalar), 1 (matrix) or 2 (nocross)");
+        SDP_REQUIRE(mode != 0 || npol == 1, "scalar mode needs npol == 1");
+        SDP_REQUIRE(mode != 1 || npol == 4, "matrix mode needs npol == 4");
+        SDP_REQUIRE(mode != 2 || npol == 2 || npol == 4, "nocross mode needs npol 2 or 4");
+        SDP_REQUIRE(refant >= 0 && refant < nants, "refant out of range");
+        SDP_REQUIRE(niter >= 0, "niter must be >= 0");
+        if (nsolve == 0) return;
+        SDP_REQUIRE(row_start && ant2 && xb && wb && gain && gwt && residual && niter_out,
+                    "null pointer argument");
+        stefcal::Dims d;
+        d.nsolve = nsolve;
+        d.nants = nants;
+        d.nbl = nbl;
+        d.nchan = nchan;
+        d.npol = npol;
+        d.mode = mode;
+        d.ncomp = mode == 0 ? 1 : 4;
+        d.nrec = mode == 0 ? 1 : 2;
+        d.phase_only = phase_only;
+        d.refant = refant;
+        d.tol = tol;
+        d.damping = damping;
+        stefcal::solve(d, row_start, ant2, xb, wb, gain, gwt, residual, niter_out, niter,
+                       as_stream(stream));
+    });
+}

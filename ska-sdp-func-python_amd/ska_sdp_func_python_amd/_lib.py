@@ -92,8 +92,8 @@ SIGNATURES = {
         c_int, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
         c_vp, c_vp] + _ERR,
     "sdp_hip_solve_gains": [
-        c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-        c_int, c_dbl, c_int, c_int, c_dbl, c_vp] + _ERR,
+        c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+        c_vp, c_vp, c_int, c_dbl, c_int, c_int, c_dbl, c_vp] + _ERR,
 }
 
 _lock = threading.Lock()

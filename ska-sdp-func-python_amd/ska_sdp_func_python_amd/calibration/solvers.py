@@ -1,0 +1,144 @@
+"""solve_gaintable on MI355X.
+
+Mirrors reference ``src/ska_sdp_func_python/calibration/solvers.py``:
+
+* ``solve_gaintable`` (:21-145): ValueError for an all-zero model (:56-59),
+  ``divide_visibility`` (:61-63), a new gain table if none is given (:70-76),
+  per gain row the weighted sums over the row's time window (and over
+  frequency when the table has one channel, :82, :99-107), rows without
+  weight get gain 1 / weight 0 / residual 0 (:130-133), and finally the
+  mean/median gain-amplitude normalisation when not ``phase_only``
+  (:135-143).
+* the inner solvers (:148-539) run batched over all rows in one call of
+  ``sdp_hip_solve_gains``: scalar (npol 1), matrix (npol 4 with crosspol)
+  and "nocrossdata" (npol 2, or 4 without crosspol), with the reference's
+  channel-coupled convergence, damping 0.5 and refant 0.
+
+The point-source sums (:99-107) are formed on the device; the reference's
+dense [nants, nants] matrix (:108-114) is replaced by a canonical packed
+baseline order (kernels.canonical_baselines).
+"""
+
+import logging
+
+import numpy as np
+import torch
+
+from .. import _device, kernels
+from ..datamodels import create_gaintable_from_visibility
+from ..visibility.operations import divide_visibility
+
+log = logging.getLogger("func-python-logger")
+
+
+def _row_sums(point_vis, gain_table, nchan_g, dev):
+    """x_b [nrow, nbl, nchan_g, npol] c128 and xwt_b f64 (solvers.py:85-107)."""
+    vis = _device.to_dev(point_vis.vis.data, None, dev).to(torch.complex128)
+    wt = _device.to_dev(point_vis.weight.data, None, dev).to(torch.float64)
+    flags = _device.to_dev(point_vis.flags.data, None, dev)
+    keep = (1 - flags).to(torch.float64)
+    vw = vis * wt * keep
+    ww = wt * keep
+    times = np.asarray(point_vis.time.data, dtype=float)
+    gtimes = np.asarray(gain_table.time.data, dtype=float)
+    interval = np.asarray(gain_table.interval.data, dtype=float)
+    nrow = len(gtimes)
+    _, nbl, nchan, npol = vw.shape
+    xb = torch.zeros((nrow, nbl, nchan_g, npol), dtype=torch.complex128, device=dev)
+    xwt = torch.zeros((nrow, nbl, nchan_g, npol), dtype=torch.float64, device=dev)
+    present = np.zeros(nrow, dtype=bool)
+    for row in range(nrow):
+        sel = np.nonzero((times >= gtimes[row] - interval[row] / 2)
+                         & (times <= gtimes[row] + interval[row] / 2))[0]
+        if len(sel) == 0:
+            continue
+        present[row] = True
+        idx = torch.as_tensor(sel, device=dev)
+        a = vw.index_select(0, idx).sum(0)
+        b = ww.index_select(0, idx).sum(0)
+        if nchan_g == 1:
+            a = a.sum(1, keepdim=True)
+            b = b.sum(1, keepdim=True)
+        xb[row] = a
+        xwt[row] = b
+    return xb, xwt, present
+
+
+def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=200, tol=1e-6,
+                    crosspol=False, normalise_gains="mean", jones_type="T", timeslice=None):
+    if modelvis is not None:
+        mv = modelvis.vis.data
+        mx = float(mv.abs().max()) if isinstance(mv, torch.Tensor) else float(np.max(np.abs(mv)))
+        if not mx > 0.0:
+            raise ValueError("solve_gaintable: Model visibility is zero")
+    point_vis = divide_visibility(vis, modelvis) if modelvis is not None else vis
+    if phase_only:
+        log.debug("solve_gaintable: Solving for phase only")
+    else:
+        log.debug("solve_gaintable: Solving for complex gain")
+    if gain_table is None:
+        log.debug("solve_gaintable: creating new gaintable")
+        gain_table = create_gaintable_from_visibility(vis, jones_type=jones_type, timeslice=timeslice)
+    else:
+        log.debug("solve_gaintable: starting from existing gaintable")
+
+    dev = _device.device()
+    nants = gain_table.gaintable_acc.nants
+    nchan = gain_table.gaintable_acc.nchan
+    npol = point_vis.visibility_acc.npol
+    xb, xwt, present = _row_sums(point_vis, gain_table, nchan, dev)
+    for row in np.nonzero(~present)[0]:
+        log.warning("Gaintable %s, vis time mismatch %s", gain_table.time.data, vis.time.data)
+
+    bl = np.asarray(point_vis.baselines.data)
+    perm, conj, row_start, ant2 = kernels.canonical_baselines(bl[:, 0], bl[:, 1], nants)
+    p = torch.as_tensor(perm, device=dev)
+    c = torch.as_tensor(conj, device=dev)
+    xb_c = xb.index_select(1, p)
+    xb_c = torch.where(c[None, :, None, None], xb_c.conj(), xb_c)
+    xwt_c = xwt.index_select(1, p)
+
+    if npol == 2 or (npol == 4 and not crosspol):
+        mode = 2
+    elif npol == 4 and crosspol:
+        mode = 1
+    else:
+        mode = 0
+
+    gain_h = gain_table["gain"].data
+    gain = _device.to_dev(gain_h, torch.complex128, dev).contiguous().clone()
+    gwt = _device.to_dev(gain_table["weight"].data, torch.float64, dev).contiguous().clone()
+    residual, used = kernels.solve_gains(xb_c, xwt_c, gain, gwt, row_start, ant2, mode,
+                                         niter=niter, tol=tol, phase_only=phase_only)
+    used_h = used.cpu().numpy()
+    for row in np.nonzero(used_h > niter)[0]:
+        if present[row]:
+            log.warning("solve_antenna_gains_itsubs: gain solution failed, retaining gain solutions")
+
+    # rows with no weight at all (solvers.py:116, :130-133) and rows without data
+    has_wt = (xwt.reshape(xwt.shape[0], -1).abs() > 0).any(dim=1).cpu().numpy() & present
+    empty = torch.as_tensor(~has_wt, device=dev)
+    gain = torch.where(empty[:, None, None, None, None], torch.ones_like(gain), gain)
+    gwt = torch.where(empty[:, None, None, None, None], torch.zeros_like(gwt), gwt)
+    residual = torch.where(empty[:, None, None, None], torch.zeros_like(residual), residual)
+    # rows whose times are absent keep their input values (solvers.py:93-97)
+    if (~present).any():
+        keep = torch.as_tensor(~present, device=dev)
+        gain = torch.where(keep[:, None, None, None, None],
+                           _device.to_dev(gain_h, torch.complex128, dev), gain)
+        gwt = torch.where(keep[:, None, None, None, None],
+                          _device.to_dev(gain_table["weight"].data, torch.float64, dev), gwt)
+        residual = torch.where(keep[:, None, None, None],
+                               _device.to_dev(gain_table["residual"].data, torch.float64, dev),
+                               residual)
+
+    if normalise_gains in ["median", "mean"] and not phase_only:
+        ga = gain.abs()
+        gabs = torch.median(ga) if normalise_gains == "median" else torch.mean(ga)
+        gain = gain / gabs
+
+    ref = gain_table["gain"].data
+    gain_table["gain"].data = _device.like_input(gain, ref)
+    gain_table["weight"].data = _device.like_input(gwt, ref)
+    gain_table["residual"].data = _device.like_input(residual, ref)
+    return gain_table

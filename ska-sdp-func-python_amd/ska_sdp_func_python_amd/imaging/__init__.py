@@ -1,0 +1,5 @@
+"""Imaging hot path: predict/invert (w-stacking NUFFT) and the sky-component DFT."""
+from .base import normalise_sumwt, shift_vis_to_image  # noqa: F401
+from .dft import dft_skycomponent_visibility, extract_direction_and_flux  # noqa: F401
+from .imaging import invert_visibility, predict_visibility  # noqa: F401
+from .ng import invert_ng, predict_ng  # noqa: F401

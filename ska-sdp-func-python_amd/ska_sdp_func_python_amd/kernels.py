@@ -131,3 +131,120 @@ def set_stage_timing(enable):
 
 def release_workspace():
     _lib.call("sdp_hip_release_workspace")
+
+
+def dft_point(direction_cosines, fluxes, uvw, freq=None, out=None, vis_dtype=torch.complex64):
+    """Sky-component DFT on device.
+
+    direction_cosines [ncomp,3] f64, fluxes [ncomp, 1|nchan, npol] c128.
+    With ``freq`` given, ``uvw`` is [nrow,3] metres (lambda scaling fused);
+    otherwise ``uvw`` is uvw_lambda [nrow, nchan, 3] (dft_point_v00 layout).
+    Returns vis [nrow, nchan, npol].
+    """
+    dc = _on_gpu(direction_cosines, "direction_cosines").to(torch.float64).contiguous()
+    fl = _on_gpu(fluxes, "fluxes").to(torch.complex128).contiguous()
+    if fl.dim() != 3 or dc.dim() != 2 or dc.shape[1] != 3 or fl.shape[0] != dc.shape[0]:
+        raise ValueError("direction_cosines [ncomp,3] and fluxes [ncomp,nchan,npol] required")
+    ncomp, fnchan, npol = fl.shape
+    uvw = _on_gpu(uvw, "uvw").to(torch.float64).contiguous()
+    if freq is not None:
+        freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
+        nrow, nchan = uvw.shape[0], freq.shape[0]
+    else:
+        nrow, nchan = uvw.shape[0], uvw.shape[1]
+    if out is None:
+        out = torch.empty((nrow, nchan, npol), dtype=vis_dtype, device=uvw.device)
+    if not out.is_contiguous() or tuple(out.shape) != (nrow, nchan, npol):
+        raise ValueError("vis out must be contiguous [nrow, nchan, npol]")
+    if freq is not None:
+        _lib.call("sdp_hip_dft_point_metres", ncomp, _ptr(dc), _ptr(fl), fnchan, npol, nrow, nchan,
+                  _ptr(uvw), _ptr(freq), _ptr(out), _DT_CODE[out.dtype], _stream(uvw.device))
+    else:
+        _lib.call("sdp_hip_dft_point_v00", ncomp, _ptr(dc), _ptr(fl), fnchan, npol, nrow, nchan,
+                  _ptr(uvw), _ptr(out), _DT_CODE[out.dtype], _stream(uvw.device))
+    return out
+
+
+def canonical_baselines(ant1, ant2, nants):
+    """Canonical (a1 < a2) CSR order of a baseline list.
+
+    Returns (perm, conj, row_start, ant2_sorted): ``perm[k]`` is the input
+    baseline placed at canonical position k, ``conj[k]`` is True when it was
+    given as (a2, a1) (its value must be conjugated), and autocorrelations
+    (a1 == a2, zeroed by the reference solver, solvers.py:251-253) are dropped.
+    """
+    import numpy as np
+    a1 = np.asarray(ant1, dtype=np.int64)
+    a2 = np.asarray(ant2, dtype=np.int64)
+    keep = np.nonzero(a1 != a2)[0]
+    lo = np.minimum(a1[keep], a2[keep])
+    hi = np.maximum(a1[keep], a2[keep])
+    order = np.lexsort((hi, lo))
+    perm = keep[order]
+    conj = (a1[perm] > a2[perm])
+    lo, hi = lo[order], hi[order]
+    row_start = np.zeros(nants + 1, dtype=np.int32)
+    np.add.at(row_start, lo + 1, 1)
+    row_start = np.cumsum(row_start).astype(np.int32)
+    return perm, conj, row_start, hi.astype(np.int32)
+
+
+def solve_gains(xb, wb, gain, gwt, row_start, ant2, mode, niter=200, tol=1e-6,
+                phase_only=True, refant=0, damping=0.5):
+    """Batched StefCal on device.
+
+    xb [nsolve, nbl, nchan, npol] c128, wb [...] f64 in canonical baseline
+    order; gain/gwt [nsolve, nants, nchan, nrec, nrec] (c128 / f64) updated
+    in place.  Returns (residual [nsolve, nchan, nrec, nrec], niter_used).
+    """
+    xb = _on_gpu(xb, "xb").to(torch.complex128).contiguous()
+    wb = _on_gpu(wb, "wb").to(torch.float64).contiguous()
+    if not (gain.is_cuda and gain.dtype == torch.complex128 and gain.is_contiguous()):
+        raise ValueError("gain must be a contiguous complex128 device tensor")
+    if not (gwt.is_cuda and gwt.dtype == torch.float64 and gwt.is_contiguous()):
+        raise ValueError("gwt must be a contiguous float64 device tensor")
+    nsolve, nbl, nchan, npol = xb.shape
+    nants = gain.shape[1]
+    nrec = gain.shape[3]
+    rs = torch.as_tensor(row_start, dtype=torch.int32, device=xb.device)
+    a2 = torch.as_tensor(ant2, dtype=torch.int32, device=xb.device)
+    residual = torch.zeros((nsolve, nchan, nrec, nrec), dtype=torch.float64, device=xb.device)
+    used = torch.zeros(nsolve, dtype=torch.int32, device=xb.device)
+    _lib.call("sdp_hip_solve_gains", nsolve, nants, nbl, _ptr(rs), _ptr(a2), nchan, npol,
+              int(mode), _ptr(xb), _ptr(wb), _ptr(gain), _ptr(gwt), _ptr(residual), _ptr(used),
+              int(niter), float(tol), int(bool(phase_only)), int(refant), float(damping),
+              _stream(xb.device))
+    return residual, used
+
+
+def grid_cf(maps, vis_to_im, vis, wt, cf, grid, sumwt):
+    """Convolution-function gridding (accumulates into grid and sumwt).
+
+    maps: dict of int32 [nchan, nrow] device tensors pu, pv, pwc, pdu, pdv;
+    vis [nrow, nchan, npol] c128, wt f64 same shape; cf [c, p, nw, ndv, ndu,
+    gv, gu] c128; grid [g_nchan, npol, ny, nx] c128; sumwt [g_nchan, npol] f64.
+    Returns the number of skipped (row, pol) samples.
+    """
+    nrow, nchan, npol = vis.shape
+    cfn, _, nw, ndv, ndu, gv, gu = cf.shape
+    gn, _, ny, nx = grid.shape
+    skipped = torch.zeros(1, dtype=torch.int64, device=vis.device)
+    for t in (vis, wt, cf, grid, sumwt):
+        if not t.is_contiguous():
+            raise ValueError("grid_cf operands must be contiguous")
+    _lib.call("sdp_hip_grid_cf", nrow, nchan, npol, _ptr(maps["pu"]), _ptr(maps["pv"]),
+              _ptr(maps["pwc"]), _ptr(maps["pdu"]), _ptr(maps["pdv"]), _ptr(vis_to_im), _ptr(vis),
+              _ptr(wt), _ptr(cf), cfn, nw, ndv, ndu, gv, gu, _ptr(grid), gn, ny, nx, _ptr(sumwt),
+              _ptr(skipped), _stream(vis.device))
+    return skipped
+
+
+def degrid_cf(maps, vis_to_im, grid, cf, nrow, nchan, out):
+    cfn, npol, nw, ndv, ndu, gv, gu = cf.shape
+    gn, _, ny, nx = grid.shape
+    skipped = torch.zeros(1, dtype=torch.int64, device=grid.device)
+    _lib.call("sdp_hip_degrid_cf", nrow, nchan, npol, _ptr(maps["pu"]), _ptr(maps["pv"]),
+              _ptr(maps["pwc"]), _ptr(maps["pdu"]), _ptr(maps["pdv"]), _ptr(vis_to_im),
+              _ptr(grid), gn, ny, nx, _ptr(cf), cfn, nw, ndv, ndu, gv, gu, _ptr(out),
+              _ptr(skipped), _stream(grid.device))
+    return skipped

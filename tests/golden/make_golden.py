@@ -1,0 +1,256 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE's own code.
+
+Run in the build container only (needs /root/reference, which never travels
+to the GPU box):  python tests/golden/make_golden.py
+
+The reference package cannot be imported (ska_sdp_datamodels, astropy,
+xarray and ducc0 are absent), so the pure-numpy function bodies on the hot
+path are AST-extracted from the reference sources and executed with numpy
+(SURVEY.md §8(c)).  Data containers come from ska_sdp_func_python_amd's
+datamodels shim (attribute-compatible subset of ska-sdp-datamodels).  Only
+inputs and outputs are stored -- no reference source text.
+
+Fixtures:
+  dft_*.npz        dft_cpu_looped                (imaging/dft.py:265-285)
+  solve_*.npz      solve_gaintable end-to-end    (calibration/solvers.py:21-539,
+                   with visibility/operations.py:145-189 divide_visibility)
+  cfgrid_*.npz     grid_visibility_to_griddata / degrid_visibility_from_griddata
+                   with spatial_mapping         (grid_data/gridding.py:33-255, :502-590)
+  fft_*.npz        fft / ifft centred transforms (fourier_transforms/fft_support.py:31-140)
+  nufft_c1.npz     ORACLE-generated (exact direct sums, oracle/nufft_oracle.py):
+                   ducc0 is unavailable, the ducc0 boundary is parity-unpinned.
+"""
+
+import ast
+import logging
+import math
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func-python_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+REF = "/root/reference/src/ska_sdp_func_python"
+
+from ska_sdp_func_python_amd import datamodels as dm  # noqa: E402
+from ska_sdp_func_python_amd import simulation  # noqa: E402
+
+
+def load_reference(relpath, names, extra=None):
+    """exec the named top-level defs of a reference module with numpy."""
+    with open(os.path.join(REF, relpath)) as f:
+        tree = ast.parse(f.read())
+    defs = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in names]
+    missing = set(names) - {d.name for d in defs}
+    assert not missing, missing
+    ns = {"numpy": np, "log": logging.getLogger("reference"), "copy": __import__("copy"),
+          "Visibility": dm.Visibility, "GainTable": dm.GainTable, "Image": dm.Image,
+          "GridData": dm.GridData}
+    ns.update(extra or {})
+    exec(compile(ast.Module(body=defs, type_ignores=[]), relpath, "exec"), ns)
+    return ns
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, {k: getattr(v, "shape", v) for k, v in arrays.items()})
+
+
+# ---------------------------------------------------------------------------
+def make_dft():
+    ns = load_reference("imaging/dft.py", ["dft_cpu_looped"])
+    rng = np.random.default_rng(3)
+    for tag, npol, fnchan in (("p4", 4, 4), ("p1_bcast", 1, 1), ("p2", 2, 4)):
+        ncomp, nt, nb, nchan = 6, 3, 15, 4
+        dc_lm = rng.uniform(-0.05, 0.05, (ncomp, 2))
+        dc = np.concatenate([dc_lm, (np.sqrt(1 - (dc_lm ** 2).sum(1)) - 1)[:, None]], 1)
+        flux = (rng.uniform(0.1, 10, (ncomp, fnchan, npol)) + 1j * rng.normal(0, 0.3, (ncomp, fnchan, npol)))
+        uvw_lambda = rng.normal(0, 1, (nt, nb, nchan, 3)) * np.array([3e4, 3e4, 2e3])
+        vis = ns["dft_cpu_looped"](dc, uvw_lambda, flux)
+        save(f"dft_{tag}.npz", direction_cosines=dc, vfluxes=flux, uvw_lambda=uvw_lambda, vis=vis)
+
+
+# ---------------------------------------------------------------------------
+def _ref_solver_namespace():
+    ops = load_reference("visibility/operations.py", ["divide_visibility"],
+                         {"Visibility": dm.Visibility})
+    return load_reference(
+        "calibration/solvers.py",
+        ["solve_gaintable", "_solve_with_mask", "_solve_antenna_gains_itsubs_scalar",
+         "_gain_substitution_scalar", "_solve_antenna_gains_itsubs_nocrossdata",
+         "_solve_antenna_gains_itsubs_matrix", "_gain_substitution_matrix",
+         "_solution_residual_scalar", "_solution_residual_matrix"],
+        {"divide_visibility": ops["divide_visibility"],
+         "create_gaintable_from_visibility": dm.create_gaintable_from_visibility})
+
+
+def _solver_case(pf, nants, ntimes, nchan, jones, phase_only, crosspol, normalise, amp_err,
+                 seed, niter=200, tol=1e-6):
+    rng = np.random.default_rng(seed)
+    vis = simulation.make_visibility("LOW", nants=nants, ntimes=ntimes, nchan=nchan, f_lo=1.0e8,
+                                     f_hi=1.1e8, ha_span_h=0.5, polarisation_frame=pf)
+    npol = vis.visibility_acc.npol
+    shape = vis.vis.shape
+    # model: a few point sources (random phases per baseline)
+    model = (rng.normal(1.0, 0.2, shape) * np.exp(1j * rng.uniform(-np.pi, np.pi, shape)))
+    if npol == 4:
+        model[..., 1:3] *= 0.1
+    modelvis = vis.copy(deep=True)
+    modelvis["vis"].data = model
+    # true gains per (time, ant, chan, rec, rec)  (cf. tests/testing_utils.py:21-83)
+    g_rng = np.random.default_rng(1805550721)
+    nrec = 1 if npol == 1 else 2
+    gshape = (ntimes, nants, nchan if jones == "B" else 1, nrec, nrec)
+    phases = g_rng.normal(0, 0.3, gshape)
+    amps = g_rng.lognormal(0, amp_err, gshape) if amp_err > 0 else 1.0
+    g = amps * np.exp(1j * phases)
+    if nrec == 2:
+        g[..., 0, 1] = 0.0
+        g[..., 1, 0] = 0.0
+    bl = np.asarray(vis.baselines.data)
+    obs = np.zeros_like(model)
+    for t in range(ntimes):
+        for ib, (a1, a2) in enumerate(bl):
+            g1 = g[t, a1]
+            g2 = g[t, a2]
+            for f in range(nchan):
+                gf1 = g1[min(f, g1.shape[0] - 1)]
+                gf2 = g2[min(f, g2.shape[0] - 1)]
+                if npol == 1:
+                    obs[t, ib, f, 0] = gf1[0, 0] * model[t, ib, f, 0] * np.conj(gf2[0, 0])
+                else:
+                    mm = model[t, ib, f]
+                    if npol == 4:
+                        M = mm.reshape(2, 2)
+                    else:
+                        M = np.diag(mm)
+                    V = gf1 @ M @ np.conj(gf2).T
+                    obs[t, ib, f] = V.reshape(4) if npol == 4 else np.diag(V)
+    obs += 1e-4 * (rng.normal(size=shape) + 1j * rng.normal(size=shape))
+    vis["vis"].data = obs
+    gt_in = dm.create_gaintable_from_visibility(vis, jones_type=jones)
+    ns = _ref_solver_namespace()
+    gt = ns["solve_gaintable"](vis, modelvis, gain_table=gt_in.copy(deep=True),
+                               phase_only=phase_only, niter=niter, tol=tol, crosspol=crosspol,
+                               normalise_gains=normalise, jones_type=jones)
+    return dict(vis=obs, model=model, uvw=np.asarray(vis.uvw.data), time=np.asarray(vis.time.data),
+                frequency=np.asarray(vis.frequency.data), baselines=bl,
+                integration_time=np.asarray(vis.integration_time.data),
+                pol_frame=np.array(pf), jones=np.array(jones), phase_only=np.array(phase_only),
+                crosspol=np.array(crosspol), normalise=np.array(str(normalise)),
+                niter=np.array(niter), tol=np.array(tol),
+                gain_in=gt_in["gain"].data, weight_in=gt_in["weight"].data,
+                gt_time=np.asarray(gt_in.time.data), gt_interval=np.asarray(gt_in.interval.data),
+                gain=gt["gain"].data, weight=gt["weight"].data, residual=gt["residual"].data)
+
+
+def make_solver():
+    cases = {
+        "scalar_T_phase": ("stokesI", 12, 3, 3, "T", True, False, None, 0.0),
+        "scalar_B_amp_mean": ("stokesI", 10, 2, 3, "B", False, False, "mean", 0.1),
+        "scalar_T_amp_median": ("stokesI", 9, 2, 2, "T", False, False, "median", 0.1),
+        "matrix_crosspol_B": ("linear", 8, 2, 2, "B", False, True, None, 0.05),
+        "nocross_linear_T": ("linear", 8, 2, 2, "T", True, False, None, 0.0),
+        "nocross_linearnp_B": ("linearnp", 9, 2, 2, "B", False, False, "mean", 0.1),
+        "nocross_circular_T": ("circular", 7, 2, 2, "T", True, False, None, 0.0),
+    }
+    for k, (pf, na, nt, nc, jones, po, cp, norm, amp) in cases.items():
+        save(f"solve_{k}.npz", **_solver_case(pf, na, nt, nc, jones, po, cp, norm, amp, seed=len(k)))
+
+
+# ---------------------------------------------------------------------------
+def _cf_objects(rng, npol, nchan, ny, nx, nw, ndv, ndu, gv, gu, du_cell, dfreq=2e6):
+    pf = dm.PolarisationFrame({1: "stokesI", 4: "linear"}[npol])
+    grid_wcs = dm.WCS(4, ["UU", "VV", "STOKES", "FREQ"], [nx // 2 + 1, ny // 2 + 1, 1, 1],
+                      [du_cell, du_cell, 1, dfreq], [0.0, 0.0, 1.0, 1e8])
+    gd = dm.GridData.constructor(np.zeros((nchan, npol, ny, nx), complex), grid_wcs, pf)
+    dw = 40.0
+    cf_wcs = dm.WCS(7, ["UU", "VV", "DUU", "DVV", "WW", "STOKES", "FREQ"],
+                    [gu // 2 + 1, gv // 2 + 1, ndu // 2 + 1, ndv // 2 + 1, nw // 2 + 1, 1, 1],
+                    [du_cell, du_cell, du_cell / ndu, du_cell / ndv, dw, 1, dfreq],
+                    [0, 0, 0, 0, 0, 1, 1e8])
+    cfp = (rng.normal(size=(nchan, npol, nw, ndv, ndu, gv, gu))
+           + 1j * rng.normal(size=(nchan, npol, nw, ndv, ndu, gv, gu)))
+    cf = dm.ConvolutionFunction.constructor(cfp, cf_wcs, pf)
+    return gd, cf, pf, dw
+
+
+def make_cfgrid():
+    ns = load_reference("grid_data/gridding.py",
+                        ["convolution_mapping_visibility", "spatial_mapping",
+                         "grid_visibility_to_griddata", "degrid_visibility_from_griddata"])
+    for tag, npol, nchan in (("p1", 1, 2), ("p4", 4, 1)):
+        rng = np.random.default_rng(11 + npol)
+        ny = nx = 48
+        nw, ndv, ndu, gv, gu = 3, 5, 5, 8, 8
+        du_cell = 20.0
+        gd, cf, pf, dw = _cf_objects(rng, npol, nchan, ny, nx, nw, ndv, ndu, gv, gu, du_cell)
+        nt, nb = 2, 40
+        freq = np.linspace(1e8, 1.02e8, nchan) if nchan > 1 else np.array([1e8])
+        lam = 299792458.0 / freq.max()
+        uvw = np.zeros((nt, nb, 3))
+        uvw[..., :2] = rng.uniform(-22 * du_cell, 22 * du_cell, (nt, nb, 2)) * lam
+        uvw[..., 2] = rng.uniform(-1.2 * dw, 1.2 * dw, (nt, nb)) * lam
+        shape = (nt, nb, nchan, npol)
+        vis = dm.Visibility.constructor(
+            frequency=freq, channel_bandwidth=np.full(nchan, 1e6), phasecentre=dm.SkyCoord(0, -0.5),
+            uvw=uvw, time=np.arange(nt, dtype=float), vis=rng.normal(size=shape) + 1j * rng.normal(size=shape),
+            weight=rng.uniform(0.5, 2.0, shape), flags=(rng.uniform(size=shape) < 0.05).astype(int),
+            baselines=np.stack(np.triu_indices(10, 1), 1)[:nb], polarisation_frame=pf,
+            imaging_weight=rng.uniform(0.5, 2.0, shape))
+        gd_out, sumwt = ns["grid_visibility_to_griddata"](vis, gd.copy(deep=True), cf)
+        gd_in = gd.copy(deep=True)
+        gd_in["pixels"].data = rng.normal(size=gd_in["pixels"].data.shape) + 1j * rng.normal(
+            size=gd_in["pixels"].data.shape)
+        dv = ns["degrid_visibility_from_griddata"](vis, gd_in, cf)
+        save(f"cfgrid_{tag}.npz", uvw=uvw, freq=freq, vis=vis.vis.data, weight=vis.weight.data,
+             imaging_weight=vis.imaging_weight.data, flags=vis.flags.data,
+             cf=cf["pixels"].data, cf_crpix=cf.attrs["cf_wcs"].wcs.crpix,
+             cf_cdelt=cf.attrs["cf_wcs"].wcs.cdelt, cf_crval=cf.attrs["cf_wcs"].wcs.crval,
+             grid_crpix=gd.attrs["grid_wcs"].wcs.crpix, grid_cdelt=gd.attrs["grid_wcs"].wcs.cdelt,
+             grid_crval=gd.attrs["grid_wcs"].wcs.crval, pol_frame=np.array(pf.type),
+             grid=gd_out["pixels"].data, sumwt=sumwt, grid_in=gd_in["pixels"].data,
+             degridded=dv.vis.data)
+
+
+def make_fft():
+    ns = load_reference("fourier_transforms/fft_support.py", ["fft", "ifft"],
+                        {"pyfftw_exists": False, "pyfftw": None})
+    rng = np.random.default_rng(5)
+    a = rng.normal(size=(2, 1, 32, 32)) + 1j * rng.normal(size=(2, 1, 32, 32))
+    save("fft_centred.npz", a=a, fft=ns["fft"](a), ifft=ns["ifft"](a))
+
+
+def make_nufft_c1():
+    """C1-style: SKA-MID 7-dish subset, 10 times, 1 channel, 256^2 (oracle exact sums)."""
+    import nufft_oracle as orc
+    vis = simulation.make_visibility("MID", nants=7, ntimes=10, nchan=1, f_lo=1.4e9, ha_span_h=2.0)
+    uvw = np.asarray(vis.uvw.data).reshape(-1, 3)
+    freq = np.asarray(vis.frequency.data)
+    umax = simulation.max_uv_lambda(vis)
+    cell = 0.5 / (2 * umax)
+    rng = np.random.default_rng(2)
+    nrow = uvw.shape[0]
+    ms = rng.normal(size=(nrow, 1)) + 1j * rng.normal(size=(nrow, 1))
+    wgt = rng.uniform(0.5, 1.5, (nrow, 1)).astype(np.float32).astype(float)
+    fuvw = uvw * np.array([-1.0, 1.0, -1.0])  # RASCIL flip (ng.py:210-213)
+    out = {}
+    for dow in (True, False):
+        d = orc.ms2dirty_exact(fuvw, freq, ms, wgt, 256, 256, cell, cell, dow)
+        out[f"dirty_w{int(dow)}"] = d
+        img = rng.normal(size=(256, 256))
+        out[f"model_w{int(dow)}"] = img
+        out[f"vis_w{int(dow)}"] = orc.dirty2ms_exact(fuvw, freq, img, None, cell, cell, dow)
+    save("nufft_c1.npz", uvw=uvw, freq=freq, ms=ms, wgt=wgt, cell=np.array(cell), **out)
+
+
+if __name__ == "__main__":
+    make_dft()
+    make_solver()
+    make_cfgrid()
+    make_fft()
+    make_nufft_c1()
