@@ -1,0 +1,205 @@
+#!/usr/bin/env python
+"""Headline benchmark: w-stacking invert (ms2dirty) throughput on MI355X.
+
+metric  "Mvis/s gridded (invert, 8k^2 w-stack grid) at 1/2/4/8 MI355X"
+        (BASELINE.json), measured on configs[1] (C2): SKA-MID-like 197 dishes,
+        64 channels x 100 times = 123.6 Mvis per GPU, 4096^2 image on the
+        8192^2 (sigma = 2) w-stacked grid, cell = 0.25 / u_max, epsilon 1e-12
+        requested as in the reference (imaging/ng.py:178) -- clamped to the
+        fp32 floor 1e-7, support W = 8.
+step    one invert of the rank's visibilities, resident in HBM: bucketing,
+        w-stack gridding, per-plane FFT, w-screen / grid-correction, the RCCL
+        all-reduce of the dirty image and sumwt, and the sumwt normalisation
+        (imaging/ng.py:146-294 + imaging/base.py:95-155).
+scaling weak: every rank grids its own 64 channels; the N-GPU job is the same
+        array observed in 64*N channels interleaved over 0.95-1.76 GHz, so
+        every shard has the same uv extent and w-plane count.
+
+Rank 0 prints ONE JSON line.  `roofline` uses the dominant kernel (k_grid):
+its launch duration is measured live with HIP events recorded by the C ABI
+on the stream the kernel runs on (sdp_hip_set_stage_timing); its algorithmic
+bytes are N_vis * 12.375 B (c64 vis + f32 weight + f64 uvw per row / nchan,
+SURVEY.md §8(d)) + n_planes * 8192^2 * 8 B (one write of the c64 grid).
+`cpu_baseline` times oracle/wgrid_cpu.c (C + OpenMP restatement of the same
+algorithm; ducc0 itself is unavailable) on a bounded sample -- rank 0, N=1.
+"""
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func-python_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "Mvis/s gridded (invert, 8k^2 w-stack grid) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+NCHAN_PER_GPU, NTIMES, NPIX = 64, 100, 4096
+F_LO, F_HI = 0.95e9, 1.76e9
+EPS_REQUESTED = 1e-12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nchan", type=int, default=NCHAN_PER_GPU, help="channels per GPU")
+    ap.add_argument("--ntimes", type=int, default=NTIMES)
+    ap.add_argument("--npix", type=int, default=NPIX)
+    ap.add_argument("--cpu-chans", type=int, default=1,
+                    help="channels in the cpu_baseline sample (0 = skip)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_k_grid.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(args, umax, nchan_total):
+    """oracle/wgrid_cpu.c on a bounded C2 sample (1 channel of the 64 by default):
+    the sample's gridding time is scaled to the full visibility count and its
+    per-plane FFT + w-screen time is counted once (the full job has the same
+    planes), giving the CPU's full-C2 invert rate."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wgrid_cpu
+    from ska_sdp_func_python_amd import simulation
+    fn, n_def, lat, dec = simulation.CONFIGS["MID"]
+    en = fn(n_def, seed=1)
+    ha = np.linspace(-0.5, 0.5, args.ntimes) * 8.0 * math.pi / 12.0
+    uvw, _ = simulation.observe(en, math.radians(lat), math.radians(dec), ha)
+    uvw = uvw.reshape(-1, 3)
+    allf = np.linspace(F_LO, F_HI, nchan_total)
+    chans = np.linspace(0, nchan_total - 1, args.cpu_chans).round().astype(int)
+    freq = allf[chans]
+    rng = np.random.default_rng(2)
+    ms = (rng.normal(size=(uvw.shape[0], len(freq)))
+          + 1j * rng.normal(size=(uvw.shape[0], len(freq)))).astype(np.complex64)
+    wgt = np.ones(ms.shape, np.float32)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = min(threads, len(os.sched_getaffinity(0)))
+    cell = 0.25 / umax
+    t0 = time.perf_counter()
+    _, tg, tf = wgrid_cpu.ms2dirty(uvw, freq, ms, wgt, args.npix, args.npix, cell, cell,
+                                   EPS_REQUESTED, True, nthreads=threads)
+    wall = time.perf_counter() - t0
+    nvis_s = ms.size
+    nvis_full = uvw.shape[0] * args.nchan
+    t_full = (wall - tf) * nvis_full / nvis_s + tf
+    return {"value": round(nvis_full / t_full / 1e6, 4), "unit": "Mvis/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"oracle/wgrid_cpu.c (C+OpenMP w-stacking restatement; ducc0 absent) on "
+                       f"{len(freq)} of {args.nchan} C2 channels ({nvis_s / 1e6:.2f} Mvis, "
+                       f"{args.npix}^2 image, same planes): {wall:.1f} s wall, of which "
+                       f"{tf:.1f} s FFT+screen; full-job rate = gridding scaled by "
+                       f"{nvis_full / nvis_s:.0f}x + FFT/screen once")}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 via torchrun")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ska_sdp_func_python_amd import kernels, parallel, simulation
+
+    nchan_total = args.nchan * world
+    chans = parallel.interleaved_channels(nchan_total, rank, world)
+    obs = simulation.device_observation(args.ntimes, args.nchan, F_LO, F_HI, config="MID",
+                                        seed=rank, device=dev, nchan_total=nchan_total,
+                                        channels=chans)
+    cell = 0.25 / obs["umax"]
+    nvis_rank = obs["nrow"] * len(chans)
+    out = torch.empty((args.npix, args.npix), dtype=torch.float64, device=dev)
+    infos = []
+
+    def grid_fn(*a, **k):
+        r = kernels.ms2dirty(*a, **k)
+        infos.append(r[1])
+        return r
+
+    def step():
+        parallel.invert_sharded(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], args.npix, cell,
+                                EPS_REQUESTED, True, flip_uw=True, normalise=True,
+                                grid_fn=grid_fn, out=out)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize(dev)
+
+    kernels.set_stage_timing(False)
+    for _ in range(args.warmup):
+        step()
+    # timed region: stage timing on, so the C ABI brackets k_grid with HIP
+    # events on its launch stream (it already synchronises the host twice per
+    # call for the plan; the events add no extra device work)
+    kernels.set_stage_timing(True)
+    infos.clear()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernels.set_stage_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    info = infos[-1]
+    ms_step = elapsed / args.steps * 1e3
+    value = nvis_rank * world / (elapsed / args.steps) / 1e6
+    ms_grid = float(np.mean([i["ms_grid"] for i in infos]))
+    launches = max(1, math.ceil(info["nplanes"] / max(1, info["plane_chunk"])))
+    alg_bytes = nvis_rank * (8 + 4 + 24.0 / len(chans)) + \
+        info["nplanes"] * info["ngrid_x"] * info["ngrid_y"] * 8
+    achieved = alg_bytes / launches / (ms_grid / launches * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        with open(args.traffic) as f:
+            traffic = json.load(f).get("bytes_per_launch")
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "k_grid<8,true>", "kernel_ms": round(ms_grid / launches, 4),
+            "alg_bytes_per_launch": int(alg_bytes / launches)}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_chans > 0:
+        cpu = cpu_baseline(args, obs["umax"], nchan_total)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mvis/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded SKA-MID-like layout, N(0,1) c64 vis, unit f32 weights, "
+                    "generated on device)",
+            "config": {"workload": "C2: SKA-MID 197 dishes, 64 chan x 100 times per GPU, "
+                                   f"{args.npix}^2 image, {info['ngrid_x']}^2 w-stack grid",
+                       "nvis_per_gpu": nvis_rank, "nchan_total": nchan_total,
+                       "npix": args.npix, "cell_rad": cell, "support": info["support"],
+                       "nplanes": info["nplanes"], "epsilon_requested": EPS_REQUESTED,
+                       "parallelism": f"channel-sharded x{world}, 1 all-reduce"},
+            "stages_ms": {k: round(float(np.mean([i[k] for i in infos])), 3)
+                          for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -792,11 +792,15 @@ struct Inputs {
     unsigned flags;
 };
 
+// Bytes of w planes kept resident per pass: SDP_HIP_GRID_BUDGET_GB if set,
+// else half of the device memory free at plan time (one 8192^2 plane is
+// 512 MiB, so a C2 invert keeps all its planes resident on a 288 GB MI355X).
 static size_t grid_budget_bytes() {
     const char *e = std::getenv("SDP_HIP_GRID_BUDGET_GB");
-    double gb = e ? std::atof(e) : 48.0;
-    if (!(gb > 0)) gb = 48.0;
-    return (size_t)(gb * 1073741824.0);
+    if (e && std::atof(e) > 0) return (size_t)(std::atof(e) * 1073741824.0);
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)8 << 30;
+    return free_b / 2;
 }
 
 // Geometry, bucketing and work items shared by both directions.
@@ -1043,13 +1047,14 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     tm.mark();
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
     const size_t plane_elems = (size_t)g.ngx * g.ngy;
-    float tgrid = 0, tfft = 0, tscr = 0;
+    float tzero = 0, tgrid = 0, tfft = 0, tscr = 0;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
         StageTimer t2(st);
         t2.mark();
         SDP_HIP_CHECK(hipMemsetAsync(P.grid, 0, (size_t)np * plane_elems * sizeof(float2), st));
+        t2.mark();
 #define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, p_lo, p_hi, st)
         SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
 #undef SDP_LAUNCH_GRID
@@ -1062,14 +1067,15 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
                                           (accumulate || p_lo > 0) ? 1 : 0, tab);
         SDP_HIP_CHECK(hipGetLastError());
         t2.mark();
-        tgrid += t2.ms(0, 1);
-        tfft += t2.ms(1, 2);
-        tscr += t2.ms(2, 3);
+        tzero += t2.ms(0, 1);
+        tgrid += t2.ms(1, 2);
+        tfft += t2.ms(2, 3);
+        tscr += t2.ms(3, 4);
     }
     tm.mark();
     fill_info(P, info);
     if (info) {
-        info->ms_prep = tm.ms(0, 1);
+        info->ms_prep = tm.ms(0, 1) + tzero;
         info->ms_grid = tgrid;
         info->ms_fft = tfft;
         info->ms_screen = tscr;
@@ -1099,13 +1105,14 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     float2 *acc = scratch<float2>("degrid_acc", std::max<int64_t>(P.nrec, 1));
     SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(P.nrec, 1) * sizeof(float2), st));
     const size_t plane_elems = (size_t)g.ngx * g.ngy;
-    float tgrid = 0, tfft = 0, tscr = 0;
+    float tzero = 0, tgrid = 0, tfft = 0, tscr = 0;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
         StageTimer t2(st);
         t2.mark();
         SDP_HIP_CHECK(hipMemsetAsync(P.grid, 0, (size_t)np * plane_elems * sizeof(float2), st));
+        t2.mark();
         const dim3 grd(grid1d(g.ny, 256), g.nx);
         k_screen_adj<<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_lo, np, P.grid, tab);
         SDP_HIP_CHECK(hipGetLastError());
@@ -1117,9 +1124,10 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
 #undef SDP_LAUNCH_DEGRID
         SDP_HIP_CHECK(hipGetLastError());
         t2.mark();
-        tscr += t2.ms(0, 1);
-        tfft += t2.ms(1, 2);
-        tgrid += t2.ms(2, 3);
+        tzero += t2.ms(0, 1);
+        tscr += t2.ms(1, 2);
+        tfft += t2.ms(2, 3);
+        tgrid += t2.ms(3, 4);
     }
     if (P.nrec > 0) {
         if (in.vis_dtype == SDP_HIP_C128)
@@ -1133,7 +1141,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     tm.mark();
     fill_info(P, info);
     if (info) {
-        info->ms_prep = tm.ms(0, 1);
+        info->ms_prep = tm.ms(0, 1) + tzero;
         info->ms_grid = tgrid;
         info->ms_fft = tfft;
         info->ms_screen = tscr;

@@ -133,8 +133,14 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
                                residual)
 
     if normalise_gains in ["median", "mean"] and not phase_only:
-        ga = gain.abs()
-        gabs = torch.median(ga) if normalise_gains == "median" else torch.mean(ga)
+        ga = gain.abs().flatten()
+        if normalise_gains == "median":
+            # numpy median (mean of the two middle values for even counts),
+            # not torch.median's lower middle (solvers.py:93-101)
+            s = torch.sort(ga).values
+            gabs = 0.5 * (s[(ga.numel() - 1) // 2] + s[ga.numel() // 2])
+        else:
+            gabs = torch.mean(ga)
         gain = gain / gabs
 
     ref = gain_table["gain"].data

@@ -123,13 +123,15 @@ def c2_geometry(nchan=64, ntimes=100):
 
 
 def device_observation(ntimes, nchan, f_lo, f_hi, config="MID", ha_span_h=8.0, dec_deg=None,
-                       seed=0, device=None, vis_dtype=None, chan_offset=0, nchan_total=None):
+                       seed=0, device=None, vis_dtype=None, chan_offset=0, nchan_total=None,
+                       channels=None):
     """Device-resident C2/C4-style arrays without a host Visibility.
 
     Returns dict(uvw [nrow,3] f64, freq [nchan] f64, vis [nrow,nchan] c64,
     wgt [nrow,nchan] f32, nrow) generated on the GPU (seeded).  With
     ``chan_offset``/``nchan_total`` the channels are a slice of a wider band
-    (one shard of a channel-sharded observation).
+    (one shard of a channel-sharded observation); ``channels`` instead picks
+    explicit indices of the ``nchan_total`` band (interleaved shards).
     """
     import torch
     fn, n_def, lat, dec_def = CONFIGS[config]
@@ -140,13 +142,17 @@ def device_observation(ntimes, nchan, f_lo, f_hi, config="MID", ha_span_h=8.0, d
     uvw, _ = observe(en, lat, dec, ha)
     nt = nchan_total or nchan
     allf = np.linspace(f_lo, f_hi, nt) if nt > 1 else np.array([f_lo])
-    freq = allf[chan_offset:chan_offset + nchan]
+    if channels is not None:
+        freq = allf[np.asarray(channels)]
+        nchan = len(freq)
+    else:
+        freq = allf[chan_offset:chan_offset + nchan]
     dev = device or torch.device("cuda")
     uvw_t = torch.as_tensor(uvw.reshape(-1, 3), device=dev)
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + seed)
     nrow = uvw_t.shape[0]
-    vis = torch.randn((nrow, nchan), generator=g, device=dev, dtype=torch.complex64)
+    vis = torch.randn((nrow, nchan), generator=g, device=dev, dtype=vis_dtype or torch.complex64)
     wgt = torch.ones((nrow, nchan), device=dev, dtype=torch.float32)
     return dict(uvw=uvw_t, freq=torch.as_tensor(freq, device=dev), vis=vis, wgt=wgt, nrow=nrow,
                 umax=float(np.max(np.abs(uvw[..., :2]))) * float(allf.max()) / C)
