@@ -18,10 +18,11 @@
  *   kernel's Fourier transform in x, y and w and by n.
  *
  * Output is ducc0's convention: dirty[x * npix_y + y], l_x = (x - nx/2) px.
- * Parallelism: planes are processed one at a time (like ducc0); the
- * scatter is split over 64-row strips of the grid, even strips then odd
- * strips, so no two threads touch the same grid row; FFT rows/columns and
- * the image accumulation are OpenMP loops.
+ * Parallelism: all w planes stay resident (as on the GPU), visibilities are
+ * bucketed by 32 x 32-cell tiles and gridded strip by strip (32-row strips,
+ * even strips then odd strips, so no two threads touch the same grid row);
+ * each visibility's u/v/w taps are evaluated once.  FFT rows/columns and the
+ * image accumulation are OpenMP loops.
  */
 #include <complex.h>
 #include <math.h>
@@ -31,7 +32,7 @@
 #include <string.h>
 
 #define C_LIGHT 299792458.0
-#define STRIP 64
+#define STRIP 32
 
 typedef float complex cf32;
 typedef double complex cf64;
@@ -190,96 +191,130 @@ int wgrid_cpu_ms2dirty(const double *uvw, const double *freq, int nchan, int64_t
         nplanes = (int)floor((wmax - w0) / dw - 0.5 * W) + 1 + W;
     }
 
-    /* per-vis records bucketed by (p0, strip) */
+    /* per-vis records bucketed by (strip, tile column) of 32 x 32 cells;
+       all w planes stay resident (like the GPU path), so each visibility's
+       u/v/w taps are evaluated once and it is gridded in one pass */
+    const int ntc = (ngy + STRIP - 1) / STRIP;
     const int nstrip = (ngx + STRIP - 1) / STRIP;
-    const int nfirst = do_wstacking ? nplanes : 1;
-    int64_t *cnt = calloc((size_t)nfirst * nstrip + 1, sizeof(int64_t));
+    const int64_t nkey = (int64_t)nstrip * ntc;
+    int64_t *cnt = calloc((size_t)nkey + 1, sizeof(int64_t));
     int32_t *key = malloc(sizeof(int32_t) * nvis);
+    typedef struct {
+        float re, im, fu, fv, fw;
+        int32_t ic, jc, p0;
+    } rec_t;
+    rec_t *rec = malloc(sizeof(rec_t) * (nvis + 1));
+#pragma omp parallel for schedule(static)
     for (int64_t r = 0; r < nrow; ++r)
         for (int c = 0; c < nchan; ++c) {
             const int64_t k = r * nchan + c;
             float wt = wgt ? wgt[k] : 1.0f;
             float re = vis ? vis[2 * k] : 1.0f, im = vis ? vis[2 * k + 1] : 0.0f;
-            if (wt == 0.0f || (re == 0.0f && im == 0.0f)) {
-                key[k] = -1;
-                continue;
-            }
+            key[k] = -1;
+            if (wt == 0.0f || (re == 0.0f && im == 0.0f)) continue;
             const double s = freq[c] / C_LIGHT;
             const double a = uvw[3 * r] * s * pixsize_x * ngx;
-            int i0 = (int)floor(a - 0.5 * W) + 1;
-            int gi = ((i0 + ngx / 2) % ngx + ngx) % ngx;
-            int p0 = 0;
-            if (do_wstacking) p0 = (int)floor((uvw[3 * r + 2] * s - w0) / dw - 0.5 * W) + 1;
-            key[k] = p0 * nstrip + gi / STRIP;
-            cnt[key[k] + 1]++;
-        }
-    for (int64_t i = 0; i < (int64_t)nfirst * nstrip; ++i) cnt[i + 1] += cnt[i];
-    int64_t *fill = malloc(sizeof(int64_t) * ((size_t)nfirst * nstrip));
-    memcpy(fill, cnt, sizeof(int64_t) * nfirst * nstrip);
-    typedef struct {
-        float re, im;
-        double a, b, pw;
-    } rec_t;
-    rec_t *rec = malloc(sizeof(rec_t) * (cnt[(size_t)nfirst * nstrip] + 1));
-    for (int64_t r = 0; r < nrow; ++r)
-        for (int c = 0; c < nchan; ++c) {
-            const int64_t k = r * nchan + c;
-            if (key[k] < 0) continue;
-            const double s = freq[c] / C_LIGHT;
+            const double b = uvw[3 * r + 1] * s * pixsize_y * ngy;
             const double w = uvw[3 * r + 2] * s;
-            cf64 v = (vis ? (vis[2 * k] + I * vis[2 * k + 1]) : 1.0) * (wgt ? wgt[k] : 1.0f);
-            if (do_wstacking) v *= cexp(2.0 * M_PI * I * w * s0);
-            rec_t q = {(float)creal(v), (float)cimag(v), uvw[3 * r] * s * pixsize_x * ngx,
-                       uvw[3 * r + 1] * s * pixsize_y * ngy, do_wstacking ? (w - w0) / dw : 0.0};
-            rec[fill[key[k]]++] = q;
+            const double fa = floor(a - 0.5 * W), fb = floor(b - 0.5 * W);
+            rec_t q;
+            q.ic = (((int)fa + 1 + ngx / 2) % ngx + ngx) % ngx;
+            q.jc = (((int)fb + 1 + ngy / 2) % ngy + ngy) % ngy;
+            q.fu = (float)(fa + 1.0 - a);
+            q.fv = (float)(fb + 1.0 - b);
+            q.p0 = 0;
+            q.fw = 0.0f;
+            cf64 v = (re + I * im) * (double)wt;
+            if (do_wstacking) {
+                const double pw = (w - w0) / dw, fp = floor(pw - 0.5 * W);
+                q.p0 = (int)fp + 1;
+                q.fw = (float)(fp + 1.0 - pw);
+                v *= cexp(2.0 * M_PI * I * w * s0);
+            }
+            q.re = (float)creal(v);
+            q.im = (float)cimag(v);
+            rec[k] = q;
+            key[k] = (q.ic / STRIP) * ntc + q.jc / STRIP;
         }
-    free(fill);
+    for (int64_t k = 0; k < nvis; ++k)
+        if (key[k] >= 0) cnt[key[k] + 1]++;
+    for (int64_t i = 0; i < nkey; ++i) cnt[i + 1] += cnt[i];
+    int64_t *order = malloc(sizeof(int64_t) * (cnt[nkey] + 1));
+    {
+        int64_t *fill = malloc(sizeof(int64_t) * nkey);
+        memcpy(fill, cnt, sizeof(int64_t) * nkey);
+        for (int64_t k = 0; k < nvis; ++k)
+            if (key[k] >= 0) order[fill[key[k]]++] = k;
+        free(fill);
+    }
     free(key);
 
-    cf32 *grid = malloc(sizeof(cf32) * (size_t)ngx * ngy);
+    const size_t plane = (size_t)ngx * ngy;
+    float *grid = calloc(plane * 2 * nplanes, sizeof(float)); /* [plane][x][y] complex */
     cf64 *rowbuf = malloc(sizeof(cf64) * (size_t)ngx * npix_y); /* [ngx][npix_y] after row FFT */
     double *acc = calloc((size_t)npix_x * npix_y, sizeof(double));
     fft_plan px, py;
     plan_init(&px, ngx);
     plan_init(&py, ngy);
     double tg = 0.0, tf = 0.0;
+    const float fbeta = (float)beta, fihw = 2.0f / W;
 
-    for (int p = 0; p < nplanes; ++p) {
-        double t0 = omp_get_wtime();
-        memset(grid, 0, sizeof(cf32) * (size_t)ngx * ngy);
-        for (int parity = 0; parity < 2; ++parity) {
+    double tg0 = omp_get_wtime();
+    /* strips of one parity never share grid rows (W <= 8 < STRIP); with an
+       odd strip count the last strip wraps onto strip 0, so it runs alone */
+    const int nst_even = nstrip & ~1;
+    for (int parity = 0; parity < 3; ++parity) {
+        const int lo = parity < 2 ? parity : nst_even, hi = parity < 2 ? nst_even : nstrip;
 #pragma omp parallel for schedule(dynamic, 1)
-            for (int st = parity; st < nstrip; st += 2) {
-                const int plo = do_wstacking ? (p - W + 1 < 0 ? 0 : p - W + 1) : 0;
-                const int phi = do_wstacking ? p : 0;
-                for (int q0 = plo; q0 <= phi; ++q0) {
-                    const int64_t b = cnt[(int64_t)q0 * nstrip + st],
-                                  e = cnt[(int64_t)q0 * nstrip + st + 1];
-                    for (int64_t k = b; k < e; ++k) {
-                        const rec_t *q = &rec[k];
-                        float kw = 1.0f;
-                        if (do_wstacking) kw = (float)es((double)p - q->pw, W, beta);
-                        const int i0 = (int)floor(q->a - 0.5 * W) + 1;
-                        const int j0 = (int)floor(q->b - 0.5 * W) + 1;
-                        float ku[8], kv[8];
-                        for (int t = 0; t < W; ++t) {
-                            ku[t] = (float)es(i0 + t - q->a, W, beta) * kw;
-                            kv[t] = (float)es(j0 + t - q->b, W, beta);
+        for (int st = lo; st < hi; st += 2) {
+            for (int64_t k = cnt[(int64_t)st * ntc]; k < cnt[(int64_t)(st + 1) * ntc]; ++k) {
+                const rec_t *q = &rec[order[k]];
+                float ku[8], kw[8], kv2[16];
+                for (int t = 0; t < W; ++t) {
+                    float x = (q->fu + t) * fihw, y = 1.0f - x * x;
+                    ku[t] = y > 0.0f ? expf(fbeta * (sqrtf(y) - 1.0f)) : 0.0f;
+                    x = (q->fv + t) * fihw;
+                    y = 1.0f - x * x;
+                    kv2[2 * t] = kv2[2 * t + 1] = y > 0.0f ? expf(fbeta * (sqrtf(y) - 1.0f)) : 0.0f;
+                    x = (q->fw + t) * fihw;
+                    y = 1.0f - x * x;
+                    kw[t] = do_wstacking ? (y > 0.0f ? expf(fbeta * (sqrtf(y) - 1.0f)) : 0.0f)
+                                         : (t == 0 ? 1.0f : 0.0f);
+                }
+                const int nq = do_wstacking ? W : 1;
+                const int fast = q->jc + W <= ngy;
+                for (int qq = 0; qq < nq; ++qq) {
+                    float *pl = grid + 2 * plane * (size_t)(q->p0 + qq);
+                    for (int t = 0; t < W; ++t) {
+                        int gi = q->ic + t;
+                        if (gi >= ngx) gi -= ngx;
+                        const float f = ku[t] * kw[qq];
+                        float cv[16];
+                        for (int e = 0; e < 8; ++e) {
+                            cv[2 * e] = q->re * f;
+                            cv[2 * e + 1] = q->im * f;
                         }
-                        const cf32 val = q->re + I * q->im;
-                        for (int t = 0; t < W; ++t) {
-                            const int gi = ((i0 + t + ngx / 2) % ngx + ngx) % ngx;
-                            const cf32 vu = val * ku[t];
-                            cf32 *row = grid + (size_t)gi * ngy;
+                        float *row = pl + 2 * (size_t)gi * ngy;
+                        if (fast && W == 8) {
+                            float *dst = row + 2 * q->jc;
+                            for (int e = 0; e < 16; ++e) dst[e] += cv[e] * kv2[e];
+                        } else {
                             for (int tt = 0; tt < W; ++tt) {
-                                const int gj = ((j0 + tt + ngy / 2) % ngy + ngy) % ngy;
-                                row[gj] += vu * kv[tt];
+                                int gj = q->jc + tt;
+                                if (gj >= ngy) gj -= ngy;
+                                row[2 * gj] += cv[2 * tt] * kv2[2 * tt];
+                                row[2 * gj + 1] += cv[2 * tt + 1] * kv2[2 * tt + 1];
                             }
                         }
                     }
                 }
             }
         }
+    }
+    tg = omp_get_wtime() - tg0;
+
+    for (int p = 0; p < nplanes; ++p) {
+        const float *gp = grid + 2 * plane * (size_t)p;
         double t1 = omp_get_wtime();
         /* pruned 2-D backward FFT: rows (length ngy) keep npix_y outputs,
            then columns (length ngx) keep npix_x outputs */
@@ -289,7 +324,8 @@ int wgrid_cpu_ms2dirty(const double *uvw, const double *freq, int nchan, int64_t
             cf64 *tmp = malloc(sizeof(cf64) * (ngx > ngy ? ngx : ngy));
 #pragma omp for schedule(static)
             for (int i = 0; i < ngx; ++i) {
-                for (int j = 0; j < ngy; ++j) line[j] = grid[(size_t)i * ngy + j];
+                for (int j = 0; j < ngy; ++j)
+                    line[j] = gp[2 * ((size_t)i * ngy + j)] + I * gp[2 * ((size_t)i * ngy + j) + 1];
                 fft_bwd(&py, line, tmp);
                 for (int y = 0; y < npix_y; ++y) {
                     const int Y = y - npix_y / 2;
@@ -321,7 +357,6 @@ int wgrid_cpu_ms2dirty(const double *uvw, const double *freq, int nchan, int64_t
             free(line);
             free(tmp);
         }
-        tg += t1 - t0;
         tf += omp_get_wtime() - t1;
     }
 
@@ -351,6 +386,7 @@ int wgrid_cpu_ms2dirty(const double *uvw, const double *freq, int nchan, int64_t
     free(rowbuf);
     free(grid);
     free(rec);
+    free(order);
     free(cnt);
     plan_free(&px);
     plan_free(&py);

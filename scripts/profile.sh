@@ -1,0 +1,15 @@
+#!/bin/bash
+# rocprofv3 evidence for bench.py: kernel trace + stats, then two PMC passes
+# (FETCH_SIZE, WRITE_SIZE -- separate passes, no runtime/sys trace).
+cd "$(dirname "$0")/.." || exit 1
+tag=${1:-r01}
+out=gpurun_out/prof_${tag}
+mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --cpu-chans 0 > $out/bench_trace.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o run -- \
+    python3 bench.py --steps 1 --warmup 1 --cpu-chans 0 > $out/bench_fetch.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o run -- \
+    python3 bench.py --steps 1 --warmup 1 --cpu-chans 0 > $out/bench_write.log 2>&1 || exit $?
+find $out -name "*.csv" | head -50

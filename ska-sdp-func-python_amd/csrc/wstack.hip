@@ -10,12 +10,13 @@
 //                  histogram (one atomic per run of equal keys)
 //   scan           hipcub exclusive sum over buckets
 //   k_bucket<1>    32-byte visibility records in bucket order
-//   k_items_*      work items = one bucket, split into <= kChunk records
+//   k_items_*      work items = one bucket, split into <= chunk records
 //   per plane chunk (all planes resident when they fit the budget):
-//     k_grid       one wave per item; the wave owns an LDS tile of W planes
-//                  x (16+W-1)^2 complex cells; per record one lane per (u,v)
-//                  tap does a plain ds_read_b64/ds_write_b64 update of all W
-//                  planes; the tile is flushed with global float atomics
+//     k_grid       one workgroup per item owning an LDS tile of W planes
+//                  x (16+W-1)^2 complex cells, planes split over its waves;
+//                  per record one lane per (u,v) tap does a plain
+//                  ds_read_b64/ds_write_b64 update of the wave's planes; the
+//                  tile is flushed with global float atomics
 //     hipFFT       batched in-place c2c over the planes
 //     k_screen_fwd w-screen phase, real part, fp64 accumulate, grid correction
 //   dirty2ms runs the stages in adjoint order (k_screen_adj, FFT, k_degrid).
@@ -41,8 +42,13 @@ namespace sdp {
 namespace wstack {
 
 constexpr double kCLight = 299792458.0;
-constexpr int kTile = 16;      // uv tile edge in grid cells
-constexpr int kChunk = 2048;   // max records per work item
+constexpr int kTileCoarse = 16;  // bucket edge (cells) of the LDS-tile gridder
+constexpr int kTileFine = 2;     // bucket edge (cells) of the register gridder
+constexpr int kGridAlign = 16;   // padded grid edges are multiples of this
+// fine buckets are used while the dense (p0, 2x2-cell) histogram stays small
+constexpr int64_t kMaxFineKeys = (int64_t)1 << 27;
+constexpr int kChunkMin = 1024;   // records per work item: chosen per call in
+constexpr int kChunkMax = 8192;   // [kChunkMin, kChunkMax] (chunk_size())
 constexpr int kPitch = 24;     // LDS row pitch in complex values (b64 conflict-free)
 constexpr int kMaxW = 8;
 constexpr int kPhiTab = 8193;  // Phi(xi) table on xi in [0, 0.5]
@@ -54,7 +60,7 @@ struct Geo {
     double px, py;
     int do_w, nplanes, nps;  // nps = number of distinct first planes
     double w0, dw, s0;
-    int nty, ntiles;
+    int sub, nty, ntiles;  // bucket edge in cells, buckets per grid column, buckets
     double su;  // sign applied to u and w (-1 with SDP_HIP_FLIP_UW)
     int nchan;
     int64_t nrow;
@@ -143,7 +149,7 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
 
 // p0-major bucket keys: the items of a range of first planes are contiguous.
 __device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c) {
-    const int tile = (c.ic0 / kTile) * g.nty + (c.jc0 / kTile);
+    const int tile = (c.ic0 / g.sub) * g.nty + (c.jc0 / g.sub);
     return (unsigned)c.p0 * (unsigned)g.ntiles + (unsigned)tile;
 }
 
@@ -266,25 +272,26 @@ __global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
     recs[pos] = rec;
 }
 
-__global__ void k_items_count(int64_t nkeys, const unsigned *__restrict__ offs, unsigned *nch) {
+__global__ void k_items_count(int64_t nkeys, const unsigned *__restrict__ offs, unsigned chunk,
+                              unsigned *nch) {
     const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (k >= nkeys) return;
     const unsigned n = offs[k + 1] - offs[k];
-    nch[k] = (n + kChunk - 1) / kChunk;
+    nch[k] = (n + chunk - 1) / chunk;
 }
 
 __global__ void k_items_fill(int64_t nkeys, int ntiles, const unsigned *__restrict__ offs,
-                             const unsigned *__restrict__ ioffs, Item *items) {
+                             const unsigned *__restrict__ ioffs, unsigned chunk, Item *items) {
     const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (k >= nkeys) return;
     const unsigned b = offs[k], e = offs[k + 1];
     unsigned o = ioffs[k];
     const uint32_t p0 = (uint32_t)(k / ntiles);
     const uint32_t tile = (uint32_t)(k - (int64_t)p0 * ntiles);
-    for (unsigned s = b; s < e; s += kChunk) {
+    for (unsigned s = b; s < e; s += chunk) {
         Item x;
         x.b = s;
-        x.e = min(e, s + (unsigned)kChunk);
+        x.e = min(e, s + chunk);
         x.tile = tile;
         x.p0 = p0;
         items[o++] = x;
@@ -300,14 +307,23 @@ __global__ void k_gather_p0_offsets(const unsigned *__restrict__ ioffs, int ntil
 // ------------------------------------------------------------------------
 // kernels: gridding / degridding (the hot loops)
 // ------------------------------------------------------------------------
-template <int W>
+template <int W, int SUB>
 struct TileShape {
-    static constexpr int R = kTile + W - 1;   // tile + halo rows/cols
-    static constexpr int PLANE = R * kPitch;  // complex values per plane in LDS
+    static constexpr int R = SUB + W - 1;                         // bucket + halo
+    static constexpr int PITCH = SUB == kTileCoarse ? kPitch : R;  // LDS row pitch
+    static constexpr int PLANE = R * PITCH;  // complex values per plane in LDS
 };
 
-__device__ __forceinline__ Item load_item(const Item *__restrict__ items) {
-    const Item raw = items[blockIdx.x];
+// Work items are visited in a strided order (stride coprime with the item
+// count): the heavy chunks of one dense tile are spread over the launch
+// instead of flushing into the same cells at the same time.
+struct ItemOrder {
+    uint32_t n, stride;
+};
+
+__device__ __forceinline__ Item load_item(const Item *__restrict__ items, ItemOrder ord) {
+    const uint32_t i = (uint32_t)(((uint64_t)blockIdx.x * ord.stride) % ord.n);
+    const Item raw = items[i];
     Item it;
     it.b = __builtin_amdgcn_readfirstlane(raw.b);
     it.e = __builtin_amdgcn_readfirstlane(raw.e);
@@ -338,6 +354,28 @@ __device__ __forceinline__ RecRegs rec_at(const VisRec &my, int k) {
     return r;
 }
 
+// Kernel taps of a 64-record batch with every lane busy: VGPR u[m] of lane
+// l holds the u tap (l % 8) of record 8m + l/8 (likewise v, w), so 24 ES
+// evaluations per lane cover the 64 records' 3 x 8 taps.  A record's taps
+// are then fetched with one ds_bpermute (u, v: lane-dependent) or
+// v_readlane (w: wave-uniform).  Taps t >= W evaluate to 0 (|x| > 1).
+struct BatchTaps {
+    float u[8], v[8], w[8];
+};
+
+__device__ __forceinline__ BatchTaps batch_taps(const VisRec &my, int lane, float ihw, float bl) {
+    BatchTaps b;
+    const float t = (float)(lane & 7);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int src = 8 * m + (lane >> 3);
+        b.u[m] = es_kernel(__shfl(my.fu, src) + t, ihw, bl);
+        b.v[m] = es_kernel(__shfl(my.fv, src) + t, ihw, bl);
+        b.w[m] = es_kernel(__shfl(my.fw, src) + t, ihw, bl);
+    }
+    return b;
+}
+
 // Per-lane roles inside a wave for support W: lane = kx*W + ky is the (u,v)
 // tap it accumulates; lanes [0,W) / [W,2W) / [2W,3W) evaluate the u / v / w
 // 1-D taps of the current record (one ES evaluation per lane).
@@ -363,61 +401,86 @@ struct LaneRole {
     }
 };
 
-// One wave per work item (= one (p0, tile) bucket chunk).  The wave owns its
-// LDS tile of W planes, so accumulation is a plain ds_read_b64/ds_write_b64
-// read-modify-write: no LDS float atomics (gfx950 runs ds_add_f32 at ~0.3
+// One workgroup of NWV waves per work item (= one (p0, tile) bucket chunk).
+// The workgroup owns an LDS tile of W planes and wave wv owns planes
+// [wv*NQW, (wv+1)*NQW): every wave walks all records of the item (coalesced
+// 2 KiB record fetches, hits in L1/L2 after the first wave) and updates only
+// its planes, so accumulation is a plain ds_read_b64/ds_write_b64
+// read-modify-write with no LDS atomics (gfx950 runs ds_add_f32 at ~0.3
 // lanes/clk/CU), exact fp32 sums, and in-order LDS execution
-// inside the wave orders the updates of consecutive records.
-template <int W, bool WS>
-__global__ __launch_bounds__(64) void k_grid(Geo g, const VisRec *__restrict__ recs,
-                                             const Item *__restrict__ items,
-                                             float *__restrict__ grid, int p_lo, int p_hi) {
+// inside each wave orders the updates of consecutive records.  Splitting the
+// planes over waves raises occupancy (the 35 KiB tile is shared by NWV waves)
+// to hide the LDS read->write latency of the update chain.
+template <int W, bool WS, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__restrict__ recs,
+                                                       const Item *__restrict__ items,
+                                                       ItemOrder ord, float *__restrict__ grid,
+                                                       int p_lo, int p_hi) {
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int R = TileShape<W>::R;
-    constexpr int PS = TileShape<W>::PLANE;
+    constexpr int kTile = kTileCoarse;
+    constexpr int R = TileShape<W, kTile>::R;
+    constexpr int PS = TileShape<W, kTile>::PLANE;
     constexpr int NQ = WS ? W : 1;
-    const Item it = load_item(items);
-    const int lane = threadIdx.x;
-    for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
+    constexpr int NQW = (NQ + NWV - 1) / NWV;  // planes per wave (the last
+    constexpr int NQP = NQW * NWV;             // wave may own padding planes)
+    const Item it = load_item(items, ord);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (int i = threadIdx.x; i < NQP * PS; i += 64 * NWV) tile[i] = make_float2(0.0f, 0.0f);
+    __syncthreads();
 
     const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
     const LaneRole<W> role(lane);
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
     const int lane_off = role.kx * kPitch + role.ky - (tx * kTile) * kPitch - ty * kTile;
+    const int q0 = wv * NQW;
+    float2 *const wtile = tile + q0 * PS;
 
     for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
         const int n = (int)min(64u, it.e - b0);
         const VisRec my = recs[b0 + min(lane, n - 1)];
-        for (int k = 0; k < n; ++k) {
-            const RecRegs rc = rec_at(my, k);
-            const float kval = role.taps(rc, ihw, bl);
-            const float ku = __shfl(kval, role.kx);
-            const float kv = __shfl(kval, W + role.ky);
-            const float kk = ku * kv;
-            const float vr = rc.cre * kk, vi = rc.cim * kk;
-            const int off = lane_off + (int)(rc.ij & 0xffffu) * kPitch + (int)(rc.ij >> 16);
-            float kw[NQ];
+        const BatchTaps bt = batch_taps(my, lane, ihw, bl);
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(kval, 2 * W + q) : 1.0f;
-            if (role.act) {
-                float2 a[NQ];
+        for (int m = 0; m < 8; ++m) {
+            const int rn = min(8, n - 8 * m);  // records of this 8-record group
+            for (int r = 0; r < rn; ++r) {
+                const int k = 8 * m + r;
+                const float cre = lane_readf(my.cre, k), cim = lane_readf(my.cim, k);
+                const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)my.ij, k);
+                const float ku = __shfl(bt.u[m], 8 * r + role.kx);
+                const float kv = __shfl(bt.v[m], 8 * r + role.ky);
+                const float kk = ku * kv;
+                const float vr = cre * kk, vi = cim * kk;
+                const int off = lane_off + (int)(ij & 0xffffu) * kPitch + (int)(ij >> 16);
+                // padding planes (q0 + q >= NQ) get a zero weight: a uniform
+                // select, so the LDS reads and writes below stay branch-free
+                float kw[NQW];
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) a[q] = tile[q * PS + off];
+                for (int q = 0; q < NQW; ++q) {
+                    const float x = WS ? lane_readf(bt.w[m], 8 * r + min(q0 + q, NQ - 1)) : 1.0f;
+                    kw[q] = (NQP == NQ || q0 + q < NQ) ? x : 0.0f;
+                }
+                if (role.act) {
+                    float2 a[NQW];
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    a[q].x = fmaf(vr, kw[q], a[q].x);
-                    a[q].y = fmaf(vi, kw[q], a[q].y);
-                    tile[q * PS + off] = a[q];
+                    for (int q = 0; q < NQW; ++q) a[q] = wtile[q * PS + off];
+#pragma unroll
+                    for (int q = 0; q < NQW; ++q) {
+                        a[q].x = fmaf(vr, kw[q], a[q].x);
+                        a[q].y = fmaf(vi, kw[q], a[q].y);
+                        wtile[q * PS + off] = a[q];
+                    }
                 }
             }
         }
     }
+    __syncthreads();
 
     // flush: float atomics into the resident planes (the halo overlaps the
     // neighbouring tiles); zero cells are skipped.
     const int cells = R * R;
     const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-    for (int c = lane; c < NQ * cells; c += 64) {
+    for (int c = threadIdx.x; c < NQ * cells; c += 64 * NWV) {
         const int q = c / cells;
         const int p = (int)it.p0 + q;
         if (p < p_lo || p >= p_hi) continue;
@@ -437,16 +500,122 @@ __global__ __launch_bounds__(64) void k_grid(Geo g, const VisRec *__restrict__ r
     }
 }
 
+// Register gridder: one wave per work item (= one (p0, 2x2-cell bucket)
+// chunk).  Lane (kx, ky) is the (u, v) tap it accumulates; a record whose
+// footprint starts at cell origin o in {0,1}^2 of the bucket adds
+// vis * ku * kv * kw[q] into VGPR accumulator acc[o][q] (q = w plane), so the
+// per-record work is FMAs on registers -- no LDS traffic except two
+// ds_bpermute for the u / v taps.  At the end the <= 4 origin sets are
+// combined in a (2+W-1)^2 x W LDS tile and flushed with global float atomics
+// (zero cells skipped).  Taps come from batch_taps() (all lanes busy).
 template <int W, bool WS>
+__global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict__ recs,
+                                                 const Item *__restrict__ items, ItemOrder ord,
+                                                 float *__restrict__ grid, int p_lo, int p_hi) {
+    constexpr int SUB = kTileFine;
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    constexpr int R = TileShape<W, SUB>::R;
+    constexpr int PS = TileShape<W, SUB>::PLANE;
+    constexpr int NQ = WS ? W : 1;
+    constexpr int NO = SUB * SUB;
+    const Item it = load_item(items, ord);
+    const int lane = threadIdx.x;
+    const LaneRole<W> role(lane);
+    const float ihw = g.inv_half_w, bl = g.beta_l2e;
+    const int sx = (int)it.tile / g.nty, sy = (int)it.tile - sx * g.nty;
+    const int ibase = sx * SUB, jbase = sy * SUB;
+
+    float acc_r[NO][NQ], acc_i[NO][NQ];
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc_r[o][q] = acc_i[o][q] = 0.0f;
+    uint32_t used = 0;
+
+    for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+        const int n = (int)min(64u, it.e - b0);
+        const VisRec my = recs[b0 + min(lane, n - 1)];
+        const BatchTaps bt = batch_taps(my, lane, ihw, bl);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int rn = min(8, n - 8 * m);
+            for (int r = 0; r < rn; ++r) {
+                const int k = 8 * m + r;
+                const float cre = lane_readf(my.cre, k), cim = lane_readf(my.cim, k);
+                const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)my.ij, k);
+                const int o = ((int)(ij & 0xffffu) - ibase) * SUB + ((int)(ij >> 16) - jbase);
+                const float ku = __shfl(bt.u[m], 8 * r + role.kx);
+                const float kv = __shfl(bt.v[m], 8 * r + role.ky);
+                const float kk = ku * kv;
+                const float vr = cre * kk, vi = cim * kk;
+                float kw[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(bt.w[m], 8 * r + q) : 1.0f;
+                used |= 1u << o;
+#pragma unroll
+                for (int oo = 0; oo < NO; ++oo) {
+                    if (o == oo) {
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q) {
+                            acc_r[oo][q] = fmaf(vr, kw[q], acc_r[oo][q]);
+                            acc_i[oo][q] = fmaf(vi, kw[q], acc_i[oo][q]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+
+    // combine the origins in LDS (plain RMW: one wave, in-order LDS), then flush
+    for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
+#pragma unroll
+    for (int oo = 0; oo < NO; ++oo) {
+        if ((used >> oo) & 1u) {
+            if (role.act) {
+                const int base = (oo / SUB + role.kx) * R + (oo % SUB) + role.ky;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    float2 a = tile[q * PS + base];
+                    a.x += acc_r[oo][q];
+                    a.y += acc_i[oo][q];
+                    tile[q * PS + base] = a;
+                }
+            }
+        }
+    }
+    const int cells = R * R;
+    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+    for (int c = lane; c < NQ * cells; c += 64) {
+        const int q = c / cells;
+        const int p = (int)it.p0 + q;
+        if (p < p_lo || p >= p_hi) continue;
+        const int rem = c - q * cells;
+        const int xl = rem / R, yl = rem - (rem / R) * R;
+        const float2 val = tile[q * PS + xl * R + yl];
+        if (val.x != 0.0f || val.y != 0.0f) {
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            float *dst =
+                grid + ((int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy) * 2;
+            atomicAdd(dst, val.x);
+            atomicAdd(dst + 1, val.y);
+        }
+    }
+}
+
+template <int W, bool WS, int SUB>
 __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__ recs,
-                                               const Item *__restrict__ items,
+                                               const Item *__restrict__ items, ItemOrder ord,
                                                const float2 *__restrict__ grid, int p_lo,
                                                int p_hi, float2 *acc) {
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int R = TileShape<W>::R;
-    constexpr int PS = TileShape<W>::PLANE;
+    constexpr int R = TileShape<W, SUB>::R;
+    constexpr int PS = TileShape<W, SUB>::PLANE;
+    constexpr int PITCH = TileShape<W, SUB>::PITCH;
     constexpr int NQ = WS ? W : 1;
-    const Item it = load_item(items);
+    const Item it = load_item(items, ord);
     const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
     const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
     const int lane = threadIdx.x;
@@ -455,11 +624,11 @@ __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__
         const int p = (int)it.p0 + q;
         const int rem = i - q * R * R;
         const int xl = rem / R, yl = rem - (rem / R) * R;
-        int gx = tx * kTile + xl;
+        int gx = tx * SUB + xl;
         if (gx >= g.ngx) gx -= g.ngx;
-        int gy = ty * kTile + yl;
+        int gy = ty * SUB + yl;
         if (gy >= g.ngy) gy -= g.ngy;
-        tile[q * PS + xl * kPitch + yl] =
+        tile[q * PS + xl * PITCH + yl] =
             (p >= p_lo && p < p_hi)
                 ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
                 : make_float2(0.0f, 0.0f);
@@ -467,7 +636,7 @@ __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__
 
     const LaneRole<W> role(lane);
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const int lane_off = role.kx * kPitch + role.ky - (tx * kTile) * kPitch - ty * kTile;
+    const int lane_off = role.kx * PITCH + role.ky - (tx * SUB) * PITCH - ty * SUB;
     for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
         const int n = (int)min(64u, it.e - b0);
         const VisRec my = recs[b0 + min(lane, n - 1)];
@@ -477,7 +646,7 @@ __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__
             const float kval = role.taps(rc, ihw, bl);
             const float ku = __shfl(kval, role.kx);
             const float kv = __shfl(kval, W + role.ky);
-            const int off = lane_off + (int)(rc.ij & 0xffffu) * kPitch + (int)(rc.ij >> 16);
+            const int off = lane_off + (int)(rc.ij & 0xffffu) * PITCH + (int)(rc.ij >> 16);
             float kw[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(kval, 2 * W + q) : 1.0f;
@@ -771,6 +940,7 @@ struct Plan {
     int64_t nitems = 0;
     std::vector<unsigned> p0_items;  // first item of every first-plane value
     int chunk_planes = 1;            // planes resident per pass
+    unsigned chunk = kChunkMin;      // max records per work item
     float2 *grid = nullptr;
 };
 
@@ -819,16 +989,15 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.beta_l2e = (float)(2.30 * g.W * 1.4426950408889634);
     g.nx = in.nx;
     g.ny = in.ny;
-    g.ngx = ((2 * in.nx + kTile - 1) / kTile) * kTile;
-    g.ngy = ((2 * in.ny + kTile - 1) / kTile) * kTile;
+    g.ngx = ((2 * in.nx + kGridAlign - 1) / kGridAlign) * kGridAlign;
+    g.ngy = ((2 * in.ny + kGridAlign - 1) / kGridAlign) * kGridAlign;
     SDP_REQUIRE(g.ngx <= 65535 && g.ngy <= 65535, "image too large (padded grid > 65535)");
     g.px = in.px;
     g.py = in.py;
     g.su = (in.flags & SDP_HIP_FLIP_UW) ? -1.0 : 1.0;
     g.nchan = in.nchan;
     g.nrow = in.nrow;
-    g.nty = g.ngy / kTile;
-    g.ntiles = (g.ngx / kTile) * g.nty;
+    g.sub = kTileCoarse;  // refined below once the plane count is known
 
     // frequency extremes (host) and uvw bounds (device)
     std::vector<double> f(in.nchan);
@@ -875,6 +1044,17 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
         g.nplanes = 1;
         g.nps = 1;
     }
+    // bucket granularity: 2x2-cell buckets feed the register gridder while
+    // the dense (first plane, bucket) histogram stays below kMaxFineKeys,
+    // else 16x16-cell buckets and the LDS-tile gridder
+    {
+        const char *e = std::getenv("SDP_HIP_BUCKET");
+        const int64_t fine = (int64_t)(g.ngx / kTileFine) * (g.ngy / kTileFine) * g.nps;
+        g.sub = fine <= kMaxFineKeys ? kTileFine : kTileCoarse;
+        if (e && std::atoi(e) == kTileCoarse) g.sub = kTileCoarse;
+    }
+    g.nty = g.ngy / g.sub;
+    g.ntiles = (g.ngx / g.sub) * g.nty;
     SDP_REQUIRE((double)g.ntiles * g.nps < 4.0e9, "too many (plane, tile) buckets");
 
     // ---- bucketing
@@ -927,7 +1107,12 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
 
     // ---- work items (p0-major, so a first-plane range is a contiguous item range)
     SDP_HIP_CHECK(hipMemsetAsync(nch + nkeys, 0, sizeof(unsigned), st));
-    k_items_count<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, offs, nch);
+    // records per item: large enough to amortise the tile flush over dense
+    // tiles, small enough to leave >= ~16k items for the 256 CUs
+    P.chunk = (unsigned)std::min<int64_t>(kChunkMax, std::max<int64_t>(kChunkMin, nvis / 16384));
+    if (const char *e = std::getenv("SDP_HIP_CHUNK"))
+        if (std::atoi(e) >= 64) P.chunk = (unsigned)std::atoi(e);
+    k_items_count<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, offs, P.chunk, nch);
     tb = tmp_bytes + 16;
     SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nch, ioffs, (int)(nkeys + 1), st));
     unsigned *pofs = scratch<unsigned>("p0_offs", g.nps + 1);
@@ -946,7 +1131,7 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     P.nitems = P.p0_items[g.nps];
     P.items = scratch<Item>("items", std::max<int64_t>(P.nitems, 1));
     k_items_fill<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, g.ntiles, offs, ioffs,
-                                                     P.items);
+                                                     P.chunk, P.items);
 
     // ---- plane chunking against the grid memory budget
     const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
@@ -970,36 +1155,80 @@ static void allow_lds(const void *fn, size_t bytes) {
             hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
 }
 
+static ItemOrder item_order(uint32_t n) {
+    static const uint32_t primes[] = {7919u, 104729u, 1299709u, 15485863u, 179424673u};
+    if (const char *e = std::getenv("SDP_HIP_ITEM_ORDER"))
+        if (std::atoi(e) == 0) return ItemOrder{std::max<uint32_t>(n, 1u), 1u};
+    for (uint32_t p : primes)
+        if (n <= 1 || n % p != 0) return ItemOrder{std::max<uint32_t>(n, 1u), p};
+    return ItemOrder{n, 1u};
+}
+
+// waves per gridding workgroup (planes split across them); SDP_HIP_GRID_WAVES
+// overrides the default for experiments
+static int grid_waves(int W, bool do_w) {
+    if (!do_w) return 1;
+    const char *e = std::getenv("SDP_HIP_GRID_WAVES");
+    const int v = e ? std::atoi(e) : 2;
+    return (v == 1 || v == 2 || v == 4) && v <= W ? v : 2;
+}
+
+template <int W, bool WS, int NWV>
+static void launch_grid_n(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
+                          hipStream_t st) {
+    constexpr int NQ = WS ? W : 1;
+    const size_t lds = (size_t)((NQ + NWV - 1) / NWV * NWV) *
+                       TileShape<W, kTileCoarse>::PLANE * sizeof(float2);
+    allow_lds((const void *)k_grid_lds<W, WS, NWV>, lds);
+    k_grid_lds<W, WS, NWV><<<r.second - r.first, 64 * NWV, lds, st>>>(
+        P.g, P.recs, P.items + r.first, item_order(r.second - r.first), (float *)P.grid, p_lo,
+        p_hi);
+}
+
+template <int W, bool WS>
+static void launch_grid_reg(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
+                            hipStream_t st) {
+    const size_t lds = (size_t)(WS ? W : 1) * TileShape<W, kTileFine>::PLANE * sizeof(float2);
+    k_grid_reg<W, WS><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
+                                                          item_order(r.second - r.first),
+                                                          (float *)P.grid, p_lo, p_hi);
+}
+
 template <int W>
 static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
     const auto r = chunk_items(P, p_lo, p_hi);
     if (r.second <= r.first) return;
-    const size_t lds = (size_t)(P.g.do_w ? W : 1) * TileShape<W>::PLANE * sizeof(float2);
-    if (P.g.do_w) {
-        allow_lds((const void *)k_grid<W, true>, lds);
-        k_grid<W, true><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
-                                                            (float *)P.grid, p_lo, p_hi);
-    } else {
-        allow_lds((const void *)k_grid<W, false>, lds);
-        k_grid<W, false><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
-                                                             (float *)P.grid, p_lo, p_hi);
+    if (P.g.sub == kTileFine) {
+        if (P.g.do_w) return launch_grid_reg<W, true>(P, r, p_lo, p_hi, st);
+        return launch_grid_reg<W, false>(P, r, p_lo, p_hi, st);
     }
+    if (!P.g.do_w) return launch_grid_n<W, false, 1>(P, r, p_lo, p_hi, st);
+    switch (grid_waves(W, true)) {
+        case 1: return launch_grid_n<W, true, 1>(P, r, p_lo, p_hi, st);
+        case 4: return launch_grid_n<W, true, (W >= 4 ? 4 : 2)>(P, r, p_lo, p_hi, st);
+        default: return launch_grid_n<W, true, 2>(P, r, p_lo, p_hi, st);
+    }
+}
+
+template <int W, bool WS, int SUB>
+static void launch_degrid_n(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
+                            float2 *acc, hipStream_t st) {
+    const size_t lds = (size_t)(WS ? W : 1) * TileShape<W, SUB>::PLANE * sizeof(float2);
+    allow_lds((const void *)k_degrid<W, WS, SUB>, lds);
+    k_degrid<W, WS, SUB><<<r.second - r.first, 64, lds, st>>>(
+        P.g, P.recs, P.items + r.first, item_order(r.second - r.first), P.grid, p_lo, p_hi, acc);
 }
 
 template <int W>
 static void launch_degrid(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
     const auto r = chunk_items(P, p_lo, p_hi);
     if (r.second <= r.first) return;
-    const size_t lds = (size_t)(P.g.do_w ? W : 1) * TileShape<W>::PLANE * sizeof(float2);
-    if (P.g.do_w) {
-        allow_lds((const void *)k_degrid<W, true>, lds);
-        k_degrid<W, true><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
-                                                              P.grid, p_lo, p_hi, acc);
-    } else {
-        allow_lds((const void *)k_degrid<W, false>, lds);
-        k_degrid<W, false><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
-                                                               P.grid, p_lo, p_hi, acc);
+    if (P.g.sub == kTileFine) {
+        if (P.g.do_w) return launch_degrid_n<W, true, kTileFine>(P, r, p_lo, p_hi, acc, st);
+        return launch_degrid_n<W, false, kTileFine>(P, r, p_lo, p_hi, acc, st);
     }
+    if (P.g.do_w) return launch_degrid_n<W, true, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
+    return launch_degrid_n<W, false, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
 }
 
 #define SDP_W_DISPATCH(W, CALL) \
