@@ -500,6 +500,16 @@ __global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__re
     }
 }
 
+template <int NQ>
+__device__ __forceinline__ void acc_add(float (&ar)[NQ], float (&ai)[NQ], float vr, float vi,
+                                        const float (&kw)[NQ]) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        ar[q] = fmaf(vr, kw[q], ar[q]);
+        ai[q] = fmaf(vi, kw[q], ai[q]);
+    }
+}
+
 // Register gridder: one wave per work item (= one (p0, 2x2-cell bucket)
 // chunk).  Lane (kx, ky) is the (u, v) tap it accumulates; a record whose
 // footprint starts at cell origin o in {0,1}^2 of the bucket adds
@@ -511,14 +521,20 @@ __global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__re
 template <int W, bool WS>
 __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict__ recs,
                                                  const Item *__restrict__ items, ItemOrder ord,
-                                                 float *__restrict__ grid, int p_lo, int p_hi) {
+                                                 float *__restrict__ grid, int p_lo, int p_hi,
+                                                 int dbg) {
     constexpr int SUB = kTileFine;
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int R = TileShape<W, SUB>::R;
     constexpr int PS = TileShape<W, SUB>::PLANE;
     constexpr int NQ = WS ? W : 1;
     constexpr int NO = SUB * SUB;
+    static_assert(NO == 4, "origin select below assumes 2x2-cell buckets");
     const Item it = load_item(items, ord);
+    if (dbg & 4) {
+        if (it.b == 0xfffffffeu) grid[0] = 1.0f;  // keep the item load live
+        return;
+    }
     const int lane = threadIdx.x;
     const LaneRole<W> role(lane);
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
@@ -532,36 +548,42 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
         for (int q = 0; q < NQ; ++q) acc_r[o][q] = acc_i[o][q] = 0.0f;
     uint32_t used = 0;
 
-    for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+    const float tap_t = (float)(lane & 7);
+    for (uint32_t b0 = it.b; b0 < ((dbg & 2) ? it.b + 1 : it.e); b0 += 64) {
         const int n = (int)min(64u, it.e - b0);
         const VisRec my = recs[b0 + min(lane, n - 1)];
-        const BatchTaps bt = batch_taps(my, lane, ihw, bl);
+        // per-lane decode of the lane's own record: records are consumed in
+        // static groups of 8, so lanes >= n carry zero-valued padding records
+        const bool live = lane < n;
+        const float cre_l = live ? my.cre : 0.0f, cim_l = live ? my.cim : 0.0f;
+        const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jbase);
+#pragma unroll
+        for (int oo = 0; oo < NO; ++oo)
+            if (__ballot(live && o_l == oo)) used |= 1u << oo;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
-            const int rn = min(8, n - 8 * m);
-            for (int r = 0; r < rn; ++r) {
+            if (8 * m >= n) break;
+            // taps of this 8-record group: lane l holds tap (l % 8) of record 8m + l/8
+            const int src = 8 * m + (lane >> 3);
+            const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
+            const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
+            const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
                 const int k = 8 * m + r;
-                const float cre = lane_readf(my.cre, k), cim = lane_readf(my.cim, k);
-                const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)my.ij, k);
-                const int o = ((int)(ij & 0xffffu) - ibase) * SUB + ((int)(ij >> 16) - jbase);
-                const float ku = __shfl(bt.u[m], 8 * r + role.kx);
-                const float kv = __shfl(bt.v[m], 8 * r + role.ky);
+                const float cre = lane_readf(cre_l, k), cim = lane_readf(cim_l, k);
+                const int o = __builtin_amdgcn_readlane(o_l, k);
+                const float ku = __shfl(tu, 8 * r + role.kx);
+                const float kv = __shfl(tv, 8 * r + role.ky);
                 const float kk = ku * kv;
                 const float vr = cre * kk, vi = cim * kk;
                 float kw[NQ];
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(bt.w[m], 8 * r + q) : 1.0f;
-                used |= 1u << o;
+                for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
+                // origin select: uniform branches (one per origin set)
 #pragma unroll
-                for (int oo = 0; oo < NO; ++oo) {
-                    if (o == oo) {
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) {
-                            acc_r[oo][q] = fmaf(vr, kw[q], acc_r[oo][q]);
-                            acc_i[oo][q] = fmaf(vi, kw[q], acc_i[oo][q]);
-                        }
-                    }
-                }
+                for (int oo = 0; oo < NO; ++oo)
+                    if (o == oo) acc_add<NQ>(acc_r[oo], acc_i[oo], vr, vi, kw);
             }
         }
     }
@@ -583,24 +605,36 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
             }
         }
     }
-    const int cells = R * R;
-    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-    for (int c = lane; c < NQ * cells; c += 64) {
-        const int q = c / cells;
-        const int p = (int)it.p0 + q;
-        if (p < p_lo || p >= p_hi) continue;
-        const int rem = c - q * cells;
-        const int xl = rem / R, yl = rem - (rem / R) * R;
-        const float2 val = tile[q * PS + xl * R + yl];
-        if (val.x != 0.0f || val.y != 0.0f) {
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            float *dst =
-                grid + ((int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy) * 2;
-            atomicAdd(dst, val.x);
-            atomicAdd(dst + 1, val.y);
+    // flush: lane f of pass i handles float (64 i + f) of each plane's
+    // (2+W-1)^2 complex cells; a wave-instruction covers 3.5 contiguous
+    // 72-byte grid rows (re/im interleaved); zero floats are skipped.  The
+    // address of a float is the same in every plane, so it is computed once.
+    constexpr int FPP = R * R * 2;  // floats per plane
+    const int64_t plane_floats = (int64_t)g.ngx * g.ngy * 2;
+    const float *ftile = reinterpret_cast<const float *>(tile);
+#pragma unroll
+    for (int i0 = 0; i0 < FPP; i0 += 64) {
+        const int f = i0 + lane;
+        if (f >= FPP) break;
+        const int c = f >> 1;
+        const int xl = c / R, yl = c - (c / R) * R;
+        int gx = ibase + xl;
+        if (gx >= g.ngx) gx -= g.ngx;
+        int gy = jbase + yl;
+        if (gy >= g.ngy) gy -= g.ngy;
+        float *dst0 = grid + ((int64_t)gx * g.ngy + gy) * 2 + (f & 1);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int p = (int)it.p0 + q;
+            const float val = ftile[q * PS * 2 + f];
+            if (p >= p_lo && p < p_hi && val != 0.0f) {
+                float *dst = dst0 + (int64_t)(p - p_lo) * plane_floats;
+                if (dbg & 1) {
+                    if (val == 1.2345f) dst[0] = val;  // keep the flush live, no atomics
+                } else {
+                    atomicAdd(dst, val);
+                }
+            }
         }
     }
 }
@@ -1189,9 +1223,10 @@ template <int W, bool WS>
 static void launch_grid_reg(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
                             hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) * TileShape<W, kTileFine>::PLANE * sizeof(float2);
+    const int dbg = std::getenv("SDP_HIP_DBG") ? std::atoi(std::getenv("SDP_HIP_DBG")) : 0;
     k_grid_reg<W, WS><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
                                                           item_order(r.second - r.first),
-                                                          (float *)P.grid, p_lo, p_hi);
+                                                          (float *)P.grid, p_lo, p_hi, dbg);
 }
 
 template <int W>
