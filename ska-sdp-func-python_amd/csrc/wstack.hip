@@ -795,6 +795,127 @@ __global__ void k_screen_adj(Geo g, const double *__restrict__ dirty, int64_t sx
     }
 }
 
+// ---- transposed y-spectrum layout for the pruned 2-D FFT -------------
+// T[q][iy][kx] (iy = image row index 0..ny-1, i.e. ky = (iy - ny/2) mod ngy;
+// kx = 0..ngx-1) holds, per plane, the needed y-frequency columns of the grid
+// transposed so the x-direction transform runs over contiguous rows.
+constexpr int kTr = 32;
+
+// grid[q][x][ky(iy)] -> T[q][iy][x]; rows x outside [row_lo, row_hi) are
+// all-zero in the grid and are written as zeros without being read.
+__global__ __launch_bounds__(256) void k_tr_grid_to_t(Geo g, const float2 *__restrict__ grid,
+                                                      float2 *__restrict__ t, int row_lo,
+                                                      int row_hi) {
+    __shared__ float2 sm[kTr][kTr + 1];
+    const int x0 = blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
+    const int64_t plane = (int64_t)g.ngx * g.ngy, tplane = (int64_t)g.ny * g.ngx;
+    const bool live = x0 + kTr > row_lo && x0 < row_hi;
+    if (live) {
+        for (int r = threadIdx.y; r < kTr; r += 8) {
+            const int x = x0 + r, iy = i0 + threadIdx.x;
+            float2 v = make_float2(0.0f, 0.0f);
+            if (x >= row_lo && x < row_hi && iy < g.ny) {
+                const int Y = iy - g.ny / 2;
+                const int ky = Y < 0 ? Y + g.ngy : Y;
+                v = grid[q * plane + (int64_t)x * g.ngy + ky];
+            }
+            sm[r][threadIdx.x] = v;
+        }
+        __syncthreads();
+    }
+    for (int r = threadIdx.y; r < kTr; r += 8) {
+        const int iy = i0 + r, x = x0 + threadIdx.x;
+        if (iy < g.ny && x < g.ngx)
+            t[q * tplane + (int64_t)iy * g.ngx + x] = live ? sm[threadIdx.x][r] : make_float2(0.0f, 0.0f);
+    }
+}
+
+// T[q][iy][x] -> grid[q][x][ky(iy)] for the rows x in [row_lo, row_hi)
+__global__ __launch_bounds__(256) void k_tr_t_to_grid(Geo g, const float2 *__restrict__ t,
+                                                      float2 *__restrict__ grid, int row_lo,
+                                                      int row_hi) {
+    __shared__ float2 sm[kTr][kTr + 1];
+    const int x0 = row_lo + blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
+    const int64_t plane = (int64_t)g.ngx * g.ngy, tplane = (int64_t)g.ny * g.ngx;
+    for (int r = threadIdx.y; r < kTr; r += 8) {
+        const int iy = i0 + r, x = x0 + threadIdx.x;
+        sm[r][threadIdx.x] = (iy < g.ny && x < row_hi) ? t[q * tplane + (int64_t)iy * g.ngx + x]
+                                                       : make_float2(0.0f, 0.0f);
+    }
+    __syncthreads();
+    for (int r = threadIdx.y; r < kTr; r += 8) {
+        const int x = x0 + r, iy = i0 + threadIdx.x;
+        if (x < row_hi && iy < g.ny) {
+            const int Y = iy - g.ny / 2;
+            const int ky = Y < 0 ? Y + g.ngy : Y;
+            grid[q * plane + (int64_t)x * g.ngy + ky] = sm[threadIdx.x][r];
+        }
+    }
+}
+
+// w screens + grid correction reading the transposed spectrum (ix fastest:
+// coalesced T reads; RASCIL's transposed output (sx = 1) is coalesced too)
+__global__ void k_screen_fwd_t(Geo g, const float2 *__restrict__ t, int p_begin, int np,
+                               double *dirty, int64_t sx, int64_t sy, int accumulate,
+                               const double *__restrict__ tab) {
+    const int ix = blockIdx.x * blockDim.x + threadIdx.x;
+    const int iy = blockIdx.y;
+    if (ix >= g.nx) return;
+    const PixelGeom p = pixel_geom(g, ix, iy, tab);
+    double res = 0.0;
+    if (p.inside) {
+        const int64_t tplane = (int64_t)g.ny * g.ngx;
+        const float2 *src = t + (int64_t)iy * g.ngx + p.gx;
+        if (g.do_w) {
+            double acc = 0.0;
+            for (int q = 0; q < np; ++q) {
+                const float2 h = src[q * tplane];
+                double ph = (g.w0 + (p_begin + q) * g.dw) * p.s;
+                ph -= rint(ph);
+                float sn, cs;
+                sincospif((float)(2.0 * ph), &sn, &cs);
+                acc += (double)h.x * cs - (double)h.y * sn;
+            }
+            res = acc * p.corr;
+        } else {
+            res = (double)src[0].x * p.corr;
+        }
+    }
+    double *o = dirty + ix * sx + iy * sy;
+    *o = accumulate ? *o + res : res;
+}
+
+// adjoint: T[q][iy][kx] = screen(q) * corr * dirty for kx in the image's
+// x-frequencies, 0 for the other kx (full rows are written)
+__global__ void k_screen_adj_t(Geo g, const double *__restrict__ dirty, int64_t sx, int64_t sy,
+                               int p_begin, int np, float2 *__restrict__ t,
+                               const double *__restrict__ tab) {
+    const int kx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int iy = blockIdx.y;
+    if (kx >= g.ngx) return;
+    const int X = kx < g.ngx / 2 ? kx : kx - g.ngx;
+    const int ix = X + g.nx / 2;
+    const int64_t tplane = (int64_t)g.ny * g.ngx;
+    float2 *dst = t + (int64_t)iy * g.ngx + kx;
+    if (ix < 0 || ix >= g.nx) {
+        for (int q = 0; q < np; ++q) dst[q * tplane] = make_float2(0.0f, 0.0f);
+        return;
+    }
+    const PixelGeom p = pixel_geom(g, ix, iy, tab);
+    const double val = p.inside ? dirty[ix * sx + iy * sy] * p.corr : 0.0;
+    if (g.do_w) {
+        for (int q = 0; q < np; ++q) {
+            double ph = (g.w0 + (p_begin + q) * g.dw) * p.s;
+            ph -= rint(ph);
+            float sn, cs;
+            sincospif((float)(2.0 * ph), &sn, &cs);
+            dst[q * tplane] = make_float2((float)(val * cs), (float)(-val * sn));
+        }
+    } else {
+        dst[0] = make_float2((float)val, 0.0f);
+    }
+}
+
 __device__ __forceinline__ void store_vis(float2 *p, float2 v, int accumulate) {
     if (accumulate) {
         const float2 o = *p;
@@ -902,18 +1023,20 @@ static const double *phi_table(int W, double beta, hipStream_t stream) {
     return d;
 }
 
-static hipfftHandle fft_plan(int ngx, int ngy, int batch, hipStream_t stream) {
+// Cached hipFFT plans: 1-D c2c of length n over `batch` transforms whose
+// elements are `stride` apart and whose starts are `dist` apart.
+static hipfftHandle fft_plan_1d(int n, int stride, int dist, int batch, hipStream_t stream) {
     static std::mutex mu;
-    static std::map<std::tuple<int, int, int, int>, hipfftHandle> plans;
+    static std::map<std::tuple<int, int, int, int, int>, hipfftHandle> plans;
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_tuple(dev, ngx, ngy, batch);
+    const auto key = std::make_tuple(dev, n, stride, dist, batch);
     auto itp = plans.find(key);
     hipfftHandle h;
     if (itp == plans.end()) {
-        int n[2] = {ngx, ngy};
-        if (hipfftPlanMany(&h, 2, n, nullptr, 1, 0, nullptr, 1, 0, HIPFFT_C2C, batch) !=
+        int nn[1] = {n};
+        if (hipfftPlanMany(&h, 1, nn, nn, stride, dist, nn, stride, dist, HIPFFT_C2C, batch) !=
             HIPFFT_SUCCESS)
             throw Error(SDP_HIP_ERR_RUNTIME, "hipfftPlanMany failed");
         plans[key] = h;
@@ -974,8 +1097,10 @@ struct Plan {
     int64_t nitems = 0;
     std::vector<unsigned> p0_items;  // first item of every first-plane value
     int chunk_planes = 1;            // planes resident per pass
+    int row_lo = 0, row_hi = 0;      // grid rows (x) the visibilities reach
     unsigned chunk = kChunkMin;      // max records per work item
     float2 *grid = nullptr;
+    float2 *spec = nullptr;  // T[q][iy][kx]: transposed y-spectra (pruned FFT)
 };
 
 struct Inputs {
@@ -1167,11 +1292,24 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     k_items_fill<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, g.ntiles, offs, ioffs,
                                                      P.chunk, P.items);
 
+    // ---- grid rows reached by any footprint (centred storage)
+    {
+        const double amax = umax * in.px * g.ngx;
+        const int reach = (int)std::ceil(amax) + g.W + 1;
+        P.row_lo = std::max(0, g.ngx / 2 - reach);
+        P.row_hi = std::min(g.ngx, g.ngx / 2 + reach);
+        if (2 * reach >= g.ngx) {
+            P.row_lo = 0;
+            P.row_hi = g.ngx;
+        }
+    }
+
     // ---- plane chunking against the grid memory budget
-    const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
+    const size_t plane_bytes = ((size_t)g.ngx * g.ngy + (size_t)g.ny * g.ngx) * sizeof(float2);
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes() / plane_bytes);
     P.chunk_planes = std::min(cp, g.nplanes);
     P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy);
+    P.spec = scratch<float2>("spec", (size_t)P.chunk_planes * g.ny * g.ngx);
     return P;
 }
 
@@ -1291,11 +1429,39 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
     info->plane_chunk = P.chunk_planes;
 }
 
-static void fft_planes(const Plan &P, int np, int direction, hipStream_t st) {
-    hipfftHandle h = fft_plan(P.g.ngx, P.g.ngy, np, st);
-    if (hipfftExecC2C(h, (hipfftComplex *)P.grid, (hipfftComplex *)P.grid, direction) !=
-        HIPFFT_SUCCESS)
+// Pruned 2-D FFT of each resident plane.  The uv grid is non-zero only in
+// the row band [row_lo, row_hi) the visibilities reach (with cell < Nyquist
+// that band is a fraction of the padded grid), and only the ny columns
+// ky = (iy - ny/2) mod ngy of the y transform feed the image.  Strided
+// column transforms are slow in hipFFT, so the x transform runs on the
+// transposed layout T[q][iy][kx] (contiguous rows):
+//   backward: y-FFT of the band rows (in place, per plane) -> transpose the
+//             needed columns into T -> x-FFT of T rows (one batched call)
+//   forward:  x-FFT of T rows -> transpose back into the band rows of the
+//             (zeroed) grid -> y-FFT of the band rows
+static void exec_fft(hipfftHandle h, float2 *p, int direction) {
+    if (hipfftExecC2C(h, (hipfftComplex *)p, (hipfftComplex *)p, direction) != HIPFFT_SUCCESS)
         throw Error(SDP_HIP_ERR_RUNTIME, "hipfftExecC2C failed");
+}
+
+static void fft_rows_y(const Plan &P, int np, int direction, hipStream_t st) {
+    const Geo &g = P.g;
+    const int nrow = P.row_hi - P.row_lo;
+    if (nrow <= 0) return;
+    hipfftHandle hr = fft_plan_1d(g.ngy, 1, g.ngy, nrow, st);
+    for (int q = 0; q < np; ++q)
+        exec_fft(hr, P.grid + (size_t)q * g.ngx * g.ngy + (size_t)P.row_lo * g.ngy, direction);
+}
+
+static void fft_rows_x(const Plan &P, int np, int direction, hipStream_t st) {
+    const Geo &g = P.g;
+    hipfftHandle hc = fft_plan_1d(g.ngx, 1, g.ngx, np * g.ny, st);
+    exec_fft(hc, P.spec, direction);
+}
+
+static dim3 tr_grid(const Geo &g, int xrows, int np) {
+    return dim3((unsigned)((xrows + kTr - 1) / kTr), (unsigned)((g.ny + kTr - 1) / kTr),
+                (unsigned)np);
 }
 
 static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
@@ -1324,11 +1490,15 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
 #undef SDP_LAUNCH_GRID
         SDP_HIP_CHECK(hipGetLastError());
         t2.mark();
-        fft_planes(P, np, HIPFFT_BACKWARD, st);
+        fft_rows_y(P, np, HIPFFT_BACKWARD, st);
+        k_tr_grid_to_t<<<tr_grid(g, g.ngx, np), dim3(kTr, 8), 0, st>>>(g, P.grid, P.spec,
+                                                                       P.row_lo, P.row_hi);
+        SDP_HIP_CHECK(hipGetLastError());
+        fft_rows_x(P, np, HIPFFT_BACKWARD, st);
         t2.mark();
-        const dim3 grd(grid1d(g.ny, 256), g.nx);
-        k_screen_fwd<<<grd, 256, 0, st>>>(g, P.grid, p_lo, np, dirty, sx, sy,
-                                          (accumulate || p_lo > 0) ? 1 : 0, tab);
+        const dim3 grd(grid1d(g.nx, 256), g.ny);
+        k_screen_fwd_t<<<grd, 256, 0, st>>>(g, P.spec, p_lo, np, dirty, sx, sy,
+                                            (accumulate || p_lo > 0) ? 1 : 0, tab);
         SDP_HIP_CHECK(hipGetLastError());
         t2.mark();
         tzero += t2.ms(0, 1);
@@ -1377,11 +1547,16 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         t2.mark();
         SDP_HIP_CHECK(hipMemsetAsync(P.grid, 0, (size_t)np * plane_elems * sizeof(float2), st));
         t2.mark();
-        const dim3 grd(grid1d(g.ny, 256), g.nx);
-        k_screen_adj<<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_lo, np, P.grid, tab);
+        const dim3 grd(grid1d(g.ngx, 256), g.ny);
+        k_screen_adj_t<<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_lo, np, P.spec, tab);
         SDP_HIP_CHECK(hipGetLastError());
         t2.mark();
-        fft_planes(P, np, HIPFFT_FORWARD, st);
+        fft_rows_x(P, np, HIPFFT_FORWARD, st);
+        if (P.row_hi > P.row_lo)
+            k_tr_t_to_grid<<<tr_grid(g, P.row_hi - P.row_lo, np), dim3(kTr, 8), 0, st>>>(
+                g, P.spec, P.grid, P.row_lo, P.row_hi);
+        SDP_HIP_CHECK(hipGetLastError());
+        fft_rows_y(P, np, HIPFFT_FORWARD, st);
         t2.mark();
 #define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, acc, st)
         SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
