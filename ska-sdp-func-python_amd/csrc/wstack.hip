@@ -156,24 +156,23 @@ __device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c) {
 // ------------------------------------------------------------------------
 // kernels: geometry and bucketing
 // ------------------------------------------------------------------------
-__global__ void k_init_bounds(unsigned long long *out) {
-    out[0] = ~0ull;
-    out[1] = 0ull;
-    out[2] = 0ull;
-    out[3] = 0ull;
-}
+// uvw extent: per-block partials (no atomics), reduced by one block after
+constexpr int kBoundsBlocks = 1024;
 
-__global__ void k_bounds(const double *__restrict__ uvw, int64_t rs, int64_t nrow, double su,
-                         double slo, double shi, unsigned long long *out) {
+// raw extremes in metres (min/max of su*w, max |u|, max |v|); the host
+// scales them by the frequency range (w*s is monotonic in w for s > 0)
+__global__ __launch_bounds__(256) void k_bounds(const double *__restrict__ uvw, int64_t rs,
+                                                int64_t nrow, double su,
+                                                double *__restrict__ part) {
+    __shared__ double red[4][4];
     double wmn = 1e300, wmx = -1e300, umx = 0.0, vmx = 0.0;
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrow;
          r += (int64_t)gridDim.x * blockDim.x) {
         const double u = uvw[r * rs], v = uvw[r * rs + 1], w = su * uvw[r * rs + 2];
-        const double w1 = w * slo, w2 = w * shi;
-        wmn = fmin(wmn, fmin(w1, w2));
-        wmx = fmax(wmx, fmax(w1, w2));
-        umx = fmax(umx, fabs(u) * shi);
-        vmx = fmax(vmx, fabs(v) * shi);
+        wmn = fmin(wmn, w);
+        wmx = fmax(wmx, w);
+        umx = fmax(umx, fabs(u));
+        vmx = fmax(vmx, fabs(v));
     }
     for (int o = 32; o > 0; o >>= 1) {
         wmn = fmin(wmn, __shfl_xor(wmn, o));
@@ -181,12 +180,46 @@ __global__ void k_bounds(const double *__restrict__ uvw, int64_t rs, int64_t nro
         umx = fmax(umx, __shfl_xor(umx, o));
         vmx = fmax(vmx, __shfl_xor(vmx, o));
     }
+    const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
-        atomicMin(&out[0], ord_enc(wmn));
-        atomicMax(&out[1], ord_enc(wmx));
-        atomicMax(&out[2], ord_enc(umx));
-        atomicMax(&out[3], ord_enc(vmx));
+        red[0][wv] = wmn;
+        red[1][wv] = wmx;
+        red[2][wv] = umx;
+        red[3][wv] = vmx;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 4; ++k) {
+            red[0][0] = fmin(red[0][0], red[0][k]);
+            red[1][0] = fmax(red[1][0], red[1][k]);
+            red[2][0] = fmax(red[2][0], red[2][k]);
+            red[3][0] = fmax(red[3][0], red[3][k]);
+        }
+        for (int k = 0; k < 4; ++k) part[k * kBoundsBlocks + blockIdx.x] = red[k][0];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_bounds_final(int nblocks, const double *__restrict__ part,
+                                                      double *__restrict__ out) {
+    __shared__ double red[4][256];
+    double a[4] = {1e300, -1e300, 0.0, 0.0};
+    for (int b = threadIdx.x; b < nblocks; b += 256) {
+        a[0] = fmin(a[0], part[b]);
+        a[1] = fmax(a[1], part[kBoundsBlocks + b]);
+        a[2] = fmax(a[2], part[2 * kBoundsBlocks + b]);
+        a[3] = fmax(a[3], part[3 * kBoundsBlocks + b]);
+    }
+    for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = a[k];
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            red[0][threadIdx.x] = fmin(red[0][threadIdx.x], red[0][threadIdx.x + st]);
+            for (int k = 1; k < 4; ++k)
+                red[k][threadIdx.x] = fmax(red[k][threadIdx.x], red[k][threadIdx.x + st]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 4) out[threadIdx.x] = red[threadIdx.x][0];
 }
 
 // Wave-level run-length aggregation: consecutive lanes with equal keys share
@@ -743,58 +776,6 @@ __device__ __forceinline__ PixelGeom pixel_geom(const Geo &g, int ix, int iy,
     return p;
 }
 
-__global__ void k_screen_fwd(Geo g, const float2 *__restrict__ grid, int p_begin, int np,
-                             double *dirty, int64_t sx, int64_t sy, int accumulate,
-                             const double *__restrict__ tab) {
-    const int iy = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ix = blockIdx.y;
-    if (iy >= g.ny) return;
-    const PixelGeom p = pixel_geom(g, ix, iy, tab);
-    double res = 0.0;
-    if (p.inside) {
-        const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-        const float2 *src = grid + (int64_t)p.gx * g.ngy + p.gy;
-        if (g.do_w) {
-            double acc = 0.0;
-            for (int q = 0; q < np; ++q) {
-                const float2 h = src[q * plane_elems];
-                double ph = (g.w0 + (p_begin + q) * g.dw) * p.s;
-                ph -= rint(ph);
-                float sn, cs;
-                sincospif((float)(2.0 * ph), &sn, &cs);
-                acc += (double)h.x * cs - (double)h.y * sn;
-            }
-            res = acc * p.corr;
-        } else {
-            res = (double)src[0].x * p.corr;
-        }
-    }
-    double *o = dirty + ix * sx + iy * sy;
-    *o = accumulate ? *o + res : res;
-}
-
-__global__ void k_screen_adj(Geo g, const double *__restrict__ dirty, int64_t sx, int64_t sy,
-                             int p_begin, int np, float2 *grid, const double *__restrict__ tab) {
-    const int iy = blockIdx.x * blockDim.x + threadIdx.x;
-    const int ix = blockIdx.y;
-    if (iy >= g.ny) return;
-    const PixelGeom p = pixel_geom(g, ix, iy, tab);
-    const double val = p.inside ? dirty[ix * sx + iy * sy] * p.corr : 0.0;
-    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-    float2 *dst = grid + (int64_t)p.gx * g.ngy + p.gy;
-    if (g.do_w) {
-        for (int q = 0; q < np; ++q) {
-            double ph = (g.w0 + (p_begin + q) * g.dw) * p.s;
-            ph -= rint(ph);
-            float sn, cs;
-            sincospif((float)(2.0 * ph), &sn, &cs);
-            dst[q * plane_elems] = make_float2((float)(val * cs), (float)(-val * sn));
-        }
-    } else {
-        dst[0] = make_float2((float)val, 0.0f);
-    }
-}
-
 // ---- transposed y-spectrum layout for the pruned 2-D FFT -------------
 // T[q][iy][kx] (iy = image row index 0..ny-1, i.e. ky = (iy - ny/2) mod ngy;
 // kx = 0..ngx-1) holds, per plane, the needed y-frequency columns of the grid
@@ -1162,23 +1143,23 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     std::vector<double> f(in.nchan);
     SDP_HIP_CHECK(hipMemcpyAsync(f.data(), in.freq, in.nchan * sizeof(double),
                                  hipMemcpyDeviceToHost, st));
-    auto *bnd = scratch<unsigned long long>("bounds", 4);
-    k_init_bounds<<<1, 1, 0, st>>>(bnd);
+    double hb[4] = {0.0, 0.0, 0.0, 0.0};
+    if (in.nrow > 0) {
+        auto *part = scratch<double>("bounds_part", 4 * kBoundsBlocks);
+        auto *bnd = scratch<double>("bounds", 4);
+        const int nb = (int)std::min<int64_t>(grid1d(in.nrow, 256), kBoundsBlocks);
+        k_bounds<<<nb, 256, 0, st>>>(in.uvw, in.uvw_rs, in.nrow, g.su, part);
+        k_bounds_final<<<1, 256, 0, st>>>(nb, part, bnd);
+        SDP_HIP_CHECK(hipMemcpyAsync(hb, bnd, sizeof(hb), hipMemcpyDeviceToHost, st));
+    }
     SDP_HIP_CHECK(hipStreamSynchronize(st));
     const double fmin_ = *std::min_element(f.begin(), f.end());
     const double fmax_ = *std::max_element(f.begin(), f.end());
     SDP_REQUIRE(fmin_ > 0, "frequencies must be positive");
-    unsigned long long hb[4] = {~0ull, 0, 0, 0};
-    if (in.nrow > 0) {
-        k_bounds<<<std::min<unsigned>(grid1d(in.nrow, 256), 2048), 256, 0, st>>>(
-            in.uvw, in.uvw_rs, in.nrow, g.su, fmin_ / kCLight, fmax_ / kCLight, bnd);
-        SDP_HIP_CHECK(hipMemcpyAsync(hb, bnd, sizeof(hb), hipMemcpyDeviceToHost, st));
-        SDP_HIP_CHECK(hipStreamSynchronize(st));
-    }
-    const double wmin = in.nrow > 0 ? ord_dec(hb[0]) : 0.0;
-    const double wmax = in.nrow > 0 ? ord_dec(hb[1]) : 0.0;
-    const double umax = in.nrow > 0 ? ord_dec(hb[2]) : 0.0;
-    const double vmax = in.nrow > 0 ? ord_dec(hb[3]) : 0.0;
+    const double slo = fmin_ / kCLight, shi = fmax_ / kCLight;
+    const double wmin = in.nrow > 0 ? std::min(hb[0] * slo, hb[0] * shi) : 0.0;
+    const double wmax = in.nrow > 0 ? std::max(hb[1] * slo, hb[1] * shi) : 0.0;
+    const double umax = hb[2] * shi, vmax = hb[3] * shi;
     SDP_REQUIRE(std::isfinite(wmin) && std::isfinite(wmax) && std::isfinite(umax) &&
                     std::isfinite(vmax),
                 "non-finite uvw coordinates");
@@ -1459,6 +1440,16 @@ static void fft_rows_x(const Plan &P, int np, int direction, hipStream_t st) {
     exec_fft(hc, P.spec, direction);
 }
 
+// Only the row band [row_lo, row_hi) of a plane is ever written or read.
+static void zero_band(const Plan &P, int np, hipStream_t st) {
+    const Geo &g = P.g;
+    if (P.row_hi <= P.row_lo || np <= 0) return;
+    const size_t width = (size_t)(P.row_hi - P.row_lo) * g.ngy * sizeof(float2);
+    for (int q = 0; q < np; ++q)
+        SDP_HIP_CHECK(hipMemsetAsync(
+            P.grid + (size_t)q * g.ngx * g.ngy + (size_t)P.row_lo * g.ngy, 0, width, st));
+}
+
 static dim3 tr_grid(const Geo &g, int xrows, int np) {
     return dim3((unsigned)((xrows + kTr - 1) / kTr), (unsigned)((g.ny + kTr - 1) / kTr),
                 (unsigned)np);
@@ -1483,7 +1474,7 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
         const int np = p_hi - p_lo;
         StageTimer t2(st);
         t2.mark();
-        SDP_HIP_CHECK(hipMemsetAsync(P.grid, 0, (size_t)np * plane_elems * sizeof(float2), st));
+        zero_band(P, np, st);
         t2.mark();
 #define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, p_lo, p_hi, st)
         SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
@@ -1545,7 +1536,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         const int np = p_hi - p_lo;
         StageTimer t2(st);
         t2.mark();
-        SDP_HIP_CHECK(hipMemsetAsync(P.grid, 0, (size_t)np * plane_elems * sizeof(float2), st));
+        zero_band(P, np, st);
         t2.mark();
         const dim3 grd(grid1d(g.ngx, 256), g.ny);
         k_screen_adj_t<<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_lo, np, P.spec, tab);
