@@ -53,14 +53,14 @@ def parse():
     ap.add_argument("--nchan", type=int, default=NCHAN_PER_GPU, help="channels per GPU")
     ap.add_argument("--ntimes", type=int, default=NTIMES)
     ap.add_argument("--npix", type=int, default=NPIX)
-    ap.add_argument("--cpu-chans", type=int, default=1,
+    ap.add_argument("--cpu-chans", type=int, default=8,
                     help="channels in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_k_grid.json"))
     return ap.parse_args()
 
 
 def cpu_baseline(args, umax, nchan_total):
-    """oracle/wgrid_cpu.c on a bounded C2 sample (1 channel of the 64 by default):
+    """oracle/wgrid_cpu.c on a bounded C2 sample (8 channels of the 64 by default):
     the sample's gridding time is scaled to the full visibility count and its
     per-plane FFT + w-screen time is counted once (the full job has the same
     planes), giving the CPU's full-C2 invert rate."""
@@ -171,7 +171,8 @@ def main():
             traffic = json.load(f).get("bytes_per_launch")
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "k_grid<8,true>", "kernel_ms": round(ms_grid / launches, 4),
+            "kernel": (f"k_grid_reg<{info['support']},true>" if info["bucket"] == 2
+                       else f"k_grid_lds<{info['support']},true,2>"), "kernel_ms": round(ms_grid / launches, 4),
             "alg_bytes_per_launch": int(alg_bytes / launches)}
 
     cpu = None

@@ -52,6 +52,8 @@ typedef struct sdp_hip_wgrid_info {
     int64_t nitems;       /* gridding work items launched                   */
     int plane_chunk;      /* planes resident per pass                       */
     float ms_prep, ms_grid, ms_fft, ms_screen; /* stage times if timing on  */
+    int bucket;           /* bucket edge in cells: 2 = register gridder,
+                             16 = LDS-tile gridder (large grids)            */
 } sdp_hip_wgrid_info;
 
 /* Library/ABI version and a device probe. */

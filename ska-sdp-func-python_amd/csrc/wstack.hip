@@ -1408,6 +1408,7 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
     info->nvis_used = P.nrec;
     info->nitems = P.nitems;
     info->plane_chunk = P.chunk_planes;
+    info->bucket = P.g.sub;
 }
 
 // Pruned 2-D FFT of each resident plane.  The uv grid is non-zero only in

@@ -51,6 +51,7 @@ class WGridInfo(ctypes.Structure):
         ("ms_grid", ctypes.c_float),
         ("ms_fft", ctypes.c_float),
         ("ms_screen", ctypes.c_float),
+        ("bucket", c_int),
     ]
 
     def as_dict(self):
