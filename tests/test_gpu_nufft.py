@@ -34,10 +34,19 @@ def _problem(seed, nrow=300, nchan=3, umax=2000.0, frac=0.45):
     return uvw, freq, ms, wgt, frac / umax
 
 
+@pytest.fixture(params=["fine", "coarse"])
+def bucket(request, monkeypatch):
+    """Both gridders: 2x2-cell buckets (register gridder, the default at these
+    sizes) and 16x16-cell buckets (LDS-tile gridder used for very large grids)."""
+    if request.param == "coarse":
+        monkeypatch.setenv("SDP_HIP_BUCKET", "16")
+    return request.param
+
+
 @pytest.mark.parametrize("dow", [False, True])
 @pytest.mark.parametrize("vdt", [torch.complex64, torch.complex128])
 @pytest.mark.parametrize("flip", [False, True])
-def test_ms2dirty_matches_exact(dow, vdt, flip):
+def test_ms2dirty_matches_exact(dow, vdt, flip, bucket):
     from ska_sdp_func_python_amd import kernels
     uvw, freq, ms, wgt, cell = _problem(1)
     npix = 64
@@ -46,11 +55,12 @@ def test_ms2dirty_matches_exact(dow, vdt, flip):
     out, info = kernels.ms2dirty(T(uvw), T(freq), T(ms, vdt), T(wgt), npix, 48 + 16 * dow, cell,
                                  cell * 0.9, 1e-7, dow, flip_uw=flip)
     assert info["support"] == 8
+    assert info["bucket"] == (16 if bucket == "coarse" else 2)
     assert rel_rms(out.cpu().numpy(), ex) < TOL
 
 
 @pytest.mark.parametrize("dow", [False, True])
-def test_dirty2ms_matches_exact(dow):
+def test_dirty2ms_matches_exact(dow, bucket):
     from ska_sdp_func_python_amd import kernels
     uvw, freq, _, wgt, cell = _problem(2)
     rng = np.random.default_rng(5)
@@ -95,7 +105,7 @@ def test_nyquist_violation_raises():
 
 
 @pytest.mark.parametrize("npix,nrow,nchan", [(1024, 20000, 16)])
-def test_adjointness_at_scale(npix, nrow, nchan):
+def test_adjointness_at_scale(npix, nrow, nchan, bucket):
     """<A x, y> == <x, A^H y> for the w-stacked pair at a size the oracle cannot
     sum directly (size-independent property)."""
     from ska_sdp_func_python_amd import kernels
@@ -110,7 +120,7 @@ def test_adjointness_at_scale(npix, nrow, nchan):
     assert abs(lhs - rhs) / abs(lhs) < 1e-5
 
 
-def test_linearity_at_scale():
+def test_linearity_at_scale(bucket):
     from ska_sdp_func_python_amd import kernels
     uvw, freq, ms, wgt, cell = _problem(8, nrow=30000, nchan=8, umax=2e4)
     a, _ = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), 512, 512, cell, cell, 1e-7, True)
@@ -165,3 +175,22 @@ def test_invert_predict_round_trip_point_source():
     np.testing.assert_allclose(pv.vis.data, 1.0, atol=1e-5)
     psf, sw = invert_visibility(pv, im, dopsf=True, context="ng")
     assert abs(psf["pixels"].data[0, 0, 128, 128] - 1.0) < 1e-5
+
+
+def test_plane_chunking_matches_resident(bucket, monkeypatch):
+    """A grid budget of one plane forces plane-by-plane passes (the path very
+    large grids take); results equal the all-planes-resident ones."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(9, nrow=3000, nchan=4, umax=4000.0)
+    args = (T(uvw), T(freq), T(ms), T(wgt), 256, 256, cell, cell, 1e-7, True)
+    full, info = kernels.ms2dirty(*args)
+    img = torch.randn(256, 256, dtype=torch.float64, device=dev())
+    vfull, _ = kernels.dirty2ms(T(uvw), T(freq), img, T(wgt), cell, cell, 1e-7, True,
+                                vis_dtype=torch.complex128)
+    monkeypatch.setenv("SDP_HIP_GRID_BUDGET_GB", "0.0001")
+    part, info2 = kernels.ms2dirty(*args)
+    vpart, _ = kernels.dirty2ms(T(uvw), T(freq), img, T(wgt), cell, cell, 1e-7, True,
+                                vis_dtype=torch.complex128)
+    assert info["nplanes"] > 2 and info2["plane_chunk"] == 1
+    assert rel_rms(part.cpu().numpy(), full.cpu().numpy()) < 1e-6
+    assert rel_rms(vpart.cpu().numpy(), vfull.cpu().numpy()) < 1e-6
