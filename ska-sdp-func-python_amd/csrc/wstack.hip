@@ -6,10 +6,11 @@
 // Pipeline (one stream, two host syncs per call):
 //   k_bounds       fp64 w range / uv extent over the rows
 //   k_bucket<0>    per-visibility fp64 grid coordinates -> bucket key
-//                  (first w plane p0, 16x16 uv tile), wave-level run-length
-//                  histogram (one atomic per run of equal keys)
+//                  (first w plane p0, 2x2 or 16x16 uv cells) and rank in the
+//                  bucket from a wave-level run-length histogram (one atomic
+//                  per run of equal keys)
 //   scan           hipcub exclusive sum over buckets
-//   k_bucket<1>    32-byte visibility records in bucket order
+//   k_bucket<1>    32-byte visibility records at offs[key] + rank (no atomics)
 //   k_items_*      work items = one bucket, split into <= chunk records
 //   per plane chunk (all planes resident when they fit the budget):
 //     k_grid       one workgroup per item owning an LDS tile of W planes
@@ -247,12 +248,17 @@ __device__ __forceinline__ float2 load_vis(const double2 *p) {
     return make_float2((float)v.x, (float)v.y);
 }
 
+// Two passes over the visibilities.  Rank pass (kScatter = false): fp64
+// coordinates -> bucket key, and the visibility's rank inside its bucket
+// from a run-aggregated atomicAdd on the histogram; (key, rank) is stored.
+// Scatter pass: position = offs[key] + rank -- no atomics -- and the 32-byte
+// record is written there.  Invalid visibilities carry key 0xffffffff.
 template <class VT, bool kScatter, bool kGrid>
 __global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
                          const double *__restrict__ freq, const VT *__restrict__ vis,
                          int64_t vrs, int64_t vcs, const float *__restrict__ wgt, int64_t wrs,
-                         int64_t wcs, unsigned *counter, VisRec *__restrict__ recs,
-                         unsigned long long *nbad) {
+                         int64_t wcs, unsigned *counter, uint2 *__restrict__ kr,
+                         VisRec *__restrict__ recs, unsigned long long *nbad) {
     const int64_t nvis = g.nrow * (int64_t)g.nchan;
     const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     bool valid = v < nvis;
@@ -261,22 +267,35 @@ __global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
     float wt = 1.0f;
     Coord c;
     c.ok = false;
-    if (valid) {
+    uint2 mine = make_uint2(0xffffffffu, 0u);
+    if (kScatter) {
+        if (!valid) return;
+        mine = kr[v];
+        if (mine.x == 0xffffffffu) return;
         row = v / g.nchan;
         chan = (int)(v - row * g.nchan);
         if (wgt) wt = wgt[row * wrs + chan * wcs];
-        valid = (wt != 0.0f);
+        c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
+    } else {
         if (valid) {
-            c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
-            if (!c.ok) {
-                valid = false;
-                if (!kScatter) atomicAdd(nbad, 1ull);
+            row = v / g.nchan;
+            chan = (int)(v - row * g.nchan);
+            if (wgt) wt = wgt[row * wrs + chan * wcs];
+            valid = (wt != 0.0f);
+            if (valid) {
+                c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
+                if (!c.ok) {
+                    valid = false;
+                    atomicAdd(nbad, 1ull);
+                }
             }
         }
+        const unsigned key = valid ? coord_key(g, c) : 0xffffffffu;
+        const unsigned rank = run_reserve<true>(key, valid, counter);
+        if (v < nvis) kr[v] = make_uint2(key, rank);
+        return;
     }
-    const unsigned key = valid ? coord_key(g, c) : 0xffffffffu;
-    const unsigned pos = run_reserve<kScatter>(key, valid, counter);
-    if (!kScatter || !valid) return;
+    const unsigned pos = counter[mine.x] + mine.y;
     float cr = wt, ci = 0.0f;
     if (kGrid) {
         const float2 x = vis ? load_vis(vis + row * vrs + chan * vcs) : make_float2(1.0f, 0.0f);
@@ -1207,26 +1226,27 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     SDP_HIP_CHECK(hipMemsetAsync(nbad, 0, sizeof(unsigned long long), st));
 
     const unsigned nb = grid1d(nvis, 256);
+    uint2 *kr = scratch<uint2>("key_rank", std::max<int64_t>(nvis, 1));
     auto launch_bucket = [&](auto scatter_tag, unsigned *counter, VisRec *recs) {
         constexpr bool S = decltype(scatter_tag)::value;
         if (in.vis_dtype == SDP_HIP_C128) {
             if (grid_mode)
                 k_bucket<double2, S, true><<<nb, 256, 0, st>>>(
                     g, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis, in.vrs, in.vcs,
-                    in.wgt, in.wrs, in.wcs, counter, recs, nbad);
+                    in.wgt, in.wrs, in.wcs, counter, kr, recs, nbad);
             else
                 k_bucket<double2, S, false><<<nb, 256, 0, st>>>(
                     g, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs, in.wcs,
-                    counter, recs, nbad);
+                    counter, kr, recs, nbad);
         } else {
             if (grid_mode)
                 k_bucket<float2, S, true><<<nb, 256, 0, st>>>(
                     g, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis, in.vrs, in.vcs,
-                    in.wgt, in.wrs, in.wcs, counter, recs, nbad);
+                    in.wgt, in.wrs, in.wcs, counter, kr, recs, nbad);
             else
                 k_bucket<float2, S, false><<<nb, 256, 0, st>>>(
                     g, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs, in.wcs,
-                    counter, recs, nbad);
+                    counter, kr, recs, nbad);
         }
     };
     if (nvis > 0) launch_bucket(std::false_type{}, hist, nullptr);
@@ -1239,11 +1259,8 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     void *tmp = scratch<char>("scan_tmp", tmp_bytes + 16);
     size_t tb = tmp_bytes + 16;
     SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, offs, (int)(nkeys + 1), st));
-    // reuse hist as the scatter cursor
-    SDP_HIP_CHECK(hipMemcpyAsync(hist, offs, (nkeys + 1) * sizeof(unsigned),
-                                 hipMemcpyDeviceToDevice, st));
     P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
-    if (nvis > 0) launch_bucket(std::true_type{}, hist, P.recs);
+    if (nvis > 0) launch_bucket(std::true_type{}, offs, P.recs);
 
     // ---- work items (p0-major, so a first-plane range is a contiguous item range)
     SDP_HIP_CHECK(hipMemsetAsync(nch + nkeys, 0, sizeof(unsigned), st));
