@@ -200,27 +200,48 @@ __global__ __launch_bounds__(256) void k_bounds(const double *__restrict__ uvw, 
     }
 }
 
+// out = {min su*w, max su*w, max|u|, max|v|, min freq, max freq}
 __global__ __launch_bounds__(256) void k_bounds_final(int nblocks, const double *__restrict__ part,
+                                                      const double *__restrict__ freq, int nchan,
                                                       double *__restrict__ out) {
-    __shared__ double red[4][256];
-    double a[4] = {1e300, -1e300, 0.0, 0.0};
+    __shared__ double red[6][256];
+    double a[6] = {1e300, -1e300, 0.0, 0.0, 1e300, -1e300};
     for (int b = threadIdx.x; b < nblocks; b += 256) {
         a[0] = fmin(a[0], part[b]);
         a[1] = fmax(a[1], part[kBoundsBlocks + b]);
         a[2] = fmax(a[2], part[2 * kBoundsBlocks + b]);
         a[3] = fmax(a[3], part[3 * kBoundsBlocks + b]);
     }
-    for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = a[k];
+    for (int c = threadIdx.x; c < nchan; c += 256) {
+        a[4] = fmin(a[4], freq[c]);
+        a[5] = fmax(a[5], freq[c]);
+    }
+    for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = a[k];
     __syncthreads();
     for (int st = 128; st > 0; st >>= 1) {
         if (threadIdx.x < st) {
-            red[0][threadIdx.x] = fmin(red[0][threadIdx.x], red[0][threadIdx.x + st]);
-            for (int k = 1; k < 4; ++k)
-                red[k][threadIdx.x] = fmax(red[k][threadIdx.x], red[k][threadIdx.x + st]);
+            const int t = threadIdx.x;
+            red[0][t] = fmin(red[0][t], red[0][t + st]);
+            red[4][t] = fmin(red[4][t], red[4][t + st]);
+            for (int k : {1, 2, 3, 5}) red[k][t] = fmax(red[k][t], red[k][t + st]);
         }
         __syncthreads();
     }
-    if (threadIdx.x < 4) out[threadIdx.x] = red[threadIdx.x][0];
+    if (threadIdx.x < 6) out[threadIdx.x] = red[threadIdx.x][0];
+}
+
+// plan metadata in one buffer for one D2H copy: {nbad (2 words), nrec,
+// first item of each first-plane value [nps + 1]}
+__global__ void k_plan_meta(const unsigned long long *__restrict__ nbad,
+                            const unsigned *__restrict__ nrec, const unsigned *__restrict__ ioffs,
+                            int ntiles, int nps, unsigned *__restrict__ meta) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) {
+        meta[0] = (unsigned)(*nbad & 0xffffffffull);
+        meta[1] = (unsigned)(*nbad >> 32);
+        meta[2] = *nrec;
+    }
+    if (k <= nps) meta[3 + k] = ioffs[(size_t)k * ntiles];
 }
 
 // Wave-level run-length aggregation: consecutive lanes with equal keys share
@@ -350,11 +371,6 @@ __global__ void k_items_fill(int64_t nkeys, int ntiles, const unsigned *__restri
     }
 }
 
-__global__ void k_gather_p0_offsets(const unsigned *__restrict__ ioffs, int ntiles, int nps,
-                                    unsigned *out) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k <= nps) out[k] = ioffs[(size_t)k * ntiles];
-}
 
 // ------------------------------------------------------------------------
 // kernels: gridding / degridding (the hot loops)
@@ -1062,6 +1078,23 @@ static int kernel_support(double epsilon) {
     return std::min(std::max(W, 2), kMaxW);
 }
 
+// Pinned host staging for the plan's small device->host reads (pageable
+// destinations go through a slow staging copy).  Byte offset `off` into a
+// per-device 1 MiB buffer; the plan uses [0, 64) and [64, ...).
+template <class T>
+static T *pinned_host(size_t off, size_t count) {
+    static std::mutex mu;
+    static std::map<int, char *> bufs;
+    constexpr size_t kBytes = 1 << 20;
+    SDP_REQUIRE(off + count * sizeof(T) <= kBytes, "plan metadata too large");
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    char *&b = bufs[dev];
+    if (!b) SDP_HIP_CHECK(hipHostMalloc((void **)&b, kBytes, hipHostMallocDefault));
+    return reinterpret_cast<T *>(b + off);
+}
+
 static bool g_stage_timing = false;
 
 struct StageTimer {
@@ -1159,21 +1192,17 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.sub = kTileCoarse;  // refined below once the plane count is known
 
     // frequency extremes (host) and uvw bounds (device)
-    std::vector<double> f(in.nchan);
-    SDP_HIP_CHECK(hipMemcpyAsync(f.data(), in.freq, in.nchan * sizeof(double),
-                                 hipMemcpyDeviceToHost, st));
-    double hb[4] = {0.0, 0.0, 0.0, 0.0};
-    if (in.nrow > 0) {
+    double *hb = pinned_host<double>(0, 6);
+    {
         auto *part = scratch<double>("bounds_part", 4 * kBoundsBlocks);
-        auto *bnd = scratch<double>("bounds", 4);
-        const int nb = (int)std::min<int64_t>(grid1d(in.nrow, 256), kBoundsBlocks);
+        auto *bnd = scratch<double>("bounds", 6);
+        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(grid1d(in.nrow, 256), kBoundsBlocks));
         k_bounds<<<nb, 256, 0, st>>>(in.uvw, in.uvw_rs, in.nrow, g.su, part);
-        k_bounds_final<<<1, 256, 0, st>>>(nb, part, bnd);
-        SDP_HIP_CHECK(hipMemcpyAsync(hb, bnd, sizeof(hb), hipMemcpyDeviceToHost, st));
+        k_bounds_final<<<1, 256, 0, st>>>(nb, part, in.freq, in.nchan, bnd);
+        SDP_HIP_CHECK(hipMemcpyAsync(hb, bnd, 6 * sizeof(double), hipMemcpyDeviceToHost, st));
+        SDP_HIP_CHECK(hipStreamSynchronize(st));
     }
-    SDP_HIP_CHECK(hipStreamSynchronize(st));
-    const double fmin_ = *std::min_element(f.begin(), f.end());
-    const double fmax_ = *std::max_element(f.begin(), f.end());
+    const double fmin_ = hb[4], fmax_ = hb[5];
     SDP_REQUIRE(fmin_ > 0, "frequencies must be positive");
     const double slo = fmin_ / kCLight, shi = fmax_ / kCLight;
     const double wmin = in.nrow > 0 ? std::min(hb[0] * slo, hb[0] * shi) : 0.0;
@@ -1272,17 +1301,16 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     k_items_count<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, offs, P.chunk, nch);
     tb = tmp_bytes + 16;
     SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nch, ioffs, (int)(nkeys + 1), st));
-    unsigned *pofs = scratch<unsigned>("p0_offs", g.nps + 1);
-    k_gather_p0_offsets<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(ioffs, g.ntiles, g.nps, pofs);
-    P.p0_items.resize(g.nps + 1);
-    unsigned long long nbad_h = 0;
-    unsigned nrec_h = 0;
-    SDP_HIP_CHECK(hipMemcpyAsync(P.p0_items.data(), pofs, (g.nps + 1) * sizeof(unsigned),
-                                 hipMemcpyDeviceToHost, st));
-    SDP_HIP_CHECK(hipMemcpyAsync(&nbad_h, nbad, sizeof(nbad_h), hipMemcpyDeviceToHost, st));
-    SDP_HIP_CHECK(
-        hipMemcpyAsync(&nrec_h, offs + nkeys, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    unsigned *meta = scratch<unsigned>("plan_meta", g.nps + 4);
+    k_plan_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(nbad, offs + nkeys, ioffs, g.ntiles, g.nps,
+                                                      meta);
+    unsigned *hm = pinned_host<unsigned>(64, g.nps + 4);
+    SDP_HIP_CHECK(hipMemcpyAsync(hm, meta, (g.nps + 4) * sizeof(unsigned), hipMemcpyDeviceToHost,
+                                 st));
     SDP_HIP_CHECK(hipStreamSynchronize(st));
+    const unsigned long long nbad_h = (unsigned long long)hm[0] | ((unsigned long long)hm[1] << 32);
+    const unsigned nrec_h = hm[2];
+    P.p0_items.assign(hm + 3, hm + 3 + g.nps + 1);
     SDP_REQUIRE(nbad_h == 0, "visibilities outside the padded grid");
     P.nrec = nrec_h;
     P.nitems = P.p0_items[g.nps];
