@@ -45,6 +45,7 @@ namespace wstack {
 constexpr double kCLight = 299792458.0;
 constexpr int kTileCoarse = 16;  // bucket edge (cells) of the LDS-tile gridder
 constexpr int kTileFine = 2;     // bucket edge (cells) of the register gridder
+constexpr int kGroupFine = 4;    // fine buckets per work-item group (along y)
 constexpr int kGridAlign = 16;   // padded grid edges are multiples of this
 // fine buckets are used while the dense (p0, 2x2-cell) histogram stays small
 constexpr int64_t kMaxFineKeys = (int64_t)1 << 27;
@@ -62,6 +63,7 @@ struct Geo {
     int do_w, nplanes, nps;  // nps = number of distinct first planes
     double w0, dw, s0;
     int sub, nty, ntiles;  // bucket edge in cells, buckets per grid column, buckets
+    int grp;               // consecutive buckets (along y) per work-item group
     double su;  // sign applied to u and w (-1 with SDP_HIP_FLIP_UW)
     int nchan;
     int64_t nrow;
@@ -234,14 +236,14 @@ __global__ __launch_bounds__(256) void k_bounds_final(int nblocks, const double 
 // first item of each first-plane value [nps + 1]}
 __global__ void k_plan_meta(const unsigned long long *__restrict__ nbad,
                             const unsigned *__restrict__ nrec, const unsigned *__restrict__ ioffs,
-                            int ntiles, int nps, unsigned *__restrict__ meta) {
+                            int groups_per_plane, int nps, unsigned *__restrict__ meta) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0) {
         meta[0] = (unsigned)(*nbad & 0xffffffffull);
         meta[1] = (unsigned)(*nbad >> 32);
         meta[2] = *nrec;
     }
-    if (k <= nps) meta[3 + k] = ioffs[(size_t)k * ntiles];
+    if (k <= nps) meta[3 + k] = ioffs[(size_t)k * groups_per_plane];
 }
 
 // Wave-level run-length aggregation: consecutive lanes with equal keys share
@@ -345,22 +347,25 @@ __global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
     recs[pos] = rec;
 }
 
-__global__ void k_items_count(int64_t nkeys, const unsigned *__restrict__ offs, unsigned chunk,
-                              unsigned *nch) {
+// work items: a group of `grp` consecutive buckets (same p0, same x) is
+// split into chunks of <= chunk records
+__global__ void k_items_count(int64_t ngroups, int grp, const unsigned *__restrict__ offs,
+                              unsigned chunk, unsigned *nch) {
     const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (k >= nkeys) return;
-    const unsigned n = offs[k + 1] - offs[k];
+    if (k >= ngroups) return;
+    const unsigned n = offs[(k + 1) * grp] - offs[k * grp];
     nch[k] = (n + chunk - 1) / chunk;
 }
 
-__global__ void k_items_fill(int64_t nkeys, int ntiles, const unsigned *__restrict__ offs,
-                             const unsigned *__restrict__ ioffs, unsigned chunk, Item *items) {
+__global__ void k_items_fill(int64_t ngroups, int grp, int groups_per_plane,
+                             const unsigned *__restrict__ offs, const unsigned *__restrict__ ioffs,
+                             unsigned chunk, Item *items) {
     const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (k >= nkeys) return;
-    const unsigned b = offs[k], e = offs[k + 1];
+    if (k >= ngroups) return;
+    const unsigned b = offs[k * grp], e = offs[(k + 1) * grp];
     unsigned o = ioffs[k];
-    const uint32_t p0 = (uint32_t)(k / ntiles);
-    const uint32_t tile = (uint32_t)(k - (int64_t)p0 * ntiles);
+    const uint32_t p0 = (uint32_t)(k / groups_per_plane);
+    const uint32_t tile = (uint32_t)(k - (int64_t)p0 * groups_per_plane);
     for (unsigned s = b; s < e; s += chunk) {
         Item x;
         x.b = s;
@@ -371,15 +376,16 @@ __global__ void k_items_fill(int64_t nkeys, int ntiles, const unsigned *__restri
     }
 }
 
-
 // ------------------------------------------------------------------------
 // kernels: gridding / degridding (the hot loops)
 // ------------------------------------------------------------------------
-template <int W, int SUB>
+// LDS tile of an SX x SY-cell work-item region plus the W-1 footprint halo
+template <int W, int SX, int SY = SX>
 struct TileShape {
-    static constexpr int R = SUB + W - 1;                         // bucket + halo
-    static constexpr int PITCH = SUB == kTileCoarse ? kPitch : R;  // LDS row pitch
-    static constexpr int PLANE = R * PITCH;  // complex values per plane in LDS
+    static constexpr int RX = SX + W - 1, RY = SY + W - 1;
+    static constexpr int R = RX;                                    // (square tiles)
+    static constexpr int PITCH = SX == kTileCoarse ? kPitch : RY;  // LDS row pitch
+    static constexpr int PLANE = RX * PITCH;  // complex values per plane in LDS
 };
 
 // Work items are visited in a strided order (stride coprime with the item
@@ -578,23 +584,29 @@ __device__ __forceinline__ void acc_add(float (&ar)[NQ], float (&ai)[NQ], float 
     }
 }
 
-// Register gridder: one wave per work item (= one (p0, 2x2-cell bucket)
-// chunk).  Lane (kx, ky) is the (u, v) tap it accumulates; a record whose
-// footprint starts at cell origin o in {0,1}^2 of the bucket adds
-// vis * ku * kv * kw[q] into VGPR accumulator acc[o][q] (q = w plane), so the
-// per-record work is FMAs on registers -- no LDS traffic except two
-// ds_bpermute for the u / v taps.  At the end the <= 4 origin sets are
-// combined in a (2+W-1)^2 x W LDS tile and flushed with global float atomics
-// (zero cells skipped).  Taps come from batch_taps() (all lanes busy).
+// Register gridder: one wave per work item = a chunk of the records of a
+// group of kGroupFine consecutive 2x2-cell buckets (same first plane p0,
+// same x), i.e. a 2 x 8-cell region.  Lane (kx, ky) is the (u, v) tap it
+// accumulates.  Bucket by bucket, a record whose footprint starts at origin
+// o in {0,1}^2 of its bucket adds vis * ku * kv * kw[q] into the VGPR
+// accumulator acc[o][q] (q = w plane): per-record work is FMAs on registers,
+// with no LDS traffic except two ds_bpermute for the u / v taps.  At the end
+// of each bucket the <= 4 origin sets are added into the group's
+// (2+W-1) x (8+W-1) x W LDS tile; the tile is flushed once per item with
+// global float atomics (zero cells skipped), so neighbouring buckets share
+// one flush of their overlapping halos.  Records of a bucket are consumed in
+// static groups of 8 (zero-valued padding at the end of a bucket).
 template <int W, bool WS>
 __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict__ recs,
                                                  const Item *__restrict__ items, ItemOrder ord,
+                                                 const unsigned *__restrict__ offs,
                                                  float *__restrict__ grid, int p_lo, int p_hi,
                                                  int dbg) {
     constexpr int SUB = kTileFine;
+    constexpr int GRP = kGroupFine;
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int R = TileShape<W, SUB>::R;
-    constexpr int PS = TileShape<W, SUB>::PLANE;
+    using TS = TileShape<W, SUB, SUB * GRP>;
+    constexpr int RX = TS::RX, RY = TS::RY, PS = TS::PLANE;
     constexpr int NQ = WS ? W : 1;
     constexpr int NO = SUB * SUB;
     static_assert(NO == 4, "origin select below assumes 2x2-cell buckets");
@@ -606,78 +618,90 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
     const int lane = threadIdx.x;
     const LaneRole<W> role(lane);
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const int sx = (int)it.tile / g.nty, sy = (int)it.tile - sx * g.nty;
-    const int ibase = sx * SUB, jbase = sy * SUB;
+    const int ntg = g.nty / GRP;
+    const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
+    const int ibase = sx * SUB, jbase = sg * GRP * SUB;
+    const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
 
-    float acc_r[NO][NQ], acc_i[NO][NQ];
-#pragma unroll
-    for (int o = 0; o < NO; ++o)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) acc_r[o][q] = acc_i[o][q] = 0.0f;
-    uint32_t used = 0;
+    for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
 
     const float tap_t = (float)(lane & 7);
-    for (uint32_t b0 = it.b; b0 < ((dbg & 2) ? it.b + 1 : it.e); b0 += 64) {
-        const int n = (int)min(64u, it.e - b0);
-        const VisRec my = recs[b0 + min(lane, n - 1)];
-        // per-lane decode of the lane's own record: records are consumed in
-        // static groups of 8, so lanes >= n carry zero-valued padding records
-        const bool live = lane < n;
-        const float cre_l = live ? my.cre : 0.0f, cim_l = live ? my.cim : 0.0f;
-        const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jbase);
+    for (int j = 0; j < GRP; ++j) {
+        const uint32_t rb = max(it.b, offs[key0 + j]);
+        const uint32_t re = min(it.e, offs[key0 + j + 1]);
+        if (rb >= re) continue;
+        const int jb = jbase + j * SUB;  // bucket's first cell along y
+
+        float acc_r[NO][NQ], acc_i[NO][NQ];
 #pragma unroll
-        for (int oo = 0; oo < NO; ++oo)
-            if (__ballot(live && o_l == oo)) used |= 1u << oo;
+        for (int o = 0; o < NO; ++o)
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            if (8 * m >= n) break;
-            // taps of this 8-record group: lane l holds tap (l % 8) of record 8m + l/8
-            const int src = 8 * m + (lane >> 3);
-            const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
-            const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
-            const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
+            for (int q = 0; q < NQ; ++q) acc_r[o][q] = acc_i[o][q] = 0.0f;
+        uint32_t used = 0;
+
+        for (uint32_t b0 = rb; b0 < ((dbg & 2) ? rb + 1 : re); b0 += 64) {
+            const int n = (int)min(64u, re - b0);
+            const VisRec my = recs[b0 + min(lane, n - 1)];
+            // per-lane decode of the lane's own record; lanes >= n carry
+            // zero-valued padding records
+            const bool live = lane < n;
+            const float cre_l = live ? my.cre : 0.0f, cim_l = live ? my.cim : 0.0f;
+            const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const int k = 8 * m + r;
-                const float cre = lane_readf(cre_l, k), cim = lane_readf(cim_l, k);
-                const int o = __builtin_amdgcn_readlane(o_l, k);
-                const float ku = __shfl(tu, 8 * r + role.kx);
-                const float kv = __shfl(tv, 8 * r + role.ky);
-                const float kk = ku * kv;
-                const float vr = cre * kk, vi = cim * kk;
-                float kw[NQ];
+            for (int oo = 0; oo < NO; ++oo)
+                if (__ballot(live && o_l == oo)) used |= 1u << oo;
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
-                // origin select: uniform branches (one per origin set)
+            for (int m = 0; m < 8; ++m) {
+                if (8 * m >= n) break;
+                // taps of this 8-record group: lane l holds tap (l % 8) of record 8m + l/8
+                const int src = 8 * m + (lane >> 3);
+                const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
+                const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
+                const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
 #pragma unroll
-                for (int oo = 0; oo < NO; ++oo)
-                    if (o == oo) acc_add<NQ>(acc_r[oo], acc_i[oo], vr, vi, kw);
+                for (int r = 0; r < 8; ++r) {
+                    const int k = 8 * m + r;
+                    const float cre = lane_readf(cre_l, k), cim = lane_readf(cim_l, k);
+                    const int o = __builtin_amdgcn_readlane(o_l, k);
+                    const float ku = __shfl(tu, 8 * r + role.kx);
+                    const float kv = __shfl(tv, 8 * r + role.ky);
+                    const float kk = ku * kv;
+                    const float vr = cre * kk, vi = cim * kk;
+                    float kw[NQ];
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
+                    // origin select: uniform branches (one per origin set)
+#pragma unroll
+                    for (int oo = 0; oo < NO; ++oo)
+                        if (o == oo) acc_add<NQ>(acc_r[oo], acc_i[oo], vr, vi, kw);
+                }
             }
         }
-    }
 
-    // combine the origins in LDS (plain RMW: one wave, in-order LDS), then flush
-    for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
+        // add the bucket's origin sets into the group tile (plain RMW: one
+        // wave, in-order LDS)
 #pragma unroll
-    for (int oo = 0; oo < NO; ++oo) {
-        if ((used >> oo) & 1u) {
-            if (role.act) {
-                const int base = (oo / SUB + role.kx) * R + (oo % SUB) + role.ky;
+        for (int oo = 0; oo < NO; ++oo) {
+            if ((used >> oo) & 1u) {
+                if (role.act) {
+                    const int base = (oo / SUB + role.kx) * RY + j * SUB + (oo % SUB) + role.ky;
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    float2 a = tile[q * PS + base];
-                    a.x += acc_r[oo][q];
-                    a.y += acc_i[oo][q];
-                    tile[q * PS + base] = a;
+                    for (int q = 0; q < NQ; ++q) {
+                        float2 a = tile[q * PS + base];
+                        a.x += acc_r[oo][q];
+                        a.y += acc_i[oo][q];
+                        tile[q * PS + base] = a;
+                    }
                 }
             }
         }
     }
+
     // flush: lane f of pass i handles float (64 i + f) of each plane's
-    // (2+W-1)^2 complex cells; a wave-instruction covers 3.5 contiguous
-    // 72-byte grid rows (re/im interleaved); zero floats are skipped.  The
-    // address of a float is the same in every plane, so it is computed once.
-    constexpr int FPP = R * R * 2;  // floats per plane
+    // RX x RY complex cells (rows of RY contiguous cells, re/im interleaved);
+    // zero floats are skipped.  The address of a float is the same in every
+    // plane, so it is computed once.
+    constexpr int FPP = RX * RY * 2;  // floats per plane
     const int64_t plane_floats = (int64_t)g.ngx * g.ngy * 2;
     const float *ftile = reinterpret_cast<const float *>(tile);
 #pragma unroll
@@ -685,7 +709,7 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
         const int f = i0 + lane;
         if (f >= FPP) break;
         const int c = f >> 1;
-        const int xl = c / R, yl = c - (c / R) * R;
+        const int xl = c / RY, yl = c - (c / RY) * RY;
         int gx = ibase + xl;
         if (gx >= g.ngx) gx -= g.ngx;
         int gy = jbase + yl;
@@ -707,28 +731,33 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
     }
 }
 
-template <int W, bool WS, int SUB>
+// Degridder: one wave per work item (an SX x SY-cell region: a 16x16 tile or
+// a group of kGroupFine 2x2 buckets).  The region's W planes are loaded into
+// LDS; per record, lane (kx, ky) reads its tap's W plane values, and a wave
+// reduction sums the footprint.
+template <int W, bool WS, int SX, int SY>
 __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__ recs,
                                                const Item *__restrict__ items, ItemOrder ord,
                                                const float2 *__restrict__ grid, int p_lo,
                                                int p_hi, float2 *acc) {
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int R = TileShape<W, SUB>::R;
-    constexpr int PS = TileShape<W, SUB>::PLANE;
-    constexpr int PITCH = TileShape<W, SUB>::PITCH;
+    using TS = TileShape<W, SX, SY>;
+    constexpr int RX = TS::RX, RY = TS::RY, PS = TS::PLANE, PITCH = TS::PITCH;
     constexpr int NQ = WS ? W : 1;
     const Item it = load_item(items, ord);
-    const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
+    const int ntg = g.nty / g.grp;
+    const int tx = (int)it.tile / ntg, tg = (int)it.tile - tx * ntg;
+    const int ibase = tx * SX, jbase = tg * SY;
     const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
     const int lane = threadIdx.x;
-    for (int i = lane; i < NQ * R * R; i += 64) {
-        const int q = i / (R * R);
+    for (int i = lane; i < NQ * RX * RY; i += 64) {
+        const int q = i / (RX * RY);
         const int p = (int)it.p0 + q;
-        const int rem = i - q * R * R;
-        const int xl = rem / R, yl = rem - (rem / R) * R;
-        int gx = tx * SUB + xl;
+        const int rem = i - q * RX * RY;
+        const int xl = rem / RY, yl = rem - (rem / RY) * RY;
+        int gx = ibase + xl;
         if (gx >= g.ngx) gx -= g.ngx;
-        int gy = ty * SUB + yl;
+        int gy = jbase + yl;
         if (gy >= g.ngy) gy -= g.ngy;
         tile[q * PS + xl * PITCH + yl] =
             (p >= p_lo && p < p_hi)
@@ -738,7 +767,7 @@ __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__
 
     const LaneRole<W> role(lane);
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const int lane_off = role.kx * PITCH + role.ky - (tx * SUB) * PITCH - ty * SUB;
+    const int lane_off = role.kx * PITCH + role.ky - ibase * PITCH - jbase;
     for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
         const int n = (int)min(64u, it.e - b0);
         const VisRec my = recs[b0 + min(lane, n - 1)];
@@ -1132,6 +1161,7 @@ struct Plan {
     int chunk_planes = 1;            // planes resident per pass
     int row_lo = 0, row_hi = 0;      // grid rows (x) the visibilities reach
     unsigned chunk = kChunkMin;      // max records per work item
+    const unsigned *offs = nullptr;  // bucket start offsets (the scan of the histogram)
     float2 *grid = nullptr;
     float2 *spec = nullptr;  // T[q][iy][kx]: transposed y-spectra (pruned FFT)
 };
@@ -1243,6 +1273,7 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     }
     g.nty = g.ngy / g.sub;
     g.ntiles = (g.ngx / g.sub) * g.nty;
+    g.grp = g.sub == kTileFine ? kGroupFine : 1;  // nty is a multiple of kGridAlign / sub
     SDP_REQUIRE((double)g.ntiles * g.nps < 4.0e9, "too many (plane, tile) buckets");
 
     // ---- bucketing
@@ -1292,17 +1323,19 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     if (nvis > 0) launch_bucket(std::true_type{}, offs, P.recs);
 
     // ---- work items (p0-major, so a first-plane range is a contiguous item range)
-    SDP_HIP_CHECK(hipMemsetAsync(nch + nkeys, 0, sizeof(unsigned), st));
+    const int64_t ngroups = (int64_t)nkeys / g.grp;
+    const int gpp = g.ntiles / g.grp;  // groups per first-plane value
+    SDP_HIP_CHECK(hipMemsetAsync(nch + ngroups, 0, sizeof(unsigned), st));
     // records per item: large enough to amortise the tile flush over dense
     // tiles, small enough to leave >= ~16k items for the 256 CUs
     P.chunk = (unsigned)std::min<int64_t>(kChunkMax, std::max<int64_t>(kChunkMin, nvis / 16384));
     if (const char *e = std::getenv("SDP_HIP_CHUNK"))
         if (std::atoi(e) >= 64) P.chunk = (unsigned)std::atoi(e);
-    k_items_count<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, offs, P.chunk, nch);
+    k_items_count<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, offs, P.chunk, nch);
     tb = tmp_bytes + 16;
-    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nch, ioffs, (int)(nkeys + 1), st));
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nch, ioffs, (int)(ngroups + 1), st));
     unsigned *meta = scratch<unsigned>("plan_meta", g.nps + 4);
-    k_plan_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(nbad, offs + nkeys, ioffs, g.ntiles, g.nps,
+    k_plan_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(nbad, offs + nkeys, ioffs, gpp, g.nps,
                                                       meta);
     unsigned *hm = pinned_host<unsigned>(64, g.nps + 4);
     SDP_HIP_CHECK(hipMemcpyAsync(hm, meta, (g.nps + 4) * sizeof(unsigned), hipMemcpyDeviceToHost,
@@ -1315,8 +1348,9 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     P.nrec = nrec_h;
     P.nitems = P.p0_items[g.nps];
     P.items = scratch<Item>("items", std::max<int64_t>(P.nitems, 1));
-    k_items_fill<<<grid1d(nkeys, 256), 256, 0, st>>>((int64_t)nkeys, g.ntiles, offs, ioffs,
-                                                     P.chunk, P.items);
+    k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, gpp, offs, ioffs, P.chunk,
+                                                       P.items);
+    P.offs = offs;
 
     // ---- grid rows reached by any footprint (centred storage)
     {
@@ -1386,10 +1420,11 @@ static void launch_grid_n(const Plan &P, std::pair<unsigned, unsigned> r, int p_
 template <int W, bool WS>
 static void launch_grid_reg(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
                             hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) * TileShape<W, kTileFine>::PLANE * sizeof(float2);
+    const size_t lds = (size_t)(WS ? W : 1) *
+                       TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
     const int dbg = std::getenv("SDP_HIP_DBG") ? std::atoi(std::getenv("SDP_HIP_DBG")) : 0;
     k_grid_reg<W, WS><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
-                                                          item_order(r.second - r.first),
+                                                          item_order(r.second - r.first), P.offs,
                                                           (float *)P.grid, p_lo, p_hi, dbg);
 }
 
@@ -1409,12 +1444,12 @@ static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
     }
 }
 
-template <int W, bool WS, int SUB>
+template <int W, bool WS, int SX, int SY>
 static void launch_degrid_n(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
                             float2 *acc, hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) * TileShape<W, SUB>::PLANE * sizeof(float2);
-    allow_lds((const void *)k_degrid<W, WS, SUB>, lds);
-    k_degrid<W, WS, SUB><<<r.second - r.first, 64, lds, st>>>(
+    const size_t lds = (size_t)(WS ? W : 1) * TileShape<W, SX, SY>::PLANE * sizeof(float2);
+    allow_lds((const void *)k_degrid<W, WS, SX, SY>, lds);
+    k_degrid<W, WS, SX, SY><<<r.second - r.first, 64, lds, st>>>(
         P.g, P.recs, P.items + r.first, item_order(r.second - r.first), P.grid, p_lo, p_hi, acc);
 }
 
@@ -1422,12 +1457,14 @@ template <int W>
 static void launch_degrid(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
     const auto r = chunk_items(P, p_lo, p_hi);
     if (r.second <= r.first) return;
+    constexpr int FX = kTileFine, FY = kTileFine * kGroupFine;
     if (P.g.sub == kTileFine) {
-        if (P.g.do_w) return launch_degrid_n<W, true, kTileFine>(P, r, p_lo, p_hi, acc, st);
-        return launch_degrid_n<W, false, kTileFine>(P, r, p_lo, p_hi, acc, st);
+        if (P.g.do_w) return launch_degrid_n<W, true, FX, FY>(P, r, p_lo, p_hi, acc, st);
+        return launch_degrid_n<W, false, FX, FY>(P, r, p_lo, p_hi, acc, st);
     }
-    if (P.g.do_w) return launch_degrid_n<W, true, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
-    return launch_degrid_n<W, false, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
+    if (P.g.do_w)
+        return launch_degrid_n<W, true, kTileCoarse, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
+    return launch_degrid_n<W, false, kTileCoarse, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
 }
 
 #define SDP_W_DISPATCH(W, CALL) \
