@@ -731,6 +731,148 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
     }
 }
 
+// Register degridder (mirror of k_grid_reg): one wave per work item = a
+// chunk of a group of kGroupFine consecutive 2x2-cell buckets.  The group's
+// (2+W-1) x (8+W-1) x W region is staged in LDS once; per bucket, lane
+// (kx, ky) loads the W plane values of its tap cell for each of the 4
+// footprint origins into VGPRs (G[o][q]).  Per record the lane forms
+// kk * sum_q kw[q] G[o][q] with 8 register FMAs; the 64 lanes' partials of
+// 8 records are then summed with one reduce-scatter butterfly (5 lane
+// exchanges per record instead of 12).  Each record belongs to exactly one
+// item, so its raw sum is added to acc[] with a plain read-modify-write; the
+// record factor wgt * exp(-2 pi i w s0) is applied by k_finalize.
+template <int W, bool WS>
+__global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restrict__ recs,
+                                                   const Item *__restrict__ items, ItemOrder ord,
+                                                   const unsigned *__restrict__ offs,
+                                                   const float2 *__restrict__ grid, int p_lo,
+                                                   int p_hi, float2 *__restrict__ acc) {
+    constexpr int SUB = kTileFine;
+    constexpr int GRP = kGroupFine;
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    using TS = TileShape<W, SUB, SUB * GRP>;
+    constexpr int RX = TS::RX, RY = TS::RY, PS = TS::PLANE;
+    constexpr int NQ = WS ? W : 1;
+    constexpr int NO = SUB * SUB;
+    static_assert(NO == 4, "origin select below assumes 2x2-cell buckets");
+    const Item it = load_item(items, ord);
+    const int lane = threadIdx.x;
+    const LaneRole<W> role(lane);
+    const float ihw = g.inv_half_w, bl = g.beta_l2e;
+    const int ntg = g.nty / GRP;
+    const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
+    const int ibase = sx * SUB, jbase = sg * GRP * SUB;
+    const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
+    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+
+    // stage the region (planes outside this pass's [p_lo, p_hi) read as 0)
+    for (int i = lane; i < NQ * RX * RY; i += 64) {
+        const int q = i / (RX * RY);
+        const int p = (int)it.p0 + q;
+        const int rem = i - q * RX * RY;
+        const int xl = rem / RY, yl = rem - (rem / RY) * RY;
+        int gx = ibase + xl;
+        if (gx >= g.ngx) gx -= g.ngx;
+        int gy = jbase + yl;
+        if (gy >= g.ngy) gy -= g.ngy;
+        tile[q * PS + xl * RY + yl] =
+            (p >= p_lo && p < p_hi)
+                ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
+                : make_float2(0.0f, 0.0f);
+    }
+
+    const float tap_t = (float)(lane & 7);
+    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+    for (int j = 0; j < GRP; ++j) {
+        const uint32_t rb = max(it.b, offs[key0 + j]);
+        const uint32_t re = min(it.e, offs[key0 + j + 1]);
+        if (rb >= re) continue;
+        const int jb = jbase + j * SUB;
+
+        float gr[NO][NQ], gi[NO][NQ];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            const int base = (o / SUB + role.kx) * RY + j * SUB + (o % SUB) + role.ky;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const float2 v = role.act ? tile[q * PS + base] : make_float2(0.0f, 0.0f);
+                gr[o][q] = v.x;
+                gi[o][q] = v.y;
+            }
+        }
+
+        for (uint32_t b0 = rb; b0 < re; b0 += 64) {
+            const int n = (int)min(64u, re - b0);
+            const VisRec my = recs[b0 + min(lane, n - 1)];
+            const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                if (8 * m >= n) break;
+                const int src = 8 * m + (lane >> 3);
+                const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
+                const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
+                const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
+                float pr[8], pim[8];
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int k = 8 * m + r;
+                    const int o = __builtin_amdgcn_readlane(o_l, k);
+                    const float ku = __shfl(tu, 8 * r + role.kx);
+                    const float kv = __shfl(tv, 8 * r + role.ky);
+                    float kw[NQ];
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
+                    float sr = 0.0f, si = 0.0f;
+#pragma unroll
+                    for (int oo = 0; oo < NO; ++oo) {
+                        if (o == oo) {
+#pragma unroll
+                            for (int q = 0; q < NQ; ++q) {
+                                sr = fmaf(kw[q], gr[oo][q], sr);
+                                si = fmaf(kw[q], gi[oo][q], si);
+                            }
+                        }
+                    }
+                    const float kk = ku * kv;
+                    pr[r] = sr * kk;
+                    pim[r] = si * kk;
+                }
+                // reduce-scatter: after the xor-32/16/8 halvings lane l holds
+                // record (l >> 3) & 7 summed over 8 lanes; xor 4/2/1 finish it
+                float a4r[4], a4i[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float sr = b5 ? pr[i] : pr[i + 4], si = b5 ? pim[i] : pim[i + 4];
+                    a4r[i] = (b5 ? pr[i + 4] : pr[i]) + __shfl_xor(sr, 32);
+                    a4i[i] = (b5 ? pim[i + 4] : pim[i]) + __shfl_xor(si, 32);
+                }
+                float a2r[2], a2i[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const float sr = b4 ? a4r[i] : a4r[i + 2], si = b4 ? a4i[i] : a4i[i + 2];
+                    a2r[i] = (b4 ? a4r[i + 2] : a4r[i]) + __shfl_xor(sr, 16);
+                    a2i[i] = (b4 ? a4i[i + 2] : a4i[i]) + __shfl_xor(si, 16);
+                }
+                float tr = (b3 ? a2r[1] : a2r[0]) + __shfl_xor(b3 ? a2r[0] : a2r[1], 8);
+                float ti = (b3 ? a2i[1] : a2i[0]) + __shfl_xor(b3 ? a2i[0] : a2i[1], 8);
+#pragma unroll
+                for (int msk = 4; msk > 0; msk >>= 1) {
+                    tr += __shfl_xor(tr, msk);
+                    ti += __shfl_xor(ti, msk);
+                }
+                const int rec = 8 * m + ((lane >> 3) & 7);
+                if ((lane & 7) == 0 && rec < n) {
+                    float2 *dst = acc + b0 + rec;
+                    float2 a = *dst;
+                    a.x += tr;
+                    a.y += ti;
+                    *dst = a;
+                }
+            }
+        }
+    }
+}
+
 // Degridder: one wave per work item (an SX x SY-cell region: a 16x16 tile or
 // a group of kGroupFine 2x2 buckets).  The region's W planes are loaded into
 // LDS; per record, lane (kx, ky) reads its tap's W plane values, and a wave
@@ -1453,14 +1595,23 @@ static void launch_degrid_n(const Plan &P, std::pair<unsigned, unsigned> r, int 
         P.g, P.recs, P.items + r.first, item_order(r.second - r.first), P.grid, p_lo, p_hi, acc);
 }
 
+template <int W, bool WS>
+static void launch_degrid_reg(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
+                              float2 *acc, hipStream_t st) {
+    const size_t lds = (size_t)(WS ? W : 1) *
+                       TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
+    k_degrid_reg<W, WS><<<r.second - r.first, 64, lds, st>>>(
+        P.g, P.recs, P.items + r.first, item_order(r.second - r.first), P.offs, P.grid, p_lo, p_hi,
+        acc);
+}
+
 template <int W>
 static void launch_degrid(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
     const auto r = chunk_items(P, p_lo, p_hi);
     if (r.second <= r.first) return;
-    constexpr int FX = kTileFine, FY = kTileFine * kGroupFine;
     if (P.g.sub == kTileFine) {
-        if (P.g.do_w) return launch_degrid_n<W, true, FX, FY>(P, r, p_lo, p_hi, acc, st);
-        return launch_degrid_n<W, false, FX, FY>(P, r, p_lo, p_hi, acc, st);
+        if (P.g.do_w) return launch_degrid_reg<W, true>(P, r, p_lo, p_hi, acc, st);
+        return launch_degrid_reg<W, false>(P, r, p_lo, p_hi, acc, st);
     }
     if (P.g.do_w)
         return launch_degrid_n<W, true, kTileCoarse, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
