@@ -161,7 +161,7 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = nvis_rank * world / (elapsed / args.steps) / 1e6
     ms_grid = float(np.mean([i["ms_grid"] for i in infos]))
-    launches = max(1, math.ceil(info["nplanes"] / max(1, info["plane_chunk"])))
+    launches = max(1, info["grid_launches"])
     alg_bytes = nvis_rank * (8 + 4 + 24.0 / len(chans)) + \
         info["nplanes"] * info["ngrid_x"] * info["ngrid_y"] * 8
     achieved = alg_bytes / launches / (ms_grid / launches * 1e-3) / 1e9

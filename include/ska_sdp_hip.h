@@ -54,6 +54,8 @@ typedef struct sdp_hip_wgrid_info {
     float ms_prep, ms_grid, ms_fft, ms_screen; /* stage times if timing on  */
     int bucket;           /* bucket edge in cells: 2 = register gridder,
                              16 = LDS-tile gridder (large grids)            */
+    int grid_launches;    /* (de)gridding kernel launches (visibility parts
+                             x plane chunks); ms_grid is their summed time  */
 } sdp_hip_wgrid_info;
 
 /* Library/ABI version and a device probe. */

@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <tuple>
 #include <type_traits>
@@ -64,6 +65,7 @@ struct Geo {
     double w0, dw, s0;
     int sub, nty, ntiles;  // bucket edge in cells, buckets per grid column, buckets
     int grp;               // consecutive buckets (along y) per work-item group
+    int dbg;               // experiment knobs (SDP_HIP_DBG)
     double su;  // sign applied to u and w (-1 with SDP_HIP_FLIP_UW)
     int nchan;
     int64_t nrow;
@@ -232,9 +234,10 @@ __global__ __launch_bounds__(256) void k_bounds_final(int nblocks, const double 
     if (threadIdx.x < 6) out[threadIdx.x] = red[threadIdx.x][0];
 }
 
-// plan metadata in one buffer for one D2H copy: {nbad (2 words), nrec,
-// first item of each first-plane value [nps + 1]}
-__global__ void k_plan_meta(const unsigned long long *__restrict__ nbad,
+// per-part plan metadata (one buffer, one D2H copy when the host needs it):
+// {nbad lo, nbad hi, nrec, nitems, first item of each first-plane value
+// [nps + 1]}; meta[3] is also the item count persistent launches read
+__global__ void k_part_meta(const unsigned long long *__restrict__ nbad,
                             const unsigned *__restrict__ nrec, const unsigned *__restrict__ ioffs,
                             int groups_per_plane, int nps, unsigned *__restrict__ meta) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -242,8 +245,9 @@ __global__ void k_plan_meta(const unsigned long long *__restrict__ nbad,
         meta[0] = (unsigned)(*nbad & 0xffffffffull);
         meta[1] = (unsigned)(*nbad >> 32);
         meta[2] = *nrec;
+        meta[3] = ioffs[(size_t)nps * groups_per_plane];
     }
-    if (k <= nps) meta[3 + k] = ioffs[(size_t)k * groups_per_plane];
+    if (k <= nps) meta[4 + k] = ioffs[(size_t)k * groups_per_plane];
 }
 
 // Wave-level run-length aggregation: consecutive lanes with equal keys share
@@ -277,13 +281,15 @@ __device__ __forceinline__ float2 load_vis(const double2 *p) {
 // Scatter pass: position = offs[key] + rank -- no atomics -- and the 32-byte
 // record is written there.  Invalid visibilities carry key 0xffffffff.
 template <class VT, bool kScatter, bool kGrid>
-__global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
-                         const double *__restrict__ freq, const VT *__restrict__ vis,
-                         int64_t vrs, int64_t vcs, const float *__restrict__ wgt, int64_t wrs,
-                         int64_t wcs, unsigned *counter, uint2 *__restrict__ kr,
-                         VisRec *__restrict__ recs, unsigned long long *nbad) {
-    const int64_t nvis = g.nrow * (int64_t)g.nchan;
+__global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__restrict__ uvw,
+                         int64_t uvw_rs, const double *__restrict__ freq,
+                         const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
+                         const float *__restrict__ wgt, int64_t wrs, int64_t wcs,
+                         unsigned *counter, uint2 *__restrict__ kr, VisRec *__restrict__ recs,
+                         unsigned long long *nbad) {
+    // v indexes the part's visibilities (rows row0...); vg the call's
     const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t vg = row0 * g.nchan + v;
     bool valid = v < nvis;
     int64_t row = 0;
     int chan = 0;
@@ -295,14 +301,14 @@ __global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
         if (!valid) return;
         mine = kr[v];
         if (mine.x == 0xffffffffu) return;
-        row = v / g.nchan;
-        chan = (int)(v - row * g.nchan);
+        row = vg / g.nchan;
+        chan = (int)(vg - row * g.nchan);
         if (wgt) wt = wgt[row * wrs + chan * wcs];
         c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
     } else {
         if (valid) {
-            row = v / g.nchan;
-            chan = (int)(v - row * g.nchan);
+            row = vg / g.nchan;
+            chan = (int)(vg - row * g.nchan);
             if (wgt) wt = wgt[row * wrs + chan * wcs];
             valid = (wt != 0.0f);
             if (valid) {
@@ -314,11 +320,11 @@ __global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
             }
         }
         const unsigned key = valid ? coord_key(g, c) : 0xffffffffu;
-        const unsigned rank = run_reserve<true>(key, valid, counter);
+        const unsigned rank = (g.dbg & 8) ? 0u : run_reserve<true>(key, valid, counter);
         if (v < nvis) kr[v] = make_uint2(key, rank);
         return;
     }
-    const unsigned pos = counter[mine.x] + mine.y;
+    const unsigned pos = (g.dbg & 16) ? (unsigned)v : counter[mine.x] + mine.y;
     float cr = wt, ci = 0.0f;
     if (kGrid) {
         const float2 x = vis ? load_vis(vis + row * vrs + chan * vcs) : make_float2(1.0f, 0.0f);
@@ -343,7 +349,7 @@ __global__ void k_bucket(Geo g, const double *__restrict__ uvw, int64_t uvw_rs,
     rec.fw = c.fw;
     rec.ij = (uint32_t)c.ic0 | ((uint32_t)c.jc0 << 16);
     rec.p0 = (uint32_t)c.p0;
-    rec.idx = (uint32_t)v;
+    rec.idx = (uint32_t)vg;
     recs[pos] = rec;
 }
 
@@ -391,13 +397,31 @@ struct TileShape {
 // Work items are visited in a strided order (stride coprime with the item
 // count): the heavy chunks of one dense tile are spread over the launch
 // instead of flushing into the same cells at the same time.
-struct ItemOrder {
-    uint32_t n, stride;
+//
+// A launch walks the items either one per workgroup (count known on the
+// host) or persistently (count read from device memory, written by the
+// bucketing of the same call -- no host round trip between the stages).
+struct ItemSrc {
+    const Item *items;
+    uint32_t n;            // item count when ndev == nullptr
+    const unsigned *ndev;  // device-side item count (persistent launches)
 };
 
-__device__ __forceinline__ Item load_item(const Item *__restrict__ items, ItemOrder ord) {
-    const uint32_t i = (uint32_t)(((uint64_t)blockIdx.x * ord.stride) % ord.n);
-    const Item raw = items[i];
+__device__ __forceinline__ uint32_t item_count(const ItemSrc &src) {
+    return src.ndev ? (uint32_t)__builtin_amdgcn_readfirstlane((int)*src.ndev) : src.n;
+}
+
+__device__ __forceinline__ uint32_t item_stride(uint32_t n) {
+    const uint32_t primes[5] = {7919u, 104729u, 1299709u, 15485863u, 179424673u};
+    for (int k = 0; k < 5; ++k)
+        if (n <= 1 || n % primes[k] != 0) return primes[k];
+    return 1u;
+}
+
+__device__ __forceinline__ Item load_item(const ItemSrc &src, uint32_t w, uint32_t n,
+                                          uint32_t stride) {
+    const uint32_t i = (uint32_t)(((uint64_t)w * stride) % n);
+    const Item raw = src.items[i];
     Item it;
     it.b = __builtin_amdgcn_readfirstlane(raw.b);
     it.e = __builtin_amdgcn_readfirstlane(raw.e);
@@ -487,8 +511,7 @@ struct LaneRole {
 // to hide the LDS read->write latency of the update chain.
 template <int W, bool WS, int NWV>
 __global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__restrict__ recs,
-                                                       const Item *__restrict__ items,
-                                                       ItemOrder ord, float *__restrict__ grid,
+                                                       ItemSrc src, float *__restrict__ grid,
                                                        int p_lo, int p_hi) {
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int kTile = kTileCoarse;
@@ -497,79 +520,84 @@ __global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__re
     constexpr int NQ = WS ? W : 1;
     constexpr int NQW = (NQ + NWV - 1) / NWV;  // planes per wave (the last
     constexpr int NQP = NQW * NWV;             // wave may own padding planes)
-    const Item it = load_item(items, ord);
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int i = threadIdx.x; i < NQP * PS; i += 64 * NWV) tile[i] = make_float2(0.0f, 0.0f);
-    __syncthreads();
+    const uint32_t n_items = item_count(src);
+    const uint32_t stride = item_stride(n_items);
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        __syncthreads();  // previous item's flush reads of the LDS tile
+        const Item it = load_item(src, w_it, n_items, stride);
+        const int lane = threadIdx.x & 63;
+        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        for (int i = threadIdx.x; i < NQP * PS; i += 64 * NWV) tile[i] = make_float2(0.0f, 0.0f);
+        __syncthreads();
 
-    const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
-    const LaneRole<W> role(lane);
-    const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const int lane_off = role.kx * kPitch + role.ky - (tx * kTile) * kPitch - ty * kTile;
-    const int q0 = wv * NQW;
-    float2 *const wtile = tile + q0 * PS;
+        const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
+        const LaneRole<W> role(lane);
+        const float ihw = g.inv_half_w, bl = g.beta_l2e;
+        const int lane_off = role.kx * kPitch + role.ky - (tx * kTile) * kPitch - ty * kTile;
+        const int q0 = wv * NQW;
+        float2 *const wtile = tile + q0 * PS;
 
-    for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
-        const int n = (int)min(64u, it.e - b0);
-        const VisRec my = recs[b0 + min(lane, n - 1)];
-        const BatchTaps bt = batch_taps(my, lane, ihw, bl);
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-            const int rn = min(8, n - 8 * m);  // records of this 8-record group
-            for (int r = 0; r < rn; ++r) {
-                const int k = 8 * m + r;
-                const float cre = lane_readf(my.cre, k), cim = lane_readf(my.cim, k);
-                const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)my.ij, k);
-                const float ku = __shfl(bt.u[m], 8 * r + role.kx);
-                const float kv = __shfl(bt.v[m], 8 * r + role.ky);
-                const float kk = ku * kv;
-                const float vr = cre * kk, vi = cim * kk;
-                const int off = lane_off + (int)(ij & 0xffffu) * kPitch + (int)(ij >> 16);
-                // padding planes (q0 + q >= NQ) get a zero weight: a uniform
-                // select, so the LDS reads and writes below stay branch-free
-                float kw[NQW];
-#pragma unroll
-                for (int q = 0; q < NQW; ++q) {
-                    const float x = WS ? lane_readf(bt.w[m], 8 * r + min(q0 + q, NQ - 1)) : 1.0f;
-                    kw[q] = (NQP == NQ || q0 + q < NQ) ? x : 0.0f;
-                }
-                if (role.act) {
-                    float2 a[NQW];
-#pragma unroll
-                    for (int q = 0; q < NQW; ++q) a[q] = wtile[q * PS + off];
-#pragma unroll
+        for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+            const int n = (int)min(64u, it.e - b0);
+            const VisRec my = recs[b0 + min(lane, n - 1)];
+            const BatchTaps bt = batch_taps(my, lane, ihw, bl);
+    #pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const int rn = min(8, n - 8 * m);  // records of this 8-record group
+                for (int r = 0; r < rn; ++r) {
+                    const int k = 8 * m + r;
+                    const float cre = lane_readf(my.cre, k), cim = lane_readf(my.cim, k);
+                    const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)my.ij, k);
+                    const float ku = __shfl(bt.u[m], 8 * r + role.kx);
+                    const float kv = __shfl(bt.v[m], 8 * r + role.ky);
+                    const float kk = ku * kv;
+                    const float vr = cre * kk, vi = cim * kk;
+                    const int off = lane_off + (int)(ij & 0xffffu) * kPitch + (int)(ij >> 16);
+                    // padding planes (q0 + q >= NQ) get a zero weight: a uniform
+                    // select, so the LDS reads and writes below stay branch-free
+                    float kw[NQW];
+    #pragma unroll
                     for (int q = 0; q < NQW; ++q) {
-                        a[q].x = fmaf(vr, kw[q], a[q].x);
-                        a[q].y = fmaf(vi, kw[q], a[q].y);
-                        wtile[q * PS + off] = a[q];
+                        const float x = WS ? lane_readf(bt.w[m], 8 * r + min(q0 + q, NQ - 1)) : 1.0f;
+                        kw[q] = (NQP == NQ || q0 + q < NQ) ? x : 0.0f;
+                    }
+                    if (role.act) {
+                        float2 a[NQW];
+    #pragma unroll
+                        for (int q = 0; q < NQW; ++q) a[q] = wtile[q * PS + off];
+    #pragma unroll
+                        for (int q = 0; q < NQW; ++q) {
+                            a[q].x = fmaf(vr, kw[q], a[q].x);
+                            a[q].y = fmaf(vi, kw[q], a[q].y);
+                            wtile[q * PS + off] = a[q];
+                        }
                     }
                 }
             }
         }
-    }
-    __syncthreads();
+        __syncthreads();
 
-    // flush: float atomics into the resident planes (the halo overlaps the
-    // neighbouring tiles); zero cells are skipped.
-    const int cells = R * R;
-    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-    for (int c = threadIdx.x; c < NQ * cells; c += 64 * NWV) {
-        const int q = c / cells;
-        const int p = (int)it.p0 + q;
-        if (p < p_lo || p >= p_hi) continue;
-        const int rem = c - q * cells;
-        const int xl = rem / R, yl = rem - (rem / R) * R;
-        const float2 val = tile[q * PS + xl * kPitch + yl];
-        if (val.x != 0.0f || val.y != 0.0f) {
-            int gx = tx * kTile + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = ty * kTile + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            float *dst =
-                grid + ((int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy) * 2;
-            atomicAdd(dst, val.x);
-            atomicAdd(dst + 1, val.y);
+        // flush: float atomics into the resident planes (the halo overlaps the
+        // neighbouring tiles); zero cells are skipped.
+        const int cells = R * R;
+        const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+        for (int c = threadIdx.x; c < NQ * cells; c += 64 * NWV) {
+            const int q = c / cells;
+            const int p = (int)it.p0 + q;
+            if (p < p_lo || p >= p_hi) continue;
+            const int rem = c - q * cells;
+            const int xl = rem / R, yl = rem - (rem / R) * R;
+            const float2 val = tile[q * PS + xl * kPitch + yl];
+            if (val.x != 0.0f || val.y != 0.0f) {
+                int gx = tx * kTile + xl;
+                if (gx >= g.ngx) gx -= g.ngx;
+                int gy = ty * kTile + yl;
+                if (gy >= g.ngy) gy -= g.ngy;
+                float *dst =
+                    grid + ((int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy) * 2;
+                atomicAdd(dst, val.x);
+                atomicAdd(dst + 1, val.y);
+            }
         }
     }
 }
@@ -598,7 +626,7 @@ __device__ __forceinline__ void acc_add(float (&ar)[NQ], float (&ai)[NQ], float 
 // static groups of 8 (zero-valued padding at the end of a bucket).
 template <int W, bool WS>
 __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict__ recs,
-                                                 const Item *__restrict__ items, ItemOrder ord,
+                                                 ItemSrc src,
                                                  const unsigned *__restrict__ offs,
                                                  float *__restrict__ grid, int p_lo, int p_hi,
                                                  int dbg) {
@@ -610,121 +638,125 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
     constexpr int NQ = WS ? W : 1;
     constexpr int NO = SUB * SUB;
     static_assert(NO == 4, "origin select below assumes 2x2-cell buckets");
-    const Item it = load_item(items, ord);
-    if (dbg & 4) {
-        if (it.b == 0xfffffffeu) grid[0] = 1.0f;  // keep the item load live
-        return;
-    }
-    const int lane = threadIdx.x;
-    const LaneRole<W> role(lane);
-    const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const int ntg = g.nty / GRP;
-    const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-    const int ibase = sx * SUB, jbase = sg * GRP * SUB;
-    const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
+    const uint32_t n_items = item_count(src);
+    const uint32_t stride = item_stride(n_items);
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        const Item it = load_item(src, w_it, n_items, stride);
+        if (dbg & 4) {
+            if (it.b == 0xfffffffeu) grid[0] = 1.0f;  // keep the item load live
+            continue;
+        }
+        const int lane = threadIdx.x;
+        const LaneRole<W> role(lane);
+        const float ihw = g.inv_half_w, bl = g.beta_l2e;
+        const int ntg = g.nty / GRP;
+        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
+        const int ibase = sx * SUB, jbase = sg * GRP * SUB;
+        const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
 
-    for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
+        for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
 
-    const float tap_t = (float)(lane & 7);
-    for (int j = 0; j < GRP; ++j) {
-        const uint32_t rb = max(it.b, offs[key0 + j]);
-        const uint32_t re = min(it.e, offs[key0 + j + 1]);
-        if (rb >= re) continue;
-        const int jb = jbase + j * SUB;  // bucket's first cell along y
+        const float tap_t = (float)(lane & 7);
+        for (int j = 0; j < GRP; ++j) {
+            const uint32_t rb = max(it.b, offs[key0 + j]);
+            const uint32_t re = min(it.e, offs[key0 + j + 1]);
+            if (rb >= re) continue;
+            const int jb = jbase + j * SUB;  // bucket's first cell along y
 
-        float acc_r[NO][NQ], acc_i[NO][NQ];
-#pragma unroll
-        for (int o = 0; o < NO; ++o)
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) acc_r[o][q] = acc_i[o][q] = 0.0f;
-        uint32_t used = 0;
+            float acc_r[NO][NQ], acc_i[NO][NQ];
+    #pragma unroll
+            for (int o = 0; o < NO; ++o)
+    #pragma unroll
+                for (int q = 0; q < NQ; ++q) acc_r[o][q] = acc_i[o][q] = 0.0f;
+            uint32_t used = 0;
 
-        for (uint32_t b0 = rb; b0 < ((dbg & 2) ? rb + 1 : re); b0 += 64) {
-            const int n = (int)min(64u, re - b0);
-            const VisRec my = recs[b0 + min(lane, n - 1)];
-            // per-lane decode of the lane's own record; lanes >= n carry
-            // zero-valued padding records
-            const bool live = lane < n;
-            const float cre_l = live ? my.cre : 0.0f, cim_l = live ? my.cim : 0.0f;
-            const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
-#pragma unroll
-            for (int oo = 0; oo < NO; ++oo)
-                if (__ballot(live && o_l == oo)) used |= 1u << oo;
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                if (8 * m >= n) break;
-                // taps of this 8-record group: lane l holds tap (l % 8) of record 8m + l/8
-                const int src = 8 * m + (lane >> 3);
-                const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
-                const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
-                const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const int k = 8 * m + r;
-                    const float cre = lane_readf(cre_l, k), cim = lane_readf(cim_l, k);
-                    const int o = __builtin_amdgcn_readlane(o_l, k);
-                    const float ku = __shfl(tu, 8 * r + role.kx);
-                    const float kv = __shfl(tv, 8 * r + role.ky);
-                    const float kk = ku * kv;
-                    const float vr = cre * kk, vi = cim * kk;
-                    float kw[NQ];
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
-                    // origin select: uniform branches (one per origin set)
-#pragma unroll
-                    for (int oo = 0; oo < NO; ++oo)
-                        if (o == oo) acc_add<NQ>(acc_r[oo], acc_i[oo], vr, vi, kw);
+            for (uint32_t b0 = rb; b0 < ((dbg & 2) ? rb + 1 : re); b0 += 64) {
+                const int n = (int)min(64u, re - b0);
+                const VisRec my = recs[b0 + min(lane, n - 1)];
+                // per-lane decode of the lane's own record; lanes >= n carry
+                // zero-valued padding records
+                const bool live = lane < n;
+                const float cre_l = live ? my.cre : 0.0f, cim_l = live ? my.cim : 0.0f;
+                const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
+    #pragma unroll
+                for (int oo = 0; oo < NO; ++oo)
+                    if (__ballot(live && o_l == oo)) used |= 1u << oo;
+    #pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    if (8 * m >= n) break;
+                    // taps of this 8-record group: lane l holds tap (l % 8) of record 8m + l/8
+                    const int src = 8 * m + (lane >> 3);
+                    const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
+                    const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
+                    const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
+    #pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const int k = 8 * m + r;
+                        const float cre = lane_readf(cre_l, k), cim = lane_readf(cim_l, k);
+                        const int o = __builtin_amdgcn_readlane(o_l, k);
+                        const float ku = __shfl(tu, 8 * r + role.kx);
+                        const float kv = __shfl(tv, 8 * r + role.ky);
+                        const float kk = ku * kv;
+                        const float vr = cre * kk, vi = cim * kk;
+                        float kw[NQ];
+    #pragma unroll
+                        for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
+                        // origin select: uniform branches (one per origin set)
+    #pragma unroll
+                        for (int oo = 0; oo < NO; ++oo)
+                            if (o == oo) acc_add<NQ>(acc_r[oo], acc_i[oo], vr, vi, kw);
+                    }
                 }
             }
-        }
 
-        // add the bucket's origin sets into the group tile (plain RMW: one
-        // wave, in-order LDS)
-#pragma unroll
-        for (int oo = 0; oo < NO; ++oo) {
-            if ((used >> oo) & 1u) {
-                if (role.act) {
-                    const int base = (oo / SUB + role.kx) * RY + j * SUB + (oo % SUB) + role.ky;
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        float2 a = tile[q * PS + base];
-                        a.x += acc_r[oo][q];
-                        a.y += acc_i[oo][q];
-                        tile[q * PS + base] = a;
+            // add the bucket's origin sets into the group tile (plain RMW: one
+            // wave, in-order LDS)
+    #pragma unroll
+            for (int oo = 0; oo < NO; ++oo) {
+                if ((used >> oo) & 1u) {
+                    if (role.act) {
+                        const int base = (oo / SUB + role.kx) * RY + j * SUB + (oo % SUB) + role.ky;
+    #pragma unroll
+                        for (int q = 0; q < NQ; ++q) {
+                            float2 a = tile[q * PS + base];
+                            a.x += acc_r[oo][q];
+                            a.y += acc_i[oo][q];
+                            tile[q * PS + base] = a;
+                        }
                     }
                 }
             }
         }
-    }
 
-    // flush: lane f of pass i handles float (64 i + f) of each plane's
-    // RX x RY complex cells (rows of RY contiguous cells, re/im interleaved);
-    // zero floats are skipped.  The address of a float is the same in every
-    // plane, so it is computed once.
-    constexpr int FPP = RX * RY * 2;  // floats per plane
-    const int64_t plane_floats = (int64_t)g.ngx * g.ngy * 2;
-    const float *ftile = reinterpret_cast<const float *>(tile);
-#pragma unroll
-    for (int i0 = 0; i0 < FPP; i0 += 64) {
-        const int f = i0 + lane;
-        if (f >= FPP) break;
-        const int c = f >> 1;
-        const int xl = c / RY, yl = c - (c / RY) * RY;
-        int gx = ibase + xl;
-        if (gx >= g.ngx) gx -= g.ngx;
-        int gy = jbase + yl;
-        if (gy >= g.ngy) gy -= g.ngy;
-        float *dst0 = grid + ((int64_t)gx * g.ngy + gy) * 2 + (f & 1);
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int p = (int)it.p0 + q;
-            const float val = ftile[q * PS * 2 + f];
-            if (p >= p_lo && p < p_hi && val != 0.0f) {
-                float *dst = dst0 + (int64_t)(p - p_lo) * plane_floats;
-                if (dbg & 1) {
-                    if (val == 1.2345f) dst[0] = val;  // keep the flush live, no atomics
-                } else {
-                    atomicAdd(dst, val);
+        // flush: lane f of pass i handles float (64 i + f) of each plane's
+        // RX x RY complex cells (rows of RY contiguous cells, re/im interleaved);
+        // zero floats are skipped.  The address of a float is the same in every
+        // plane, so it is computed once.
+        constexpr int FPP = RX * RY * 2;  // floats per plane
+        const int64_t plane_floats = (int64_t)g.ngx * g.ngy * 2;
+        const float *ftile = reinterpret_cast<const float *>(tile);
+    #pragma unroll
+        for (int i0 = 0; i0 < FPP; i0 += 64) {
+            const int f = i0 + lane;
+            if (f >= FPP) break;
+            const int c = f >> 1;
+            const int xl = c / RY, yl = c - (c / RY) * RY;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            float *dst0 = grid + ((int64_t)gx * g.ngy + gy) * 2 + (f & 1);
+    #pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int p = (int)it.p0 + q;
+                const float val = ftile[q * PS * 2 + f];
+                if (p >= p_lo && p < p_hi && val != 0.0f) {
+                    float *dst = dst0 + (int64_t)(p - p_lo) * plane_floats;
+                    if (dbg & 1) {
+                        if (val == 1.2345f) dst[0] = val;  // keep the flush live, no atomics
+                    } else {
+                        atomicAdd(dst, val);
+                    }
                 }
             }
         }
@@ -743,7 +775,7 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
 // record factor wgt * exp(-2 pi i w s0) is applied by k_finalize.
 template <int W, bool WS>
 __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restrict__ recs,
-                                                   const Item *__restrict__ items, ItemOrder ord,
+                                                   ItemSrc src,
                                                    const unsigned *__restrict__ offs,
                                                    const float2 *__restrict__ grid, int p_lo,
                                                    int p_hi, float2 *__restrict__ acc) {
@@ -755,118 +787,122 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
     constexpr int NQ = WS ? W : 1;
     constexpr int NO = SUB * SUB;
     static_assert(NO == 4, "origin select below assumes 2x2-cell buckets");
-    const Item it = load_item(items, ord);
-    const int lane = threadIdx.x;
-    const LaneRole<W> role(lane);
-    const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const int ntg = g.nty / GRP;
-    const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-    const int ibase = sx * SUB, jbase = sg * GRP * SUB;
-    const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
-    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+    const uint32_t n_items = item_count(src);
+    const uint32_t stride = item_stride(n_items);
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        const Item it = load_item(src, w_it, n_items, stride);
+        const int lane = threadIdx.x;
+        const LaneRole<W> role(lane);
+        const float ihw = g.inv_half_w, bl = g.beta_l2e;
+        const int ntg = g.nty / GRP;
+        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
+        const int ibase = sx * SUB, jbase = sg * GRP * SUB;
+        const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
+        const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
 
-    // stage the region (planes outside this pass's [p_lo, p_hi) read as 0)
-    for (int i = lane; i < NQ * RX * RY; i += 64) {
-        const int q = i / (RX * RY);
-        const int p = (int)it.p0 + q;
-        const int rem = i - q * RX * RY;
-        const int xl = rem / RY, yl = rem - (rem / RY) * RY;
-        int gx = ibase + xl;
-        if (gx >= g.ngx) gx -= g.ngx;
-        int gy = jbase + yl;
-        if (gy >= g.ngy) gy -= g.ngy;
-        tile[q * PS + xl * RY + yl] =
-            (p >= p_lo && p < p_hi)
-                ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
-                : make_float2(0.0f, 0.0f);
-    }
-
-    const float tap_t = (float)(lane & 7);
-    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
-    for (int j = 0; j < GRP; ++j) {
-        const uint32_t rb = max(it.b, offs[key0 + j]);
-        const uint32_t re = min(it.e, offs[key0 + j + 1]);
-        if (rb >= re) continue;
-        const int jb = jbase + j * SUB;
-
-        float gr[NO][NQ], gi[NO][NQ];
-#pragma unroll
-        for (int o = 0; o < NO; ++o) {
-            const int base = (o / SUB + role.kx) * RY + j * SUB + (o % SUB) + role.ky;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const float2 v = role.act ? tile[q * PS + base] : make_float2(0.0f, 0.0f);
-                gr[o][q] = v.x;
-                gi[o][q] = v.y;
-            }
+        // stage the region (planes outside this pass's [p_lo, p_hi) read as 0)
+        for (int i = lane; i < NQ * RX * RY; i += 64) {
+            const int q = i / (RX * RY);
+            const int p = (int)it.p0 + q;
+            const int rem = i - q * RX * RY;
+            const int xl = rem / RY, yl = rem - (rem / RY) * RY;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            tile[q * PS + xl * RY + yl] =
+                (p >= p_lo && p < p_hi)
+                    ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
+                    : make_float2(0.0f, 0.0f);
         }
 
-        for (uint32_t b0 = rb; b0 < re; b0 += 64) {
-            const int n = (int)min(64u, re - b0);
-            const VisRec my = recs[b0 + min(lane, n - 1)];
-            const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                if (8 * m >= n) break;
-                const int src = 8 * m + (lane >> 3);
-                const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
-                const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
-                const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
-                float pr[8], pim[8];
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    const int k = 8 * m + r;
-                    const int o = __builtin_amdgcn_readlane(o_l, k);
-                    const float ku = __shfl(tu, 8 * r + role.kx);
-                    const float kv = __shfl(tv, 8 * r + role.ky);
-                    float kw[NQ];
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
-                    float sr = 0.0f, si = 0.0f;
-#pragma unroll
-                    for (int oo = 0; oo < NO; ++oo) {
-                        if (o == oo) {
-#pragma unroll
-                            for (int q = 0; q < NQ; ++q) {
-                                sr = fmaf(kw[q], gr[oo][q], sr);
-                                si = fmaf(kw[q], gi[oo][q], si);
+        const float tap_t = (float)(lane & 7);
+        const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+        for (int j = 0; j < GRP; ++j) {
+            const uint32_t rb = max(it.b, offs[key0 + j]);
+            const uint32_t re = min(it.e, offs[key0 + j + 1]);
+            if (rb >= re) continue;
+            const int jb = jbase + j * SUB;
+
+            float gr[NO][NQ], gi[NO][NQ];
+    #pragma unroll
+            for (int o = 0; o < NO; ++o) {
+                const int base = (o / SUB + role.kx) * RY + j * SUB + (o % SUB) + role.ky;
+    #pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const float2 v = role.act ? tile[q * PS + base] : make_float2(0.0f, 0.0f);
+                    gr[o][q] = v.x;
+                    gi[o][q] = v.y;
+                }
+            }
+
+            for (uint32_t b0 = rb; b0 < re; b0 += 64) {
+                const int n = (int)min(64u, re - b0);
+                const VisRec my = recs[b0 + min(lane, n - 1)];
+                const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
+    #pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    if (8 * m >= n) break;
+                    const int src = 8 * m + (lane >> 3);
+                    const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
+                    const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
+                    const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
+                    float pr[8], pim[8];
+    #pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const int k = 8 * m + r;
+                        const int o = __builtin_amdgcn_readlane(o_l, k);
+                        const float ku = __shfl(tu, 8 * r + role.kx);
+                        const float kv = __shfl(tv, 8 * r + role.ky);
+                        float kw[NQ];
+    #pragma unroll
+                        for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
+                        float sr = 0.0f, si = 0.0f;
+    #pragma unroll
+                        for (int oo = 0; oo < NO; ++oo) {
+                            if (o == oo) {
+    #pragma unroll
+                                for (int q = 0; q < NQ; ++q) {
+                                    sr = fmaf(kw[q], gr[oo][q], sr);
+                                    si = fmaf(kw[q], gi[oo][q], si);
+                                }
                             }
                         }
+                        const float kk = ku * kv;
+                        pr[r] = sr * kk;
+                        pim[r] = si * kk;
                     }
-                    const float kk = ku * kv;
-                    pr[r] = sr * kk;
-                    pim[r] = si * kk;
-                }
-                // reduce-scatter: after the xor-32/16/8 halvings lane l holds
-                // record (l >> 3) & 7 summed over 8 lanes; xor 4/2/1 finish it
-                float a4r[4], a4i[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float sr = b5 ? pr[i] : pr[i + 4], si = b5 ? pim[i] : pim[i + 4];
-                    a4r[i] = (b5 ? pr[i + 4] : pr[i]) + __shfl_xor(sr, 32);
-                    a4i[i] = (b5 ? pim[i + 4] : pim[i]) + __shfl_xor(si, 32);
-                }
-                float a2r[2], a2i[2];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const float sr = b4 ? a4r[i] : a4r[i + 2], si = b4 ? a4i[i] : a4i[i + 2];
-                    a2r[i] = (b4 ? a4r[i + 2] : a4r[i]) + __shfl_xor(sr, 16);
-                    a2i[i] = (b4 ? a4i[i + 2] : a4i[i]) + __shfl_xor(si, 16);
-                }
-                float tr = (b3 ? a2r[1] : a2r[0]) + __shfl_xor(b3 ? a2r[0] : a2r[1], 8);
-                float ti = (b3 ? a2i[1] : a2i[0]) + __shfl_xor(b3 ? a2i[0] : a2i[1], 8);
-#pragma unroll
-                for (int msk = 4; msk > 0; msk >>= 1) {
-                    tr += __shfl_xor(tr, msk);
-                    ti += __shfl_xor(ti, msk);
-                }
-                const int rec = 8 * m + ((lane >> 3) & 7);
-                if ((lane & 7) == 0 && rec < n) {
-                    float2 *dst = acc + b0 + rec;
-                    float2 a = *dst;
-                    a.x += tr;
-                    a.y += ti;
-                    *dst = a;
+                    // reduce-scatter: after the xor-32/16/8 halvings lane l holds
+                    // record (l >> 3) & 7 summed over 8 lanes; xor 4/2/1 finish it
+                    float a4r[4], a4i[4];
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float sr = b5 ? pr[i] : pr[i + 4], si = b5 ? pim[i] : pim[i + 4];
+                        a4r[i] = (b5 ? pr[i + 4] : pr[i]) + __shfl_xor(sr, 32);
+                        a4i[i] = (b5 ? pim[i + 4] : pim[i]) + __shfl_xor(si, 32);
+                    }
+                    float a2r[2], a2i[2];
+    #pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const float sr = b4 ? a4r[i] : a4r[i + 2], si = b4 ? a4i[i] : a4i[i + 2];
+                        a2r[i] = (b4 ? a4r[i + 2] : a4r[i]) + __shfl_xor(sr, 16);
+                        a2i[i] = (b4 ? a4i[i + 2] : a4i[i]) + __shfl_xor(si, 16);
+                    }
+                    float tr = (b3 ? a2r[1] : a2r[0]) + __shfl_xor(b3 ? a2r[0] : a2r[1], 8);
+                    float ti = (b3 ? a2i[1] : a2i[0]) + __shfl_xor(b3 ? a2i[0] : a2i[1], 8);
+    #pragma unroll
+                    for (int msk = 4; msk > 0; msk >>= 1) {
+                        tr += __shfl_xor(tr, msk);
+                        ti += __shfl_xor(ti, msk);
+                    }
+                    const int rec = 8 * m + ((lane >> 3) & 7);
+                    if ((lane & 7) == 0 && rec < n) {
+                        float2 *dst = acc + b0 + rec;
+                        float2 a = *dst;
+                        a.x += tr;
+                        a.y += ti;
+                        *dst = a;
+                    }
                 }
             }
         }
@@ -879,76 +915,80 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
 // reduction sums the footprint.
 template <int W, bool WS, int SX, int SY>
 __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__ recs,
-                                               const Item *__restrict__ items, ItemOrder ord,
+                                               ItemSrc src,
                                                const float2 *__restrict__ grid, int p_lo,
                                                int p_hi, float2 *acc) {
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     using TS = TileShape<W, SX, SY>;
     constexpr int RX = TS::RX, RY = TS::RY, PS = TS::PLANE, PITCH = TS::PITCH;
     constexpr int NQ = WS ? W : 1;
-    const Item it = load_item(items, ord);
-    const int ntg = g.nty / g.grp;
-    const int tx = (int)it.tile / ntg, tg = (int)it.tile - tx * ntg;
-    const int ibase = tx * SX, jbase = tg * SY;
-    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-    const int lane = threadIdx.x;
-    for (int i = lane; i < NQ * RX * RY; i += 64) {
-        const int q = i / (RX * RY);
-        const int p = (int)it.p0 + q;
-        const int rem = i - q * RX * RY;
-        const int xl = rem / RY, yl = rem - (rem / RY) * RY;
-        int gx = ibase + xl;
-        if (gx >= g.ngx) gx -= g.ngx;
-        int gy = jbase + yl;
-        if (gy >= g.ngy) gy -= g.ngy;
-        tile[q * PS + xl * PITCH + yl] =
-            (p >= p_lo && p < p_hi)
-                ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
-                : make_float2(0.0f, 0.0f);
-    }
+    const uint32_t n_items = item_count(src);
+    const uint32_t stride = item_stride(n_items);
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        const Item it = load_item(src, w_it, n_items, stride);
+        const int ntg = g.nty / g.grp;
+        const int tx = (int)it.tile / ntg, tg = (int)it.tile - tx * ntg;
+        const int ibase = tx * SX, jbase = tg * SY;
+        const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+        const int lane = threadIdx.x;
+        for (int i = lane; i < NQ * RX * RY; i += 64) {
+            const int q = i / (RX * RY);
+            const int p = (int)it.p0 + q;
+            const int rem = i - q * RX * RY;
+            const int xl = rem / RY, yl = rem - (rem / RY) * RY;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            tile[q * PS + xl * PITCH + yl] =
+                (p >= p_lo && p < p_hi)
+                    ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
+                    : make_float2(0.0f, 0.0f);
+        }
 
-    const LaneRole<W> role(lane);
-    const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const int lane_off = role.kx * PITCH + role.ky - ibase * PITCH - jbase;
-    for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
-        const int n = (int)min(64u, it.e - b0);
-        const VisRec my = recs[b0 + min(lane, n - 1)];
-        float mine_r = 0.0f, mine_i = 0.0f;
-        for (int k = 0; k < n; ++k) {
-            const RecRegs rc = rec_at(my, k);
-            const float kval = role.taps(rc, ihw, bl);
-            const float ku = __shfl(kval, role.kx);
-            const float kv = __shfl(kval, W + role.ky);
-            const int off = lane_off + (int)(rc.ij & 0xffffu) * PITCH + (int)(rc.ij >> 16);
-            float kw[NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(kval, 2 * W + q) : 1.0f;
-            float sr = 0.0f, si = 0.0f;
-            if (role.act) {
-                float2 a[NQ];
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) a[q] = tile[q * PS + off];
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    sr = fmaf(kw[q], a[q].x, sr);
-                    si = fmaf(kw[q], a[q].y, si);
+        const LaneRole<W> role(lane);
+        const float ihw = g.inv_half_w, bl = g.beta_l2e;
+        const int lane_off = role.kx * PITCH + role.ky - ibase * PITCH - jbase;
+        for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+            const int n = (int)min(64u, it.e - b0);
+            const VisRec my = recs[b0 + min(lane, n - 1)];
+            float mine_r = 0.0f, mine_i = 0.0f;
+            for (int k = 0; k < n; ++k) {
+                const RecRegs rc = rec_at(my, k);
+                const float kval = role.taps(rc, ihw, bl);
+                const float ku = __shfl(kval, role.kx);
+                const float kv = __shfl(kval, W + role.ky);
+                const int off = lane_off + (int)(rc.ij & 0xffffu) * PITCH + (int)(rc.ij >> 16);
+                float kw[NQ];
+    #pragma unroll
+                for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(kval, 2 * W + q) : 1.0f;
+                float sr = 0.0f, si = 0.0f;
+                if (role.act) {
+                    float2 a[NQ];
+    #pragma unroll
+                    for (int q = 0; q < NQ; ++q) a[q] = tile[q * PS + off];
+    #pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        sr = fmaf(kw[q], a[q].x, sr);
+                        si = fmaf(kw[q], a[q].y, si);
+                    }
+                }
+                const float kk = role.act ? ku * kv : 0.0f;
+                sr *= kk;
+                si *= kk;
+                for (int o = 32; o > 0; o >>= 1) {
+                    sr += __shfl_xor(sr, o);
+                    si += __shfl_xor(si, o);
+                }
+                if (k == lane) {
+                    mine_r = sr;
+                    mine_i = si;
                 }
             }
-            const float kk = role.act ? ku * kv : 0.0f;
-            sr *= kk;
-            si *= kk;
-            for (int o = 32; o > 0; o >>= 1) {
-                sr += __shfl_xor(sr, o);
-                si += __shfl_xor(si, o);
+            if (lane < n) {
+                atomicAdd(&acc[b0 + lane].x, mine_r);
+                atomicAdd(&acc[b0 + lane].y, mine_i);
             }
-            if (k == lane) {
-                mine_r = sr;
-                mine_i = si;
-            }
-        }
-        if (lane < n) {
-            atomicAdd(&acc[b0 + lane].x, mine_r);
-            atomicAdd(&acc[b0 + lane].y, mine_i);
         }
     }
 }
@@ -1133,18 +1173,22 @@ __global__ void k_zero_vis(int64_t nrow, int nchan, VT *vis, int64_t vrs, int64_
     vis[row * vrs + chan * vcs] = z;
 }
 
+// record factor and scatter back to visibility order; the record count is
+// read from device memory when `ndev` is given (pipelined plans)
 template <class VT>
-__global__ void k_finalize(int64_t nrec, int nchan, const VisRec *__restrict__ recs,
-                           const float2 *__restrict__ acc, VT *vis, int64_t vrs, int64_t vcs,
-                           int accumulate) {
-    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
-    const VisRec rc = recs[r];
-    const float2 a = acc[r];
-    const float2 v = make_float2(rc.cre * a.x - rc.cim * a.y, rc.cre * a.y + rc.cim * a.x);
-    const int64_t row = rc.idx / (uint32_t)nchan;
-    const int chan = (int)(rc.idx - row * nchan);
-    store_vis(vis + row * vrs + chan * vcs, v, accumulate);
+__global__ void k_finalize(int64_t nrec, const unsigned *__restrict__ ndev, int nchan,
+                           const VisRec *__restrict__ recs, const float2 *__restrict__ acc, VT *vis,
+                           int64_t vrs, int64_t vcs, int accumulate) {
+    const int64_t n = ndev ? (int64_t)*ndev : nrec;
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const VisRec rc = recs[r];
+        const float2 a = acc[r];
+        const float2 v = make_float2(rc.cre * a.x - rc.cim * a.y, rc.cre * a.y + rc.cim * a.x);
+        const int64_t row = rc.idx / (uint32_t)nchan;
+        const int chan = (int)(rc.idx - row * nchan);
+        store_vis(vis + row * vrs + chan * vcs, v, accumulate);
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -1293,17 +1337,30 @@ struct StageTimer {
     }
 };
 
+// One visibility part: a contiguous row range with its own buckets and work
+// items.  Its records occupy recs[vbase, vbase + nvis) of the call's record
+// array (positions are part-local offsets).
+struct Part {
+    int64_t r0 = 0, r1 = 0, vbase = 0, nvis = 0;
+    unsigned *hist = nullptr, *offs = nullptr, *nch = nullptr, *ioffs = nullptr;
+    unsigned long long *nbad = nullptr;
+    Item *items = nullptr;
+    unsigned *meta = nullptr;  // device: see k_part_meta
+    // host copies (filled by read_part_meta; synchronous plans only)
+    int64_t nrec = 0, nitems = 0;
+    std::vector<unsigned> p0_items;
+};
+
 struct Plan {
     Geo g;
     VisRec *recs = nullptr;
-    Item *items = nullptr;
-    int64_t nrec = 0;
-    int64_t nitems = 0;
-    std::vector<unsigned> p0_items;  // first item of every first-plane value
+    std::vector<Part> parts;
+    bool pipelined = false;          // row parts, persistent launches, no host syncs
+    bool aux_bucketing = false;      // bucketing on the auxiliary stream
     int chunk_planes = 1;            // planes resident per pass
     int row_lo = 0, row_hi = 0;      // grid rows (x) the visibilities reach
     unsigned chunk = kChunkMin;      // max records per work item
-    const unsigned *offs = nullptr;  // bucket start offsets (the scan of the histogram)
+    int64_t nrec = 0, nitems = 0;    // totals
     float2 *grid = nullptr;
     float2 *spec = nullptr;  // T[q][iy][kx]: transposed y-spectra (pruned FFT)
 };
@@ -1337,8 +1394,33 @@ static size_t grid_budget_bytes() {
     return free_b / 2;
 }
 
-// Geometry, bucketing and work items shared by both directions.
-static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
+// SDP_HIP_PIPELINE: 0 (default) = bucket on the caller's stream; 1 = dirty2ms
+// buckets on an auxiliary stream under its screen + FFT; 2 = additionally
+// split the rows in two parts bucketed on the auxiliary stream while the
+// previous part (de)grids, with persistent launches reading the device-side
+// item counts.  Both overlaps measured slower on C2: the
+// bucketing is memory/atomic bound and contends with the FFT, and the row
+// halves add 24% work items.
+constexpr int kPipelineParts = 2;
+
+static hipStream_t aux_stream() {
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = streams.find(dev);
+    if (it != streams.end()) return it->second;
+    hipStream_t s;
+    SDP_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    streams[dev] = s;
+    return s;
+}
+
+// Geometry shared by both directions: kernel, padded grid, w planes, bucket
+// granularity, row band, plane chunking, part split.  One host sync (uvw and
+// frequency extremes).
+static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     SDP_REQUIRE(in.nx > 0 && in.ny > 0 && in.nx % 2 == 0 && in.ny % 2 == 0,
                 "npix_x and npix_y must be positive and even");
     SDP_REQUIRE(in.px > 0 && in.py > 0, "pixel sizes must be positive");
@@ -1361,14 +1443,15 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.su = (in.flags & SDP_HIP_FLIP_UW) ? -1.0 : 1.0;
     g.nchan = in.nchan;
     g.nrow = in.nrow;
-    g.sub = kTileCoarse;  // refined below once the plane count is known
+    g.dbg = std::getenv("SDP_HIP_DBG") ? std::atoi(std::getenv("SDP_HIP_DBG")) : 0;
 
-    // frequency extremes (host) and uvw bounds (device)
+    // uvw and frequency extremes (device) -> host
     double *hb = pinned_host<double>(0, 6);
     {
         auto *part = scratch<double>("bounds_part", 4 * kBoundsBlocks);
         auto *bnd = scratch<double>("bounds", 6);
-        const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(grid1d(in.nrow, 256), kBoundsBlocks));
+        const int nb = (int)std::max<int64_t>(
+            1, std::min<int64_t>(grid1d(in.nrow, 256), kBoundsBlocks));
         k_bounds<<<nb, 256, 0, st>>>(in.uvw, in.uvw_rs, in.nrow, g.su, part);
         k_bounds_final<<<1, 256, 0, st>>>(nb, part, in.freq, in.nchan, bnd);
         SDP_HIP_CHECK(hipMemcpyAsync(hb, bnd, 6 * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1418,83 +1501,7 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.grp = g.sub == kTileFine ? kGroupFine : 1;  // nty is a multiple of kGridAlign / sub
     SDP_REQUIRE((double)g.ntiles * g.nps < 4.0e9, "too many (plane, tile) buckets");
 
-    // ---- bucketing
-    const int64_t nvis = in.nrow * (int64_t)in.nchan;
-    const size_t nkeys = (size_t)g.ntiles * g.nps;
-    unsigned *hist = scratch<unsigned>("hist", nkeys + 1);
-    unsigned *offs = scratch<unsigned>("offs", nkeys + 1);
-    auto *nbad = scratch<unsigned long long>("nbad", 1);
-    SDP_HIP_CHECK(hipMemsetAsync(hist, 0, (nkeys + 1) * sizeof(unsigned), st));
-    SDP_HIP_CHECK(hipMemsetAsync(nbad, 0, sizeof(unsigned long long), st));
-
-    const unsigned nb = grid1d(nvis, 256);
-    uint2 *kr = scratch<uint2>("key_rank", std::max<int64_t>(nvis, 1));
-    auto launch_bucket = [&](auto scatter_tag, unsigned *counter, VisRec *recs) {
-        constexpr bool S = decltype(scatter_tag)::value;
-        if (in.vis_dtype == SDP_HIP_C128) {
-            if (grid_mode)
-                k_bucket<double2, S, true><<<nb, 256, 0, st>>>(
-                    g, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis, in.vrs, in.vcs,
-                    in.wgt, in.wrs, in.wcs, counter, kr, recs, nbad);
-            else
-                k_bucket<double2, S, false><<<nb, 256, 0, st>>>(
-                    g, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs, in.wcs,
-                    counter, kr, recs, nbad);
-        } else {
-            if (grid_mode)
-                k_bucket<float2, S, true><<<nb, 256, 0, st>>>(
-                    g, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis, in.vrs, in.vcs,
-                    in.wgt, in.wrs, in.wcs, counter, kr, recs, nbad);
-            else
-                k_bucket<float2, S, false><<<nb, 256, 0, st>>>(
-                    g, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs, in.wcs,
-                    counter, kr, recs, nbad);
-        }
-    };
-    if (nvis > 0) launch_bucket(std::false_type{}, hist, nullptr);
-
-    unsigned *nch = scratch<unsigned>("nch", nkeys + 1);
-    unsigned *ioffs = scratch<unsigned>("ioffs", nkeys + 1);
-    size_t tmp_bytes = 0;
-    SDP_HIP_CHECK(
-        hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, hist, offs, (int)(nkeys + 1), st));
-    void *tmp = scratch<char>("scan_tmp", tmp_bytes + 16);
-    size_t tb = tmp_bytes + 16;
-    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, hist, offs, (int)(nkeys + 1), st));
-    P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
-    if (nvis > 0) launch_bucket(std::true_type{}, offs, P.recs);
-
-    // ---- work items (p0-major, so a first-plane range is a contiguous item range)
-    const int64_t ngroups = (int64_t)nkeys / g.grp;
-    const int gpp = g.ntiles / g.grp;  // groups per first-plane value
-    SDP_HIP_CHECK(hipMemsetAsync(nch + ngroups, 0, sizeof(unsigned), st));
-    // records per item: large enough to amortise the tile flush over dense
-    // tiles, small enough to leave >= ~16k items for the 256 CUs
-    P.chunk = (unsigned)std::min<int64_t>(kChunkMax, std::max<int64_t>(kChunkMin, nvis / 16384));
-    if (const char *e = std::getenv("SDP_HIP_CHUNK"))
-        if (std::atoi(e) >= 64) P.chunk = (unsigned)std::atoi(e);
-    k_items_count<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, offs, P.chunk, nch);
-    tb = tmp_bytes + 16;
-    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, nch, ioffs, (int)(ngroups + 1), st));
-    unsigned *meta = scratch<unsigned>("plan_meta", g.nps + 4);
-    k_plan_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(nbad, offs + nkeys, ioffs, gpp, g.nps,
-                                                      meta);
-    unsigned *hm = pinned_host<unsigned>(64, g.nps + 4);
-    SDP_HIP_CHECK(hipMemcpyAsync(hm, meta, (g.nps + 4) * sizeof(unsigned), hipMemcpyDeviceToHost,
-                                 st));
-    SDP_HIP_CHECK(hipStreamSynchronize(st));
-    const unsigned long long nbad_h = (unsigned long long)hm[0] | ((unsigned long long)hm[1] << 32);
-    const unsigned nrec_h = hm[2];
-    P.p0_items.assign(hm + 3, hm + 3 + g.nps + 1);
-    SDP_REQUIRE(nbad_h == 0, "visibilities outside the padded grid");
-    P.nrec = nrec_h;
-    P.nitems = P.p0_items[g.nps];
-    P.items = scratch<Item>("items", std::max<int64_t>(P.nitems, 1));
-    k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, gpp, offs, ioffs, P.chunk,
-                                                       P.items);
-    P.offs = offs;
-
-    // ---- grid rows reached by any footprint (centred storage)
+    // grid rows reached by any footprint (centred storage)
     {
         const double amax = umax * in.px * g.ngx;
         const int reach = (int)std::ceil(amax) + g.W + 1;
@@ -1506,36 +1513,184 @@ static Plan make_plan(const Inputs &in, bool grid_mode, hipStream_t st) {
         }
     }
 
-    // ---- plane chunking against the grid memory budget
+    // plane chunking against the grid memory budget
     const size_t plane_bytes = ((size_t)g.ngx * g.ngy + (size_t)g.ny * g.ngx) * sizeof(float2);
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes() / plane_bytes);
     P.chunk_planes = std::min(cp, g.nplanes);
     P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy);
     P.spec = scratch<float2>("spec", (size_t)P.chunk_planes * g.ny * g.ngx);
+
+    // records per item: large enough to amortise the tile flush over dense
+    // tiles, small enough to leave >= ~16k items for the 256 CUs
+    const int64_t nvis = in.nrow * (int64_t)in.nchan;
+    P.chunk = (unsigned)std::min<int64_t>(kChunkMax, std::max<int64_t>(kChunkMin, nvis / 16384));
+    if (const char *e = std::getenv("SDP_HIP_CHUNK"))
+        if (std::atoi(e) >= 64) P.chunk = (unsigned)std::atoi(e);
+
+    // part split
+    const char *pe = std::getenv("SDP_HIP_PIPELINE");
+    const int pmode = pe ? std::atoi(pe) : 0;
+    P.pipelined = pmode == 2 && g.sub == kTileFine && P.chunk_planes == g.nplanes && in.nrow >= 2;
+    P.aux_bucketing = P.pipelined || (pmode == 1 && !grid_mode);
+    const int nparts = P.pipelined ? kPipelineParts : 1;
+    for (int i = 0; i < nparts; ++i) {
+        Part pt;
+        pt.r0 = in.nrow * i / nparts;
+        pt.r1 = in.nrow * (i + 1) / nparts;
+        pt.vbase = pt.r0 * in.nchan;
+        pt.nvis = (pt.r1 - pt.r0) * in.nchan;
+        P.parts.push_back(pt);
+    }
+    P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
     return P;
 }
 
-// Item range whose W-plane windows intersect planes [p_lo, p_hi).
-static std::pair<unsigned, unsigned> chunk_items(const Plan &P, int p_lo, int p_hi) {
+// Bucketing of one part on stream `st` (no host sync): histogram with ranks,
+// scan, scatter of the 32-byte records, work items, part metadata.
+static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipStream_t st) {
+    const Geo &g = P.g;
+    Part &pt = P.parts[ip];
+    const std::string sfx = "#" + std::to_string(ip);
+    const size_t nkeys = (size_t)g.ntiles * g.nps;
+    const int64_t ngroups = (int64_t)nkeys / g.grp;
+    const int gpp = g.ntiles / g.grp;  // groups per first-plane value
+    pt.hist = scratch<unsigned>("hist" + sfx, nkeys + 1);
+    pt.offs = scratch<unsigned>("offs" + sfx, nkeys + 1);
+    pt.nch = scratch<unsigned>("nch" + sfx, ngroups + 1);
+    pt.ioffs = scratch<unsigned>("ioffs" + sfx, ngroups + 1);
+    pt.nbad = scratch<unsigned long long>("nbad" + sfx, 1);
+    pt.meta = scratch<unsigned>("meta" + sfx, g.nps + 5);
+    const int64_t icap = std::min<int64_t>(ngroups, pt.nvis) + pt.nvis / P.chunk + 1;
+    pt.items = scratch<Item>("items" + sfx, icap);
+    uint2 *kr = scratch<uint2>("key_rank", std::max<int64_t>(in.nrow * (int64_t)in.nchan, 1)) +
+                pt.vbase;
+    VisRec *recs = P.recs + pt.vbase;
+    SDP_HIP_CHECK(hipMemsetAsync(pt.hist, 0, (nkeys + 1) * sizeof(unsigned), st));
+    SDP_HIP_CHECK(hipMemsetAsync(pt.nbad, 0, sizeof(unsigned long long), st));
+    SDP_HIP_CHECK(hipMemsetAsync(pt.nch + ngroups, 0, sizeof(unsigned), st));
+
+    const unsigned nb = grid1d(std::max<int64_t>(pt.nvis, 1), 256);
+    auto launch_bucket = [&](auto scatter_tag, unsigned *counter) {
+        constexpr bool S = decltype(scatter_tag)::value;
+        VisRec *out = S ? recs : nullptr;
+        if (in.vis_dtype == SDP_HIP_C128) {
+            if (grid_mode)
+                k_bucket<double2, S, true><<<nb, 256, 0, st>>>(
+                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
+                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, counter, kr, out, pt.nbad);
+            else
+                k_bucket<double2, S, false><<<nb, 256, 0, st>>>(
+                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
+                    in.wcs, counter, kr, out, pt.nbad);
+        } else {
+            if (grid_mode)
+                k_bucket<float2, S, true><<<nb, 256, 0, st>>>(
+                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
+                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, counter, kr, out, pt.nbad);
+            else
+                k_bucket<float2, S, false><<<nb, 256, 0, st>>>(
+                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
+                    in.wcs, counter, kr, out, pt.nbad);
+        }
+    };
+    if (pt.nvis > 0) launch_bucket(std::false_type{}, pt.hist);
+    size_t tmp_bytes = 0;
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, pt.hist, pt.offs,
+                                                   (int)(nkeys + 1), st));
+    void *tmp = scratch<char>("scan_tmp" + sfx, tmp_bytes + 16);
+    size_t tb = tmp_bytes + 16;
+    SDP_HIP_CHECK(
+        hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.hist, pt.offs, (int)(nkeys + 1), st));
+    if (pt.nvis > 0) launch_bucket(std::true_type{}, pt.offs);
+
+    // work items (p0-major, so a first-plane range is a contiguous item range)
+    k_items_count<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, pt.offs, P.chunk, pt.nch);
+    tb = tmp_bytes + 16;
+    SDP_HIP_CHECK(
+        hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.nch, pt.ioffs, (int)(ngroups + 1), st));
+    k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, gpp, pt.offs, pt.ioffs,
+                                                       P.chunk, pt.items);
+    k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys, pt.ioffs, gpp,
+                                                      g.nps, pt.meta);
+    SDP_HIP_CHECK(hipGetLastError());
+}
+
+// Host copy of every part's metadata (one sync): counts, the first-plane item
+// offsets (plane-chunked launches need them) and the out-of-grid check.
+static void read_part_meta(Plan &P, hipStream_t st) {
+    const int nps = P.g.nps;
+    const size_t per = (size_t)nps + 5;
+    unsigned *hm = pinned_host<unsigned>(64, per * P.parts.size());
+    for (size_t i = 0; i < P.parts.size(); ++i)
+        SDP_HIP_CHECK(hipMemcpyAsync(hm + i * per, P.parts[i].meta, per * sizeof(unsigned),
+                                     hipMemcpyDeviceToHost, st));
+    SDP_HIP_CHECK(hipStreamSynchronize(st));
+    P.nrec = P.nitems = 0;
+    for (size_t i = 0; i < P.parts.size(); ++i) {
+        const unsigned *m = hm + i * per;
+        const unsigned long long nbad = (unsigned long long)m[0] | ((unsigned long long)m[1] << 32);
+        SDP_REQUIRE(nbad == 0, "visibilities outside the padded grid");
+        Part &pt = P.parts[i];
+        pt.nrec = m[2];
+        pt.nitems = m[3];
+        pt.p0_items.assign(m + 4, m + 4 + nps + 1);
+        P.nrec += pt.nrec;
+        P.nitems += pt.nitems;
+    }
+}
+
+// Item range of a part whose W-plane windows intersect planes [p_lo, p_hi).
+static std::pair<unsigned, unsigned> chunk_items(const Plan &P, const Part &pt, int p_lo,
+                                                 int p_hi) {
     const int a = std::max(0, p_lo - (P.g.do_w ? P.g.W : 1) + 1);
     const int b = std::min(P.g.nps - 1, p_hi - 1);
     if (a > b) return {0u, 0u};
-    return {P.p0_items[a], P.p0_items[b + 1]};
+    return {pt.p0_items[a], pt.p0_items[b + 1]};
+}
+
+// Launch shape of one gridding pass over a part: one workgroup per item when
+// the host knows the range, else a persistent grid reading the count.
+struct Launch {
+    ItemSrc src;
+    unsigned blocks;
+};
+
+static unsigned persistent_blocks(const void *fn, int threads, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::pair<const void *, size_t>, unsigned> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair(fn, lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int dev = 0, ncu = 0, per = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    SDP_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    SDP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds));
+    unsigned nb = (unsigned)std::max(1, ncu * std::max(1, per));
+    if (const char *e = std::getenv("SDP_HIP_PBLOCKS")) nb = (unsigned)std::max(1, std::atoi(e));
+    else nb *= 8;  // several workgroups per slot: the hardware balances the uneven items
+    cache[key] = nb;
+    return nb;
+}
+
+static Launch part_launch(const Plan &P, const Part &pt, int p_lo, int p_hi, const void *fn,
+                          int threads, size_t lds) {
+    Launch L;
+    if (P.pipelined) {
+        L.src = ItemSrc{pt.items, 0u, pt.meta + 3};
+        L.blocks = persistent_blocks(fn, threads, lds);
+    } else {
+        const auto r = chunk_items(P, pt, p_lo, p_hi);
+        L.src = ItemSrc{pt.items + r.first, r.second - r.first, nullptr};
+        L.blocks = r.second - r.first;
+    }
+    return L;
 }
 
 static void allow_lds(const void *fn, size_t bytes) {
     if (bytes > 65536)
         SDP_HIP_CHECK(
             hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-}
-
-static ItemOrder item_order(uint32_t n) {
-    static const uint32_t primes[] = {7919u, 104729u, 1299709u, 15485863u, 179424673u};
-    if (const char *e = std::getenv("SDP_HIP_ITEM_ORDER"))
-        if (std::atoi(e) == 0) return ItemOrder{std::max<uint32_t>(n, 1u), 1u};
-    for (uint32_t p : primes)
-        if (n <= 1 || n % p != 0) return ItemOrder{std::max<uint32_t>(n, 1u), p};
-    return ItemOrder{n, 1u};
 }
 
 // waves per gridding workgroup (planes split across them); SDP_HIP_GRID_WAVES
@@ -1548,74 +1703,77 @@ static int grid_waves(int W, bool do_w) {
 }
 
 template <int W, bool WS, int NWV>
-static void launch_grid_n(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
-                          hipStream_t st) {
+static void launch_grid_n(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
     constexpr int NQ = WS ? W : 1;
     const size_t lds = (size_t)((NQ + NWV - 1) / NWV * NWV) *
                        TileShape<W, kTileCoarse>::PLANE * sizeof(float2);
-    allow_lds((const void *)k_grid_lds<W, WS, NWV>, lds);
-    k_grid_lds<W, WS, NWV><<<r.second - r.first, 64 * NWV, lds, st>>>(
-        P.g, P.recs, P.items + r.first, item_order(r.second - r.first), (float *)P.grid, p_lo,
-        p_hi);
+    const void *fn = (const void *)k_grid_lds<W, WS, NWV>;
+    allow_lds(fn, lds);
+    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64 * NWV, lds);
+    if (L.blocks == 0) return;
+    k_grid_lds<W, WS, NWV><<<L.blocks, 64 * NWV, lds, st>>>(P.g, P.recs + pt.vbase, L.src,
+                                                          (float *)P.grid, p_lo, p_hi);
 }
 
 template <int W, bool WS>
-static void launch_grid_reg(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
-                            hipStream_t st) {
+static void launch_grid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) *
                        TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
-    const int dbg = std::getenv("SDP_HIP_DBG") ? std::atoi(std::getenv("SDP_HIP_DBG")) : 0;
-    k_grid_reg<W, WS><<<r.second - r.first, 64, lds, st>>>(P.g, P.recs, P.items + r.first,
-                                                          item_order(r.second - r.first), P.offs,
-                                                          (float *)P.grid, p_lo, p_hi, dbg);
+    const void *fn = (const void *)k_grid_reg<W, WS>;
+    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
+    if (L.blocks == 0) return;
+    k_grid_reg<W, WS><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
+                                                (float *)P.grid, p_lo, p_hi, P.g.dbg);
 }
 
 template <int W>
-static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
-    const auto r = chunk_items(P, p_lo, p_hi);
-    if (r.second <= r.first) return;
+static void launch_grid(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
     if (P.g.sub == kTileFine) {
-        if (P.g.do_w) return launch_grid_reg<W, true>(P, r, p_lo, p_hi, st);
-        return launch_grid_reg<W, false>(P, r, p_lo, p_hi, st);
+        if (P.g.do_w) return launch_grid_reg<W, true>(P, pt, p_lo, p_hi, st);
+        return launch_grid_reg<W, false>(P, pt, p_lo, p_hi, st);
     }
-    if (!P.g.do_w) return launch_grid_n<W, false, 1>(P, r, p_lo, p_hi, st);
+    if (!P.g.do_w) return launch_grid_n<W, false, 1>(P, pt, p_lo, p_hi, st);
     switch (grid_waves(W, true)) {
-        case 1: return launch_grid_n<W, true, 1>(P, r, p_lo, p_hi, st);
-        case 4: return launch_grid_n<W, true, (W >= 4 ? 4 : 2)>(P, r, p_lo, p_hi, st);
-        default: return launch_grid_n<W, true, 2>(P, r, p_lo, p_hi, st);
+        case 1: return launch_grid_n<W, true, 1>(P, pt, p_lo, p_hi, st);
+        case 4: return launch_grid_n<W, true, (W >= 4 ? 4 : 2)>(P, pt, p_lo, p_hi, st);
+        default: return launch_grid_n<W, true, 2>(P, pt, p_lo, p_hi, st);
     }
 }
 
 template <int W, bool WS, int SX, int SY>
-static void launch_degrid_n(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
-                            float2 *acc, hipStream_t st) {
+static void launch_degrid_n(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
+                            hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) * TileShape<W, SX, SY>::PLANE * sizeof(float2);
-    allow_lds((const void *)k_degrid<W, WS, SX, SY>, lds);
-    k_degrid<W, WS, SX, SY><<<r.second - r.first, 64, lds, st>>>(
-        P.g, P.recs, P.items + r.first, item_order(r.second - r.first), P.grid, p_lo, p_hi, acc);
+    const void *fn = (const void *)k_degrid<W, WS, SX, SY>;
+    allow_lds(fn, lds);
+    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
+    if (L.blocks == 0) return;
+    k_degrid<W, WS, SX, SY><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, P.grid,
+                                                      p_lo, p_hi, acc + pt.vbase);
 }
 
 template <int W, bool WS>
-static void launch_degrid_reg(const Plan &P, std::pair<unsigned, unsigned> r, int p_lo, int p_hi,
-                              float2 *acc, hipStream_t st) {
+static void launch_degrid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
+                              hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) *
                        TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
-    k_degrid_reg<W, WS><<<r.second - r.first, 64, lds, st>>>(
-        P.g, P.recs, P.items + r.first, item_order(r.second - r.first), P.offs, P.grid, p_lo, p_hi,
-        acc);
+    const void *fn = (const void *)k_degrid_reg<W, WS>;
+    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
+    if (L.blocks == 0) return;
+    k_degrid_reg<W, WS><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs, P.grid,
+                                                  p_lo, p_hi, acc + pt.vbase);
 }
 
 template <int W>
-static void launch_degrid(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
-    const auto r = chunk_items(P, p_lo, p_hi);
-    if (r.second <= r.first) return;
+static void launch_degrid(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
+                          hipStream_t st) {
     if (P.g.sub == kTileFine) {
-        if (P.g.do_w) return launch_degrid_reg<W, true>(P, r, p_lo, p_hi, acc, st);
-        return launch_degrid_reg<W, false>(P, r, p_lo, p_hi, acc, st);
+        if (P.g.do_w) return launch_degrid_reg<W, true>(P, pt, p_lo, p_hi, acc, st);
+        return launch_degrid_reg<W, false>(P, pt, p_lo, p_hi, acc, st);
     }
     if (P.g.do_w)
-        return launch_degrid_n<W, true, kTileCoarse, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
-    return launch_degrid_n<W, false, kTileCoarse, kTileCoarse>(P, r, p_lo, p_hi, acc, st);
+        return launch_degrid_n<W, true, kTileCoarse, kTileCoarse>(P, pt, p_lo, p_hi, acc, st);
+    return launch_degrid_n<W, false, kTileCoarse, kTileCoarse>(P, pt, p_lo, p_hi, acc, st);
 }
 
 #define SDP_W_DISPATCH(W, CALL) \
@@ -1642,6 +1800,8 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
     info->nitems = P.nitems;
     info->plane_chunk = P.chunk_planes;
     info->bucket = P.g.sub;
+    info->grid_launches = (int)P.parts.size() *
+                          ((P.g.nplanes + P.chunk_planes - 1) / P.chunk_planes);
 }
 
 // Pruned 2-D FFT of each resident plane.  The uv grid is non-zero only in
@@ -1689,6 +1849,39 @@ static dim3 tr_grid(const Geo &g, int xrows, int np) {
                 (unsigned)np);
 }
 
+// Bucket every part.  Synchronous plans bucket on `st` and read the
+// metadata back (plane-chunked launches need the item offsets).  Pipelined
+// plans bucket on the auxiliary stream after an event on `st` (inputs ready)
+// and record one event per part for the consumer launches to wait on.
+static std::vector<hipEvent_t> bucket_parts(Plan &P, const Inputs &in, bool grid_mode,
+                                            hipStream_t st) {
+    std::vector<hipEvent_t> ev;
+    if (!P.aux_bucketing) {
+        for (size_t i = 0; i < P.parts.size(); ++i) bucket_part(P, (int)i, in, grid_mode, st);
+        read_part_meta(P, st);
+        return ev;
+    }
+    hipStream_t aux = aux_stream();
+    hipEvent_t ready;
+    SDP_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    SDP_HIP_CHECK(hipEventRecord(ready, st));
+    SDP_HIP_CHECK(hipStreamWaitEvent(aux, ready, 0));
+    SDP_HIP_CHECK(hipEventDestroy(ready));
+    for (size_t i = 0; i < P.parts.size(); ++i) {
+        bucket_part(P, (int)i, in, grid_mode, aux);
+        hipEvent_t e;
+        SDP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        SDP_HIP_CHECK(hipEventRecord(e, aux));
+        ev.push_back(e);
+    }
+    return ev;
+}
+
+static void release_events(std::vector<hipEvent_t> &ev) {
+    for (auto e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+}
+
 static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
                      sdp_hip_wgrid_info *info, hipStream_t st) {
     SDP_REQUIRE(in.vis == nullptr || in.vis_dtype == SDP_HIP_C64 ||
@@ -1696,24 +1889,28 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
                 "vis must be complex64 or complex128");
     StageTimer tm(st);
     tm.mark();
-    Plan P = make_plan(in, true, st);
+    Plan P = plan_geometry(in, true, st);
     const Geo &g = P.g;
     const double *tab = phi_table(g.W, g.beta, st);
-    tm.mark();
+    std::vector<hipEvent_t> ev = bucket_parts(P, in, true, st);
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
-    const size_t plane_elems = (size_t)g.ngx * g.ngy;
-    float tzero = 0, tgrid = 0, tfft = 0, tscr = 0;
+    float tprep = 0, tgrid = 0, tfft = 0, tscr = 0;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
-        StageTimer t2(st);
-        t2.mark();
         zero_band(P, np, st);
-        t2.mark();
-#define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, p_lo, p_hi, st)
-        SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
+        for (size_t i = 0; i < P.parts.size(); ++i) {
+            if (!ev.empty()) SDP_HIP_CHECK(hipStreamWaitEvent(st, ev[i], 0));
+            StageTimer tg(st);
+            tg.mark();
+#define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, P.parts[i], p_lo, p_hi, st)
+            SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
 #undef SDP_LAUNCH_GRID
-        SDP_HIP_CHECK(hipGetLastError());
+            SDP_HIP_CHECK(hipGetLastError());
+            tg.mark();
+            tgrid += tg.ms(0, 1);
+        }
+        StageTimer t2(st);
         t2.mark();
         fft_rows_y(P, np, HIPFFT_BACKWARD, st);
         k_tr_grid_to_t<<<tr_grid(g, g.ngx, np), dim3(kTr, 8), 0, st>>>(g, P.grid, P.spec,
@@ -1726,15 +1923,18 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
                                             (accumulate || p_lo > 0) ? 1 : 0, tab);
         SDP_HIP_CHECK(hipGetLastError());
         t2.mark();
-        tzero += t2.ms(0, 1);
-        tgrid += t2.ms(1, 2);
-        tfft += t2.ms(2, 3);
-        tscr += t2.ms(3, 4);
+        tfft += t2.ms(0, 1);
+        tscr += t2.ms(1, 2);
     }
     tm.mark();
+    if (P.pipelined) read_part_meta(P, st);
+    release_events(ev);
     fill_info(P, info);
     if (info) {
-        info->ms_prep = tm.ms(0, 1) + tzero;
+        // everything on the call's stream that is not gridding, FFT or screen:
+        // geometry, bucketing not hidden behind gridding, band zeroing
+        tprep = tm.ms(0, 1) - tgrid - tfft - tscr;
+        info->ms_prep = tm.on ? tprep : 0.0f;
         info->ms_grid = tgrid;
         info->ms_fft = tfft;
         info->ms_screen = tscr;
@@ -1747,10 +1947,11 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
                 "vis must be complex64 or complex128");
     StageTimer tm(st);
     tm.mark();
-    Plan P = make_plan(in, false, st);
+    Plan P = plan_geometry(in, false, st);
     const Geo &g = P.g;
     const double *tab = phi_table(g.W, g.beta, st);
-    tm.mark();
+    // the bucketing runs on the aux stream under the screen + FFT
+    std::vector<hipEvent_t> ev = bucket_parts(P, in, false, st);
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
     const int64_t nvis = in.nrow * (int64_t)in.nchan;
     if (!accumulate && nvis > 0) {
@@ -1761,15 +1962,14 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
             k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, st>>>(
                 in.nrow, in.nchan, (float2 *)vis, in.vrs, in.vcs);
     }
-    float2 *acc = scratch<float2>("degrid_acc", std::max<int64_t>(P.nrec, 1));
-    SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(P.nrec, 1) * sizeof(float2), st));
-    const size_t plane_elems = (size_t)g.ngx * g.ngy;
-    float tzero = 0, tgrid = 0, tfft = 0, tscr = 0;
+    float2 *acc = scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));
+    SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(nvis, 1) * sizeof(float2), st));
+    float tgrid = 0, tfft = 0, tscr = 0;
+    bool waited = false;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
         StageTimer t2(st);
-        t2.mark();
         zero_band(P, np, st);
         t2.mark();
         const dim3 grd(grid1d(g.ngx, 256), g.ny);
@@ -1783,29 +1983,44 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         SDP_HIP_CHECK(hipGetLastError());
         fft_rows_y(P, np, HIPFFT_FORWARD, st);
         t2.mark();
-#define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, acc, st)
-        SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
+        tscr += t2.ms(0, 1);
+        tfft += t2.ms(1, 2);
+        if (P.aux_bucketing && !P.pipelined && !waited)
+            read_part_meta(P, aux_stream());  // host waits for the bucketing only
+        for (size_t i = 0; i < P.parts.size(); ++i) {
+            if (!ev.empty() && !waited) SDP_HIP_CHECK(hipStreamWaitEvent(st, ev[i], 0));
+            StageTimer tg(st);
+            tg.mark();
+#define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, P.parts[i], p_lo, p_hi, acc, st)
+            SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
 #undef SDP_LAUNCH_DEGRID
-        SDP_HIP_CHECK(hipGetLastError());
-        t2.mark();
-        tzero += t2.ms(0, 1);
-        tscr += t2.ms(1, 2);
-        tfft += t2.ms(2, 3);
-        tgrid += t2.ms(3, 4);
+            SDP_HIP_CHECK(hipGetLastError());
+            tg.mark();
+            tgrid += tg.ms(0, 1);
+        }
+        waited = true;
     }
-    if (P.nrec > 0) {
+    for (size_t i = 0; i < P.parts.size(); ++i) {
+        const Part &pt = P.parts[i];
+        if (pt.nvis == 0) continue;
+        const unsigned *ndev = P.pipelined ? pt.meta + 2 : nullptr;
+        const unsigned nb = std::min<unsigned>(grid1d(pt.nvis, 256), 16384);
         if (in.vis_dtype == SDP_HIP_C128)
-            k_finalize<double2><<<grid1d(P.nrec, 256), 256, 0, st>>>(
-                P.nrec, in.nchan, P.recs, acc, (double2 *)vis, in.vrs, in.vcs, accumulate);
+            k_finalize<double2><<<nb, 256, 0, st>>>(pt.nrec, ndev, in.nchan, P.recs + pt.vbase,
+                                                    acc + pt.vbase, (double2 *)vis, in.vrs,
+                                                    in.vcs, accumulate);
         else
-            k_finalize<float2><<<grid1d(P.nrec, 256), 256, 0, st>>>(
-                P.nrec, in.nchan, P.recs, acc, (float2 *)vis, in.vrs, in.vcs, accumulate);
+            k_finalize<float2><<<nb, 256, 0, st>>>(pt.nrec, ndev, in.nchan, P.recs + pt.vbase,
+                                                   acc + pt.vbase, (float2 *)vis, in.vrs, in.vcs,
+                                                   accumulate);
         SDP_HIP_CHECK(hipGetLastError());
     }
     tm.mark();
+    if (P.pipelined) read_part_meta(P, st);
+    release_events(ev);
     fill_info(P, info);
     if (info) {
-        info->ms_prep = tm.ms(0, 1) + tzero;
+        info->ms_prep = tm.on ? tm.ms(0, 1) - tgrid - tfft - tscr : 0.0f;
         info->ms_grid = tgrid;
         info->ms_fft = tfft;
         info->ms_screen = tscr;

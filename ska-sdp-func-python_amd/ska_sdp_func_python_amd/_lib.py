@@ -52,6 +52,7 @@ class WGridInfo(ctypes.Structure):
         ("ms_fft", ctypes.c_float),
         ("ms_screen", ctypes.c_float),
         ("bucket", c_int),
+        ("grid_launches", c_int),
     ]
 
     def as_dict(self):

@@ -34,12 +34,18 @@ def _problem(seed, nrow=300, nchan=3, umax=2000.0, frac=0.45):
     return uvw, freq, ms, wgt, frac / umax
 
 
-@pytest.fixture(params=["fine", "coarse"])
+@pytest.fixture(params=["fine", "coarse", "fine-pipelined", "fine-aux"])
 def bucket(request, monkeypatch):
     """Both gridders: 2x2-cell buckets (register gridder, the default at these
-    sizes) and 16x16-cell buckets (LDS-tile gridder used for very large grids)."""
+    sizes) and 16x16-cell buckets (LDS-tile gridder used for very large grids);
+    and the pipelined plan (two row parts bucketed on the auxiliary stream,
+    persistent gridding launches) that large calls take."""
     if request.param == "coarse":
         monkeypatch.setenv("SDP_HIP_BUCKET", "16")
+    if request.param == "fine-pipelined":
+        monkeypatch.setenv("SDP_HIP_PIPELINE", "2")
+    if request.param == "fine-aux":  # bucketing on the auxiliary stream
+        monkeypatch.setenv("SDP_HIP_PIPELINE", "1")
     return request.param
 
 
@@ -56,6 +62,7 @@ def test_ms2dirty_matches_exact(dow, vdt, flip, bucket):
                                  cell * 0.9, 1e-7, dow, flip_uw=flip)
     assert info["support"] == 8
     assert info["bucket"] == (16 if bucket == "coarse" else 2)
+    assert info["grid_launches"] == (2 if bucket == "fine-pipelined" else 1)
     assert rel_rms(out.cpu().numpy(), ex) < TOL
 
 
