@@ -541,7 +541,7 @@ __global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__re
             const int n = (int)min(64u, it.e - b0);
             const VisRec my = recs[b0 + min(lane, n - 1)];
             const BatchTaps bt = batch_taps(my, lane, ihw, bl);
-    #pragma unroll
+#pragma unroll
             for (int m = 0; m < 8; ++m) {
                 const int rn = min(8, n - 8 * m);  // records of this 8-record group
                 for (int r = 0; r < rn; ++r) {
@@ -556,16 +556,16 @@ __global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__re
                     // padding planes (q0 + q >= NQ) get a zero weight: a uniform
                     // select, so the LDS reads and writes below stay branch-free
                     float kw[NQW];
-    #pragma unroll
+#pragma unroll
                     for (int q = 0; q < NQW; ++q) {
                         const float x = WS ? lane_readf(bt.w[m], 8 * r + min(q0 + q, NQ - 1)) : 1.0f;
                         kw[q] = (NQP == NQ || q0 + q < NQ) ? x : 0.0f;
                     }
                     if (role.act) {
                         float2 a[NQW];
-    #pragma unroll
+#pragma unroll
                         for (int q = 0; q < NQW; ++q) a[q] = wtile[q * PS + off];
-    #pragma unroll
+#pragma unroll
                         for (int q = 0; q < NQW; ++q) {
                             a[q].x = fmaf(vr, kw[q], a[q].x);
                             a[q].y = fmaf(vi, kw[q], a[q].y);
@@ -664,9 +664,9 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
             const int jb = jbase + j * SUB;  // bucket's first cell along y
 
             float acc_r[NO][NQ], acc_i[NO][NQ];
-    #pragma unroll
+#pragma unroll
             for (int o = 0; o < NO; ++o)
-    #pragma unroll
+#pragma unroll
                 for (int q = 0; q < NQ; ++q) acc_r[o][q] = acc_i[o][q] = 0.0f;
             uint32_t used = 0;
 
@@ -678,31 +678,31 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
                 const bool live = lane < n;
                 const float cre_l = live ? my.cre : 0.0f, cim_l = live ? my.cim : 0.0f;
                 const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
-    #pragma unroll
+#pragma unroll
                 for (int oo = 0; oo < NO; ++oo)
                     if (__ballot(live && o_l == oo)) used |= 1u << oo;
-    #pragma unroll
+#pragma unroll
                 for (int m = 0; m < 8; ++m) {
                     if (8 * m >= n) break;
-                    // taps of this 8-record group: lane l holds tap (l % 8) of record 8m + l/8
+                    // taps of this 8-record group: lane l holds tap (l % 8) of record
+                    // 8m + l/8; the u tap is pre-multiplied by the record's value
                     const int src = 8 * m + (lane >> 3);
                     const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
+                    const float tur = tu * __shfl(cre_l, src), tui = tu * __shfl(cim_l, src);
                     const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
                     const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
-    #pragma unroll
+#pragma unroll
                     for (int r = 0; r < 8; ++r) {
                         const int k = 8 * m + r;
-                        const float cre = lane_readf(cre_l, k), cim = lane_readf(cim_l, k);
                         const int o = __builtin_amdgcn_readlane(o_l, k);
-                        const float ku = __shfl(tu, 8 * r + role.kx);
                         const float kv = __shfl(tv, 8 * r + role.ky);
-                        const float kk = ku * kv;
-                        const float vr = cre * kk, vi = cim * kk;
+                        const float vr = __shfl(tur, 8 * r + role.kx) * kv;
+                        const float vi = __shfl(tui, 8 * r + role.kx) * kv;
                         float kw[NQ];
-    #pragma unroll
+#pragma unroll
                         for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
                         // origin select: uniform branches (one per origin set)
-    #pragma unroll
+#pragma unroll
                         for (int oo = 0; oo < NO; ++oo)
                             if (o == oo) acc_add<NQ>(acc_r[oo], acc_i[oo], vr, vi, kw);
                     }
@@ -711,12 +711,12 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
 
             // add the bucket's origin sets into the group tile (plain RMW: one
             // wave, in-order LDS)
-    #pragma unroll
+#pragma unroll
             for (int oo = 0; oo < NO; ++oo) {
                 if ((used >> oo) & 1u) {
                     if (role.act) {
                         const int base = (oo / SUB + role.kx) * RY + j * SUB + (oo % SUB) + role.ky;
-    #pragma unroll
+#pragma unroll
                         for (int q = 0; q < NQ; ++q) {
                             float2 a = tile[q * PS + base];
                             a.x += acc_r[oo][q];
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
         constexpr int FPP = RX * RY * 2;  // floats per plane
         const int64_t plane_floats = (int64_t)g.ngx * g.ngy * 2;
         const float *ftile = reinterpret_cast<const float *>(tile);
-    #pragma unroll
+#pragma unroll
         for (int i0 = 0; i0 < FPP; i0 += 64) {
             const int f = i0 + lane;
             if (f >= FPP) break;
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
             int gy = jbase + yl;
             if (gy >= g.ngy) gy -= g.ngy;
             float *dst0 = grid + ((int64_t)gx * g.ngy + gy) * 2 + (f & 1);
-    #pragma unroll
+#pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int p = (int)it.p0 + q;
                 const float val = ftile[q * PS * 2 + f];
@@ -825,10 +825,10 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
             const int jb = jbase + j * SUB;
 
             float gr[NO][NQ], gi[NO][NQ];
-    #pragma unroll
+#pragma unroll
             for (int o = 0; o < NO; ++o) {
                 const int base = (o / SUB + role.kx) * RY + j * SUB + (o % SUB) + role.ky;
-    #pragma unroll
+#pragma unroll
                 for (int q = 0; q < NQ; ++q) {
                     const float2 v = role.act ? tile[q * PS + base] : make_float2(0.0f, 0.0f);
                     gr[o][q] = v.x;
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
                 const int n = (int)min(64u, re - b0);
                 const VisRec my = recs[b0 + min(lane, n - 1)];
                 const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
-    #pragma unroll
+#pragma unroll
                 for (int m = 0; m < 8; ++m) {
                     if (8 * m >= n) break;
                     const int src = 8 * m + (lane >> 3);
@@ -848,20 +848,20 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
                     const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
                     const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
                     float pr[8], pim[8];
-    #pragma unroll
+#pragma unroll
                     for (int r = 0; r < 8; ++r) {
                         const int k = 8 * m + r;
                         const int o = __builtin_amdgcn_readlane(o_l, k);
                         const float ku = __shfl(tu, 8 * r + role.kx);
                         const float kv = __shfl(tv, 8 * r + role.ky);
                         float kw[NQ];
-    #pragma unroll
+#pragma unroll
                         for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
                         float sr = 0.0f, si = 0.0f;
-    #pragma unroll
+#pragma unroll
                         for (int oo = 0; oo < NO; ++oo) {
                             if (o == oo) {
-    #pragma unroll
+#pragma unroll
                                 for (int q = 0; q < NQ; ++q) {
                                     sr = fmaf(kw[q], gr[oo][q], sr);
                                     si = fmaf(kw[q], gi[oo][q], si);
@@ -875,14 +875,14 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
                     // reduce-scatter: after the xor-32/16/8 halvings lane l holds
                     // record (l >> 3) & 7 summed over 8 lanes; xor 4/2/1 finish it
                     float a4r[4], a4i[4];
-    #pragma unroll
+#pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const float sr = b5 ? pr[i] : pr[i + 4], si = b5 ? pim[i] : pim[i + 4];
                         a4r[i] = (b5 ? pr[i + 4] : pr[i]) + __shfl_xor(sr, 32);
                         a4i[i] = (b5 ? pim[i + 4] : pim[i]) + __shfl_xor(si, 32);
                     }
                     float a2r[2], a2i[2];
-    #pragma unroll
+#pragma unroll
                     for (int i = 0; i < 2; ++i) {
                         const float sr = b4 ? a4r[i] : a4r[i + 2], si = b4 ? a4i[i] : a4i[i + 2];
                         a2r[i] = (b4 ? a4r[i + 2] : a4r[i]) + __shfl_xor(sr, 16);
@@ -890,7 +890,7 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
                     }
                     float tr = (b3 ? a2r[1] : a2r[0]) + __shfl_xor(b3 ? a2r[0] : a2r[1], 8);
                     float ti = (b3 ? a2i[1] : a2i[0]) + __shfl_xor(b3 ? a2i[0] : a2i[1], 8);
-    #pragma unroll
+#pragma unroll
                     for (int msk = 4; msk > 0; msk >>= 1) {
                         tr += __shfl_xor(tr, msk);
                         ti += __shfl_xor(ti, msk);
@@ -960,14 +960,14 @@ __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__
                 const float kv = __shfl(kval, W + role.ky);
                 const int off = lane_off + (int)(rc.ij & 0xffffu) * PITCH + (int)(rc.ij >> 16);
                 float kw[NQ];
-    #pragma unroll
+#pragma unroll
                 for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(kval, 2 * W + q) : 1.0f;
                 float sr = 0.0f, si = 0.0f;
                 if (role.act) {
                     float2 a[NQ];
-    #pragma unroll
+#pragma unroll
                     for (int q = 0; q < NQ; ++q) a[q] = tile[q * PS + off];
-    #pragma unroll
+#pragma unroll
                     for (int q = 0; q < NQ; ++q) {
                         sr = fmaf(kw[q], a[q].x, sr);
                         si = fmaf(kw[q], a[q].y, si);
