@@ -65,7 +65,8 @@ if "dft" in which:
     del uvw, uvwl, out
 
 if "stefcal" in which:
-    nants, ntime, nchan = 512, 8, 64
+    nants, nchan = 512, 64
+    ntime = int(os.environ.get("STEFCAL_NTIME", "8"))
     a1, a2 = np.triu_indices(nants, 1)
     rng = np.random.default_rng(1805550721)
     g = (rng.lognormal(0, 0.1, (ntime, nants, nchan)) * np.exp(1j * rng.normal(0, 0.1, (ntime, nants, nchan))))
@@ -82,7 +83,7 @@ if "stefcal" in which:
     nsub = ntime * nchan
     iters = int(used.max())
     nbl = len(a1)
-    print(json.dumps({"path": "StefCal C5-shaped batch (B jones: per-chan solutions, 8 times x 64 chans)",
+    print(json.dumps({"path": f"StefCal C5-shaped batch (B jones: per-chan solutions, {ntime} times x {nchan} chans)",
                       "nants": nants, "nbl": nbl, "sub_solves": nsub, "iterations": iters, "ms": round(t * 1e3, 3),
                       "solves_s": round(nsub / t, 1), "iter_GBs": round(12 * nbl * nsub * iters / t / 1e9, 1),
                       "max_residual": float(res.max())}), flush=True)
