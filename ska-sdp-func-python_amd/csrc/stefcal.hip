@@ -28,6 +28,7 @@ namespace stefcal {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxAnts = 1024;
+constexpr int kUnroll = 8;  // baseline batches in flight per wave (k_iter, k_residual)
 
 enum Mode { kScalar = 0, kMatrix = 1, kNoCross = 2 };
 
@@ -65,33 +66,48 @@ __global__ void k_rowmax(Dims d, const double *__restrict__ wb, unsigned long lo
     if ((threadIdx.x & 63) == 0 && m > 0.0) atomicMax(&rowmax[s], dbits(m));
 }
 
-// x = xb / wb, w = wb / max  (masked where wb <= 0), into [s][chan][comp][bl]
-__global__ void k_fill(Dims d, const double2 *__restrict__ xb, const double *__restrict__ wb,
-                       const unsigned long long *__restrict__ rowmax, float2 *x, float *w) {
-    const size_t nsub = (size_t)d.nsolve * d.nchan * d.ncomp;
-    const size_t total = nsub * d.nbl;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * blockDim.x) {
-        const int b = (int)(i % d.nbl);
-        const size_t sub = i / d.nbl;
-        const int comp = (int)(sub % d.ncomp);
-        const int chan = (int)((sub / d.ncomp) % d.nchan);
-        const int s = (int)(sub / ((size_t)d.ncomp * d.nchan));
-        const int p = comp_pol(d, comp);
+// x = xb / wb, w = wb / max  (masked where wb <= 0), into [s][chan][comp][bl]:
+// an LDS-tiled transpose of each solve's [bl][chan*pol] block (coalesced
+// reads along chan*pol, coalesced writes along bl)
+constexpr int kTr = 32;
+__global__ __launch_bounds__(256) void k_fill(Dims d, const double2 *__restrict__ xb,
+                                              const double *__restrict__ wb,
+                                              const unsigned long long *__restrict__ rowmax,
+                                              float2 *x, float *w) {
+    __shared__ float2 sx[kTr][kTr + 1];
+    __shared__ float sw[kTr][kTr + 1];
+    const int s = blockIdx.z;
+    const int b0 = blockIdx.x * kTr, c0 = blockIdx.y * kTr;  // c = chan * ncomp + comp
+    const int ncc = d.nchan * d.ncomp;
+    const double mx = __longlong_as_double((long long)rowmax[s]);
+    for (int r = threadIdx.y; r < kTr; r += 8) {
+        const int b = b0 + r, c = c0 + threadIdx.x;
         float2 xv = make_float2(0.0f, 0.0f);
         float wv = 0.0f;
-        if (p >= 0) {
-            const size_t src = (((size_t)s * d.nbl + b) * d.nchan + chan) * d.npol + p;
-            const double ww = wb[src];
-            const double mx = __longlong_as_double((long long)rowmax[s]);
-            if (ww > 0.0 && mx > 0.0) {
-                const double2 xx = xb[src];
-                xv = make_float2((float)(xx.x / ww), (float)(xx.y / ww));
-                wv = (float)(ww / mx);
+        if (b < d.nbl && c < ncc) {
+            const int chan = c / d.ncomp, comp = c - chan * d.ncomp;
+            const int p = comp_pol(d, comp);
+            if (p >= 0) {
+                const size_t src = (((size_t)s * d.nbl + b) * d.nchan + chan) * d.npol + p;
+                const double ww = wb[src];
+                if (ww > 0.0 && mx > 0.0) {
+                    const double2 xx = xb[src];
+                    xv = make_float2((float)(xx.x / ww), (float)(xx.y / ww));
+                    wv = (float)(ww / mx);
+                }
             }
         }
-        x[i] = xv;
-        w[i] = wv;
+        sx[r][threadIdx.x] = xv;
+        sw[r][threadIdx.x] = wv;
+    }
+    __syncthreads();
+    for (int r = threadIdx.y; r < kTr; r += 8) {
+        const int c = c0 + r, b = b0 + threadIdx.x;
+        if (b < d.nbl && c < ncc) {
+            const size_t dst = ((size_t)s * ncc + c) * d.nbl + b;
+            x[dst] = sx[threadIdx.x][r];
+            w[dst] = sw[threadIdx.x][r];
+        }
     }
 }
 
@@ -135,6 +151,7 @@ __global__ __launch_bounds__(kThreads) void k_iter(Dims d, const int32_t *__rest
     double2 *gl = reinterpret_cast<double2 *>(lds);  // [na]
     double2 *top = gl + na;                          // [kWaves][na]
     double *bot = reinterpret_cast<double *>(top + (size_t)kWaves * na);  // [kWaves][na]
+    int *rs = reinterpret_cast<int *>(bot + (size_t)kWaves * na);          // [na + 1]
     const size_t gbase = (size_t)sub * na;
     const size_t xbase = (size_t)sub * d.nbl;
     for (int a = threadIdx.x; a < na; a += kThreads) {
@@ -144,33 +161,74 @@ __global__ __launch_bounds__(kThreads) void k_iter(Dims d, const int32_t *__rest
             bot[k * na + a] = 0.0;
         }
     }
+    // the CSR row offsets: staged once (each row's bounds were a dependent
+    // global load per antenna row)
+    for (int a = threadIdx.x; a <= na; a += kThreads) rs[a] = row_start[a];
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     double2 *tw = top + (size_t)wave * na;
     double *bw = bot + (size_t)wave * na;
+    // Each wave walks antenna rows a1 = wave, wave + kWaves, ...  The next
+    // row's baselines (up to 64 * kUnroll per pass) are loaded into registers
+    // while the current row is accumulated and reduced, so a row's global
+    // load latency is hidden behind the previous row's work.
+    struct RowBuf {
+        int a2[kUnroll];
+        float2 xv[kUnroll];
+        float wv[kUnroll];
+    };
+    auto load_row = [&](int a1, int bstart, RowBuf &rb) {
+        const int b1 = a1 < na ? rs[a1 + 1] : 0;
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int b = bstart + lane + 64 * u;
+            const bool ok = a1 < na && b < b1;
+            rb.a2[u] = ok ? ant2[b] : 0;
+            rb.xv[u] = ok ? x[xbase + b] : make_float2(0.0f, 0.0f);
+            rb.wv[u] = ok ? w[xbase + b] : 0.0f;
+        }
+    };
+    RowBuf cur;
+    load_row(wave, wave < na ? rs[wave] : 0, cur);
     for (int a1 = wave; a1 < na; a1 += kWaves) {
         const double2 g1 = gl[a1];
         const double p1 = g1.x * g1.x + g1.y * g1.y;
         double tr = 0.0, ti = 0.0, bs = 0.0;
-        const int b1 = row_start[a1 + 1];
-        for (int b = row_start[a1] + lane; b < b1; b += 64) {
-            const int a2 = ant2[b];
-            const float2 xv = x[xbase + b];
-            const double wv = w[xbase + b];
-            const double2 g2 = gl[a2];
-            // antenna a2 (i = a1): x[a1,a2] = conj(x_b)
-            const double2 c1 = cmul(g1, make_double2(xv.x * wv, -xv.y * wv));
-            double2 t = tw[a2];
-            t.x += c1.x;
-            t.y += c1.y;
-            tw[a2] = t;
-            bw[a2] += p1 * wv;
-            // antenna a1 (i = a2): x[a2,a1] = x_b
-            const double2 c2 = cmul(g2, make_double2(xv.x * wv, xv.y * wv));
-            tr += c2.x;
-            ti += c2.y;
-            bs += (g2.x * g2.x + g2.y * g2.y) * wv;
+        const int bb = rs[a1], b1 = rs[a1 + 1];
+        for (int b0 = bb; b0 < b1; b0 += 64 * kUnroll) {
+            RowBuf nxt;
+            // prefetch: the rest of this row, else the next row of this wave
+            if (b0 + 64 * kUnroll < b1) load_row(a1, b0 + 64 * kUnroll, nxt);
+            else {
+                const int an = a1 + kWaves;
+                load_row(an, an < na ? rs[an] : 0, nxt);
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                if (b0 + lane + 64 * u >= b1) break;
+                const int a2 = cur.a2[u];
+                const float2 xv = cur.xv[u];
+                const double wv = cur.wv[u];
+                const double2 g2 = gl[a2];
+                // antenna a2 (i = a1): x[a1,a2] = conj(x_b)
+                const double2 c1 = cmul(g1, make_double2(xv.x * wv, -xv.y * wv));
+                double2 t = tw[a2];
+                t.x += c1.x;
+                t.y += c1.y;
+                tw[a2] = t;
+                bw[a2] += p1 * wv;
+                // antenna a1 (i = a2): x[a2,a1] = x_b
+                const double2 c2 = cmul(g2, make_double2(xv.x * wv, xv.y * wv));
+                tr += c2.x;
+                ti += c2.y;
+                bs += (g2.x * g2.x + g2.y * g2.y) * wv;
+            }
+            cur = nxt;
+        }
+        if (bb >= b1) {  // empty row: the prefetched buffer holds the next row
+            const int an = a1 + kWaves;
+            load_row(an, an < na ? rs[an] : 0, cur);
         }
         for (int o = 32; o > 0; o >>= 1) {
             tr += __shfl_xor(tr, o);
@@ -382,12 +440,17 @@ static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, 
     k_rowmax<<<dim3(std::max<unsigned>(1, std::min<unsigned>(64, (unsigned)((per + 255) / 256))),
                     d.nsolve),
                256, 0, st>>>(d, wb, rowmax);
-    k_fill<<<blocks_for(nx), 256, 0, st>>>(d, static_cast<const double2 *>(xb), wb, rowmax, x, w);
+    {
+        const dim3 grd((unsigned)((d.nbl + kTr - 1) / kTr),
+                       (unsigned)((d.nchan * d.ncomp + kTr - 1) / kTr), (unsigned)d.nsolve);
+        k_fill<<<grd, dim3(kTr, 8), 0, st>>>(d, static_cast<const double2 *>(xb), wb, rowmax, x, w);
+    }
     k_load_gains<<<blocks_for(ng), 256, 0, st>>>(d, static_cast<const double2 *>(gain), gwt, g,
                                                   gw);
     SDP_HIP_CHECK(hipGetLastError());
 
-    const size_t lds = (size_t)d.nants * (sizeof(double2) * (1 + kWaves) + sizeof(double) * kWaves);
+    const size_t lds = (size_t)d.nants * (sizeof(double2) * (1 + kWaves) + sizeof(double) * kWaves) +
+                       (size_t)(d.nants + 1) * sizeof(int);
     if (lds > 65536)
         SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_iter,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
