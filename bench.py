@@ -40,6 +40,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "Mvis/s gridded (invert, 8k^2 w-stack grid) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3       # fp32 vector (packed FMA) peak
 NCHAN_PER_GPU, NTIMES, NPIX = 64, 100, 4096
 F_LO, F_HI = 0.95e9, 1.76e9
 EPS_REQUESTED = 1e-12
@@ -173,7 +174,13 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": (f"k_grid_reg<{info['support']},true>" if info["bucket"] == 2
                        else f"k_grid_lds<{info['support']},true,2>"), "kernel_ms": round(ms_grid / launches, 4),
-            "alg_bytes_per_launch": int(alg_bytes / launches)}
+            "alg_bytes_per_launch": int(alg_bytes / launches),
+            # the gridder is VALU-issue bound: the same kernel against the
+            # fp32 vector peak (4 W^3 flops per visibility)
+            "compute": {"achieved": round(nvis_rank * 4 * info["support"] ** 3 / (ms_grid * 1e-3) / 1e12, 2),
+                        "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(nvis_rank * 4 * info["support"] ** 3 / (ms_grid * 1e-3) / 1e12
+                                      / FP32_PEAK_TFLOPS, 4)}}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_chans > 0:
