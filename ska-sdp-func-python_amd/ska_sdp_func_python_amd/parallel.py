@@ -61,3 +61,114 @@ def invert_sharded(uvw, freq, vis, wgt, npix, cell, epsilon=1e-7, do_wstacking=T
         else:
             out.zero_()
     return out, sumwt
+
+
+def _dist_on():
+    return dist.is_available() and dist.is_initialized()
+
+
+def _degridder():
+    from . import kernels
+    return kernels.dirty2ms
+
+
+def predict_sharded(uvw, freq, model, cell, epsilon=1e-7, do_wstacking=True, flip_uw=True,
+                    group=None, src=0, degrid_fn=None, vis_dtype=torch.complex64):
+    """Channel-sharded predict (SURVEY.md §8(e) "predict: broadcast model,
+    no exchange"; reference imaging/ng.py:38-143).
+
+    ``model`` [npix, npix] f64 in RASCIL [y, x] order is broadcast from rank
+    ``src`` (one npix^2 * 8 B broadcast); every rank then degrids its own
+    channels ``freq`` for rows ``uvw``.  Returns the rank-local vis
+    [nrow, nchan_shard].
+    """
+    degrid_fn = degrid_fn or _degridder()
+    if _dist_on():
+        dist.broadcast(model, src=src, group=group)
+    npix = model.shape[-1]
+    if freq.numel() == 0 or uvw.shape[0] == 0:
+        return torch.zeros((uvw.shape[0], freq.numel()), dtype=vis_dtype, device=uvw.device)
+    # the model is [y, x]: hand it to the ducc0-convention kernel as x-major
+    vis, _ = degrid_fn(uvw, freq, model, None, cell, cell, epsilon, do_wstacking,
+                       flip_uw=flip_uw, dirty_strides=(1, npix), npix=(npix, npix),
+                       vis_dtype=vis_dtype)
+    return vis
+
+
+def dft_sharded(direction_cosines, fluxes, uvw, freq=None, group=None, src=0, dft_fn=None):
+    """Row-sharded sky-component DFT (SURVEY.md §8(e) "DFT: shard rows,
+    components replicated"; reference imaging/dft.py:32-182).  The component
+    table is broadcast from rank ``src`` so every rank uses the same one; the
+    rank's rows of ``uvw`` are predicted with no exchange."""
+    if dft_fn is None:
+        from . import kernels
+        dft_fn = kernels.dft_point
+    if _dist_on():
+        dist.broadcast(direction_cosines, src=src, group=group)
+        dist.broadcast(fluxes, src=src, group=group)
+    return dft_fn(direction_cosines, fluxes, uvw, freq=freq)
+
+
+def normalise_gains_global(gain, normalise_gains, group=None):
+    """The reference's gain normalisation over the WHOLE table
+    (calibration/solvers.py:135-143) when the gain rows are sharded:
+    mean -> one all-reduce of (sum |g|, count); median -> all-gather of |g|
+    (numpy median: mean of the two middle values for even counts)."""
+    ga = gain.abs().flatten()
+    if normalise_gains == "mean":
+        acc = torch.stack([ga.sum(), torch.tensor(float(ga.numel()), dtype=ga.dtype,
+                                                  device=ga.device)])
+        if _dist_on():
+            dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=group)
+        gabs = acc[0] / acc[1]
+    elif normalise_gains == "median":
+        if _dist_on():
+            world = dist.get_world_size(group)
+            n = torch.tensor([ga.numel()], device=ga.device)
+            ns = [torch.zeros_like(n) for _ in range(world)]
+            dist.all_gather(ns, n, group=group)
+            nmax = int(max(int(x.item()) for x in ns))
+            pad = torch.full((nmax,), float("nan"), dtype=ga.dtype, device=ga.device)
+            pad[:ga.numel()] = ga
+            parts = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(parts, pad, group=group)
+            allg = torch.cat([p[:int(k.item())] for p, k in zip(parts, ns)])
+        else:
+            allg = ga
+        srt = torch.sort(allg).values
+        m = srt.numel()
+        gabs = 0.5 * (srt[(m - 1) // 2] + srt[m // 2])
+    else:
+        return gain
+    return gain / gabs
+
+
+def solve_gains_sharded(xb, wb, gain, gwt, row_start, ant2, mode, niter=200, tol=1e-6,
+                        phase_only=True, normalise_gains=None, group=None, solve_fn=None):
+    """Gain rows sharded across ranks (SURVEY.md §8(e) "solve_gaintable:
+    embarrassingly parallel ... except the global normalise_gains").  Each
+    rank solves its rows ``xb/wb/gain/gwt`` [rows_local, ...] with no
+    collective, then the optional mean/median normalisation is global."""
+    if solve_fn is None:
+        from . import kernels
+        solve_fn = kernels.solve_gains
+    residual, used = solve_fn(xb, wb, gain, gwt, row_start, ant2, mode, niter=niter, tol=tol,
+                              phase_only=phase_only)
+    if normalise_gains in ("mean", "median") and not phase_only:
+        gain.copy_(normalise_gains_global(gain, normalise_gains, group))
+    return residual, used
+
+
+def grid_cf_sharded(maps, vis_to_im, vis, wt, cf, grid, sumwt, group=None, grid_fn=None):
+    """Row-sharded convolution-function gridding (SURVEY.md §8(e) "AW
+    grid/degrid: one exchange step"; reference grid_data/gridding.py:160-255):
+    each rank grids its rows into ``grid``/``sumwt`` (zeroed by the caller),
+    then one all-reduce of the GridData and of sumwt."""
+    if grid_fn is None:
+        from . import kernels
+        grid_fn = kernels.grid_cf
+    grid_fn(maps, vis_to_im, vis, wt, cf, grid, sumwt)
+    if _dist_on():
+        dist.all_reduce(grid, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(sumwt, op=dist.ReduceOp.SUM, group=group)
+    return grid, sumwt

@@ -59,3 +59,174 @@ def test_sharded_invert_equals_full():
     for _, img, sw in res:
         np.testing.assert_allclose(sw, wgt.sum(), rtol=1e-12)
         np.testing.assert_allclose(img, full, rtol=1e-10, atol=1e-12)
+
+
+# ---------------------------------------------------------------------------
+# predict / DFT / StefCal / CF gridding shards; the compute
+# is the oracle (test injection), the partitioning and collectives are the
+# product's parallel.py
+# ---------------------------------------------------------------------------
+import ref_oracle as ro  # noqa: E402
+
+FLIP = np.array([-1.0, 1.0, -1.0])
+
+
+def _oracle_degrid(uvw, freq, dirty, wgt, px, py, eps, dow, flip_uw, dirty_strides, npix,
+                   vis_dtype):
+    img = dirty.numpy()
+    if tuple(dirty_strides) == (1, npix[0]):  # [y, x] storage
+        img = img.T
+    v = orc.dirty2ms_exact(uvw.numpy() * (FLIP if flip_uw else 1.0), freq.numpy(), img, None, px,
+                           py, dow)
+    return torch.as_tensor(v), {}
+
+
+def _oracle_dft(dc, fl, uvw, freq=None):
+    uvwl = uvw.numpy()[:, None, :] * (freq.numpy() / 299792458.0)[None, :, None]
+    return torch.as_tensor(ro.dft_cpu_looped(dc.numpy(), uvwl, fl.numpy()))
+
+
+def _pairs(row_start, ant2):
+    a1 = np.repeat(np.arange(len(row_start) - 1), np.diff(row_start))
+    return np.stack([a1, np.asarray(ant2)], 1)
+
+
+def _oracle_solve(xb, wb, gain, gwt, row_start, ant2, mode, niter=200, tol=1e-6,
+                  phase_only=True):
+    bl = _pairs(row_start, ant2)
+    nants = gain.shape[1]
+    res = []
+    for s in range(xb.shape[0]):
+        g0 = gain[s].numpy()
+        g, w, r, _ = ro.stefcal_row(xb[s].numpy().copy(), wb[s].numpy().copy(), bl, nants, g0,
+                                    gwt[s].numpy(), niter, tol, phase_only)
+        gain[s] = torch.as_tensor(np.asarray(g).reshape(g0.shape))
+        res.append(r)
+    return torch.as_tensor(np.array(res)), None
+
+
+def _oracle_grid_cf(maps, vis_to_im, vis, wt, cf, grid, sumwt):
+    g, s = ro.grid_cf({k: v.numpy() for k, v in maps.items()}, vis_to_im.numpy(), vis.numpy(),
+                      wt.numpy(), cf.numpy(), tuple(grid.shape))
+    grid += torch.as_tensor(g)
+    sumwt += torch.as_tensor(s)
+
+
+def _shard_worker(rank, world, port, kind, data, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ska_sdp_func_python_amd import parallel as par
+    T = torch.as_tensor
+    if kind == "predict":
+        uvw, freq, model, cell = data
+        ch = par.interleaved_channels(len(freq), rank, world)
+        m = T(model.copy()) if rank == 0 else torch.zeros_like(T(model))  # broadcast from 0
+        out = par.predict_sharded(T(uvw), T(freq[ch]), m, cell, degrid_fn=_oracle_degrid)
+        q.put((rank, ch, out.numpy()))
+    elif kind == "dft":
+        dc, fl, uvw, freq = data
+        lo, hi = par.shard_range(uvw.shape[0], rank, world)
+        dcs = T(dc.copy()) if rank == 0 else torch.zeros_like(T(dc))
+        fls = T(fl.copy()) if rank == 0 else torch.zeros_like(T(fl))
+        out = par.dft_sharded(dcs, fls, T(uvw[lo:hi]), T(freq), dft_fn=_oracle_dft)
+        q.put((rank, (lo, hi), out.numpy()))
+    elif kind == "solve":
+        xb, wb, gain, gwt, rs, a2, norm = data
+        lo, hi = par.shard_range(xb.shape[0], rank, world)
+        g = T(gain[lo:hi].copy())
+        par.solve_gains_sharded(T(xb[lo:hi]), T(wb[lo:hi]), g, T(gwt[lo:hi].copy()), rs, a2, 0,
+                                phase_only=False, normalise_gains=norm, solve_fn=_oracle_solve)
+        q.put((rank, (lo, hi), g.numpy()))
+    elif kind == "cf":
+        maps, v2i, vis, wt, cf, gshape = data
+        lo, hi = par.shard_range(vis.shape[0], rank, world)
+        grid = torch.zeros(gshape, dtype=torch.complex128)
+        sumwt = torch.zeros(gshape[:2], dtype=torch.float64)
+        mp_ = {k: T(v[:, lo:hi]) for k, v in maps.items()}
+        par.grid_cf_sharded(mp_, T(v2i), T(vis[lo:hi]), T(wt[lo:hi]), T(cf), grid, sumwt,
+                            grid_fn=_oracle_grid_cf)
+        q.put((rank, None, (grid.numpy(), sumwt.numpy())))
+    dist.destroy_process_group()
+
+
+def _run(kind, data, seed):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30000 + seed * 7 + int(np.random.default_rng(seed).integers(0, 400))
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, kind, data, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+def test_sharded_predict_equals_full():
+    rng = np.random.default_rng(11)
+    nrow, nchan, npix = 40, 4, 24
+    freq = np.linspace(1e9, 1.2e9, nchan)
+    uvw = rng.uniform(-1, 1, (nrow, 3)) * 800 * 299792458.0 / freq.max()
+    model = rng.normal(size=(npix, npix))  # [y, x]
+    cell = 0.25 / 800
+    res = _run("predict", (uvw, freq, model, cell), 1)
+    full = orc.dirty2ms_exact(uvw * FLIP, freq, model.T, None, cell, cell, True)
+    for _, ch, v in res:
+        np.testing.assert_allclose(v, full[:, ch], rtol=1e-10, atol=1e-12)
+
+
+def test_sharded_dft_equals_full():
+    rng = np.random.default_rng(12)
+    nrow, ncomp = 30, 5
+    freq = np.array([1.0e9, 1.1e9])
+    uvw = rng.normal(0, 2000, (nrow, 3))
+    lm = rng.uniform(-0.02, 0.02, (ncomp, 2))
+    dc = np.concatenate([lm, (np.sqrt(1 - (lm ** 2).sum(1)) - 1)[:, None]], 1)
+    fl = (rng.uniform(0.5, 2, (ncomp, 1, 1)) + 0j)
+    res = _run("dft", (dc, fl, uvw, freq), 2)
+    full = ro.dft_cpu_looped(dc, uvw[:, None, :] * (freq / 299792458.0)[None, :, None], fl)
+    for _, (lo, hi), v in res:
+        np.testing.assert_allclose(v, full[lo:hi], rtol=1e-12)
+
+
+@pytest.mark.parametrize("norm", ["mean", "median"])
+def test_sharded_solve_global_normalisation(norm):
+    rng = np.random.default_rng(13)
+    nants, nrows, nchan = 6, 3, 2
+    a1, a2 = np.triu_indices(nants, 1)
+    g = rng.lognormal(0, 0.2, (nrows, nants, nchan)) * np.exp(1j * rng.normal(0, 0.3, (nrows, nants, nchan)))
+    xb = (g[:, a1] * np.conj(g[:, a2]))[..., None]
+    wb = np.ones(xb.shape)
+    rs = np.concatenate([[0], np.cumsum(np.bincount(a1, minlength=nants))]).astype(np.int32)
+    gain = np.ones((nrows, nants, nchan, 1, 1), complex)
+    gwt = np.zeros(gain.shape)
+    res = _run("solve", (xb, wb, gain, gwt, rs, a2.astype(np.int32), norm), 3 + len(norm))
+    # unsharded reference: all rows, then the same global normalisation
+    gfull = torch.as_tensor(gain.copy())
+    _oracle_solve(torch.as_tensor(xb), torch.as_tensor(wb), gfull, torch.as_tensor(gwt.copy()), rs,
+                  a2, 0, phase_only=False)
+    ga = np.abs(gfull.numpy())
+    gfull = gfull.numpy() / (np.median(ga) if norm == "median" else np.mean(ga))
+    for _, (lo, hi), gs in res:
+        np.testing.assert_allclose(gs, gfull[lo:hi], rtol=1e-10, atol=1e-12)
+
+
+def test_sharded_cf_gridding_equals_full():
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "cfgrid_p4.npz"))
+    rng = np.random.default_rng(14)
+    nrow, nchan, npol = 20, 1, 4
+    ny = nx = 48
+    maps = {k: rng.integers(lo, hi, (nchan, nrow)).astype(np.int32)
+            for k, lo, hi in (("pu", 4, 44), ("pv", 4, 44), ("pwc", 0, 3), ("pdu", 0, 5),
+                              ("pdv", 0, 5))}
+    v2i = np.zeros(nchan, np.int32)
+    vis = rng.normal(size=(nrow, nchan, npol)) + 1j * rng.normal(size=(nrow, nchan, npol))
+    wt = rng.uniform(0.5, 1.5, (nrow, nchan, npol))
+    cf = g["cf"]
+    gshape = (1, npol, ny, nx)
+    res = _run("cf", (maps, v2i, vis, wt, cf, gshape), 5)
+    full, sw = ro.grid_cf(maps, v2i, vis, wt, cf, gshape)
+    for _, _, (grid, sumwt) in res:
+        np.testing.assert_allclose(grid, full, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(sumwt, sw, rtol=1e-12)
