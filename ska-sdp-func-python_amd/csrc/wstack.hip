@@ -1026,34 +1026,31 @@ __device__ __forceinline__ PixelGeom pixel_geom(const Geo &g, int ix, int iy,
 // T[q][iy][kx] (iy = image row index 0..ny-1, i.e. ky = (iy - ny/2) mod ngy;
 // kx = 0..ngx-1) holds, per plane, the needed y-frequency columns of the grid
 // transposed so the x-direction transform runs over contiguous rows.
-constexpr int kTr = 32;
+constexpr int kTr = 64;      // transpose tile edge
+constexpr int kTrRows = 4;   // threads along the tile's second axis (64 x 4 = 256)
 
-// grid[q][x][ky(iy)] -> T[q][iy][x]; rows x outside [row_lo, row_hi) are
-// all-zero in the grid and are written as zeros without being read.
+// grid[q][x][ky(iy)] -> T[q][iy][x] for the rows x in [row_lo, row_hi); the
+// rest of each T row is kept zero by the caller (persistent zeros)
 __global__ __launch_bounds__(256) void k_tr_grid_to_t(Geo g, const float2 *__restrict__ grid,
                                                       float2 *__restrict__ t, int row_lo,
                                                       int row_hi) {
     __shared__ float2 sm[kTr][kTr + 1];
-    const int x0 = blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
+    const int x0 = row_lo + blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
     const int64_t plane = (int64_t)g.ngx * g.ngy, tplane = (int64_t)g.ny * g.ngx;
-    const bool live = x0 + kTr > row_lo && x0 < row_hi;
-    if (live) {
-        for (int r = threadIdx.y; r < kTr; r += 8) {
-            const int x = x0 + r, iy = i0 + threadIdx.x;
-            float2 v = make_float2(0.0f, 0.0f);
-            if (x >= row_lo && x < row_hi && iy < g.ny) {
-                const int Y = iy - g.ny / 2;
-                const int ky = Y < 0 ? Y + g.ngy : Y;
-                v = grid[q * plane + (int64_t)x * g.ngy + ky];
-            }
-            sm[r][threadIdx.x] = v;
+    for (int r = threadIdx.y; r < kTr; r += kTrRows) {
+        const int x = x0 + r, iy = i0 + threadIdx.x;
+        float2 v = make_float2(0.0f, 0.0f);
+        if (x < row_hi && iy < g.ny) {
+            const int Y = iy - g.ny / 2;
+            const int ky = Y < 0 ? Y + g.ngy : Y;
+            v = grid[q * plane + (int64_t)x * g.ngy + ky];
         }
-        __syncthreads();
+        sm[r][threadIdx.x] = v;
     }
-    for (int r = threadIdx.y; r < kTr; r += 8) {
+    __syncthreads();
+    for (int r = threadIdx.y; r < kTr; r += kTrRows) {
         const int iy = i0 + r, x = x0 + threadIdx.x;
-        if (iy < g.ny && x < g.ngx)
-            t[q * tplane + (int64_t)iy * g.ngx + x] = live ? sm[threadIdx.x][r] : make_float2(0.0f, 0.0f);
+        if (iy < g.ny && x < row_hi) t[q * tplane + (int64_t)iy * g.ngx + x] = sm[threadIdx.x][r];
     }
 }
 
@@ -1064,13 +1061,13 @@ __global__ __launch_bounds__(256) void k_tr_t_to_grid(Geo g, const float2 *__res
     __shared__ float2 sm[kTr][kTr + 1];
     const int x0 = row_lo + blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
     const int64_t plane = (int64_t)g.ngx * g.ngy, tplane = (int64_t)g.ny * g.ngx;
-    for (int r = threadIdx.y; r < kTr; r += 8) {
+    for (int r = threadIdx.y; r < kTr; r += kTrRows) {
         const int iy = i0 + r, x = x0 + threadIdx.x;
         sm[r][threadIdx.x] = (iy < g.ny && x < row_hi) ? t[q * tplane + (int64_t)iy * g.ngx + x]
                                                        : make_float2(0.0f, 0.0f);
     }
     __syncthreads();
-    for (int r = threadIdx.y; r < kTr; r += 8) {
+    for (int r = threadIdx.y; r < kTr; r += kTrRows) {
         const int x = x0 + r, iy = i0 + threadIdx.x;
         if (x < row_hi && iy < g.ny) {
             const int Y = iy - g.ny / 2;
@@ -1362,7 +1359,8 @@ struct Plan {
     unsigned chunk = kChunkMin;      // max records per work item
     int64_t nrec = 0, nitems = 0;    // totals
     float2 *grid = nullptr;
-    float2 *spec = nullptr;  // T[q][iy][kx]: transposed y-spectra (pruned FFT)
+    float2 *spec = nullptr;     // T[q][iy][kx]: transposed y-spectra (pruned FFT)
+    float2 *spec_in = nullptr;  // band-only input of the backward x-FFT (zeros elsewhere)
 };
 
 struct Inputs {
@@ -1415,6 +1413,34 @@ static hipStream_t aux_stream() {
     SDP_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     streams[dev] = s;
     return s;
+}
+
+// The backward x-FFT input T_in holds the transposed band [row_lo, row_hi)
+// of every T row and zeros elsewhere.  The transpose writes only the band,
+// so the zeros are kept across calls: the buffer is cleared only when it is
+// (re)allocated or the band / shape changes.
+struct BandState {
+    float2 *ptr = nullptr;
+    size_t elems = 0;
+    int lo = -1, hi = -1, ny = 0, ngx = 0;
+};
+
+static float2 *band_input(const Plan &P, hipStream_t st) {
+    static std::mutex mu;
+    static std::map<int, BandState> states;
+    const Geo &g = P.g;
+    const size_t elems = (size_t)P.chunk_planes * g.ny * g.ngx;
+    float2 *buf = scratch<float2>("spec_in", elems);
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    BandState &b = states[dev];
+    if (b.ptr != buf || b.elems < elems || b.lo != P.row_lo || b.hi != P.row_hi || b.ny != g.ny ||
+        b.ngx != g.ngx) {
+        SDP_HIP_CHECK(hipMemsetAsync(buf, 0, elems * sizeof(float2), st));
+        b = BandState{buf, elems, P.row_lo, P.row_hi, g.ny, g.ngx};
+    }
+    return buf;
 }
 
 // Geometry shared by both directions: kernel, padded grid, w planes, bucket
@@ -1514,11 +1540,13 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     }
 
     // plane chunking against the grid memory budget
-    const size_t plane_bytes = ((size_t)g.ngx * g.ngy + (size_t)g.ny * g.ngx) * sizeof(float2);
+    const size_t plane_bytes =
+        ((size_t)g.ngx * g.ngy + 2 * (size_t)g.ny * g.ngx) * sizeof(float2);
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes() / plane_bytes);
     P.chunk_planes = std::min(cp, g.nplanes);
     P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy);
     P.spec = scratch<float2>("spec", (size_t)P.chunk_planes * g.ny * g.ngx);
+    if (grid_mode) P.spec_in = band_input(P, st);
 
     // records per item: large enough to amortise the tile flush over dense
     // tiles, small enough to leave >= ~16k items for the 256 CUs
@@ -1828,10 +1856,15 @@ static void fft_rows_y(const Plan &P, int np, int direction, hipStream_t st) {
         exec_fft(hr, P.grid + (size_t)q * g.ngx * g.ngy + (size_t)P.row_lo * g.ngy, direction);
 }
 
-static void fft_rows_x(const Plan &P, int np, int direction, hipStream_t st) {
+// x transforms of the T rows into P.spec, in place or from `in`
+static void fft_rows_x(const Plan &P, int np, int direction, hipStream_t st,
+                       float2 *in = nullptr) {
     const Geo &g = P.g;
     hipfftHandle hc = fft_plan_1d(g.ngx, 1, g.ngx, np * g.ny, st);
-    exec_fft(hc, P.spec, direction);
+    if (!in) return exec_fft(hc, P.spec, direction);
+    if (hipfftExecC2C(hc, (hipfftComplex *)in, (hipfftComplex *)P.spec, direction) !=
+        HIPFFT_SUCCESS)
+        throw Error(SDP_HIP_ERR_RUNTIME, "hipfftExecC2C failed");
 }
 
 // Only the row band [row_lo, row_hi) of a plane is ever written or read.
@@ -1913,10 +1946,11 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
         StageTimer t2(st);
         t2.mark();
         fft_rows_y(P, np, HIPFFT_BACKWARD, st);
-        k_tr_grid_to_t<<<tr_grid(g, g.ngx, np), dim3(kTr, 8), 0, st>>>(g, P.grid, P.spec,
-                                                                       P.row_lo, P.row_hi);
+        if (P.row_hi > P.row_lo)
+            k_tr_grid_to_t<<<tr_grid(g, P.row_hi - P.row_lo, np), dim3(kTr, kTrRows), 0, st>>>(
+                g, P.grid, P.spec_in, P.row_lo, P.row_hi);
         SDP_HIP_CHECK(hipGetLastError());
-        fft_rows_x(P, np, HIPFFT_BACKWARD, st);
+        fft_rows_x(P, np, HIPFFT_BACKWARD, st, P.spec_in);
         t2.mark();
         const dim3 grd(grid1d(g.nx, 256), g.ny);
         k_screen_fwd_t<<<grd, 256, 0, st>>>(g, P.spec, p_lo, np, dirty, sx, sy,
@@ -1978,7 +2012,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         t2.mark();
         fft_rows_x(P, np, HIPFFT_FORWARD, st);
         if (P.row_hi > P.row_lo)
-            k_tr_t_to_grid<<<tr_grid(g, P.row_hi - P.row_lo, np), dim3(kTr, 8), 0, st>>>(
+            k_tr_t_to_grid<<<tr_grid(g, P.row_hi - P.row_lo, np), dim3(kTr, kTrRows), 0, st>>>(
                 g, P.spec, P.grid, P.row_lo, P.row_hi);
         SDP_HIP_CHECK(hipGetLastError());
         fft_rows_y(P, np, HIPFFT_FORWARD, st);
