@@ -69,18 +69,19 @@ __global__ __launch_bounds__(kThreads) void k_grid_cf(Shape s, const int32_t *__
                 const double2 x = vis[vi];
                 const double w = wt[vi];
                 const double xr = x.x * w, xi = x.y * w;
-                const double2 *sub = cf + cf_index(s, imchan, p, iw, idv, idu) * taps;
-                double2 *g = grid + ((size_t)imchan * s.npol + p) * s.ny * s.nx;
-                for (int t = lane; t < taps; t += 64) {
+                const double *sub =
+                    reinterpret_cast<const double *>(cf + cf_index(s, imchan, p, iw, idv, idu) * taps);
+                double *g = reinterpret_cast<double *>(grid + ((size_t)imchan * s.npol + p) * s.ny * s.nx);
+                // one double per lane (re/im interleaved): a wave-instruction
+                // covers 32 taps = whole contiguous rows of the footprint
+                for (int f = lane; f < 2 * taps; f += 64) {
+                    const int t = f >> 1;
                     const int iv = t / s.gu, iu = t - (t / s.gu) * s.gu;
-                    const double2 c = sub[t];
-                    // conj(cf) * x
-                    const double re = c.x * xr + c.y * xi;
-                    const double im = c.x * xi - c.y * xr;
-                    double *dst = reinterpret_cast<double *>(
-                        g + (size_t)(v0 - dv + iv) * s.nx + (u0 - du + iu));
-                    if (re != 0.0) atomicAdd(dst, re);
-                    if (im != 0.0) atomicAdd(dst + 1, im);
+                    const double cr = sub[2 * t], ci = sub[2 * t + 1];
+                    // conj(cf) * x: re = cr xr + ci xi, im = cr xi - ci xr
+                    const double val = (f & 1) ? (cr * xi - ci * xr) : (cr * xr + ci * xi);
+                    double *dst = g + 2 * ((size_t)(v0 - dv + iv) * s.nx + (u0 - du + iu)) + (f & 1);
+                    if (val != 0.0) atomicAdd(dst, val);
                 }
                 if (lane == 0) atomicAdd(&s_wt[p], w);
             }
