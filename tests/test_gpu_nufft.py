@@ -14,6 +14,7 @@ from gpu_helpers import vis_from_arrays
 
 pytestmark = pytest.mark.gpu
 TOL = 5e-6
+FLIP_UW = np.array([-1.0, 1.0, -1.0])
 
 
 def dev():
@@ -201,3 +202,31 @@ def test_plane_chunking_matches_resident(bucket, monkeypatch):
     assert info["nplanes"] > 2 and info2["plane_chunk"] == 1
     assert rel_rms(part.cpu().numpy(), full.cpu().numpy()) < 1e-6
     assert rel_rms(vpart.cpu().numpy(), vfull.cpu().numpy()) < 1e-6
+
+
+def test_full_size_invert_matches_c_restatement():
+    """C2 geometry at the full 4096^2 image (8192^2 grid, 9 w planes): the HIP
+    invert of 2 of the 64 channels against oracle/wgrid_cpu.c (the C
+    restatement of the same w-gridding algorithm, itself pinned to the exact
+    direct sums in tests/test_oracle_golden.py).  Both sides approximate the
+    exact sum to ~1e-6, so they agree to that level."""
+    import math
+    import wgrid_cpu
+    from ska_sdp_func_python_amd import kernels, simulation
+    fn, n_def, lat, dec = simulation.CONFIGS["MID"]
+    ha = np.linspace(-0.5, 0.5, 100) * 8.0 * math.pi / 12.0
+    uvw, _ = simulation.observe(fn(n_def, seed=1), math.radians(lat), math.radians(dec), ha)
+    uvw = uvw.reshape(-1, 3)
+    allf = np.linspace(0.95e9, 1.76e9, 64)
+    umax = float(np.max(np.abs(uvw[:, :2]))) * allf.max() / orc.C_LIGHT
+    freq = allf[[0, 63]]
+    rng = np.random.default_rng(17)
+    ms = (rng.normal(size=(uvw.shape[0], 2)) + 1j * rng.normal(size=(uvw.shape[0], 2))).astype(np.complex64)
+    cell = 0.25 / umax
+    fuvw = uvw * FLIP_UW
+    ref, _, _ = wgrid_cpu.ms2dirty(fuvw, freq, ms, None, 4096, 4096, cell, cell, 1e-12, True,
+                                   nthreads=16)
+    out, info = kernels.ms2dirty(T(uvw), T(freq), T(ms), None, 4096, 4096, cell, cell, 1e-12, True,
+                                 flip_uw=True)
+    assert info["nplanes"] >= 8 and info["ngrid_x"] == 8192
+    assert rel_rms(out.cpu().numpy(), ref) < 5e-6
