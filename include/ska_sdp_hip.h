@@ -202,6 +202,57 @@ int sdp_hip_solve_gains(int nsolve, int nants, int nbl, const int32_t *row_start
                         int phase_only, int refant, double damping, void *stream,
                         char *errbuf, size_t errbuf_len);
 
+/*
+ * Imaging weights, replacing the Python row loops of
+ * grid_visibility_weight_to_griddata (reference
+ * src/ska_sdp_func_python/grid_data/gridding.py:258-334) and
+ * griddata_visibility_reweight (:362-499), which weight_visibility
+ * (src/ska_sdp_func_python/imaging/weighting.py:35-68) chains, and the two
+ * tapers (weighting.py:71-136).
+ *   uvw          [nrow, 3] f64 metres (nrow = ntimes * nbaselines)
+ *   freq         [nchan] f64 Hz
+ *   weight       [nrow, nchan, npol] f64 (the Visibility's weight)
+ *   flags        [nrow, nchan, npol] integers of flag_bytes (1, 4 or 8) or
+ *                NULL; flagged weight = weight * (1 - flags) as in the
+ *                datamodels' flagged_weight
+ *   vis_to_im    [nchan] int32 image channel of each visibility channel
+ *   grid_wcs     [6] f64: crval, cdelt, crpix of the GridData's UU axis, then
+ *                of its VV axis; cell = round((uv - crval) / cdelt + crpix - 1)
+ *   grid         [g_nchan, npol, ny, nx] f64: real part of the GridData
+ *   npol         1, 2 or 4
+ */
+/* Accumulates the flagged weight into grid at the sample's cell and at its
+ * conjugate's; sumwt [g_nchan, npol] += 2 * weight; rows whose cell or
+ * conjugate cell is off the grid add npol to *nskipped (int64, accumulated). */
+int sdp_hip_grid_weights(int64_t nrow, int nchan, int npol, const double *uvw,
+                         const double *freq, const double *weight,
+                         const void *flags, int flag_bytes,
+                         const int32_t *vis_to_im, const double *grid_wcs,
+                         double *grid, int g_nchan, int ny, int nx,
+                         double *sumwt, int64_t *nskipped, void *stream,
+                         char *errbuf, size_t errbuf_len);
+/* weighting 0 natural (imaging_weight = weight), 1 uniform (flagged weight /
+ * grid weight), 2 robust (flagged weight / (1 + f2 * grid weight), f2 =
+ * robust_coef * sum(sumwt) / sum(grid^2), robust_coef = (5 * 10^-robustness)^2;
+ * sumwt NULL means 2 * sum of flagged weights).  imaging_weight
+ * [nrow, nchan, npol] f64 is overwritten (it is read only where the grid
+ * weight is NaN, as the reference keeps the flagged imaging weight there). */
+int sdp_hip_reweight(int64_t nrow, int nchan, int npol, const double *uvw,
+                     const double *freq, const double *weight,
+                     const void *flags, int flag_bytes,
+                     const int32_t *vis_to_im, const double *grid_wcs,
+                     const double *grid, int g_nchan, int ny, int nx,
+                     int weighting, double robust_coef, const double *sumwt,
+                     int n_sumwt, double *imaging_weight, void *stream,
+                     char *errbuf, size_t errbuf_len);
+/* imaging_weight = flagged imaging weight * taper(row, chan), in place.
+ * kind 0 gaussian: exp(-param * |uv|^2 / lambda^2), param = pi^2 beam^2 / (4 ln 2);
+ * kind 1 tukey: tukey_filter(|uv| / max|uv|, param). */
+int sdp_hip_taper(int64_t nrow, int nchan, int npol, const double *uvw,
+                  const double *freq, const void *flags, int flag_bytes,
+                  int kind, double param, double *imaging_weight, void *stream,
+                  char *errbuf, size_t errbuf_len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,13 @@ One JSON line per path (SURVEY.md §8(d) work formulas):
            stokesI. fp64 global atomics (2 per tap).
            CPU: the reference's per-visibility loop restated (ref_oracle.grid_cf)
            on 30000 visibilities, scaled linearly.
+* weighting C2 layout (123.6 Mvis, weight f64 + flags int64, the datamodels'
+           dtypes) on the 4096^2 uv grid of the C2 image: weight_visibility
+           uniform = grid_weights + reweight.  HBM bound; algorithmic bytes
+           per sample: grid pass 8 (weight) + 8 (flags) + 24/nchan (uvw),
+           reweight pass the same + 8 (imaging weight out).
+           CPU: oracle/weighting_oracle.py (vectorised numpy restatement) on
+           8 of the 64 channels, scaled linearly.
 """
 
 import json
@@ -37,7 +44,8 @@ from ska_sdp_func_python_amd import kernels, simulation  # noqa: E402
 HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3
 dev = torch.device("cuda:0")
-which = sys.argv[1].split(",") if len(sys.argv) > 1 else ["dft", "stefcal", "predict", "cfgrid"]
+which = (sys.argv[1].split(",") if len(sys.argv) > 1
+         else ["dft", "stefcal", "predict", "cfgrid", "weighting"])
 CORES = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0)),
             len(os.sched_getaffinity(0)))
 
@@ -212,3 +220,63 @@ if "cfgrid" in which:
                            "kind": "port",
                            "sample": f"ref_oracle.grid_cf (the reference's per-visibility loop), "
                                      f"{ns} vis in {tc:.1f} s"}})
+
+if "weighting" in which:
+    import weighting_oracle as wo
+    nchan = 64
+    obs = simulation.device_observation(100, nchan, 0.95e9, 1.76e9, device=dev)
+    nrow = obs["nrow"]
+    uvw, freq = obs["uvw"].contiguous(), obs["freq"]
+    del obs
+    torch.manual_seed(3)
+    wt = torch.rand((nrow, nchan, 1), dtype=torch.float64, device=dev) + 0.5
+    flags = (torch.rand((nrow, nchan, 1), device=dev) < 0.01).to(torch.int64)
+    iw = torch.empty_like(wt)
+    freq_h = freq.cpu().numpy()
+    uvw_h = uvw.cpu().numpy()
+    umax = float(np.abs(uvw_h[:, :2]).max() * freq_h.max() / wo.C_M_S)
+    n = 4096
+    cell = 0.25 / umax
+    du = 1.0 / (n * cell)
+    wcs = ((0.0, -du, n // 2 + 1), (0.0, du, n // 2 + 1))
+    v2i = torch.zeros(nchan, dtype=torch.int32, device=dev)
+    grid = torch.zeros((1, 1, n, n), dtype=torch.float64, device=dev)
+    sumwt = torch.zeros((1, 1), dtype=torch.float64, device=dev)
+
+    def gridw():
+        grid.zero_()
+        sumwt.zero_()
+        return kernels.grid_weights(uvw, freq, wt, flags, v2i, wcs, grid, sumwt)
+
+    t_grid, sk = gpu_time(gridw)
+    t_uni, _ = gpu_time(lambda: kernels.reweight(uvw, freq, wt, flags, v2i, wcs, grid, iw, "uniform"))
+    t_rob, _ = gpu_time(lambda: kernels.reweight(uvw, freq, wt, flags, v2i, wcs, grid, iw, "robust",
+                                                 robustness=0.0, sumwt=sumwt))
+    t_tap, _ = gpu_time(lambda: kernels.taper(uvw, freq, flags, iw, "gaussian", 1e-6))
+    nvis = nrow * nchan
+    b_grid = nvis * (8 + 8 + 24.0 / nchan)
+    b_rew = nvis * (8 + 8 + 8 + 24.0 / nchan)
+    t_wv = t_grid + t_uni
+    # CPU: 8-channel sample through the numpy restatement
+    cs = 8
+    sel = np.arange(cs) * (nchan // cs)
+    wt_h = wt[:, sel].cpu().numpy()
+    fl_h = flags[:, sel].cpu().numpy()
+    t0 = time.perf_counter()
+    g_h, s_h, _ = wo.grid_weights(uvw_h, freq_h[sel], wt_h * (1 - fl_h), np.zeros(cs, int), wcs, 1, n, n)
+    wo.reweight(uvw_h, freq_h[sel], wt_h * (1 - fl_h), wt_h * (1 - fl_h), np.zeros(cs, int), wcs, g_h,
+                "uniform")
+    tc = (time.perf_counter() - t0) * nchan / cs
+    emit({"path": "weight_visibility uniform (C2 layout, 4096^2 uv grid)", "nvis": nvis,
+          "gpu_ms": round(t_wv * 1e3, 3), "value": round(nvis / t_wv / 1e6, 1), "unit": "Mvis/s",
+          "stages_ms": {"grid_weights": round(t_grid * 1e3, 3), "reweight_uniform": round(t_uni * 1e3, 3),
+                        "reweight_robust": round(t_rob * 1e3, 3), "taper_gaussian": round(t_tap * 1e3, 3)},
+          "skipped": int(sk.item()),
+          "roofline": {"bound": "hbm", "grid_weights_GBs": round(b_grid / t_grid / 1e9, 1),
+                       "reweight_GBs": round(b_rew / t_uni / 1e9, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round((b_grid + b_rew) / t_wv / 1e9 / HBM_PEAK_GBS, 4),
+                       "note": "16.4 B/sample in (weight f64, flags int64, uvw), +8 B out for reweight"},
+          "cpu_baseline": {"value": round(nvis / tc / 1e6, 3), "unit": "Mvis/s", "cores": 1,
+                           "kind": "port",
+                           "sample": f"weighting_oracle grid_weights + reweight (numpy) on {cs} of "
+                                     f"{nchan} channels, {tc * cs / nchan:.1f} s, scaled x{nchan // cs}"}})

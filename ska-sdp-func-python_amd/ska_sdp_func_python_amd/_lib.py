@@ -96,6 +96,14 @@ SIGNATURES = {
     "sdp_hip_solve_gains": [
         c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
         c_vp, c_vp, c_int, c_dbl, c_int, c_int, c_dbl, c_vp] + _ERR,
+    "sdp_hip_grid_weights": [
+        c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int,
+        c_int, c_vp, c_vp, c_vp] + _ERR,
+    "sdp_hip_reweight": [
+        c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int,
+        c_int, c_int, c_dbl, c_vp, c_int, c_vp, c_vp] + _ERR,
+    "sdp_hip_taper": [
+        c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_dbl, c_vp, c_vp] + _ERR,
 }
 
 _lock = threading.Lock()

@@ -209,6 +209,18 @@ class DataArray:
         return self.data.sum(*a, **k)
 
 
+class _Derived(DataArray):
+    """Read-only DataArray over a computed value (``visibility_acc.u`` etc.,
+    which the reference reads through ``.data``, weighting.py:93)."""
+
+    def __init__(self, value):
+        object.__setattr__(self, "_value", value)
+
+    @property
+    def data(self):
+        return self._value
+
+
 class Dataset:
     """Variables live in ``_vars``; ``ds[name].data`` and ``ds.name`` both work."""
 
@@ -381,15 +393,15 @@ class _VisAcc:
 
     @property
     def u(self):
-        return self._v._vars["uvw"][..., 0]
+        return _Derived(self._v._vars["uvw"][..., 0])
 
     @property
     def v(self):
-        return self._v._vars["uvw"][..., 1]
+        return _Derived(self._v._vars["uvw"][..., 1])
 
     @property
     def w(self):
-        return self._v._vars["uvw"][..., 2]
+        return _Derived(self._v._vars["uvw"][..., 2])
 
     def qa_visibility(self, context=None):
         avis = np.abs(np.asarray(_host(self._v._vars["vis"])))

@@ -12,11 +12,16 @@ Mirrors reference ``src/ska_sdp_func_python/grid_data/gridding.py``:
   kernel sdp_hip_grid_cf (fp64 atomics).
 * ``degrid_visibility_from_griddata`` (:502-590): einsum("ij,ij") of the grid
   window with the CF, in sdp_hip_degrid_cf.
+* ``grid_visibility_weight_to_griddata`` (:258-334) and
+  ``griddata_visibility_reweight`` (:362-499): imaging weights in
+  sdp_hip_grid_weights / sdp_hip_reweight (same nearest-cell mapping and
+  skip rules; fp64 atomics), ``griddata_merge_weights`` (:337-359).
 * ``fft_griddata_to_image`` / ``fft_image_to_griddata`` (:593-645): centred
   2-D FFTs (reference fft_support.py:31-140) via rocFFT (torch.fft on the
   HIP device), times nx*ny on the inverse, with the optional gcf.
 """
 
+import copy
 import logging
 
 import numpy as np
@@ -142,6 +147,113 @@ def degrid_visibility_from_griddata(vis, griddata, cf):
     newvis["vis"].data = _device.like_input(out.reshape(nrows, nbaselines, nvchan, nvpol),
                                            vis["vis"].data)
     return newvis
+
+
+def _uv_wcs(griddata):
+    w = griddata.griddata_acc.griddata_wcs.wcs
+    return ((w.crval[0], w.cdelt[0], w.crpix[0]), (w.crval[1], w.cdelt[1], w.crpix[1]))
+
+
+def _weight_inputs(vis, dev):
+    """Device views of uvw [nrow, 3], frequency, weight / flags [nrow, nchan, npol]."""
+    nrows, nbaselines, nvchan, nvpol = vis.vis.shape
+    nrow = nrows * nbaselines
+    uvw = _device.to_dev(vis.uvw.data, torch.float64, dev).reshape(nrow, 3).contiguous()
+    freq = _device.to_dev(np.asarray(vis.frequency.data, dtype=float), torch.float64, dev)
+    wt = _device.to_dev(vis.weight.data, torch.float64, dev).reshape(nrow, nvchan, nvpol).contiguous()
+    fl = _device.to_dev(vis.flags.data, None, dev)
+    if fl.dtype not in kernels._FLAG_BYTES:
+        fl = fl.to(torch.int64)
+    fl = fl.reshape(nrow, nvchan, nvpol).contiguous()
+    return uvw, freq, wt, fl
+
+
+def grid_weights_device(vis, griddata):
+    """Weight grid (real f64, device) and sumwt (device) of
+    grid_visibility_weight_to_griddata, without leaving the device."""
+    assert vis.visibility_acc.polarisation_frame == griddata.griddata_acc.polarisation_frame
+    dev = _device.device()
+    nchan, npol, ny, nx = griddata["pixels"].data.shape
+    uvw, freq, wt, fl = _weight_inputs(vis, dev)
+    v2i = torch.as_tensor(_vis_to_im(griddata, vis.frequency.data), dtype=torch.int32, device=dev)
+    grid = torch.zeros((nchan, npol, ny, nx), dtype=torch.float64, device=dev)
+    sumwt = torch.zeros((nchan, npol), dtype=torch.float64, device=dev)
+    skipped = int(kernels.grid_weights(uvw, freq, wt, fl, v2i, _uv_wcs(griddata), grid, sumwt).item())
+    if skipped > 0:
+        log.warning("warning visibility_weight_to_griddata gridding: skipped %d visbility", skipped)
+    return grid, sumwt
+
+
+def grid_visibility_weight_to_griddata(vis, griddata):
+    """Reference gridding.py:258-334: both the sample's cell and its
+    conjugate's receive the flagged weight; returns (griddata, sumwt)."""
+    grid, sumwt = grid_weights_device(vis, griddata)
+    griddata["pixels"].data = _device.like_input(grid.to(torch.complex128),
+                                                 griddata["pixels"].data)
+    return griddata, sumwt.cpu().numpy()
+
+
+def griddata_merge_weights(gd_list):
+    """Reference gridding.py:337-359: sum the weight grids onto the centre one."""
+    centre = len(gd_list) // 2
+    gd = copy.deepcopy(gd_list[centre][0])
+    sumwt = gd_list[centre][1]
+    frequency = 0.0
+    bandwidth = 0.0
+    for i, g in enumerate(gd_list):
+        if i != centre:
+            gd["pixels"].data += g[0]["pixels"].data
+            sumwt += g[1]
+        frequency += g[0].griddata_acc.griddata_wcs.wcs.crval[3]
+        bandwidth += g[0].griddata_acc.griddata_wcs.wcs.cdelt[3]
+    gd.griddata_acc.griddata_wcs.wcs.cdelt[3] = bandwidth
+    gd.griddata_acc.griddata_wcs.wcs.crval[3] = frequency / len(gd_list)
+    return gd, sumwt
+
+
+def _store(vis, name, value):
+    """Write a device result into vis[name] in place, on the variable's side."""
+    cur = vis[name].data
+    if _device.is_device(cur):
+        if cur.dtype == value.dtype and cur.is_contiguous() and cur.data_ptr() == value.data_ptr():
+            return
+        cur.copy_(value.reshape(cur.shape))
+    else:
+        cur[...] = value.reshape(cur.shape).cpu().numpy()
+
+
+def _reweight_device(vis, grid, wcs, v2i, weighting, robustness, sumwt):
+    dev = _device.device()
+    nrows, nbaselines, nvchan, nvpol = vis.vis.shape
+    uvw, freq, wt, fl = _weight_inputs(vis, dev)
+    iw = _device.to_dev(vis.imaging_weight.data, torch.float64, dev).reshape(
+        nrows * nbaselines, nvchan, nvpol)
+    if not iw.is_contiguous():
+        iw = iw.contiguous()
+    sw = None if sumwt is None else _device.to_dev(np.asarray(sumwt, dtype=float) if not
+                                                   _device.is_device(sumwt) else sumwt,
+                                                   torch.float64, dev).contiguous()
+    kernels.reweight(uvw, freq, wt, fl, v2i, wcs, grid, iw, weighting=weighting,
+                     robustness=robustness, sumwt=sw)
+    _store(vis, "imaging_weight", iw)
+    return vis
+
+
+def griddata_visibility_reweight(vis, griddata, weighting="uniform", robustness=0.0, sumwt=None):
+    """Reference gridding.py:362-499: natural copies the weight; uniform
+    divides the flagged weight by the gridded weight at the sample's cell;
+    robust (Briggs) divides by 1 + f2 * gridded weight; samples off the grid
+    or on an empty cell get zero."""
+    if griddata is not None:
+        assert vis.visibility_acc.polarisation_frame == griddata.griddata_acc.polarisation_frame
+    assert weighting in ["natural", "uniform", "robust"], f"Weighting {weighting} not supported"
+    if weighting == "natural":
+        return _reweight_device(vis, None, None, None, "natural", robustness, None)
+    dev = _device.device()
+    grid = torch.real(_device.to_dev(griddata["pixels"].data, None, dev)).to(torch.float64)
+    v2i = torch.as_tensor(_vis_to_im(griddata, vis.frequency.data), dtype=torch.int32, device=dev)
+    return _reweight_device(vis, grid.contiguous(), _uv_wcs(griddata), v2i, weighting, robustness,
+                            sumwt)
 
 
 def _centred(x, inverse):

@@ -248,3 +248,85 @@ def degrid_cf(maps, vis_to_im, grid, cf, nrow, nchan, out):
               _ptr(grid), gn, ny, nx, _ptr(cf), cfn, nw, ndv, ndu, gv, gu, _ptr(out),
               _ptr(skipped), _stream(grid.device))
     return skipped
+
+
+# ---- imaging weights (sdp_hip_grid_weights / sdp_hip_reweight / sdp_hip_taper)
+_FLAG_BYTES = {torch.int64: 8, torch.int32: 4, torch.int8: 1, torch.uint8: 1, torch.bool: 1}
+WEIGHTING = {"natural": 0, "uniform": 1, "robust": 2}
+
+
+def _weight_operands(uvw, freq, weight, flags):
+    _check_uvw(uvw)
+    for t, n in ((freq, "freq"), (weight, "weight")):
+        _on_gpu(t, n)
+        if t.dtype != torch.float64 or not t.is_contiguous():
+            raise ValueError(f"{n} must be a contiguous float64 device tensor")
+    if not uvw.is_contiguous():
+        raise ValueError("uvw must be contiguous [nrow, 3]")
+    nrow, nchan, npol = weight.shape
+    if uvw.shape[0] != nrow or freq.numel() != nchan:
+        raise ValueError("weight must be [nrow, nchan, npol] matching uvw and freq")
+    fb = 0
+    if flags is not None:
+        _on_gpu(flags, "flags")
+        if flags.shape != weight.shape or not flags.is_contiguous() or flags.dtype not in _FLAG_BYTES:
+            raise ValueError("flags must be a contiguous integer tensor shaped like weight")
+        fb = _FLAG_BYTES[flags.dtype]
+    return nrow, nchan, npol, fb
+
+
+def _wcs6(wcs):
+    return torch.tensor([float(x) for ax in wcs for x in ax], dtype=torch.float64)
+
+
+def grid_weights(uvw, freq, weight, flags, vis_to_im, wcs, grid, sumwt):
+    """Accumulate flagged weights into ``grid`` [g_nchan, npol, ny, nx] f64 and
+    ``sumwt`` [g_nchan, npol]; ``wcs`` = ((crval, cdelt, crpix) of UU, of VV).
+    Returns the device count of skipped (row, chan, pol) samples."""
+    nrow, nchan, npol, fb = _weight_operands(uvw, freq, weight, flags)
+    gn, gp, ny, nx = grid.shape
+    if gp != npol or grid.dtype != torch.float64 or not grid.is_contiguous():
+        raise ValueError("grid must be contiguous float64 [g_nchan, npol, ny, nx]")
+    if sumwt.shape != (gn, npol) or sumwt.dtype != torch.float64:
+        raise ValueError("sumwt must be float64 [g_nchan, npol]")
+    w6 = _wcs6(wcs).to(uvw.device)
+    skipped = torch.zeros(1, dtype=torch.int64, device=uvw.device)
+    _lib.call("sdp_hip_grid_weights", nrow, nchan, npol, _ptr(uvw), _ptr(freq), _ptr(weight),
+              _ptr(flags), fb, _ptr(vis_to_im), _ptr(w6), _ptr(grid), gn, ny, nx, _ptr(sumwt),
+              _ptr(skipped), _stream(uvw.device))
+    return skipped
+
+
+def reweight(uvw, freq, weight, flags, vis_to_im, wcs, grid, imaging_weight, weighting="uniform",
+             robustness=0.0, sumwt=None):
+    """Overwrite ``imaging_weight`` [nrow, nchan, npol] f64 in place."""
+    if weighting not in WEIGHTING:
+        raise AssertionError(f"Weighting {weighting} not supported")
+    nrow, nchan, npol, fb = _weight_operands(uvw, freq, weight, flags)
+    _on_gpu(imaging_weight, "imaging_weight")
+    if (imaging_weight.shape != weight.shape or imaging_weight.dtype != torch.float64
+            or not imaging_weight.is_contiguous()):
+        raise ValueError("imaging_weight must be contiguous float64 shaped like weight")
+    coef = (5.0 * 10.0 ** (-robustness)) ** 2
+    if grid is None:
+        gn, ny, nx, w6 = 1, 1, 1, torch.tensor([0.0, 1.0, 1.0, 0.0, 1.0, 1.0], dtype=torch.float64)
+    else:
+        gn, _, ny, nx = grid.shape
+        w6 = _wcs6(wcs)
+    w6 = w6.to(uvw.device)
+    ns = 0 if sumwt is None else sumwt.numel()
+    _lib.call("sdp_hip_reweight", nrow, nchan, npol, _ptr(uvw), _ptr(freq), _ptr(weight),
+              _ptr(flags), fb, _ptr(vis_to_im), _ptr(w6), _ptr(grid), gn, ny, nx,
+              WEIGHTING[weighting], coef, _ptr(sumwt), ns, _ptr(imaging_weight),
+              _stream(uvw.device))
+    return imaging_weight
+
+
+def taper(uvw, freq, flags, imaging_weight, kind, param):
+    """In place: imaging_weight = flagged imaging weight * taper; kind
+    "gaussian" (param = pi^2 beam^2 / (4 ln 2)) or "tukey" (param = r)."""
+    nrow, nchan, npol, fb = _weight_operands(uvw, freq, imaging_weight, flags)
+    _lib.call("sdp_hip_taper", nrow, nchan, npol, _ptr(uvw), _ptr(freq), _ptr(flags), fb,
+              {"gaussian": 0, "tukey": 1}[kind], float(param), _ptr(imaging_weight),
+              _stream(uvw.device))
+    return imaging_weight

@@ -172,3 +172,26 @@ def grid_cf_sharded(maps, vis_to_im, vis, wt, cf, grid, sumwt, group=None, grid_
         dist.all_reduce(grid, op=dist.ReduceOp.SUM, group=group)
         dist.all_reduce(sumwt, op=dist.ReduceOp.SUM, group=group)
     return grid, sumwt
+
+
+def weight_sharded(uvw, freq, weight, flags, vis_to_im, wcs, grid, sumwt, imaging_weight,
+                   weighting="uniform", robustness=0.0, group=None, grid_fn=None,
+                   reweight_fn=None):
+    """Channel-sharded weight_visibility (reference imaging/weighting.py:35-68
+    with grid_data/gridding.py:258-499): each rank grids the flagged weights
+    of its channels into ``grid``/``sumwt`` (zeroed by the caller), one
+    all-reduce of the weight grid and of sumwt gives every rank the global
+    grid, then each rank reweights its own samples with no further exchange.
+    Robust weighting uses the all-reduced sumwt, as weight_visibility passes
+    the gridding's sumwt.  Returns the rank-local imaging_weight."""
+    if grid_fn is None or reweight_fn is None:
+        from . import kernels
+        grid_fn = grid_fn or kernels.grid_weights
+        reweight_fn = reweight_fn or kernels.reweight
+    if weighting != "natural":
+        grid_fn(uvw, freq, weight, flags, vis_to_im, wcs, grid, sumwt)
+        if _dist_on():
+            dist.all_reduce(grid, op=dist.ReduceOp.SUM, group=group)
+            dist.all_reduce(sumwt, op=dist.ReduceOp.SUM, group=group)
+    return reweight_fn(uvw, freq, weight, flags, vis_to_im, wcs, grid, imaging_weight,
+                       weighting=weighting, robustness=robustness, sumwt=sumwt)

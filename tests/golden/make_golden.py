@@ -17,6 +17,10 @@ Fixtures:
   cfgrid_*.npz     grid_visibility_to_griddata / degrid_visibility_from_griddata
                    with spatial_mapping         (grid_data/gridding.py:33-255, :502-590)
   fft_*.npz        fft / ifft centred transforms (fourier_transforms/fft_support.py:31-140)
+  weight_*.npz     weight_visibility, grid_visibility_weight_to_griddata,
+                   griddata_visibility_reweight, taper_visibility_gaussian/_tukey
+                   (imaging/weighting.py:35-136, grid_data/gridding.py:33-60,
+                   :258-499, util/array_functions.py:85-99)
   nufft_c1.npz     ORACLE-generated (exact direct sums, oracle/nufft_oracle.py):
                    ducc0 is unavailable, the ducc0 boundary is parity-unpinned.
 """
@@ -217,6 +221,82 @@ def make_cfgrid():
              degridded=dv.vis.data)
 
 
+def _weight_vis(rng, pf, nchan, f_lo, f_hi, nants=12, ntimes=6):
+    import math
+    fn, _, lat, dec = simulation.CONFIGS["MID"]
+    layout = fn(nants, seed=3)
+    ha = np.linspace(-1.0, 1.0, ntimes) * math.pi / 12.0
+    uvw, bl = simulation.observe(layout, math.radians(lat), math.radians(dec), ha)
+    npol = pf.npol
+    freq = np.linspace(f_lo, f_hi, nchan)
+    shape = uvw.shape[:2] + (nchan, npol)
+    return dm.Visibility.constructor(
+        frequency=freq, channel_bandwidth=np.full(nchan, 1e6), phasecentre=dm.SkyCoord(0, -0.5),
+        uvw=uvw, time=np.arange(ntimes, dtype=float),
+        vis=rng.normal(size=shape) + 1j * rng.normal(size=shape),
+        weight=rng.uniform(0.5, 2.0, shape), flags=(rng.uniform(size=shape) < 0.05).astype(int),
+        baselines=bl, polarisation_frame=pf, imaging_weight=rng.uniform(0.5, 2.0, shape))
+
+
+def make_weighting():
+    """Imaging weights.  The cell size puts ~10% of the
+    samples (or their conjugates) outside the weight grid, exercising the
+    skip/zero rules (gridding.py:299-310, :435-446)."""
+    from ska_sdp_func_python_amd.util import coordinate_support  # noqa: F401
+    gns = load_reference("grid_data/gridding.py",
+                         ["convolution_mapping_visibility", "spatial_mapping",
+                          "grid_visibility_weight_to_griddata", "griddata_visibility_reweight"])
+    ans = load_reference("util/array_functions.py", ["tukey_filter"])
+
+    class _PC:
+        C_M_S = dm.C_M_S
+    wns = load_reference("imaging/weighting.py",
+                         ["weight_visibility", "taper_visibility_gaussian", "taper_visibility_tukey"],
+                         {"create_griddata_from_image": dm.create_griddata_from_image,
+                          "grid_visibility_weight_to_griddata":
+                              gns["grid_visibility_weight_to_griddata"],
+                          "griddata_visibility_reweight": gns["griddata_visibility_reweight"],
+                          "tukey_filter": ans["tukey_filter"], "physical_constants": _PC})
+    cases = (("p1", "stokesI", 4, 1.30e9, 1.40e9, 1, 64),
+             ("p4", "linear", 2, 1.30e9, 1.34e9, 2, 48))
+    for tag, pname, nchan, f_lo, f_hi, im_nchan, npix in cases:
+        rng = np.random.default_rng(31 + nchan)
+        pf = dm.PolarisationFrame(pname)
+        vis = _weight_vis(rng, pf, nchan, f_lo, f_hi)
+        uvmax = simulation.max_uv_lambda(vis)
+        cell = 1.0 / (2.0 * 0.85 * uvmax)
+        if im_nchan == 1:
+            fc, bw = 0.5 * (f_lo + f_hi), 2.0 * (f_hi - f_lo)
+        else:
+            fc, bw = f_lo, (f_hi - f_lo) / (nchan - 1)
+        model = dm.create_image(npix, cell, vis.phasecentre, polarisation_frame=pf,
+                                frequency=fc, channel_bandwidth=bw, nchan=im_nchan)
+        gd = dm.create_griddata_from_image(model, polarisation_frame=pf)
+        gd, sumwt = gns["grid_visibility_weight_to_griddata"](vis.copy(deep=True), gd)
+        out = {"grid": gd["pixels"].data.real.copy(), "sumwt": sumwt}
+        for key, kw in (("uniform", dict(weighting="uniform")),
+                        ("robust0", dict(weighting="robust", robustness=0.0, sumwt=sumwt)),
+                        ("robustm1p5", dict(weighting="robust", robustness=-1.5)),
+                        ("natural", dict(weighting="natural"))):
+            v = gns["griddata_visibility_reweight"](vis.copy(deep=True),
+                                                    None if key == "natural" else gd, **kw)
+            out[f"iw_{key}"] = v.imaging_weight.data.copy()
+        vu = wns["weight_visibility"](vis.copy(deep=True), model, weighting="robust",
+                                      robustness=0.5)
+        out["iw_wv_robust0p5"] = vu.imaging_weight.data.copy()
+        vu = wns["weight_visibility"](vis.copy(deep=True), model, weighting="uniform")
+        out["iw_wv_uniform"] = vu.imaging_weight.data.copy()
+        out["iw_gauss"] = wns["taper_visibility_gaussian"](vu.copy(deep=True), beam=4 * cell) \
+            .imaging_weight.data.copy()
+        out["iw_tukey"] = wns["taper_visibility_tukey"](vu.copy(deep=True), tukey=0.3) \
+            .imaging_weight.data.copy()
+        save(f"weight_{tag}.npz", uvw=vis.uvw.data, freq=vis.frequency.data,
+             weight=vis.weight.data, flags=vis.flags.data, imaging_weight=vis.imaging_weight.data,
+             pol_frame=np.array(pname), npix=np.array(npix), cell=np.array(cell),
+             model_freq=np.array(fc), model_bw=np.array(bw), model_nchan=np.array(im_nchan),
+             gauss_beam=np.array(4 * cell), tukey=np.array(0.3), **out)
+
+
 def make_fft():
     ns = load_reference("fourier_transforms/fft_support.py", ["fft", "ifft"],
                         {"pyfftw_exists": False, "pyfftw": None})
@@ -249,8 +329,13 @@ def make_nufft_c1():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()[f"make_{name}"]()
+        sys.exit(0)
     make_dft()
     make_solver()
     make_cfgrid()
     make_fft()
     make_nufft_c1()
+    make_weighting()

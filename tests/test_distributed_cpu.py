@@ -230,3 +230,71 @@ def test_sharded_cf_gridding_equals_full():
     for _, _, (grid, sumwt) in res:
         np.testing.assert_allclose(grid, full, rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(sumwt, sw, rtol=1e-12)
+
+
+def _oracle_grid_weights(uvw, freq, weight, flags, v2i, wcs, grid, sumwt):
+    import weighting_oracle as wo
+    fw = (weight * (1 - flags)).numpy()
+    g, s, _ = wo.grid_weights(uvw.numpy(), freq.numpy(), fw, v2i.numpy(), wcs, grid.shape[0],
+                              grid.shape[2], grid.shape[3])
+    grid += torch.as_tensor(g)
+    sumwt += torch.as_tensor(s)
+
+
+def _oracle_reweight(uvw, freq, weight, flags, v2i, wcs, grid, imaging_weight, weighting,
+                     robustness, sumwt):
+    import weighting_oracle as wo
+    m = (1 - flags).numpy()
+    out = wo.reweight(uvw.numpy(), freq.numpy(), weight.numpy() * m,
+                      imaging_weight.numpy() * m, v2i.numpy(), wcs, grid.numpy(), weighting,
+                      robustness, sumwt.numpy())
+    imaging_weight.copy_(torch.as_tensor(out))
+    return imaging_weight
+
+
+def _weight_worker(rank, world, port, data, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ska_sdp_func_python_amd.parallel import interleaved_channels, weight_sharded
+    uvw, freq, wt, flags, imw, wcs, n, weighting = data
+    ch = interleaved_channels(len(freq), rank, world)
+    grid = torch.zeros((1, 1, n, n), dtype=torch.float64)
+    sumwt = torch.zeros((1, 1), dtype=torch.float64)
+    out = weight_sharded(torch.as_tensor(uvw), torch.as_tensor(freq[ch]),
+                         torch.as_tensor(wt[:, ch].copy()), torch.as_tensor(flags[:, ch].copy()),
+                         torch.zeros(len(ch), dtype=torch.int32), wcs, grid, sumwt,
+                         torch.as_tensor(imw[:, ch].copy()), weighting=weighting, robustness=0.5,
+                         grid_fn=_oracle_grid_weights, reweight_fn=_oracle_reweight)
+    q.put((rank, ch, out.numpy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("weighting", ["uniform", "robust"])
+def test_sharded_weighting_equals_full(weighting):
+    import weighting_oracle as wo
+    rng = np.random.default_rng(8)
+    nrow, nchan, n = 300, 6, 32
+    freq = np.linspace(1e9, 1.2e9, nchan)
+    uvw = rng.normal(size=(nrow, 3)) * 300.0
+    wt = rng.uniform(0.5, 2.0, (nrow, nchan, 1))
+    flags = (rng.uniform(size=(nrow, nchan, 1)) < 0.1).astype(np.int64)
+    imw = rng.uniform(0.5, 2.0, (nrow, nchan, 1))
+    du = 2 * np.abs(uvw[:, :2]).max() * freq.max() / wo.C_M_S / n
+    wcs = ((0.0, -du, n // 2 + 1), (0.0, du, n // 2 + 1))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + int(rng.integers(500, 1000))
+    args = (uvw, freq, wt, flags, imw, wcs, n, weighting)
+    procs = [ctx.Process(target=_weight_worker, args=(r, 2, port, args, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    fw = wt * (1 - flags)
+    v2i = np.zeros(nchan, int)
+    grid, sumwt, _ = wo.grid_weights(uvw, freq, fw, v2i, wcs, 1, n, n)
+    full = wo.reweight(uvw, freq, fw, imw * (1 - flags), v2i, wcs, grid, weighting, 0.5, sumwt)
+    for _, ch, out in res:
+        np.testing.assert_allclose(out, full[:, ch], rtol=1e-12)
