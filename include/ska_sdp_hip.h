@@ -96,6 +96,42 @@ int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride,
                      size_t errbuf_len);
 
 /*
+ * sdp_hip_ms2dirty_vis -- sdp_hip_ms2dirty with the visibility-side prologue
+ * of invert_ng fused into its first pass, so the
+ * Visibility's own arrays are read in place:
+ *   flagged_vis / flagged_imaging_weight (reference imaging/ng.py:191, :202;
+ *   value * (1 - flags)), convert_pol_frame (ng.py:193-198) and the weight sum
+ *   sumwt (ng.py:258, :289).
+ * vis       [nrow, nchan, npol_vis] c64/c128 at pol 0, element strides
+ *           (row, chan, pol); NULL = unit visibilities (PSF)
+ * pol_coeff host array of 2*npol_vis doubles (re, im): image-pol visibility =
+ *           sum_k coeff_k * vis_k * (1 - flag_k) (one row of the conversion
+ *           matrix); NULL = no conversion, the image pol is vis pol `pol`
+ * wgt       weights of image pol `pol` (f32 or f64, wgt_dtype), strides
+ *           (row, chan); NULL = ones
+ * vis_flags [nrow, nchan, npol_vis] integers of flag_bytes at pol 0 with
+ *           strides, or NULL; the weight is masked with flag pol `pol`
+ * sumwt     device double, += sum over rows and channels of the masked
+ *           weights (NULL: not computed)
+ * Other arguments as sdp_hip_ms2dirty.
+ */
+int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride,
+                         const double *freq, int nchan, int64_t nrow,
+                         const void *vis, int vis_dtype, int64_t vis_row_stride,
+                         int64_t vis_chan_stride, int64_t vis_pol_stride,
+                         int npol_vis, const double *pol_coeff, const void *wgt,
+                         int wgt_dtype, int64_t wgt_row_stride,
+                         int64_t wgt_chan_stride, const void *vis_flags,
+                         int flag_bytes, int64_t flag_row_stride,
+                         int64_t flag_chan_stride, int64_t flag_pol_stride,
+                         int pol, int npix_x, int npix_y, double pixsize_x,
+                         double pixsize_y, double epsilon, int do_wstacking,
+                         unsigned flags, double *dirty, int64_t dirty_stride_x,
+                         int64_t dirty_stride_y, double *sumwt, void *stream,
+                         sdp_hip_wgrid_info *info, char *errbuf,
+                         size_t errbuf_len);
+
+/*
  * sdp_hip_dirty2ms -- replaces ducc0.wgridder.dirty2ms as called by
  * predict_ng (reference src/ska_sdp_func_python/imaging/ng.py:99-112 MFS,
  * :117-129 per channel).  Exact adjoint of sdp_hip_ms2dirty:

@@ -269,6 +269,53 @@ __device__ __forceinline__ unsigned run_reserve(unsigned key, bool valid, unsign
     return hb + (unsigned)(lane - head);
 }
 
+// Visibility-side prologue fused into the bucketing pass (sdp_hip_ms2dirty_vis,
+// SURVEY.md §8(f) rank 2): flag masking of the visibilities and weights,
+// fp64 weights, the polarisation-frame conversion of the reference's
+// convert_pol_frame (imaging/ng.py:193-198) as one row of its matrix, and
+// the weight sum the reference takes with numpy.sum (ng.py:258, :289).
+struct VisExtra {
+    int64_t vps = 0;           // vis pol stride (elements); vis points at pol 0 when conv
+    int npv = 1;               // vis pols combined
+    bool conv = false;         // vis_eff = sum_k coef_k * vis_k * (1 - flag_k)
+    double cre[4] = {1.0, 0.0, 0.0, 0.0}, cim[4] = {0.0, 0.0, 0.0, 0.0};
+    int wgt_f64 = 0;           // weights are f64 (else f32)
+    const void *flags = nullptr;
+    int fbytes = 0;            // 1 / 4 / 8 byte integer flags at pol 0
+    int64_t frs = 0, fcs = 0, fps = 0;
+    int fpol = 0;              // pol whose flag masks the weight (and the vis when !conv)
+    double *sumwt = nullptr;   // += sum of the effective weights (device, may be null)
+};
+
+constexpr int kSumSlots = 1024;
+
+__device__ __forceinline__ double flag_mask(const VisExtra &x, int64_t row, int chan, int pol) {
+    const int64_t i = row * x.frs + chan * x.fcs + pol * x.fps;
+    double f;
+    if (x.fbytes == 8) f = (double)static_cast<const int64_t *>(x.flags)[i];
+    else if (x.fbytes == 4) f = (double)static_cast<const int32_t *>(x.flags)[i];
+    else f = (double)static_cast<const int8_t *>(x.flags)[i];
+    return 1.0 - f;
+}
+
+__device__ __forceinline__ double eff_weight(const void *wgt, int64_t wrs, int64_t wcs,
+                                             const VisExtra &x, int64_t row, int chan) {
+    double w = 1.0;
+    if (wgt) {
+        const int64_t i = row * wrs + chan * wcs;
+        w = x.wgt_f64 ? static_cast<const double *>(wgt)[i]
+                      : (double)static_cast<const float *>(wgt)[i];
+    }
+    if (x.fbytes) w *= flag_mask(x, row, chan, x.fpol);
+    return w;
+}
+
+__device__ __forceinline__ double2 load_vis_d(const float2 *p) {
+    const float2 v = *p;
+    return make_double2(v.x, v.y);
+}
+__device__ __forceinline__ double2 load_vis_d(const double2 *p) { return *p; }
+
 __device__ __forceinline__ float2 load_vis(const float2 *p) { return *p; }
 __device__ __forceinline__ float2 load_vis(const double2 *p) {
     const double2 v = *p;
@@ -280,13 +327,38 @@ __device__ __forceinline__ float2 load_vis(const double2 *p) {
 // from a run-aggregated atomicAdd on the histogram; (key, rank) is stored.
 // Scatter pass: position = offs[key] + rank -- no atomics -- and the 32-byte
 // record is written there.  Invalid visibilities carry key 0xffffffff.
+template <class VT>
+__device__ __forceinline__ float2 eff_vis(const VT *vis, int64_t vrs, int64_t vcs,
+                                          const VisExtra &x, int64_t row, int chan) {
+    const VT *p = vis + row * vrs + chan * vcs;
+    if (!x.conv) {
+        if (!x.fbytes) return load_vis(p);
+        const double2 v = load_vis_d(p);
+        const double m = flag_mask(x, row, chan, x.fpol);
+        return make_float2((float)(v.x * m), (float)(v.y * m));
+    }
+    double re = 0.0, im = 0.0;
+    for (int k = 0; k < x.npv; ++k) {
+        if (x.cre[k] == 0.0 && x.cim[k] == 0.0) continue;
+        double2 v = load_vis_d(p + k * x.vps);
+        if (x.fbytes) {
+            const double m = flag_mask(x, row, chan, k);
+            v.x *= m;
+            v.y *= m;
+        }
+        re += x.cre[k] * v.x - x.cim[k] * v.y;
+        im += x.cre[k] * v.y + x.cim[k] * v.x;
+    }
+    return make_float2((float)re, (float)im);
+}
+
 template <class VT, bool kScatter, bool kGrid>
 __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__restrict__ uvw,
                          int64_t uvw_rs, const double *__restrict__ freq,
                          const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
-                         const float *__restrict__ wgt, int64_t wrs, int64_t wcs,
-                         unsigned *counter, uint2 *__restrict__ kr, VisRec *__restrict__ recs,
-                         unsigned long long *nbad) {
+                         const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x,
+                         double *sw_slots, unsigned *counter, uint2 *__restrict__ kr,
+                         VisRec *__restrict__ recs, unsigned long long *nbad) {
     // v indexes the part's visibilities (rows row0...); vg the call's
     const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t vg = row0 * g.nchan + v;
@@ -303,13 +375,15 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
         if (mine.x == 0xffffffffu) return;
         row = vg / g.nchan;
         chan = (int)(vg - row * g.nchan);
-        if (wgt) wt = wgt[row * wrs + chan * wcs];
+        wt = (float)eff_weight(wgt, wrs, wcs, x, row, chan);
         c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
     } else {
+        double wd = 0.0;
         if (valid) {
             row = vg / g.nchan;
             chan = (int)(vg - row * g.nchan);
-            if (wgt) wt = wgt[row * wrs + chan * wcs];
+            wd = eff_weight(wgt, wrs, wcs, x, row, chan);
+            wt = (float)wd;
             valid = (wt != 0.0f);
             if (valid) {
                 c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
@@ -322,14 +396,23 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
         const unsigned key = valid ? coord_key(g, c) : 0xffffffffu;
         const unsigned rank = (g.dbg & 8) ? 0u : run_reserve<true>(key, valid, counter);
         if (v < nvis) kr[v] = make_uint2(key, rank);
+        if (sw_slots) {
+            // weight sum: wave reduction, one atomic per wave into a slot
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) wd += __shfl_xor(wd, o, 64);
+            if ((threadIdx.x & 63) == 0 && wd != 0.0)
+                atomicAdd(&sw_slots[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) &
+                                    (kSumSlots - 1)],
+                          wd);
+        }
         return;
     }
     const unsigned pos = (g.dbg & 16) ? (unsigned)v : counter[mine.x] + mine.y;
     float cr = wt, ci = 0.0f;
     if (kGrid) {
-        const float2 x = vis ? load_vis(vis + row * vrs + chan * vcs) : make_float2(1.0f, 0.0f);
-        cr = x.x * wt;
-        ci = x.y * wt;
+        const float2 xv = vis ? eff_vis(vis, vrs, vcs, x, row, chan) : make_float2(1.0f, 0.0f);
+        cr = xv.x * wt;
+        ci = xv.y * wt;
     }
     if (g.do_w) {
         double ph = c.w * g.s0;
@@ -351,6 +434,14 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
     rec.p0 = (uint32_t)c.p0;
     rec.idx = (uint32_t)vg;
     recs[pos] = rec;
+}
+
+__global__ __launch_bounds__(64) void k_sum_slots(const double *__restrict__ slots, double *out) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < kSumSlots; i += 64) s += slots[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (threadIdx.x == 0) *out += s;
 }
 
 // work items: a group of `grp` consecutive buckets (same p0, same x) is
@@ -1372,13 +1463,14 @@ struct Inputs {
     const void *vis;
     int vis_dtype;
     int64_t vrs, vcs;
-    const float *wgt;
+    const void *wgt;  // f32, or f64 when x.wgt_f64
     int64_t wrs, wcs;
     int nx, ny;
     double px, py;
     double eps;
     int do_w;
     unsigned flags;
+    VisExtra x{};
 };
 
 // Bytes of w planes kept resident per pass: SDP_HIP_GRID_BUDGET_GB if set,
@@ -1598,27 +1690,29 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     SDP_HIP_CHECK(hipMemsetAsync(pt.nch + ngroups, 0, sizeof(unsigned), st));
 
     const unsigned nb = grid1d(std::max<int64_t>(pt.nvis, 1), 256);
+    double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
     auto launch_bucket = [&](auto scatter_tag, unsigned *counter) {
         constexpr bool S = decltype(scatter_tag)::value;
         VisRec *out = S ? recs : nullptr;
+        double *sl = S ? nullptr : slots;
         if (in.vis_dtype == SDP_HIP_C128) {
             if (grid_mode)
                 k_bucket<double2, S, true><<<nb, 256, 0, st>>>(
                     g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
-                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, counter, kr, out, pt.nbad);
+                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
             else
                 k_bucket<double2, S, false><<<nb, 256, 0, st>>>(
                     g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
-                    in.wcs, counter, kr, out, pt.nbad);
+                    in.wcs, in.x, sl, counter, kr, out, pt.nbad);
         } else {
             if (grid_mode)
                 k_bucket<float2, S, true><<<nb, 256, 0, st>>>(
                     g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
-                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, counter, kr, out, pt.nbad);
+                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
             else
                 k_bucket<float2, S, false><<<nb, 256, 0, st>>>(
                     g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
-                    in.wcs, counter, kr, out, pt.nbad);
+                    in.wcs, in.x, sl, counter, kr, out, pt.nbad);
         }
     };
     if (pt.nvis > 0) launch_bucket(std::false_type{}, pt.hist);
@@ -1889,8 +1983,16 @@ static dim3 tr_grid(const Geo &g, int xrows, int np) {
 static std::vector<hipEvent_t> bucket_parts(Plan &P, const Inputs &in, bool grid_mode,
                                             hipStream_t st) {
     std::vector<hipEvent_t> ev;
+    // weight sum of the fused prologue: slots zeroed before the parts' count
+    // passes, folded into *sumwt after the first part (all parts share slots)
+    double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
+    auto sum_end = [&](hipStream_t s) {
+        if (slots) k_sum_slots<<<1, 64, 0, s>>>(slots, in.x.sumwt);
+    };
     if (!P.aux_bucketing) {
+        if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
         for (size_t i = 0; i < P.parts.size(); ++i) bucket_part(P, (int)i, in, grid_mode, st);
+        sum_end(st);
         read_part_meta(P, st);
         return ev;
     }
@@ -1900,8 +2002,10 @@ static std::vector<hipEvent_t> bucket_parts(Plan &P, const Inputs &in, bool grid
     SDP_HIP_CHECK(hipEventRecord(ready, st));
     SDP_HIP_CHECK(hipStreamWaitEvent(aux, ready, 0));
     SDP_HIP_CHECK(hipEventDestroy(ready));
+    if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), aux));
     for (size_t i = 0; i < P.parts.size(); ++i) {
         bucket_part(P, (int)i, in, grid_mode, aux);
+        if (i + 1 == P.parts.size()) sum_end(aux);
         hipEvent_t e;
         SDP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         SDP_HIP_CHECK(hipEventRecord(e, aux));
@@ -2105,6 +2209,57 @@ int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride, const double *fr
                                 vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
                                 npix_x,      npix_y,          pixsize_x,      pixsize_y,
                                 epsilon,     do_wstacking,    flags};
+        wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
+    });
+}
+
+int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride, const double *freq, int nchan,
+                         int64_t nrow, const void *vis, int vis_dtype, int64_t vis_row_stride,
+                         int64_t vis_chan_stride, int64_t vis_pol_stride, int npol_vis,
+                         const double *pol_coeff, const void *wgt, int wgt_dtype,
+                         int64_t wgt_row_stride, int64_t wgt_chan_stride, const void *vis_flags,
+                         int flag_bytes, int64_t flag_row_stride, int64_t flag_chan_stride,
+                         int64_t flag_pol_stride, int pol, int npix_x, int npix_y,
+                         double pixsize_x, double pixsize_y, double epsilon, int do_wstacking,
+                         unsigned flags, double *dirty, int64_t dirty_stride_x,
+                         int64_t dirty_stride_y, double *sumwt, void *stream,
+                         sdp_hip_wgrid_info *info, char *errbuf, size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(dirty != nullptr && freq != nullptr && (uvw != nullptr || nrow == 0),
+                    "null pointer argument");
+        SDP_REQUIRE(npol_vis >= 1 && npol_vis <= 4, "npol_vis must be 1..4");
+        SDP_REQUIRE(pol >= 0 && pol < npol_vis, "pol out of range");
+        SDP_REQUIRE(wgt_dtype == SDP_HIP_F32 || wgt_dtype == SDP_HIP_F64,
+                    "weights must be f32 or f64");
+        SDP_REQUIRE(vis_flags == nullptr || flag_bytes == 1 || flag_bytes == 4 || flag_bytes == 8,
+                    "flag element size must be 1, 4 or 8 bytes");
+        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                          nrow,        vis,             vis_dtype,      vis_row_stride,
+                          vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
+                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                          epsilon,     do_wstacking,    flags};
+        wstack::VisExtra &x = in.x;
+        x.vps = vis_pol_stride;
+        x.npv = npol_vis;
+        x.wgt_f64 = wgt_dtype == SDP_HIP_F64;
+        x.flags = vis_flags;
+        x.fbytes = vis_flags ? flag_bytes : 0;
+        x.frs = flag_row_stride;
+        x.fcs = flag_chan_stride;
+        x.fps = flag_pol_stride;
+        x.fpol = pol;
+        x.sumwt = sumwt;
+        if (pol_coeff) {
+            x.conv = true;
+            for (int k = 0; k < npol_vis; ++k) {
+                x.cre[k] = pol_coeff[2 * k];
+                x.cim[k] = pol_coeff[2 * k + 1];
+            }
+        } else if (vis) {
+            // no conversion: the image pol is the vis pol `pol`
+            in.vis = static_cast<const char *>(vis) +
+                     pol * vis_pol_stride * (vis_dtype == SDP_HIP_C128 ? 16 : 8);
+        }
         wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
     });
 }

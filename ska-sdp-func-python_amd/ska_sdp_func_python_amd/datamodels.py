@@ -253,11 +253,14 @@ class Dataset:
         else:
             object.__setattr__(self, name, value)
 
-    def _copy_with(self, deep=True, zero_vars=()):
+    def _copy_with(self, deep=True, zero_vars=(), replace=None):
         new = object.__new__(type(self))
         variables = {}
+        replace = replace or {}
         for k, v in self._vars.items():
-            if deep:
+            if k in replace:
+                variables[k] = replace[k]
+            elif deep:
                 variables[k] = _clone(v, zero=k in zero_vars)
             else:
                 variables[k] = v
@@ -587,7 +590,9 @@ class Image(Dataset):
         return _ImageAcc(self)
 
     def copy(self, deep=True, data=None, zero=False):
-        return self._copy_with(deep=deep, zero_vars=("pixels",) if zero else ())
+        """``data`` (xarray's copy(data=...)) becomes the copy's pixels as is."""
+        return self._copy_with(deep=deep, zero_vars=("pixels",) if zero else (),
+                               replace=None if data is None else {"pixels": data})
 
 
 def create_image(npixel, cellsize, phasecentre, polarisation_frame=PolarisationFrame("stokesI"),

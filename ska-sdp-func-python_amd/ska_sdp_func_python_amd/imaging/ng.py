@@ -12,6 +12,11 @@ Mirrors reference ``src/ska_sdp_func_python/imaging/ng.py``:
   one channel and the vis several (:228), PSF puts 1 in pol 0 only
   (:231-233), pols whose vis are all zero are not gridded but their weights
   still enter ``sumwt`` (:238, :258, :267, :289), then ``normalise_sumwt``.
+  The flag masking, pol conversion, weight conversion and weight sums run
+  inside the HIP prologue of sdp_hip_ms2dirty_vis on the Visibility's own
+  arrays.  Gridding a pol whose visibilities are all
+  zero yields exactly the zero image the reference keeps, so that check
+  (ng.py:238) is not a separate pass here.
 
 The image transpose (:102, :257) is folded into the C ABI's output strides.
 Kwargs ``epsilon`` (default 1e-12, clamped to the fp32 floor 1e-7),
@@ -25,7 +30,7 @@ import numpy as np
 import torch
 
 from .. import _device, kernels
-from ..datamodels import Image, convert_pol_frame
+from ..datamodels import Image, convert_pol_frame, pol_conversion_matrix
 from .base import normalise_sumwt, shift_vis_to_image
 
 log = logging.getLogger("func-python-logger")
@@ -95,65 +100,75 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     assert isinstance(model, Image) or hasattr(model, "image_acc"), model
     assert model.image_acc.is_canonical()
 
-    im = model.copy(deep=True)
     epsilon = kwargs.get("epsilon", 1e-12)
     do_wstacking = kwargs.get("do_wstacking", True)
     verbosity = kwargs.get("verbosity", 0)
 
     dev = _device.device()
+    nchan, npol, ny, nx = model["pixels"].data.shape
+    image = torch.zeros((nchan, npol, ny, nx), dtype=torch.float64, device=dev)
+    # the reference's deep copy + zero fill (ng.py:173, :218) without
+    # copying the model's pixels
+    im = model.copy(deep=True, data=image)
     sbvis = shift_vis_to_image(bvis, im, tangent=True, inverse=False)
     freq = np.asarray(sbvis.frequency.data, dtype=float)
     nrows, nbaselines, vnchan, vnpol = sbvis.vis.shape
     nrow = nrows * nbaselines
 
+    # The Visibility's own arrays, read in place by the fused prologue of
+    # sdp_hip_ms2dirty_vis: flag masking (ng.py:191, :202), the pol-frame
+    # conversion (ng.py:193-198) as one matrix row per image pol, f64 weights
+    # and the weight sums (ng.py:258, :289) -- no O(Nvis) passes here.
     flags = _device.to_dev(sbvis.flags.data, None, dev)
-    keep = (1 - flags).to(torch.float32)
-    wgt = (_device.to_dev(sbvis.imaging_weight.data, torch.float32, dev) * keep).reshape(
-        nrow, vnchan, vnpol)
+    if flags.dtype not in kernels._FLAG_DT:
+        flags = flags.to(torch.int64)
+    flags = flags.reshape(nrow, vnchan, vnpol)
+    wgt = _device.to_dev(sbvis.imaging_weight.data, None, dev)
+    if wgt.dtype not in (torch.float32, torch.float64):
+        wgt = wgt.to(torch.float64)
+    wgt = wgt.reshape(nrow, vnchan, vnpol)
     ms = None
     if not dopsf:
         ms = _device.to_dev(sbvis.vis.data, None, dev)
         if ms.dtype not in (torch.complex64, torch.complex128):
             ms = ms.to(torch.complex128)
-        ms = (ms * keep.to(ms.real.dtype)).reshape(nrow, vnchan, vnpol)
-        ms = convert_pol_frame(ms, bvis.visibility_acc.polarisation_frame,
-                               im.image_acc.polarisation_frame, polaxis=2)
+        ms = ms.reshape(nrow, vnchan, vnpol)
+    conv = pol_conversion_matrix(bvis.visibility_acc.polarisation_frame,
+                                 im.image_acc.polarisation_frame)
     uvw = _device.to_dev(sbvis.uvw.data, torch.float64, dev).reshape(nrow, 3).contiguous()
     freq_t = _device.to_dev(freq, torch.float64, dev)
 
-    nchan, npol, ny, nx = im["pixels"].data.shape
     npixdirty = nx
     pixsize = _pixsize(im)
-    image = torch.zeros((nchan, npol, ny, nx), dtype=torch.float64, device=dev)
-    sumwt = np.zeros([nchan, npol])
+    sumwt_d = torch.zeros((nchan, npol), dtype=torch.float64, device=dev)
     vis_to_im = _vis_to_im(model, freq)
     mfs = nchan == 1 and vnchan > 1
 
     def grid_pol(pol, chans, ichan):
-        # dopsf: pol 0 is unit visibilities, the others are zero (ng.py:231-233)
-        if dopsf:
-            lms = None
-            nonzero = pol == 0
-        else:
-            lms = ms[:, chans, pol]
-            nonzero = bool(torch.any(lms != 0).item())
-        if nonzero:
-            _, info = kernels.ms2dirty(uvw, freq_t[chans], lms, wgt[:, chans, pol], npixdirty,
-                                       npixdirty, pixsize, pixsize, epsilon, do_wstacking,
-                                       flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
-                                       accumulate=True)
-            if verbosity:
-                log.info("invert_ng: %s", info)
-        return float(wgt[:, chans, pol].sum().item())
+        sw = sumwt_d[ichan, pol:pol + 1]
+        if dopsf and pol != 0:
+            # PSF: pol 0 holds unit visibilities, the others are zero and are
+            # not gridded (ng.py:231-233, :238); their weights still count
+            m = 1 - flags[:, chans, pol].to(torch.float64)
+            sw += (wgt[:, chans, pol].to(torch.float64) * m).sum()
+            return
+        coef = None if (dopsf or conv is None) else conv[pol]
+        _, info = kernels.ms2dirty_vis(
+            uvw, freq_t[chans], None if dopsf else ms[:, chans, :], pol, wgt[:, chans, pol],
+            flags[:, chans, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
+            do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
+            accumulate=True, sumwt=sw)
+        if verbosity:
+            log.info("invert_ng: %s", info)
 
     if mfs:
         for pol in range(npol):
-            sumwt[0, pol] += grid_pol(pol, slice(0, vnchan), 0)
+            grid_pol(pol, slice(0, vnchan), 0)
     else:
         for pol in range(npol):
             for vchan in range(vnchan):
-                ichan = int(vis_to_im[vchan])
-                sumwt[ichan, pol] += grid_pol(pol, slice(vchan, vchan + 1), ichan)
+                grid_pol(pol, slice(vchan, vchan + 1), int(vis_to_im[vchan]))
+    sumwt = sumwt_d.cpu().numpy()
 
     im["pixels"].data = image
     if normalise:

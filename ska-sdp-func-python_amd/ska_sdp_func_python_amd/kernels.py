@@ -85,6 +85,76 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
     return out, info.as_dict()
 
 
+_FLAG_DT = {torch.int64: 8, torch.int32: 4, torch.int8: 1, torch.uint8: 1, torch.bool: 1}
+
+
+def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_x, pixsize_y,
+                 epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None, out_strides=None,
+                 accumulate=False, sumwt=None):
+    """ms2dirty with invert_ng's visibility prologue fused in
+    (sdp_hip_ms2dirty_vis): ``vis`` [nrow, nchan, npol_vis] complex (any
+    strides, read in place; None = unit visibilities), ``flags`` the same
+    shape (integer / bool, or None), ``wgt`` [nrow, nchan] f32/f64 weights of
+    image pol ``pol``, ``coef`` the conversion-matrix row for that pol
+    (complex [npol_vis]) or None for no conversion, ``sumwt`` a one-element
+    f64 device view that receives += the masked weight sum."""
+    _check_uvw(uvw)
+    dev = uvw.device
+    freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
+    nrow, nchan = uvw.shape[0], freq.shape[0]
+    npv = 1
+    if vis is not None:
+        _on_gpu(vis, "vis")
+        if vis.dtype not in (torch.complex64, torch.complex128) or vis.dim() != 3 or \
+                tuple(vis.shape[:2]) != (nrow, nchan):
+            raise ValueError("vis must be complex [nrow, nchan, npol]")
+        npv = vis.shape[2]
+    if flags is not None:
+        _on_gpu(flags, "flags")
+        if flags.dtype not in _FLAG_DT or flags.dim() != 3 or tuple(flags.shape[:2]) != (nrow, nchan):
+            raise ValueError("flags must be an integer [nrow, nchan, npol] tensor")
+        npv = max(npv, flags.shape[2])
+    if wgt is not None:
+        _on_gpu(wgt, "wgt")
+        if wgt.dtype not in (torch.float32, torch.float64) or tuple(wgt.shape) != (nrow, nchan):
+            raise ValueError("wgt must be float32/float64 [nrow, nchan]")
+    if not 0 <= pol < npv:
+        raise ValueError("pol out of range")
+    cbuf = None
+    if coef is not None:
+        c = [complex(x) for x in coef]
+        if len(c) != npv:
+            raise ValueError("coef must have one entry per visibility pol")
+        cbuf = (ctypes.c_double * (2 * npv))(*[v for z in c for v in (z.real, z.imag)])
+    if out is None:
+        out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=dev)
+        out_strides = (npix_y, 1)
+    elif out_strides is None:
+        out_strides = out.stride()
+    _on_gpu(out, "out")
+    if out.dtype != torch.float64:
+        raise ValueError("dirty output must be float64")
+    if sumwt is not None and (sumwt.dtype != torch.float64 or not sumwt.is_cuda):
+        raise ValueError("sumwt must be a float64 device tensor")
+    bits = (_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+    info = _lib.WGridInfo()
+    _lib.call(
+        "sdp_hip_ms2dirty_vis",
+        _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
+        _ptr(vis), _DT_CODE[vis.dtype] if vis is not None else _lib.SDP_HIP_C64,
+        *(vis.stride() if vis is not None else (0, 0, 0)), npv,
+        ctypes.cast(cbuf, ctypes.c_void_p) if cbuf is not None else None,
+        _ptr(wgt), _DT_CODE[wgt.dtype] if wgt is not None else _lib.SDP_HIP_F32,
+        *(wgt.stride() if wgt is not None else (0, 0)),
+        _ptr(flags), _FLAG_DT[flags.dtype] if flags is not None else 0,
+        *(flags.stride() if flags is not None else (0, 0, 0)), int(pol),
+        int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
+        int(bool(do_wstacking)), bits,
+        _ptr(out), int(out_strides[0]), int(out_strides[1]), _ptr(sumwt),
+        _stream(dev), ctypes.byref(info))
+    return out, info.as_dict()
+
+
 def dirty2ms(uvw, freq, dirty, wgt, pixsize_x, pixsize_y, epsilon=1e-7,
              do_wstacking=True, flip_uw=False, out=None, dirty_strides=None,
              npix=None, accumulate=False, vis_dtype=torch.complex64):

@@ -230,3 +230,74 @@ def test_full_size_invert_matches_c_restatement():
                                  flip_uw=True)
     assert info["nplanes"] >= 8 and info["ngrid_x"] == 8192
     assert rel_rms(out.cpu().numpy(), ref) < 5e-6
+
+
+def _prologue_reference(vis, im, dopsf):
+    """numpy restatement of invert_ng's visibility prologue (reference
+    imaging/ng.py:191-204, :231-233): flagged vis -> image pol frame, flagged
+    imaging weights; returns (ms [nrow, nchan, npol], wgt, uvw)."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    nt, nb, nchan, npol = vis.vis.data.shape
+    ms = (vis.vis.data * (1 - vis.flags.data)).reshape(nt * nb, nchan, npol)
+    ms = dm.convert_pol_frame(ms, vis.visibility_acc.polarisation_frame,
+                              im.image_acc.polarisation_frame, polaxis=2)
+    wgt = (vis.imaging_weight.data * (1 - vis.flags.data)).reshape(nt * nb, nchan, npol)
+    if dopsf:
+        ms = np.zeros_like(ms)
+        ms[..., 0] = 1.0
+    return ms, wgt, vis.uvw.data.reshape(-1, 3)
+
+
+@pytest.mark.parametrize("pf,ipf", [("stokesI", "stokesI"), ("linear", "stokesIQUV"),
+                                    ("circular", "stokesIQUV"), ("linear", "linear")])
+@pytest.mark.parametrize("mfs", [True, False])
+@pytest.mark.parametrize("dopsf", [False, True])
+@pytest.mark.parametrize("device", [False, True])
+def test_invert_ng_fused_prologue(pf, ipf, mfs, dopsf, device):
+    """invert_ng reads the Visibility in place through sdp_hip_ms2dirty_vis:
+    flag masking of vis and weights, the pol-frame conversion, f64 weights
+    and sumwt, against the numpy prologue + exact sums (tolerance TOL; sumwt
+    rtol 1e-12).  Device-resident inputs use c64 vis, f32 weights, int32
+    flags; host inputs the datamodels' c128 / f64 / int64."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import invert_ng
+    rng = np.random.default_rng(21)
+    nt, nb, nchan = 5, 40, 3
+    npol = dm.PolarisationFrame(pf).npol
+    freq = np.linspace(1.0e9, 1.1e9, nchan)
+    umax = 1500.0
+    uvw = rng.uniform(-1, 1, (nt, nb, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw[..., 2] *= 0.5
+    shape = (nt, nb, nchan, npol)
+    v = rng.normal(size=shape) + 1j * rng.normal(size=shape)
+    w = rng.uniform(0.5, 2.0, shape)
+    fl = (rng.uniform(size=shape) < 0.15).astype(int)
+    vis = vis_from_arrays(uvw, freq, v, weight=w, flags=fl, pf=pf,
+                          phasecentre=dm.SkyCoord(0.0, -0.6))
+    vis["imaging_weight"] = rng.uniform(0.5, 2.0, shape)
+    npix, cell = 128, 0.4 / umax
+    fc, bw = (float(freq.mean()), 1e9) if mfs else (float(freq[0]), float(freq[1] - freq[0]))
+    im = dm.create_image(npix, cell, dm.SkyCoord(0.0, -0.6), polarisation_frame=dm.PolarisationFrame(ipf),
+                         frequency=fc, channel_bandwidth=bw, nchan=1 if mfs else nchan)
+    ms, wgt, fuvw = _prologue_reference(vis, im, dopsf)
+    if device:
+        for name, dt in (("vis", torch.complex64), ("imaging_weight", torch.float32),
+                         ("flags", torch.int32)):
+            vis[name] = torch.as_tensor(np.asarray(vis[name].data), device="cuda").to(dt)
+        vis["uvw"] = torch.as_tensor(uvw, device="cuda")
+    dirty, sumwt = invert_ng(vis, im, dopsf=dopsf, normalise=False)
+    img = dirty["pixels"].data
+    img = img.cpu().numpy() if isinstance(img, torch.Tensor) else img
+    nimch = 1 if mfs else nchan
+    exp_sw = np.zeros((nimch, npol))
+    for pol in range(npol):
+        for c in range(nimch):
+            chans = slice(0, nchan) if mfs else slice(c, c + 1)
+            exp_sw[c, pol] = wgt[:, chans, pol].sum()
+            if dopsf and pol > 0:
+                assert not np.any(img[c, pol])
+                continue
+            ref = orc.ms2dirty_exact(fuvw * FLIP_UW, freq[chans], ms[:, chans, pol],
+                                     wgt[:, chans, pol], npix, npix, cell, cell, True).T
+            assert rel_rms(img[c, pol], ref) < TOL, (pol, c)
+    np.testing.assert_allclose(sumwt, exp_sw, rtol=1e-6 if device else 1e-12)
