@@ -150,6 +150,30 @@ int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride,
                      size_t errbuf_len);
 
 /*
+ * sdp_hip_dirty2ms_vis -- sdp_hip_dirty2ms for ONE image pol of predict_ng
+ * with the image -> visibility pol-frame conversion (reference
+ * imaging/ng.py:131-136) fused into the write-back: every output pol k of
+ * vis [nrow, nchan, npol_vis] (element strides row, chan, pol; vis points at
+ * pol 0) receives coeff_k * (this pol's predicted visibility), coeff_k =
+ * column `pol` of the conversion matrix, host array of 2*npol_vis doubles
+ * (NULL: output pol 0 only).  Without SDP_HIP_ACCUMULATE all npol_vis pols
+ * are overwritten (zero where nothing is predicted); call the first image pol
+ * without and the others with SDP_HIP_ACCUMULATE.  No weights (predict_ng
+ * passes none, ng.py:99-129).
+ */
+int sdp_hip_dirty2ms_vis(const double *uvw, int64_t uvw_row_stride,
+                         const double *freq, int nchan, int64_t nrow,
+                         const double *dirty, int64_t dirty_stride_x,
+                         int64_t dirty_stride_y, int npix_x, int npix_y,
+                         double pixsize_x, double pixsize_y, double epsilon,
+                         int do_wstacking, unsigned flags, void *vis,
+                         int vis_dtype, int64_t vis_row_stride,
+                         int64_t vis_chan_stride, int64_t vis_pol_stride,
+                         int npol_vis, const double *pol_coeff, void *stream,
+                         sdp_hip_wgrid_info *info, char *errbuf,
+                         size_t errbuf_len);
+
+/*
  * sdp_hip_dft_point_v00 -- replaces ska_sdp_func.visibility.dft_point_v00
  * (reference src/ska_sdp_func_python/imaging/dft.py:173-178) and the cupy
  * dft_kernel (:185-262, :288-337).  Caller-allocated output, replaced (not

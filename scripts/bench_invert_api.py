@@ -19,7 +19,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from ska_sdp_func_python_amd import datamodels as dm, kernels, simulation  # noqa: E402
-from ska_sdp_func_python_amd.imaging import invert_ng  # noqa: E402
+from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng  # noqa: E402
 
 npol = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 nchan = int(sys.argv[2]) if len(sys.argv) > 2 else 64
@@ -70,7 +70,16 @@ wgt = torch.ones((nrow, nchan), dtype=torch.float32, device=dev)
 out = torch.zeros((4096, 4096), dtype=torch.float64, device=dev)
 t_kernel = timed(lambda: kernels.ms2dirty(uvw, freq, ms, wgt, 4096, 4096, cell, cell, 1e-12, True,
                                           flip_uw=True, out=out, out_strides=(1, 4096)))
+model["pixels"].data = torch.randn((1, npol, 4096, 4096), dtype=torch.float64, device=dev)
+t_pred = timed(lambda: predict_ng(bvis, model, epsilon=1e-12))
+img = model["pixels"].data[0, 0]
+vout = torch.empty((nrow, nchan), dtype=torch.complex64, device=dev)
+t_dk = timed(lambda: kernels.dirty2ms(uvw, freq, img, None, cell, cell, 1e-12, True, flip_uw=True,
+                                      out=vout, dirty_strides=(1, 4096), npix=(4096, 4096)))
 print(json.dumps({"npol": npol, "nchan": nchan, "nvis": nrow * nchan,
                   "invert_ng_ms": round(t_api * 1e3, 2),
                   "ms2dirty_per_pol_ms": round(t_kernel * 1e3, 2),
-                  "prologue_overhead_ms": round((t_api - npol * t_kernel) * 1e3, 2)}))
+                  "prologue_overhead_ms": round((t_api - npol * t_kernel) * 1e3, 2),
+                  "predict_ng_ms": round(t_pred * 1e3, 2),
+                  "dirty2ms_per_pol_ms": round(t_dk * 1e3, 2),
+                  "predict_overhead_ms": round((t_pred - npol * t_dk) * 1e3, 2)}))

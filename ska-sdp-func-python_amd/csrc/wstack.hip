@@ -1248,9 +1248,37 @@ __device__ __forceinline__ void store_vis(double2 *p, float2 v, int accumulate) 
     }
     *p = w;
 }
+__device__ __forceinline__ void store_vis_d(float2 *p, double xr, double xi, int accumulate) {
+    float2 w = make_float2((float)xr, (float)xi);
+    if (accumulate) {
+        const float2 o = *p;
+        w.x += o.x;
+        w.y += o.y;
+    }
+    *p = w;
+}
+__device__ __forceinline__ void store_vis_d(double2 *p, double xr, double xi, int accumulate) {
+    double2 w = make_double2(xr, xi);
+    if (accumulate) {
+        const double2 o = *p;
+        w.x += o.x;
+        w.y += o.y;
+    }
+    *p = w;
+}
+
+// Predict-side pol conversion (sdp_hip_dirty2ms_vis, reference
+// imaging/ng.py:131-136): the degridded image-pol visibility x goes to every
+// output pol v as coef_v * x.  Disabled (npv 1, coef 1) for sdp_hip_dirty2ms.
+struct OutConv {
+    int npv = 1;
+    int64_t vps = 0;
+    double cre[4] = {1.0, 0.0, 0.0, 0.0}, cim[4] = {0.0, 0.0, 0.0, 0.0};
+};
 
 template <class VT>
-__global__ void k_zero_vis(int64_t nrow, int nchan, VT *vis, int64_t vrs, int64_t vcs) {
+__global__ void k_zero_vis(int64_t nrow, int nchan, VT *vis, int64_t vrs, int64_t vcs,
+                           OutConv oc) {
     const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (v >= nrow * nchan) return;
     const int64_t row = v / nchan;
@@ -1258,7 +1286,7 @@ __global__ void k_zero_vis(int64_t nrow, int nchan, VT *vis, int64_t vrs, int64_
     VT z;
     z.x = 0;
     z.y = 0;
-    vis[row * vrs + chan * vcs] = z;
+    for (int k = 0; k < oc.npv; ++k) vis[row * vrs + chan * vcs + k * oc.vps] = z;
 }
 
 // record factor and scatter back to visibility order; the record count is
@@ -1266,7 +1294,7 @@ __global__ void k_zero_vis(int64_t nrow, int nchan, VT *vis, int64_t vrs, int64_
 template <class VT>
 __global__ void k_finalize(int64_t nrec, const unsigned *__restrict__ ndev, int nchan,
                            const VisRec *__restrict__ recs, const float2 *__restrict__ acc, VT *vis,
-                           int64_t vrs, int64_t vcs, int accumulate) {
+                           int64_t vrs, int64_t vcs, int accumulate, OutConv oc) {
     const int64_t n = ndev ? (int64_t)*ndev : nrec;
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
@@ -1275,7 +1303,17 @@ __global__ void k_finalize(int64_t nrec, const unsigned *__restrict__ ndev, int 
         const float2 v = make_float2(rc.cre * a.x - rc.cim * a.y, rc.cre * a.y + rc.cim * a.x);
         const int64_t row = rc.idx / (uint32_t)nchan;
         const int chan = (int)(rc.idx - row * nchan);
-        store_vis(vis + row * vrs + chan * vcs, v, accumulate);
+        VT *p = vis + row * vrs + chan * vcs;
+        if (oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0) {
+            store_vis(p, v, accumulate);
+            continue;
+        }
+        for (int k = 0; k < oc.npv; ++k) {
+            if (oc.cre[k] == 0.0 && oc.cim[k] == 0.0) continue;
+            const double xr = oc.cre[k] * v.x - oc.cim[k] * v.y;
+            const double xi = oc.cre[k] * v.y + oc.cim[k] * v.x;
+            store_vis_d(p + k * oc.vps, xr, xi, accumulate);
+        }
     }
 }
 
@@ -2080,7 +2118,7 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
 }
 
 static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t sy, void *vis,
-                     sdp_hip_wgrid_info *info, hipStream_t st) {
+                     sdp_hip_wgrid_info *info, hipStream_t st, const OutConv &oc = OutConv{}) {
     SDP_REQUIRE(in.vis_dtype == SDP_HIP_C64 || in.vis_dtype == SDP_HIP_C128,
                 "vis must be complex64 or complex128");
     StageTimer tm(st);
@@ -2095,10 +2133,10 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     if (!accumulate && nvis > 0) {
         if (in.vis_dtype == SDP_HIP_C128)
             k_zero_vis<double2><<<grid1d(nvis, 256), 256, 0, st>>>(
-                in.nrow, in.nchan, (double2 *)vis, in.vrs, in.vcs);
+                in.nrow, in.nchan, (double2 *)vis, in.vrs, in.vcs, oc);
         else
             k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, st>>>(
-                in.nrow, in.nchan, (float2 *)vis, in.vrs, in.vcs);
+                in.nrow, in.nchan, (float2 *)vis, in.vrs, in.vcs, oc);
     }
     float2 *acc = scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));
     SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(nvis, 1) * sizeof(float2), st));
@@ -2146,11 +2184,11 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         if (in.vis_dtype == SDP_HIP_C128)
             k_finalize<double2><<<nb, 256, 0, st>>>(pt.nrec, ndev, in.nchan, P.recs + pt.vbase,
                                                     acc + pt.vbase, (double2 *)vis, in.vrs,
-                                                    in.vcs, accumulate);
+                                                    in.vcs, accumulate, oc);
         else
             k_finalize<float2><<<nb, 256, 0, st>>>(pt.nrec, ndev, in.nchan, P.recs + pt.vbase,
                                                    acc + pt.vbase, (float2 *)vis, in.vrs, in.vcs,
-                                                   accumulate);
+                                                   accumulate, oc);
         SDP_HIP_CHECK(hipGetLastError());
     }
     tm.mark();
@@ -2282,6 +2320,36 @@ int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride, const double *fr
                                 epsilon,     do_wstacking,    flags};
         wstack::dirty2ms(in, dirty, dirty_stride_x, dirty_stride_y, vis, info,
                          as_stream(stream));
+    });
+}
+
+int sdp_hip_dirty2ms_vis(const double *uvw, int64_t uvw_row_stride, const double *freq, int nchan,
+                         int64_t nrow, const double *dirty, int64_t dirty_stride_x,
+                         int64_t dirty_stride_y, int npix_x, int npix_y, double pixsize_x,
+                         double pixsize_y, double epsilon, int do_wstacking, unsigned flags,
+                         void *vis, int vis_dtype, int64_t vis_row_stride, int64_t vis_chan_stride,
+                         int64_t vis_pol_stride, int npol_vis, const double *pol_coeff,
+                         void *stream, sdp_hip_wgrid_info *info, char *errbuf,
+                         size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(dirty != nullptr && freq != nullptr && vis != nullptr &&
+                        (uvw != nullptr || nrow == 0),
+                    "null pointer argument");
+        SDP_REQUIRE(npol_vis >= 1 && npol_vis <= 4, "npol_vis must be 1..4");
+        const wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                                nrow,        nullptr,         vis_dtype,      vis_row_stride,
+                                vis_chan_stride, nullptr,     0,              0,
+                                npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                                epsilon,     do_wstacking,    flags};
+        wstack::OutConv oc;
+        oc.npv = npol_vis;
+        oc.vps = vis_pol_stride;
+        for (int k = 0; k < npol_vis; ++k) {
+            oc.cre[k] = pol_coeff ? pol_coeff[2 * k] : (k == 0 ? 1.0 : 0.0);
+            oc.cim[k] = pol_coeff ? pol_coeff[2 * k + 1] : 0.0;
+        }
+        wstack::dirty2ms(in, dirty, dirty_stride_x, dirty_stride_y, vis, info, as_stream(stream),
+                         oc);
     });
 }
 

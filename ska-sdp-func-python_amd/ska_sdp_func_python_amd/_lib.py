@@ -89,6 +89,13 @@ SIGNATURES = {
         c_dbl, c_int, c_u32,
         c_vp, c_int, c_i64, c_i64,
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
+    "sdp_hip_dirty2ms_vis": [
+        c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
+        c_vp, c_i64, c_i64, c_int, c_int, c_dbl, c_dbl,
+        c_dbl, c_int, c_u32,
+        c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # vis, dtype, strides, npol_vis
+        c_vp,                                     # pol_coeff (host doubles) or NULL
+        c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_dft_point_v00": [
         c_int, c_vp, c_vp, c_int, c_int, c_i64, c_int, c_vp, c_vp, c_int, c_vp] + _ERR,
     "sdp_hip_dft_point_metres": [

@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from .. import _device, kernels
-from ..datamodels import Image, convert_pol_frame, pol_conversion_matrix
+from ..datamodels import Image, pol_conversion_matrix
 from .base import normalise_sumwt, shift_vis_to_image
 
 log = logging.getLogger("func-python-logger")
@@ -56,10 +56,9 @@ def predict_ng(bvis, model, **kwargs):
     verbosity = kwargs.get("verbosity", 0)
 
     dev = _device.device()
-    newbvis = bvis.copy(deep=True, zero=True)
     freq = np.asarray(bvis.frequency.data, dtype=float)
     nrows, nbaselines, vnchan, vnpol = bvis.vis.shape
-    uvw = _device.to_dev(newbvis.uvw.data, torch.float64, dev).reshape(nrows * nbaselines, 3)
+    uvw = _device.to_dev(bvis.uvw.data, torch.float64, dev).reshape(nrows * nbaselines, 3)
     uvw = torch.nan_to_num(uvw).contiguous()
     freq_t = _device.to_dev(freq, torch.float64, dev)
 
@@ -68,30 +67,47 @@ def predict_ng(bvis, model, **kwargs):
     assert m_npol == vnpol
     pixsize = _pixsize(model)
     vis_to_im = _vis_to_im(model, freq)
+    # image -> vis pol frame (ng.py:131-136) fused into the write-back: image
+    # pol p adds column p of the conversion matrix times its prediction to
+    # every vis pol; the result lands in the output's own dtype and layout
+    conv = pol_conversion_matrix(model.image_acc.polarisation_frame,
+                                 bvis.visibility_acc.polarisation_frame)
+    src = bvis["vis"].data
+    vdt = src.dtype if _device.is_device(src) and src.is_complex() else torch.complex128
+    vist = torch.empty((nrows * nbaselines, vnchan, vnpol), dtype=vdt, device=dev)
 
-    vist = torch.zeros((nrows * nbaselines, vnchan, vnpol), dtype=torch.complex128, device=dev)
+    def coef(p):
+        if conv is None:
+            c = np.zeros(vnpol, complex)
+            c[p] = 1.0
+            return c
+        return conv[:, p]
+
     info = None
-    if m_nchan == 1:
-        for vpol in range(vnpol):
-            img = pixels[0, vpol]
-            _, info = kernels.dirty2ms(uvw, freq_t, img, None, pixsize, pixsize, epsilon,
-                                       do_wstacking, flip_uw=True, out=vist[:, :, vpol],
-                                       dirty_strides=(1, nx), npix=(nx, ny))
-    else:
-        for vpol in range(vnpol):
+    for vpol in range(vnpol):
+        if m_nchan == 1:
+            _, info = kernels.dirty2ms_vis(uvw, freq_t, pixels[0, vpol], vist, coef(vpol), pixsize,
+                                           pixsize, epsilon, do_wstacking, flip_uw=True,
+                                           dirty_strides=(1, nx), npix=(nx, ny),
+                                           accumulate=vpol > 0)
+        else:
             for vchan in range(vnchan):
                 img = pixels[int(vis_to_im[vchan]), vpol]
-                _, info = kernels.dirty2ms(uvw, freq_t[vchan:vchan + 1], img, None, pixsize,
-                                           pixsize, epsilon, do_wstacking, flip_uw=True,
-                                           out=vist[:, vchan:vchan + 1, vpol],
-                                           dirty_strides=(1, nx), npix=(nx, ny))
+                _, info = kernels.dirty2ms_vis(uvw, freq_t[vchan:vchan + 1], img,
+                                               vist[:, vchan:vchan + 1, :], coef(vpol), pixsize,
+                                               pixsize, epsilon, do_wstacking, flip_uw=True,
+                                               dirty_strides=(1, nx), npix=(nx, ny),
+                                               accumulate=vpol > 0)
     if verbosity and info is not None:
         log.info("predict_ng: %s", info)
 
-    vis = convert_pol_frame(vist, model.image_acc.polarisation_frame,
-                            bvis.visibility_acc.polarisation_frame, polaxis=2)
-    vis = vis.reshape(nrows, nbaselines, vnchan, vnpol)
-    newbvis["vis"].data = _device.like_input(vis, bvis["vis"].data)
+    vis = vist.reshape(nrows, nbaselines, vnchan, vnpol)
+    # the reference's bvis.copy(deep=True, zero=True) (ng.py:77), with the
+    # predicted visibilities in place of the zeroed copy
+    out = _device.like_input(vis, src)
+    if isinstance(out, np.ndarray) and out.dtype != np.asarray(src).dtype:
+        out = out.astype(np.asarray(src).dtype)
+    newbvis = bvis._copy_with(deep=True, replace={"vis": out})
     return shift_vis_to_image(newbvis, model, tangent=True, inverse=True)
 
 

@@ -155,6 +155,44 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
     return out, info.as_dict()
 
 
+def dirty2ms_vis(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7,
+                 do_wstacking=True, flip_uw=False, dirty_strides=None, npix=None,
+                 accumulate=False):
+    """One image pol of predict_ng with the pol conversion fused into the
+    write-back (sdp_hip_dirty2ms_vis): ``out`` [nrow, nchan, npol_vis] complex
+    (any strides) gets coef[k] * predicted vis in pol k (coef None: pol 0)."""
+    _check_uvw(uvw)
+    dev = uvw.device
+    freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
+    nrow, nchan = uvw.shape[0], freq.shape[0]
+    _on_gpu(dirty, "dirty")
+    if dirty.dtype != torch.float64:
+        raise ValueError("dirty must be float64")
+    npix_x, npix_y = (dirty.shape[-2], dirty.shape[-1]) if npix is None else npix
+    if dirty_strides is None:
+        dirty_strides = dirty.stride()[-2:]
+    _on_gpu(out, "out")
+    if out.dtype not in (torch.complex64, torch.complex128) or out.dim() != 3 or \
+            tuple(out.shape[:2]) != (nrow, nchan):
+        raise ValueError("out must be complex [nrow, nchan, npol]")
+    npv = out.shape[2]
+    cbuf = None
+    if coef is not None:
+        c = [complex(x) for x in coef]
+        if len(c) != npv:
+            raise ValueError("coef must have one entry per visibility pol")
+        cbuf = (ctypes.c_double * (2 * npv))(*[v for z in c for v in (z.real, z.imag)])
+    bits = (_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+    info = _lib.WGridInfo()
+    _lib.call("sdp_hip_dirty2ms_vis", _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
+              _ptr(dirty), int(dirty_strides[0]), int(dirty_strides[1]), int(npix_x), int(npix_y),
+              float(pixsize_x), float(pixsize_y), float(epsilon), int(bool(do_wstacking)), bits,
+              _ptr(out), _DT_CODE[out.dtype], *out.stride(), npv,
+              ctypes.cast(cbuf, ctypes.c_void_p) if cbuf is not None else None,
+              _stream(dev), ctypes.byref(info))
+    return out, info.as_dict()
+
+
 def dirty2ms(uvw, freq, dirty, wgt, pixsize_x, pixsize_y, epsilon=1e-7,
              do_wstacking=True, flip_uw=False, out=None, dirty_strides=None,
              npix=None, accumulate=False, vis_dtype=torch.complex64):

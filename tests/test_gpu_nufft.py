@@ -301,3 +301,55 @@ def test_invert_ng_fused_prologue(pf, ipf, mfs, dopsf, device):
                                      wgt[:, chans, pol], npix, npix, cell, cell, True).T
             assert rel_rms(img[c, pol], ref) < TOL, (pol, c)
     np.testing.assert_allclose(sumwt, exp_sw, rtol=1e-6 if device else 1e-12)
+
+
+@pytest.mark.parametrize("ipf,pf", [("stokesI", "stokesI"), ("stokesIQUV", "linear"),
+                                    ("stokesIQUV", "circular"), ("linear", "linear")])
+@pytest.mark.parametrize("mfs", [True, False])
+@pytest.mark.parametrize("device", [False, True])
+def test_predict_ng_fused_pol_conversion(ipf, pf, mfs, device):
+    """predict_ng writes each image pol's prediction times its column of the
+    conversion matrix (ng.py:131-136) straight into the output Visibility
+    (sdp_hip_dirty2ms_vis), in the input's dtype; against exact sums + numpy
+    conversion, TOL relative RMS per vis pol."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import predict_ng
+    rng = np.random.default_rng(23)
+    nt, nb, nchan = 4, 30, 3
+    npol = dm.PolarisationFrame(pf).npol
+    freq = np.linspace(1.0e9, 1.1e9, nchan)
+    umax = 1500.0
+    uvw = rng.uniform(-1, 1, (nt, nb, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw[..., 2] *= 0.5
+    shape = (nt, nb, nchan, npol)
+    vis = vis_from_arrays(uvw, freq, np.zeros(shape, complex), pf=pf,
+                          phasecentre=dm.SkyCoord(0.0, -0.6))
+    npix, cell = 96, 0.4 / umax
+    fc, bw = (float(freq.mean()), 1e9) if mfs else (float(freq[0]), float(freq[1] - freq[0]))
+    im = dm.create_image(npix, cell, dm.SkyCoord(0.0, -0.6), polarisation_frame=dm.PolarisationFrame(ipf),
+                         frequency=fc, channel_bandwidth=bw, nchan=1 if mfs else nchan)
+    im["pixels"].data[...] = rng.normal(size=im["pixels"].data.shape)
+    fuvw = uvw.reshape(-1, 3) * FLIP_UW
+    nimch = 1 if mfs else nchan
+    pred = np.zeros((nt * nb, nchan, npol), complex)
+    for p in range(npol):
+        for c in range(nchan):
+            ic = 0 if mfs else c
+            pred[:, c, p] = orc.dirty2ms_exact(fuvw, freq[c:c + 1], im["pixels"].data[ic, p].T, None,
+                                               cell, cell, True)[:, 0]
+    expect = dm.convert_pol_frame(pred, im.image_acc.polarisation_frame,
+                                  vis.visibility_acc.polarisation_frame, polaxis=2)
+    if device:
+        vis["vis"] = torch.zeros(shape, dtype=torch.complex64, device="cuda")
+        vis["uvw"] = torch.as_tensor(uvw, device="cuda")
+    out = predict_ng(vis, im)
+    got = out.vis.data
+    if device:
+        assert got.dtype == torch.complex64
+        got = got.cpu().numpy()
+    else:
+        assert got.dtype == np.complex128
+    got = got.reshape(nt * nb, nchan, npol)
+    for p in range(npol):
+        assert rel_rms(got[..., p], expect[..., p]) < TOL, p
+    assert nimch in (1, nchan)
