@@ -113,6 +113,11 @@ int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride,
  *           strides, or NULL; the weight is masked with flag pol `pol`
  * sumwt     device double, += sum over rows and channels of the masked
  *           weights (NULL: not computed)
+ * shift_lmn host array (l, m, n-1) of the image phase centre relative to the
+ *           visibility phase centre, or NULL: shift_vis_to_image's tangent
+ *           phase rotation (reference imaging/base.py:48-92,
+ *           visibility/base.py:27-90) applied on the fly, vis *
+ *           exp(+2 pi i uvw_lambda . lmn) (uvw as given, before FLIP_UW)
  * Other arguments as sdp_hip_ms2dirty.
  */
 int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride,
@@ -127,7 +132,8 @@ int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride,
                          int pol, int npix_x, int npix_y, double pixsize_x,
                          double pixsize_y, double epsilon, int do_wstacking,
                          unsigned flags, double *dirty, int64_t dirty_stride_x,
-                         int64_t dirty_stride_y, double *sumwt, void *stream,
+                         int64_t dirty_stride_y, double *sumwt,
+                         const double *shift_lmn, void *stream,
                          sdp_hip_wgrid_info *info, char *errbuf,
                          size_t errbuf_len);
 
@@ -159,7 +165,8 @@ int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride,
  * (NULL: output pol 0 only).  Without SDP_HIP_ACCUMULATE all npol_vis pols
  * are overwritten (zero where nothing is predicted); call the first image pol
  * without and the others with SDP_HIP_ACCUMULATE.  No weights (predict_ng
- * passes none, ng.py:99-129).
+ * passes none, ng.py:99-129).  shift_lmn (host (l, m, n-1) or NULL) applies
+ * shift_vis_to_image(inverse=True): vis * exp(-2 pi i uvw_lambda . lmn).
  */
 int sdp_hip_dirty2ms_vis(const double *uvw, int64_t uvw_row_stride,
                          const double *freq, int nchan, int64_t nrow,
@@ -169,7 +176,8 @@ int sdp_hip_dirty2ms_vis(const double *uvw, int64_t uvw_row_stride,
                          int do_wstacking, unsigned flags, void *vis,
                          int vis_dtype, int64_t vis_row_stride,
                          int64_t vis_chan_stride, int64_t vis_pol_stride,
-                         int npol_vis, const double *pol_coeff, void *stream,
+                         int npol_vis, const double *pol_coeff,
+                         const double *shift_lmn, void *stream,
                          sdp_hip_wgrid_info *info, char *errbuf,
                          size_t errbuf_len);
 

@@ -285,6 +285,12 @@ struct VisExtra {
     int64_t frs = 0, fcs = 0, fps = 0;
     int fpol = 0;              // pol whose flag masks the weight (and the vis when !conv)
     double *sumwt = nullptr;   // += sum of the effective weights (device, may be null)
+    // shift_vis_to_image with tangent=True (reference imaging/base.py:48-92,
+    // visibility/base.py:27-45, :60-90): phase d = uvw_lambda . (l, m, n-1)
+    // in turns, folded into the record factor as exp(+2 pi i d) for invert
+    // (vis * conj(phasor)) and exp(-2 pi i d) for predict (vis * phasor)
+    bool shift = false;
+    double sl = 0.0, sm = 0.0, sn = 0.0;
 };
 
 constexpr int kSumSlots = 1024;
@@ -414,8 +420,12 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
         cr = xv.x * wt;
         ci = xv.y * wt;
     }
-    if (g.do_w) {
-        double ph = c.w * g.s0;
+    if (g.do_w || x.shift) {
+        double ph = g.do_w ? c.w * g.s0 : 0.0;
+        if (x.shift) {
+            const double *u = uvw + row * uvw_rs;
+            ph += (u[0] * x.sl + u[1] * x.sm + u[2] * x.sn) * (freq[chan] / kCLight);
+        }
         ph -= rint(ph);
         float sn, cs;
         sincospif((float)(2.0 * ph), &sn, &cs);
@@ -2260,8 +2270,9 @@ int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride, const double
                          int64_t flag_pol_stride, int pol, int npix_x, int npix_y,
                          double pixsize_x, double pixsize_y, double epsilon, int do_wstacking,
                          unsigned flags, double *dirty, int64_t dirty_stride_x,
-                         int64_t dirty_stride_y, double *sumwt, void *stream,
-                         sdp_hip_wgrid_info *info, char *errbuf, size_t errbuf_len) {
+                         int64_t dirty_stride_y, double *sumwt, const double *shift_lmn,
+                         void *stream, sdp_hip_wgrid_info *info, char *errbuf,
+                         size_t errbuf_len) {
     return guarded(errbuf, errbuf_len, [&] {
         SDP_REQUIRE(dirty != nullptr && freq != nullptr && (uvw != nullptr || nrow == 0),
                     "null pointer argument");
@@ -2287,6 +2298,12 @@ int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride, const double
         x.fps = flag_pol_stride;
         x.fpol = pol;
         x.sumwt = sumwt;
+        if (shift_lmn) {
+            x.shift = true;
+            x.sl = shift_lmn[0];
+            x.sm = shift_lmn[1];
+            x.sn = shift_lmn[2];
+        }
         if (pol_coeff) {
             x.conv = true;
             for (int k = 0; k < npol_vis; ++k) {
@@ -2329,18 +2346,24 @@ int sdp_hip_dirty2ms_vis(const double *uvw, int64_t uvw_row_stride, const double
                          double pixsize_y, double epsilon, int do_wstacking, unsigned flags,
                          void *vis, int vis_dtype, int64_t vis_row_stride, int64_t vis_chan_stride,
                          int64_t vis_pol_stride, int npol_vis, const double *pol_coeff,
-                         void *stream, sdp_hip_wgrid_info *info, char *errbuf,
-                         size_t errbuf_len) {
+                         const double *shift_lmn, void *stream, sdp_hip_wgrid_info *info,
+                         char *errbuf, size_t errbuf_len) {
     return guarded(errbuf, errbuf_len, [&] {
         SDP_REQUIRE(dirty != nullptr && freq != nullptr && vis != nullptr &&
                         (uvw != nullptr || nrow == 0),
                     "null pointer argument");
         SDP_REQUIRE(npol_vis >= 1 && npol_vis <= 4, "npol_vis must be 1..4");
-        const wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
-                                nrow,        nullptr,         vis_dtype,      vis_row_stride,
-                                vis_chan_stride, nullptr,     0,              0,
-                                npix_x,      npix_y,          pixsize_x,      pixsize_y,
-                                epsilon,     do_wstacking,    flags};
+        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                          nrow,        nullptr,         vis_dtype,      vis_row_stride,
+                          vis_chan_stride, nullptr,     0,              0,
+                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                          epsilon,     do_wstacking,    flags};
+        if (shift_lmn) {
+            in.x.shift = true;
+            in.x.sl = shift_lmn[0];
+            in.x.sm = shift_lmn[1];
+            in.x.sn = shift_lmn[2];
+        }
         wstack::OutConv oc;
         oc.npv = npol_vis;
         oc.vps = vis_pol_stride;

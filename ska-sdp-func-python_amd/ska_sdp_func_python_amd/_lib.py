@@ -81,6 +81,7 @@ SIGNATURES = {
         c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # flags, bytes, strides, pol
         c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,
         c_vp, c_i64, c_i64, c_vp,                 # dirty, strides, sumwt
+        c_vp,                                     # shift_lmn (host doubles) or NULL
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_dirty2ms": [
         c_vp, c_i64, c_vp, c_int, c_i64,
@@ -95,6 +96,7 @@ SIGNATURES = {
         c_dbl, c_int, c_u32,
         c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # vis, dtype, strides, npol_vis
         c_vp,                                     # pol_coeff (host doubles) or NULL
+        c_vp,                                     # shift_lmn (host doubles) or NULL
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_dft_point_v00": [
         c_int, c_vp, c_vp, c_int, c_int, c_i64, c_int, c_vp, c_vp, c_int, c_vp] + _ERR,

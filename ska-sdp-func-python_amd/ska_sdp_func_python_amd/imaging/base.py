@@ -16,6 +16,7 @@ import torch
 
 from .. import _device
 from ..datamodels import (PolarisationFrame, create_griddata_from_image, pixel_to_skycoord)
+from ..util.coordinate_support import skycoord_to_lmn
 from ..visibility.base import phaserotate_visibility
 
 log = logging.getLogger("func-python-logger")
@@ -35,6 +36,23 @@ def shift_vis_to_image(vis, im, tangent=True, inverse=False):
         vis = phaserotate_visibility(vis, image_phasecentre, tangent=tangent, inverse=inverse)
         vis.attrs["phasecentre"] = im.image_acc.phasecentre
     return vis
+
+
+def shift_lmn(vis, im):
+    """(l, m, n-1) by which ``shift_vis_to_image(vis, im, tangent=True)``
+    would rotate the visibilities, or None when it would leave them alone
+    (same two tests: phase-centre separation > 1e-15 rad, reference
+    imaging/base.py:71-75, and |n-1| >= 1e-15, visibility/base.py:78-82).
+    The fused NUFFT entry points apply that rotation on the fly."""
+    ny = im["pixels"].data.shape[2]
+    nx = im["pixels"].data.shape[3]
+    image_phasecentre = pixel_to_skycoord(nx // 2 + 1, ny // 2 + 1, im.image_acc.wcs, origin=1)
+    if vis.phasecentre.separation(image_phasecentre).rad <= 1e-15:
+        return None
+    l, m, n = skycoord_to_lmn(image_phasecentre, vis.phasecentre)
+    if abs(n) < 1e-15:
+        return None
+    return l, m, n
 
 
 def normalise_sumwt(im, sumwt, min_weight=0.1, flat_sky=False):

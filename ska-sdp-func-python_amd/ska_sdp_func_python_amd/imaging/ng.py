@@ -6,15 +6,16 @@ Mirrors reference ``src/ska_sdp_func_python/imaging/ng.py``:
 * ``predict_ng`` (:38-143): copy with zeroed vis, u and w negated (:80-85),
   MFS when the model has one channel (:95), per (pol, chan) otherwise
   (:113-129), image -> vis polarisation conversion (:131-136), then
-  ``shift_vis_to_image(inverse=True)`` (:143).
+  ``shift_vis_to_image(inverse=True)`` (:143); the conversion and the
+  phase shift run inside the degridder's write-back (sdp_hip_dirty2ms_vis).
 * ``invert_ng`` (:146-294): shift to the image phase centre (:183), flagged
   vis/weights (:191-204), u and w negated (:210-213), MFS when the image has
   one channel and the vis several (:228), PSF puts 1 in pol 0 only
   (:231-233), pols whose vis are all zero are not gridded but their weights
   still enter ``sumwt`` (:238, :258, :267, :289), then ``normalise_sumwt``.
-  The flag masking, pol conversion, weight conversion and weight sums run
-  inside the HIP prologue of sdp_hip_ms2dirty_vis on the Visibility's own
-  arrays.  Gridding a pol whose visibilities are all
+  The phase shift, flag masking, pol conversion, weight conversion and
+  weight sums run inside the HIP prologue of sdp_hip_ms2dirty_vis on the
+  Visibility's own arrays.  Gridding a pol whose visibilities are all
   zero yields exactly the zero image the reference keeps, so that check
   (ng.py:238) is not a separate pass here.
 
@@ -31,7 +32,7 @@ import torch
 
 from .. import _device, kernels
 from ..datamodels import Image, pol_conversion_matrix
-from .base import normalise_sumwt, shift_vis_to_image
+from .base import normalise_sumwt, shift_lmn
 
 log = logging.getLogger("func-python-logger")
 
@@ -73,6 +74,7 @@ def predict_ng(bvis, model, **kwargs):
     conv = pol_conversion_matrix(model.image_acc.polarisation_frame,
                                  bvis.visibility_acc.polarisation_frame)
     src = bvis["vis"].data
+    lmn = shift_lmn(bvis, model)  # shift_vis_to_image(inverse=True) (ng.py:143), in-kernel
     vdt = src.dtype if _device.is_device(src) and src.is_complex() else torch.complex128
     vist = torch.empty((nrows * nbaselines, vnchan, vnpol), dtype=vdt, device=dev)
 
@@ -89,7 +91,7 @@ def predict_ng(bvis, model, **kwargs):
             _, info = kernels.dirty2ms_vis(uvw, freq_t, pixels[0, vpol], vist, coef(vpol), pixsize,
                                            pixsize, epsilon, do_wstacking, flip_uw=True,
                                            dirty_strides=(1, nx), npix=(nx, ny),
-                                           accumulate=vpol > 0)
+                                           accumulate=vpol > 0, shift_lmn=lmn)
         else:
             for vchan in range(vnchan):
                 img = pixels[int(vis_to_im[vchan]), vpol]
@@ -97,7 +99,7 @@ def predict_ng(bvis, model, **kwargs):
                                                vist[:, vchan:vchan + 1, :], coef(vpol), pixsize,
                                                pixsize, epsilon, do_wstacking, flip_uw=True,
                                                dirty_strides=(1, nx), npix=(nx, ny),
-                                               accumulate=vpol > 0)
+                                               accumulate=vpol > 0, shift_lmn=lmn)
     if verbosity and info is not None:
         log.info("predict_ng: %s", info)
 
@@ -108,7 +110,11 @@ def predict_ng(bvis, model, **kwargs):
     if isinstance(out, np.ndarray) and out.dtype != np.asarray(src).dtype:
         out = out.astype(np.asarray(src).dtype)
     newbvis = bvis._copy_with(deep=True, replace={"vis": out})
-    return shift_vis_to_image(newbvis, model, tangent=True, inverse=True)
+    if lmn is not None:
+        # the reference's shift_vis_to_image relabels the phase centre
+        # (imaging/base.py:90)
+        newbvis.attrs["phasecentre"] = model.image_acc.phasecentre
+    return newbvis
 
 
 def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
@@ -126,7 +132,9 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     # the reference's deep copy + zero fill (ng.py:173, :218) without
     # copying the model's pixels
     im = model.copy(deep=True, data=image)
-    sbvis = shift_vis_to_image(bvis, im, tangent=True, inverse=False)
+    # shift_vis_to_image (ng.py:183) is applied inside the kernel's prologue
+    lmn = None if dopsf else shift_lmn(bvis, im)
+    sbvis = bvis
     freq = np.asarray(sbvis.frequency.data, dtype=float)
     nrows, nbaselines, vnchan, vnpol = sbvis.vis.shape
     nrow = nrows * nbaselines
@@ -173,7 +181,7 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
             uvw, freq_t[chans], None if dopsf else ms[:, chans, :], pol, wgt[:, chans, pol],
             flags[:, chans, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
             do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
-            accumulate=True, sumwt=sw)
+            accumulate=True, sumwt=sw, shift_lmn=lmn)
         if verbosity:
             log.info("invert_ng: %s", info)
 

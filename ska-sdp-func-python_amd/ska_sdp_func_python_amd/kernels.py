@@ -85,12 +85,19 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
     return out, info.as_dict()
 
 
+def _host3(v):
+    """(l, m, n-1) as a host double[3] for the C ABI, or NULL."""
+    if v is None:
+        return None
+    return ctypes.cast((ctypes.c_double * 3)(*[float(x) for x in v]), ctypes.c_void_p)
+
+
 _FLAG_DT = {torch.int64: 8, torch.int32: 4, torch.int8: 1, torch.uint8: 1, torch.bool: 1}
 
 
 def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_x, pixsize_y,
                  epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None, out_strides=None,
-                 accumulate=False, sumwt=None):
+                 accumulate=False, sumwt=None, shift_lmn=None):
     """ms2dirty with invert_ng's visibility prologue fused in
     (sdp_hip_ms2dirty_vis): ``vis`` [nrow, nchan, npol_vis] complex (any
     strides, read in place; None = unit visibilities), ``flags`` the same
@@ -150,14 +157,14 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
         *(flags.stride() if flags is not None else (0, 0, 0)), int(pol),
         int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
         int(bool(do_wstacking)), bits,
-        _ptr(out), int(out_strides[0]), int(out_strides[1]), _ptr(sumwt),
+        _ptr(out), int(out_strides[0]), int(out_strides[1]), _ptr(sumwt), _host3(shift_lmn),
         _stream(dev), ctypes.byref(info))
     return out, info.as_dict()
 
 
 def dirty2ms_vis(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7,
                  do_wstacking=True, flip_uw=False, dirty_strides=None, npix=None,
-                 accumulate=False):
+                 accumulate=False, shift_lmn=None):
     """One image pol of predict_ng with the pol conversion fused into the
     write-back (sdp_hip_dirty2ms_vis): ``out`` [nrow, nchan, npol_vis] complex
     (any strides) gets coef[k] * predicted vis in pol k (coef None: pol 0)."""
@@ -189,7 +196,7 @@ def dirty2ms_vis(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7
               float(pixsize_x), float(pixsize_y), float(epsilon), int(bool(do_wstacking)), bits,
               _ptr(out), _DT_CODE[out.dtype], *out.stride(), npv,
               ctypes.cast(cbuf, ctypes.c_void_p) if cbuf is not None else None,
-              _stream(dev), ctypes.byref(info))
+              _host3(shift_lmn), _stream(dev), ctypes.byref(info))
     return out, info.as_dict()
 
 
