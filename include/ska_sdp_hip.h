@@ -271,6 +271,63 @@ int sdp_hip_solve_gains(int nsolve, int nants, int nbl, const int32_t *row_start
                         char *errbuf, size_t errbuf_len);
 
 /*
+ * Calibration neighbours of StefCal.  Visibility
+ * arrays are the Visibility's [ntimes, nbl, nchan, npol] in C order:
+ * vis / model c64 or c128 (vis_dtype), weight f64, flags integers of
+ * flag_bytes (1, 4, 8) or NULL; model_flags (same type) masks the model
+ * where the model Visibility carries flags of its own (NULL: the vis flags).
+ *
+ * sdp_hip_point_sums: divide_visibility (reference
+ * src/ska_sdp_func_python/visibility/operations.py:145-189; model may be
+ * NULL = no division) fused with solve_gaintable's per-gain-row sums
+ * (calibration/solvers.py:82-107):
+ *   x_b[r, j, fg, p]  = sum_{t in row r} sum_{f} x * xwt * (1 - flag)
+ *   xwt_b[r, j, fg, p] = sum ... xwt * (1 - flag)
+ * over all channels f when nchan_g == 1, else f = fg.  Row r's vis time
+ * indices are time_idx[row_ptr[r] .. row_ptr[r+1]) (device int32 CSR).
+ * Output baseline j < nbl_out reads source baseline bl_perm[j] (NULL =
+ * identity, nbl_out = nbl) and is conjugated where bl_conj[j] (NULL = never):
+ * StefCal's canonical order.  xb c128 / xwt f64 [nrow_g, nbl_out, nchan_g,
+ * npol], overwritten.
+ */
+int sdp_hip_point_sums(int64_t ntimes, int nbl, int nchan, int npol,
+                       const void *vis, const void *model, int vis_dtype,
+                       const double *weight, const void *flags,
+                       const void *model_flags, int flag_bytes,
+                       int nrow_g, const int32_t *row_ptr,
+                       const int32_t *time_idx, int nchan_g, int nbl_out,
+                       const int32_t *bl_perm, const uint8_t *bl_conj, void *xb,
+                       double *xwt, void *stream, char *errbuf,
+                       size_t errbuf_len);
+/* divide_visibility alone over n samples: x_out = fv / fm where
+ * xwt_out = |fm|^2 fw > 0, else 0 (f = flagged); x_out has vis_dtype. */
+int sdp_hip_divide_vis(int64_t n, const void *vis, const void *model,
+                       int vis_dtype, const double *weight, const void *flags,
+                       const void *model_flags, int flag_bytes, void *x_out,
+                       double *xwt_out, void *stream, char *errbuf,
+                       size_t errbuf_len);
+/*
+ * sdp_hip_apply_gains: apply_gaintable (calibration/operations.py:23-256) in
+ * place on vis / weight.  time_row[ntimes] (device int32) is the gain row
+ * applied to each vis time, or -1; ant1/ant2 [nbl] int32 the baseline's
+ * antennas; gain c128 [nrow_g, nants, nchan_g, nrec, nrec].  Gain channel c
+ * acts on vis channel c only (channels >= nchan_g keep their values, as in
+ * the reference).  npol 1: V * sum_lm g1 conj(g2) (1/g where |g| > 0 for
+ * inverse), zero vis + weight where that is 0; npol 2 / 4: G1 V conj(G2)
+ * (elementwise conj) with V diagonal / 2x2, inverse = the 2x2 inverses; a
+ * baseline with a singular gain zeroes pol 0 (npol 2) or all pols (npol 4)
+ * and their weights.  use_flags: a gain row whose window holds any set flag
+ * works on the flagged vis / weights of that window.
+ */
+int sdp_hip_apply_gains(int64_t ntimes, int nbl, int nchan, int npol,
+                        void *vis, int vis_dtype, double *weight,
+                        const void *flags, int flag_bytes, int use_flags,
+                        const int32_t *ant1, const int32_t *ant2,
+                        const int32_t *time_row, const void *gain, int nrow_g,
+                        int nants, int nchan_g, int nrec, int inverse,
+                        void *stream, char *errbuf, size_t errbuf_len);
+
+/*
  * Imaging weights, replacing the Python row loops of
  * grid_visibility_weight_to_griddata (reference
  * src/ska_sdp_func_python/grid_data/gridding.py:258-334) and

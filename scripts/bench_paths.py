@@ -24,6 +24,13 @@ One JSON line per path (SURVEY.md §8(d) work formulas):
            reweight pass the same + 8 (imaging weight out).
            CPU: oracle/weighting_oracle.py (vectorised numpy restatement) on
            8 of the 64 channels, scaled linearly.
+* calops   C5-shaped chunk: 512 stations (130,816 baselines), 16 times x 64
+           channels, stokesI, c128 vis + model, f64 weight, int64 flags.
+           point_sums (divide_visibility + solve_gaintable's per-row sums,
+           B jones: one gain row per time) and apply_gaintable (forward).
+           HBM bound: point_sums reads 16+16+8+8 B per sample; apply reads
+           16+8 and writes 16+8 B per sample.
+           CPU: oracle/calops_oracle.py (vectorised numpy) on 1 time, scaled.
 """
 
 import json
@@ -45,7 +52,7 @@ HBM_PEAK_GBS = 8000.0
 FP32_PEAK_TFLOPS = 157.3
 dev = torch.device("cuda:0")
 which = (sys.argv[1].split(",") if len(sys.argv) > 1
-         else ["dft", "stefcal", "predict", "cfgrid", "weighting"])
+         else ["dft", "stefcal", "predict", "cfgrid", "weighting", "calops"])
 CORES = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0)),
             len(os.sched_getaffinity(0)))
 
@@ -280,3 +287,51 @@ if "weighting" in which:
                            "kind": "port",
                            "sample": f"weighting_oracle grid_weights + reweight (numpy) on {cs} of "
                                      f"{nchan} channels, {tc * cs / nchan:.1f} s, scaled x{nchan // cs}"}})
+
+if "calops" in which:
+    import calops_oracle as co
+    nants, ntimes, nchan = 512, 16, 64
+    a1, a2 = np.triu_indices(nants, 1)
+    nbl = len(a1)
+    shape = (ntimes, nbl, nchan, 1)
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    v = torch.randn(shape, dtype=torch.complex128, device=dev, generator=g)
+    m = torch.randn(shape, dtype=torch.complex128, device=dev, generator=g)
+    w = torch.rand(shape, dtype=torch.float64, device=dev, generator=g) + 0.5
+    f = (torch.rand(shape, device=dev, generator=g) < 0.01).to(torch.int64)
+    ptr = torch.arange(ntimes + 1, dtype=torch.int32, device=dev)
+    tidx = torch.arange(ntimes, dtype=torch.int32, device=dev)
+    perm, conj, _, _ = kernels.canonical_baselines(a1, a2, nants)
+    perm_d = torch.as_tensor(np.asarray(perm, np.int32), device=dev)
+    conj_d = torch.as_tensor(np.asarray(conj, np.uint8), device=dev)
+    t_ps, _ = gpu_time(lambda: kernels.point_sums(v, m, w, f, ptr, tidx, nchan, perm=perm_d,
+                                                  conj=conj_d))
+    gain = (torch.randn((ntimes, nants, nchan, 1, 1), dtype=torch.complex128, device=dev,
+                        generator=g) + 2.0)
+    a1d = torch.as_tensor(a1.astype(np.int32), device=dev)
+    a2d = torch.as_tensor(a2.astype(np.int32), device=dev)
+    trow = torch.arange(ntimes, dtype=torch.int32, device=dev)
+    vv, ww = v.clone(), w.clone()
+    t_ap, _ = gpu_time(lambda: kernels.apply_gains(vv, ww, None, False, a1d, a2d, trow, gain, False))
+    nsamp = ntimes * nbl * nchan
+    b_ps, b_ap = nsamp * 48, nsamp * 48
+    # CPU: the numpy restatements on one time slot
+    vh, mh, wh, fh = (x[:1].cpu().numpy() for x in (v, m, w, f))
+    t0 = time.perf_counter()
+    co.point_sums(vh, wh, fh, np.zeros(1), np.zeros(1), np.ones(1), nchan, model=mh)
+    tc_ps = (time.perf_counter() - t0) * ntimes
+    gh = gain[:1].cpu().numpy()
+    t0 = time.perf_counter()
+    co.apply_gaintable(vh, wh, fh, np.zeros(1), np.stack([a1, a2], 1), gh, np.zeros(1), np.ones(1))
+    tc_ap = (time.perf_counter() - t0) * ntimes
+    emit({"path": "calibration neighbours: point_sums (divide_visibility + x_b sums) and "
+                  "apply_gaintable, 512 stations x 16 times x 64 chans", "nsamples": nsamp,
+          "stages_ms": {"point_sums": round(t_ps * 1e3, 3), "apply_gaintable": round(t_ap * 1e3, 3)},
+          "value": round(nsamp / t_ps / 1e9, 2), "unit": "Gsamples/s (point_sums)",
+          "roofline": {"bound": "hbm", "point_sums_GBs": round(b_ps / t_ps / 1e9, 1),
+                       "apply_GBs": round(b_ap / t_ap / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(b_ps / t_ps / 1e9 / HBM_PEAK_GBS, 4)},
+          "cpu_baseline": {"value": round(nsamp / tc_ps / 1e9, 4), "unit": "Gsamples/s (point_sums)",
+                           "apply_s": round(tc_ap, 2), "cores": 1, "kind": "port",
+                           "sample": f"calops_oracle (numpy) on 1 of {ntimes} times, scaled"}})

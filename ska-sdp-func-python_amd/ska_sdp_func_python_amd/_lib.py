@@ -114,6 +114,14 @@ SIGNATURES = {
     "sdp_hip_solve_gains": [
         c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
         c_vp, c_vp, c_int, c_dbl, c_int, c_int, c_dbl, c_vp] + _ERR,
+    "sdp_hip_point_sums": [
+        c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
+        c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp] + _ERR,
+    "sdp_hip_divide_vis": [
+        c_i64, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp] + _ERR,
+    "sdp_hip_apply_gains": [
+        c_i64, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp,
+        c_vp, c_int, c_int, c_int, c_int, c_int, c_vp] + _ERR,
     "sdp_hip_grid_weights": [
         c_i64, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int,
         c_int, c_vp, c_vp, c_vp] + _ERR,

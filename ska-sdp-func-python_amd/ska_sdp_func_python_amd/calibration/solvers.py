@@ -26,42 +26,22 @@ import torch
 
 from .. import _device, kernels
 from ..datamodels import create_gaintable_from_visibility
-from ..visibility.operations import divide_visibility
 
 log = logging.getLogger("func-python-logger")
 
 
-def _row_sums(point_vis, gain_table, nchan_g, dev):
-    """x_b [nrow, nbl, nchan_g, npol] c128 and xwt_b f64 (solvers.py:85-107)."""
-    vis = _device.to_dev(point_vis.vis.data, None, dev).to(torch.complex128)
-    wt = _device.to_dev(point_vis.weight.data, None, dev).to(torch.float64)
-    flags = _device.to_dev(point_vis.flags.data, None, dev)
-    keep = (1 - flags).to(torch.float64)
-    vw = vis * wt * keep
-    ww = wt * keep
-    times = np.asarray(point_vis.time.data, dtype=float)
+def _windows(vis_time, gain_table):
+    """CSR of each gain row's vis times (inclusive xarray slice, solvers.py:84-91)."""
     gtimes = np.asarray(gain_table.time.data, dtype=float)
     interval = np.asarray(gain_table.interval.data, dtype=float)
-    nrow = len(gtimes)
-    _, nbl, nchan, npol = vw.shape
-    xb = torch.zeros((nrow, nbl, nchan_g, npol), dtype=torch.complex128, device=dev)
-    xwt = torch.zeros((nrow, nbl, nchan_g, npol), dtype=torch.float64, device=dev)
-    present = np.zeros(nrow, dtype=bool)
-    for row in range(nrow):
-        sel = np.nonzero((times >= gtimes[row] - interval[row] / 2)
-                         & (times <= gtimes[row] + interval[row] / 2))[0]
-        if len(sel) == 0:
-            continue
-        present[row] = True
-        idx = torch.as_tensor(sel, device=dev)
-        a = vw.index_select(0, idx).sum(0)
-        b = ww.index_select(0, idx).sum(0)
-        if nchan_g == 1:
-            a = a.sum(1, keepdim=True)
-            b = b.sum(1, keepdim=True)
-        xb[row] = a
-        xwt[row] = b
-    return xb, xwt, present
+    idx, ptr = [], [0]
+    for row in range(len(gtimes)):
+        sel = np.nonzero((vis_time >= gtimes[row] - interval[row] / 2)
+                         & (vis_time <= gtimes[row] + interval[row] / 2))[0]
+        idx.extend(sel.tolist())
+        ptr.append(len(idx))
+    ptr = np.asarray(ptr, dtype=np.int32)
+    return ptr, np.asarray(idx, dtype=np.int32), np.diff(ptr) > 0
 
 
 def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=200, tol=1e-6,
@@ -71,7 +51,6 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
         mx = float(mv.abs().max()) if isinstance(mv, torch.Tensor) else float(np.max(np.abs(mv)))
         if not mx > 0.0:
             raise ValueError("solve_gaintable: Model visibility is zero")
-    point_vis = divide_visibility(vis, modelvis) if modelvis is not None else vis
     if phase_only:
         log.debug("solve_gaintable: Solving for phase only")
     else:
@@ -85,18 +64,43 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
     dev = _device.device()
     nants = gain_table.gaintable_acc.nants
     nchan = gain_table.gaintable_acc.nchan
-    npol = point_vis.visibility_acc.npol
-    xb, xwt, present = _row_sums(point_vis, gain_table, nchan, dev)
+    npol = vis.visibility_acc.npol
+    # divide_visibility (solvers.py:61-63) and the per-row sums (:82-107) in
+    # one HIP pass, written in StefCal's canonical baseline order
+    v = _device.to_dev(vis["vis"].data, None, dev)
+    if v.dtype not in (torch.complex64, torch.complex128):
+        v = v.to(torch.complex128)
+    v = v.contiguous()
+    m = None
+    if modelvis is not None:
+        m = _device.to_dev(modelvis["vis"].data, v.dtype, dev).contiguous()
+    w = _device.to_dev(vis["weight"].data, torch.float64, dev).contiguous()
+    fl = _device.to_dev(vis["flags"].data, None, dev)
+    if fl.dtype not in kernels._FLAG_DT:
+        fl = fl.to(torch.int64)
+    ptr, tidx, present = _windows(np.asarray(vis.time.data, dtype=float), gain_table)
     for row in np.nonzero(~present)[0]:
         log.warning("Gaintable %s, vis time mismatch %s", gain_table.time.data, vis.time.data)
-
-    bl = np.asarray(point_vis.baselines.data)
+    bl = np.asarray(vis.baselines.data)
     perm, conj, row_start, ant2 = kernels.canonical_baselines(bl[:, 0], bl[:, 1], nants)
-    p = torch.as_tensor(perm, device=dev)
-    c = torch.as_tensor(conj, device=dev)
-    xb_c = xb.index_select(1, p)
-    xb_c = torch.where(c[None, :, None, None], xb_c.conj(), xb_c)
-    xwt_c = xwt.index_select(1, p)
+    # autocorrelations go after the canonical baselines: the solver never
+    # sees them, but they count in the reference's "any weight" test (:116)
+    autos = np.nonzero(bl[:, 0] == bl[:, 1])[0]
+    nc = len(perm)
+    full_perm = np.concatenate([np.asarray(perm, dtype=np.int64), autos]).astype(np.int32)
+    full_conj = np.concatenate([np.asarray(conj, dtype=bool), np.zeros(len(autos), bool)])
+    mfl = None
+    if modelvis is not None and modelvis["flags"].data is not vis["flags"].data:
+        mfl = _device.to_dev(modelvis["flags"].data, None, dev)
+    xb_all, xwt = kernels.point_sums(
+        v, m, w, fl.contiguous(), torch.as_tensor(ptr, device=dev),
+        torch.as_tensor(tidx if len(tidx) else np.zeros(1, np.int32), device=dev), nchan,
+        perm=torch.as_tensor(full_perm, device=dev),
+        conj=torch.as_tensor(full_conj.astype(np.uint8), device=dev), model_flags=mfl)
+    if len(autos):
+        xb_c, xwt_c = xb_all[:, :nc].contiguous(), xwt[:, :nc].contiguous()
+    else:
+        xb_c, xwt_c = xb_all, xwt
 
     if npol == 2 or (npol == 4 and not crosspol):
         mode = 2

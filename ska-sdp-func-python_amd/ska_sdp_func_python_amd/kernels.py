@@ -445,3 +445,92 @@ def taper(uvw, freq, flags, imaging_weight, kind, param):
               {"gaussian": 0, "tukey": 1}[kind], float(param), _ptr(imaging_weight),
               _stream(uvw.device))
     return imaging_weight
+
+
+# ---- calibration neighbours (sdp_hip_point_sums / divide_vis / apply_gains)
+def _vis4(t, name):
+    _on_gpu(t, name)
+    if t.dtype not in (torch.complex64, torch.complex128) or t.dim() != 4 or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous complex [t, b, f, p] tensor")
+    return t
+
+
+def _flags_of(flags, shape):
+    if flags is None:
+        return None, 0
+    _on_gpu(flags, "flags")
+    if tuple(flags.shape) != tuple(shape) or not flags.is_contiguous() or flags.dtype not in _FLAG_DT:
+        raise ValueError("flags must be a contiguous integer tensor shaped like vis")
+    return flags, _FLAG_DT[flags.dtype]
+
+
+def point_sums(vis, model, weight, flags, row_ptr, time_idx, nchan_g, perm=None, conj=None,
+               model_flags=None):
+    """x_b, xwt_b [nrow_g, nbl, nchan_g, npol] (c128, f64) of solve_gaintable
+    over divide_visibility(vis, model) (model None: vis itself)."""
+    _vis4(vis, "vis")
+    if model is not None:
+        _vis4(model, "model")
+        if model.shape != vis.shape or model.dtype != vis.dtype:
+            raise ValueError("model must match vis")
+    nt, nbl, nchan, npol = vis.shape
+    if weight is not None and (weight.shape != vis.shape or weight.dtype != torch.float64
+                               or not weight.is_contiguous()):
+        raise ValueError("weight must be contiguous float64 shaped like vis")
+    fl, fb = _flags_of(flags, vis.shape)
+    nrow_g = row_ptr.numel() - 1
+    nout = nbl if perm is None else perm.numel()
+    if perm is not None and (perm.dtype != torch.int32 or (conj is not None and (
+            conj.dtype != torch.uint8 or conj.numel() != nout))):
+        raise ValueError("perm must be int32 and conj uint8 of the same length")
+    xb = torch.empty((nrow_g, nout, nchan_g, npol), dtype=torch.complex128, device=vis.device)
+    xwt = torch.empty((nrow_g, nout, nchan_g, npol), dtype=torch.float64, device=vis.device)
+    mfl = _model_flags(model_flags, fl)
+    _lib.call("sdp_hip_point_sums", nt, nbl, nchan, npol, _ptr(vis), _ptr(model),
+              _DT_CODE[vis.dtype], _ptr(weight), _ptr(fl), _ptr(mfl), fb, nrow_g, _ptr(row_ptr),
+              _ptr(time_idx), int(nchan_g), int(nout), _ptr(perm), _ptr(conj), _ptr(xb),
+              _ptr(xwt), _stream(vis.device))
+    return xb, xwt
+
+
+def _model_flags(model_flags, fl):
+    """The model's own flags in the vis flags' dtype, or None."""
+    if model_flags is None or fl is None:
+        return None
+    _on_gpu(model_flags, "model_flags")
+    if model_flags.shape != fl.shape:
+        raise ValueError("model flags must be shaped like vis")
+    return model_flags.to(fl.dtype).contiguous()
+
+
+def divide_vis(vis, model, weight, flags, model_flags=None):
+    """(x, xwt) of divide_visibility, same shapes as vis."""
+    _vis4(vis, "vis")
+    _vis4(model, "model")
+    if model.shape != vis.shape or model.dtype != vis.dtype:
+        raise ValueError("model must match vis")
+    fl, fb = _flags_of(flags, vis.shape)
+    x = torch.empty_like(vis)
+    xwt = torch.empty(vis.shape, dtype=torch.float64, device=vis.device)
+    mfl = _model_flags(model_flags, fl)
+    _lib.call("sdp_hip_divide_vis", vis.numel(), _ptr(vis), _ptr(model), _DT_CODE[vis.dtype],
+              _ptr(weight), _ptr(fl), _ptr(mfl), fb, _ptr(x), _ptr(xwt), _stream(vis.device))
+    return x, xwt
+
+
+def apply_gains(vis, weight, flags, use_flags, ant1, ant2, time_row, gain, inverse):
+    """apply_gaintable in place on device vis / weight [t, b, f, p]."""
+    _vis4(vis, "vis")
+    nt, nbl, nchan, npol = vis.shape
+    if weight.shape != vis.shape or weight.dtype != torch.float64 or not weight.is_contiguous():
+        raise ValueError("weight must be contiguous float64 shaped like vis")
+    fl, fb = _flags_of(flags, vis.shape)
+    _on_gpu(gain, "gain")
+    if gain.dtype != torch.complex128 or gain.dim() != 5 or not gain.is_contiguous():
+        raise ValueError("gain must be contiguous complex128 [rows, nants, nchan, nrec, nrec]")
+    nrow_g, nants, nchan_g, nrec, _ = gain.shape
+    _lib.call("sdp_hip_apply_gains", nt, nbl, nchan, npol, _ptr(vis), _DT_CODE[vis.dtype],
+              _ptr(weight), _ptr(fl), fb, int(bool(use_flags)), _ptr(ant1), _ptr(ant2),
+              _ptr(time_row), _ptr(gain), nrow_g, nants, nchan_g, nrec, int(bool(inverse)),
+              _stream(vis.device))
+    return vis, weight

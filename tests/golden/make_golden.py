@@ -21,6 +21,7 @@ Fixtures:
                    griddata_visibility_reweight, taper_visibility_gaussian/_tukey
                    (imaging/weighting.py:35-136, grid_data/gridding.py:33-60,
                    :258-499, util/array_functions.py:85-99)
+  applygt_*.npz    apply_gaintable               (calibration/operations.py:23-256)
   nufft_c1.npz     ORACLE-generated (exact direct sums, oracle/nufft_oracle.py):
                    ducc0 is unavailable, the ducc0 boundary is parity-unpinned.
 """
@@ -297,6 +298,49 @@ def make_weighting():
              gauss_beam=np.array(4 * cell), tukey=np.array(0.3), **out)
 
 
+def make_applygt():
+    """apply_gaintable for npol 1 / 2 / 4, forward and inverse, with and
+    without use_flags; one antenna's gain made singular in one channel (the
+    inverse path's zeroing), a gain table with fewer channels than the vis
+    (the reference applies gain channel c to vis channel c only), and a vis
+    time outside every gain window (left untouched)."""
+    ns = load_reference("calibration/operations.py", ["apply_gaintable"],
+                        {"copy": __import__("copy"), "numpy": np, "Time": None})
+    cases = (("p1", "stokesI", 3, 3), ("p1_g1chan", "stokesI", 3, 1), ("p2", "linearnp", 2, 2),
+             ("p4", "linear", 2, 2), ("p4_circ_g1chan", "circular", 3, 1))
+    for tag, pname, nchan, gchan in cases:
+        rng = np.random.default_rng(41 + len(tag))
+        pf = dm.PolarisationFrame(pname)
+        nants, ntimes = 6, 4
+        vis = simulation.make_visibility("LOW", nants=nants, ntimes=ntimes, nchan=nchan, f_lo=1.0e8,
+                                         f_hi=1.1e8, ha_span_h=0.5, polarisation_frame=pf)
+        shape = vis.vis.shape
+        vis["vis"].data = rng.normal(size=shape) + 1j * rng.normal(size=shape)
+        vis["weight"].data = rng.uniform(0.5, 2.0, shape)
+        vis["flags"].data = (rng.uniform(size=shape) < 0.1).astype(int)
+        times = np.asarray(vis.time.data)
+        nrec = 1 if pf.npol == 1 else 2
+        gt_times = times[:3].copy()  # the last vis time has no gain row
+        interval = np.full(3, float(np.median(np.diff(times))))
+        gain = (rng.normal(1.0, 0.3, (3, nants, gchan, nrec, nrec))
+                * np.exp(1j * rng.uniform(-np.pi, np.pi, (3, nants, gchan, nrec, nrec))))
+        if nrec == 2 and pf.npol == 2:
+            gain[..., 0, 1] = gain[..., 1, 0] = 0.0
+        gain[1, 2, 0] = 0.0  # singular (no inverse) for antenna 2, channel 0, row 1
+        gt = dm.GainTable.constructor(gain, gt_times, interval, np.ones(gain.shape),
+                                      np.zeros((3, gchan, nrec, nrec)), np.linspace(1e8, 1.1e8, gchan),
+                                      dm.PolarisationFrame("stokesI" if nrec == 1 else pname))
+        out = {}
+        for inverse in (False, True):
+            for use_flags in (False, True):
+                v = ns["apply_gaintable"](vis.copy(deep=True), gt, inverse=inverse, use_flags=use_flags)
+                out[f"vis_i{int(inverse)}_f{int(use_flags)}"] = v["vis"].data
+                out[f"wt_i{int(inverse)}_f{int(use_flags)}"] = v["weight"].data
+        save(f"applygt_{tag}.npz", vis=vis["vis"].data, weight=vis["weight"].data,
+             flags=vis["flags"].data, time=times, baselines=np.asarray(vis.baselines.data),
+             gain=gain, gt_time=gt_times, gt_interval=interval, pol_frame=np.array(pname), **out)
+
+
 def make_fft():
     ns = load_reference("fourier_transforms/fft_support.py", ["fft", "ifft"],
                         {"pyfftw_exists": False, "pyfftw": None})
@@ -339,3 +383,4 @@ if __name__ == "__main__":
     make_fft()
     make_nufft_c1()
     make_weighting()
+    make_applygt()
