@@ -324,6 +324,29 @@ class WCS:
         return _copy.deepcopy(self)
 
 
+def skycoord_to_pixel(coords, wcs, origin=1, mode="wcs"):
+    """SIN (orthographic) projection of ICRS directions to pixels: the inverse
+    of ``pixel_to_skycoord``; NaN for directions behind the tangent plane.
+    ``coords`` is a SkyCoord or a sequence of them; returns (x, y) arrays."""
+    w = wcs.wcs
+    items = coords if isinstance(coords, (list, tuple)) else [coords]
+    ra0, dec0 = math.radians(w.crval[0]), math.radians(w.crval[1])
+    xs, ys = [], []
+    for c in items:
+        ra, dec = c.ra.rad, c.dec.rad
+        da = ra - ra0
+        l = math.cos(dec) * math.sin(da)
+        m = math.sin(dec) * math.cos(dec0) - math.cos(dec) * math.sin(dec0) * math.cos(da)
+        n = math.sin(dec) * math.sin(dec0) + math.cos(dec) * math.cos(dec0) * math.cos(da)
+        if n < 0.0:
+            xs.append(float("nan"))
+            ys.append(float("nan"))
+            continue
+        xs.append(l / math.radians(w.cdelt[0]) + w.crpix[0] - 1 + origin)
+        ys.append(m / math.radians(w.cdelt[1]) + w.crpix[1] - 1 + origin)
+    return np.array(xs), np.array(ys)
+
+
 def pixel_to_skycoord(xp, yp, wcs, origin=1):
     """SIN (orthographic) deprojection of a pixel to an ICRS direction."""
     w = wcs.wcs
@@ -758,7 +781,9 @@ def create_gaintable_from_visibility(vis, timeslice=None, jones_type="T"):
 
 
 class SkyComponent:
-    def __init__(self, direction, frequency, flux, name="", shape="Point",
+    """Positional order of ska-sdp-datamodels: direction, frequency, name, flux."""
+
+    def __init__(self, direction=None, frequency=None, name=None, flux=None, shape="Point",
                  polarisation_frame=PolarisationFrame("stokesIQUV"), params=None):
         self.direction = direction
         self.frequency = np.asarray(frequency, dtype=float)
@@ -778,3 +803,35 @@ class SkyComponent:
 
     def copy(self):
         return _copy.deepcopy(self)
+
+
+# ---------------------------------------------------------------------------
+# SkyModel
+# ---------------------------------------------------------------------------
+class SkyModel:
+    """image + point components + optional gain table and mask
+    (ska-sdp-datamodels' SkyModel attributes used by the sky_model drivers)."""
+
+    def __init__(self, image=None, components=None, gaintable=None, mask=None, fixed=False):
+        self.image = image
+        self.components = list(components) if components is not None else []
+        self.gaintable = gaintable
+        self.mask = mask
+        self.fixed = fixed
+
+    def copy(self):
+        return _copy.deepcopy(self)
+
+
+_TIME_VARS = ("vis", "uvw", "weight", "imaging_weight", "flags", "time", "integration_time")
+
+
+def visibility_time_slices(vis):
+    """One Visibility per time sample, as ``vis.groupby("time", squeeze=False)``
+    yields them (views of the parent's arrays)."""
+    nt = vis.vis.shape[0]
+    out = []
+    for t in range(nt):
+        rep = {k: vis._vars[k][t:t + 1] for k in _TIME_VARS if k in vis._vars}
+        out.append(vis._copy_with(deep=False, replace=rep))
+    return out

@@ -6,10 +6,33 @@ weight as the reference's visibility_acc.flagged_* give them.  One HIP
 kernel (sdp_hip_divide_vis) with numpy's complex division.
 """
 
+import numpy as np
 import torch
 
 from .. import _device, kernels
 from ..datamodels import Visibility
+
+
+def concatenate_visibility(vis_list, dim="time"):
+    """Reference visibility/operations.py:38-72 for ``dim="time"`` (the only
+    use on this path, sky_model drivers): time-dimension arrays joined,
+    the rest taken from the first."""
+    if not len(vis_list) > 0:
+        raise ValueError("concatenate_visibility: vis_list is empty")
+    if dim != "time":
+        raise ValueError(f"concatenate_visibility: dim {dim} is not supported here")
+    first = vis_list[0]
+    rep = {}
+    for k in ("vis", "uvw", "weight", "imaging_weight", "flags", "time", "integration_time"):
+        if k not in first._vars:
+            continue
+        parts = [v._vars[k] for v in vis_list]
+        if isinstance(parts[0], torch.Tensor):
+            rep[k] = torch.cat([p if isinstance(p, torch.Tensor) else torch.as_tensor(p, device=parts[0].device)
+                                for p in parts], dim=0)
+        else:
+            rep[k] = np.concatenate([np.asarray(p) for p in parts], axis=0)
+    return first._copy_with(deep=True, replace=rep)
 
 
 def divide_visibility(vis, modelvis):

@@ -37,7 +37,7 @@ def test_dft_skycomponent_qa_known_answers():
     vis = simulation.make_visibility("LOW", nants=40, ntimes=2, nchan=6, f_lo=1.0e8, f_hi=1.1e8,
                                      polarisation_frame="linear", phasecentre=pc)
     comp = dm.SkyComponent(dm.SkyCoord(181.0, -35.0, unit="deg"), freq,
-                           np.array(6 * [100.0, 20.0, -10.0, 1.0]).reshape(6, 4),
+                           flux=np.array(6 * [100.0, 20.0, -10.0, 1.0]).reshape(6, 4),
                            polarisation_frame=dm.PolarisationFrame("stokesIQUV"))
     res = dft_skycomponent_visibility(vis, 20 * [comp])
     qa = res.visibility_acc.qa_visibility()

@@ -104,3 +104,29 @@ def test_wcs_and_image_centre():
     east = pixel_to_skycoord(128, 129, im.image_acc.wcs, origin=1)  # one pixel left = east
     assert east.ra.rad > pc.ra.rad
     assert abs(im.image_acc.wcs.sub([4]).wcs_world2pix(np.array([1e8]), 0)[0][0]) < 1e-12
+
+
+def test_skycoord_pixel_round_trip_and_apply_beam():
+    """skycoord_to_pixel inverts pixel_to_skycoord (SIN, origin 1); the
+    reference's apply_beam_to_skycomponent rules (sky_component/operations.py:
+    411-425): flux x beam at the rounded pixel, / beam for inverse, zero off
+    the image."""
+    import math
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.sky_component import apply_beam_to_skycomponent
+    pc = dm.SkyCoord(math.radians(30.0), math.radians(-40.0))
+    im = dm.create_image(64, 0.002, pc)
+    for x, y in ((33.0, 33.0), (10.25, 50.5), (60.0, 3.0)):
+        c = dm.pixel_to_skycoord(x, y, im.image_acc.wcs, origin=1)
+        px, py = dm.skycoord_to_pixel(c, im.image_acc.wcs, origin=1)
+        assert abs(px[0] - x) < 1e-9 and abs(py[0] - y) < 1e-9
+    im["pixels"].data[0, 0] = np.arange(64 * 64, dtype=float).reshape(64, 64) + 1.0
+    comps = [dm.SkyComponent(dm.pixel_to_skycoord(20.0, 30.0, im.image_acc.wcs), [1e8], flux=[[2.0]]),
+             dm.SkyComponent(dm.pixel_to_skycoord(200.0, 30.0, im.image_acc.wcs), [1e8], flux=[[2.0]])]
+    out = apply_beam_to_skycomponent(comps, im)
+    # the reference indexes the beam with the 1-relative pixel coordinates
+    # (origin=1) as they are: pixel (20, 30) reads data[..., 30, 20]
+    assert out[0].flux[0, 0] == 2.0 * im["pixels"].data[0, 0, 30, 20]
+    assert out[1].flux[0, 0] == 0.0
+    inv = apply_beam_to_skycomponent(comps[0], im, inverse=True)
+    assert inv.flux[0, 0] == 2.0 / im["pixels"].data[0, 0, 30, 20]
