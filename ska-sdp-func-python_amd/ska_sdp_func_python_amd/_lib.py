@@ -10,7 +10,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libska_sdp_hip.so")
+# SDP_HIP_LIB_OVERRIDE: load another build of the same C ABI (kernel-variant
+# experiments, scripts/build_variants.sh); the default is the in-tree build.
+LIB_PATH = os.environ.get("SDP_HIP_LIB_OVERRIDE") or os.path.join(_HERE, "_lib", "libska_sdp_hip.so")
 
 SDP_HIP_OK = 0
 SDP_HIP_ERR_INVALID_ARG = 1
