@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -81,7 +82,9 @@ class Workspace {
                 b.ptr = nullptr;
                 b.bytes = 0;
             }
-            size_t want = bytes + bytes / 8 + 256;  // headroom against regrowth
+            // headroom against regrowth, capped so that the large plane and
+            // record buffers do not take memory the call has budgeted elsewhere
+            size_t want = bytes + std::min<size_t>(bytes / 8, (size_t)1 << 30) + 256;
             hipError_t e = hipMalloc(&b.ptr, want);
             if (e != hipSuccess) {
                 (void)hipGetLastError();
@@ -98,6 +101,14 @@ class Workspace {
             b.bytes = want;
         }
         return b.ptr;
+    }
+    // bytes currently held under `name` on the current device (0 if none)
+    size_t held(const std::string &name) {
+        int dev = 0;
+        SDP_HIP_CHECK(hipGetDevice(&dev));
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = bufs_.find({dev, name});
+        return it == bufs_.end() ? 0 : it->second.bytes;
     }
     void release() {
         std::lock_guard<std::mutex> lk(mu_);

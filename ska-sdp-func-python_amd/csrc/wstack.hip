@@ -55,6 +55,8 @@ constexpr int kChunkMax = 8192;   // [kChunkMin, kChunkMax] (chunk_size())
 constexpr int kPitch = 24;     // LDS row pitch in complex values (b64 conflict-free)
 constexpr int kMaxW = 8;
 constexpr int kPhiTab = 8193;  // Phi(xi) table on xi in [0, 0.5]
+constexpr int kFftBatchMax = 16;                      // planes per FFT batch
+constexpr size_t kFftBatchBytes = (size_t)16 << 30;  // y-spectra buffers per batch
 
 struct Geo {
     int W;
@@ -1494,6 +1496,7 @@ struct Plan {
     bool pipelined = false;          // row parts, persistent launches, no host syncs
     bool aux_bucketing = false;      // bucketing on the auxiliary stream
     int chunk_planes = 1;            // planes resident per pass
+    int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
     int row_lo = 0, row_hi = 0;      // grid rows (x) the visibilities reach
     unsigned chunk = kChunkMin;      // max records per work item
     int64_t nrec = 0, nitems = 0;    // totals
@@ -1522,14 +1525,24 @@ struct Inputs {
 };
 
 // Bytes of w planes kept resident per pass: SDP_HIP_GRID_BUDGET_GB if set,
-// else half of the device memory free at plan time (one 8192^2 plane is
-// 512 MiB, so a C2 invert keeps all its planes resident on a 288 GB MI355X).
-static size_t grid_budget_bytes() {
+// else the device memory this call can still use -- free memory plus what the
+// workspace already holds for the planes and the records, less the records
+// and key/rank arrays still to be allocated (`need_other`) and a reserve of
+// 6 GiB.  A C2 invert keeps its 9 planes resident, and so does a C4 shard
+// (70 planes of 16384^2, 150 GB) on a 288 GB MI355X, gridding every record
+// once instead of once per plane chunk.
+static size_t grid_budget_bytes(size_t need_other) {
     const char *e = std::getenv("SDP_HIP_GRID_BUDGET_GB");
     if (e && std::atof(e) > 0) return (size_t)(std::atof(e) * 1073741824.0);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)8 << 30;
-    return free_b / 2;
+    Workspace &ws = Workspace::get();
+    const size_t held_planes = ws.held("grid") + ws.held("spec") + ws.held("spec_in");
+    const size_t held_other = ws.held("recs") + ws.held("key_rank") + ws.held("degrid_acc");
+    const size_t avail = free_b + held_planes + held_other;
+    const size_t reserve = (size_t)6 << 30;
+    const size_t need = need_other + reserve;
+    return avail > need ? avail - need : (size_t)1 << 30;
 }
 
 // SDP_HIP_PIPELINE: 0 (default) = bucket on the caller's stream; 1 = dirty2ms
@@ -1569,7 +1582,7 @@ static float2 *band_input(const Plan &P, hipStream_t st) {
     static std::mutex mu;
     static std::map<int, BandState> states;
     const Geo &g = P.g;
-    const size_t elems = (size_t)P.chunk_planes * g.ny * g.ngx;
+    const size_t elems = (size_t)P.fft_planes * g.ny * g.ngx;
     float2 *buf = scratch<float2>("spec_in", elems);
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
@@ -1679,13 +1692,25 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         }
     }
 
-    // plane chunking against the grid memory budget
-    const size_t plane_bytes =
-        ((size_t)g.ngx * g.ngy + 2 * (size_t)g.ny * g.ngx) * sizeof(float2);
-    const int cp = (int)std::max<size_t>(1, grid_budget_bytes() / plane_bytes);
+    // plane chunking against the grid memory budget.  The y-spectra buffers
+    // (spec, spec_in: ny x ngx per plane) serve batches of fft_planes planes,
+    // so the resident planes cost one grid each (C4: 70 planes of 16384^2)
+    const size_t grid_plane = (size_t)g.ngx * g.ngy * sizeof(float2);
+    const size_t spec_plane = 2 * (size_t)g.ny * g.ngx * sizeof(float2);
+    P.fft_planes = (int)std::max<size_t>(
+        1, std::min<size_t>(kFftBatchMax, kFftBatchBytes / spec_plane));
+    if (const char *e = std::getenv("SDP_HIP_FFT_PLANES"))  // tests: force small batches
+        if (std::atoi(e) > 0) P.fft_planes = std::atoi(e);
+    P.fft_planes = std::min(P.fft_planes, g.nplanes);
+    const int64_t nvis_all = in.nrow * (int64_t)in.nchan;
+    const size_t need_other =
+        (size_t)nvis_all * (sizeof(VisRec) + sizeof(uint2) + (grid_mode ? 0 : sizeof(float2))) +
+        (size_t)g.ntiles * g.nps * 2 * sizeof(unsigned) + (size_t)P.fft_planes * spec_plane;
+    const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
     P.chunk_planes = std::min(cp, g.nplanes);
+    P.fft_planes = std::min(P.fft_planes, P.chunk_planes);
     P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy);
-    P.spec = scratch<float2>("spec", (size_t)P.chunk_planes * g.ny * g.ngx);
+    P.spec = scratch<float2>("spec", (size_t)P.fft_planes * g.ny * g.ngx);
     if (grid_mode) P.spec_in = band_input(P, st);
 
     // records per item: large enough to amortise the tile flush over dense
@@ -1989,12 +2014,12 @@ static void exec_fft(hipfftHandle h, float2 *p, int direction) {
         throw Error(SDP_HIP_ERR_RUNTIME, "hipfftExecC2C failed");
 }
 
-static void fft_rows_y(const Plan &P, int np, int direction, hipStream_t st) {
+static void fft_rows_y(const Plan &P, int q0, int np, int direction, hipStream_t st) {
     const Geo &g = P.g;
     const int nrow = P.row_hi - P.row_lo;
     if (nrow <= 0) return;
     hipfftHandle hr = fft_plan_1d(g.ngy, 1, g.ngy, nrow, st);
-    for (int q = 0; q < np; ++q)
+    for (int q = q0; q < q0 + np; ++q)
         exec_fft(hr, P.grid + (size_t)q * g.ngx * g.ngy + (size_t)P.row_lo * g.ngy, direction);
 }
 
@@ -2095,22 +2120,26 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
             tg.mark();
             tgrid += tg.ms(0, 1);
         }
-        StageTimer t2(st);
-        t2.mark();
-        fft_rows_y(P, np, HIPFFT_BACKWARD, st);
-        if (P.row_hi > P.row_lo)
-            k_tr_grid_to_t<<<tr_grid(g, P.row_hi - P.row_lo, np), dim3(kTr, kTrRows), 0, st>>>(
-                g, P.grid, P.spec_in, P.row_lo, P.row_hi);
-        SDP_HIP_CHECK(hipGetLastError());
-        fft_rows_x(P, np, HIPFFT_BACKWARD, st, P.spec_in);
-        t2.mark();
-        const dim3 grd(grid1d(g.nx, 256), g.ny);
-        k_screen_fwd_t<<<grd, 256, 0, st>>>(g, P.spec, p_lo, np, dirty, sx, sy,
-                                            (accumulate || p_lo > 0) ? 1 : 0, tab);
-        SDP_HIP_CHECK(hipGetLastError());
-        t2.mark();
-        tfft += t2.ms(0, 1);
-        tscr += t2.ms(1, 2);
+        for (int sb = 0; sb < np; sb += P.fft_planes) {
+            const int nb = std::min(P.fft_planes, np - sb);
+            StageTimer t2(st);
+            t2.mark();
+            fft_rows_y(P, sb, nb, HIPFFT_BACKWARD, st);
+            if (P.row_hi > P.row_lo)
+                k_tr_grid_to_t<<<tr_grid(g, P.row_hi - P.row_lo, nb), dim3(kTr, kTrRows), 0,
+                                 st>>>(g, P.grid + (size_t)sb * g.ngx * g.ngy, P.spec_in,
+                                       P.row_lo, P.row_hi);
+            SDP_HIP_CHECK(hipGetLastError());
+            fft_rows_x(P, nb, HIPFFT_BACKWARD, st, P.spec_in);
+            t2.mark();
+            const dim3 grd(grid1d(g.nx, 256), g.ny);
+            k_screen_fwd_t<<<grd, 256, 0, st>>>(g, P.spec, p_lo + sb, nb, dirty, sx, sy,
+                                                (accumulate || p_lo + sb > 0) ? 1 : 0, tab);
+            SDP_HIP_CHECK(hipGetLastError());
+            t2.mark();
+            tfft += t2.ms(0, 1);
+            tscr += t2.ms(1, 2);
+        }
     }
     tm.mark();
     if (P.pipelined) read_part_meta(P, st);
@@ -2155,22 +2184,26 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
-        StageTimer t2(st);
         zero_band(P, np, st);
-        t2.mark();
-        const dim3 grd(grid1d(g.ngx, 256), g.ny);
-        k_screen_adj_t<<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_lo, np, P.spec, tab);
-        SDP_HIP_CHECK(hipGetLastError());
-        t2.mark();
-        fft_rows_x(P, np, HIPFFT_FORWARD, st);
-        if (P.row_hi > P.row_lo)
-            k_tr_t_to_grid<<<tr_grid(g, P.row_hi - P.row_lo, np), dim3(kTr, kTrRows), 0, st>>>(
-                g, P.spec, P.grid, P.row_lo, P.row_hi);
-        SDP_HIP_CHECK(hipGetLastError());
-        fft_rows_y(P, np, HIPFFT_FORWARD, st);
-        t2.mark();
-        tscr += t2.ms(0, 1);
-        tfft += t2.ms(1, 2);
+        for (int sb = 0; sb < np; sb += P.fft_planes) {
+            const int nb = std::min(P.fft_planes, np - sb);
+            StageTimer t2(st);
+            t2.mark();
+            const dim3 grd(grid1d(g.ngx, 256), g.ny);
+            k_screen_adj_t<<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_lo + sb, nb, P.spec, tab);
+            SDP_HIP_CHECK(hipGetLastError());
+            t2.mark();
+            fft_rows_x(P, nb, HIPFFT_FORWARD, st);
+            if (P.row_hi > P.row_lo)
+                k_tr_t_to_grid<<<tr_grid(g, P.row_hi - P.row_lo, nb), dim3(kTr, kTrRows), 0,
+                                 st>>>(g, P.spec, P.grid + (size_t)sb * g.ngx * g.ngy, P.row_lo,
+                                       P.row_hi);
+            SDP_HIP_CHECK(hipGetLastError());
+            fft_rows_y(P, sb, nb, HIPFFT_FORWARD, st);
+            t2.mark();
+            tscr += t2.ms(0, 1);
+            tfft += t2.ms(1, 2);
+        }
         if (P.aux_bucketing && !P.pipelined && !waited)
             read_part_meta(P, aux_stream());  // host waits for the bucketing only
         for (size_t i = 0; i < P.parts.size(); ++i) {

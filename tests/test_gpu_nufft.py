@@ -204,6 +204,30 @@ def test_plane_chunking_matches_resident(bucket, monkeypatch):
     assert rel_rms(vpart.cpu().numpy(), vfull.cpu().numpy()) < 1e-6
 
 
+@pytest.mark.parametrize("fft_planes,budget", [("2", None), ("3", "0.002")])
+def test_fft_batches_match_single_batch(fft_planes, budget, monkeypatch):
+    """The per-plane FFT / w-screen stages run in batches of fft_planes planes
+    (the y-spectra buffers of very large grids hold only a batch): batches of
+    2 or 3 planes, with all planes resident or in plane chunks, equal one
+    batch over all planes for both directions."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(10, nrow=3000, nchan=4, umax=4000.0)
+    args = (T(uvw), T(freq), T(ms), T(wgt), 256, 256, cell, cell, 1e-7, True)
+    img = torch.randn(256, 256, dtype=torch.float64, device=dev())
+    full, info = kernels.ms2dirty(*args)
+    vfull, _ = kernels.dirty2ms(T(uvw), T(freq), img, T(wgt), cell, cell, 1e-7, True,
+                                vis_dtype=torch.complex128)
+    monkeypatch.setenv("SDP_HIP_FFT_PLANES", fft_planes)
+    if budget:
+        monkeypatch.setenv("SDP_HIP_GRID_BUDGET_GB", budget)
+    part, info2 = kernels.ms2dirty(*args)
+    vpart, _ = kernels.dirty2ms(T(uvw), T(freq), img, T(wgt), cell, cell, 1e-7, True,
+                                vis_dtype=torch.complex128)
+    assert info["nplanes"] > 3
+    assert rel_rms(part.cpu().numpy(), full.cpu().numpy()) < 1e-6
+    assert rel_rms(vpart.cpu().numpy(), vfull.cpu().numpy()) < 1e-6
+
+
 def test_full_size_invert_matches_c_restatement():
     """C2 geometry at the full 4096^2 image (8192^2 grid, 9 w planes): the HIP
     invert of 2 of the 64 channels against oracle/wgrid_cpu.c (the C
