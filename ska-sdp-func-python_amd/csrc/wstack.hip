@@ -86,6 +86,14 @@ struct Item {
     uint32_t b, e, tile, p0;
 };
 
+// Large grids (16x16-cell buckets): work item of one group of 4 2x2-cell
+// buckets (a 2 x 8-cell region) inside a sub-sorted coarse item; records
+// [b, e) ordered by bucket, bucket j of the group ending at o[j] (k_subsort)
+struct FineItem {
+    uint32_t b, e, tile, p0;
+    uint32_t o[4];
+};
+
 // ------------------------------------------------------------------------
 // device helpers
 // ------------------------------------------------------------------------
@@ -485,6 +493,65 @@ __global__ void k_items_fill(int64_t ngroups, int grp, int groups_per_plane,
     }
 }
 
+// Large grids: the dense 2x2-cell histogram would be too large (C4: 70
+// planes of 8192^2 buckets), so visibilities are bucketed by 16x16 cells and
+// each coarse item's records are then re-ordered in place by 2x2-cell bucket
+// -- x pair major, y pair minor, so the 4 buckets of a 2 x 8-cell group are
+// consecutive -- through an LDS copy.  The item's 16 groups become register
+// gridder / degridder work items (FineItem; empty groups have b == e).  One
+// 256-thread workgroup per coarse item of <= kSubChunk records (the plan caps
+// the chunk on this path).
+constexpr int kSubChunk = 4096;
+
+__device__ __forceinline__ int sub_class(uint32_t ij) {
+    const int ic = (int)(ij & 0xffffu), jc = (int)(ij >> 16);
+    return ((ic & 15) >> 1) * 8 + ((jc & 15) >> 1);
+}
+
+__global__ __launch_bounds__(256) void k_subsort(Geo g, const Item *__restrict__ items,
+                                                 VisRec *recs, FineItem *__restrict__ fitems) {
+    __shared__ VisRec stage[kSubChunk];
+    __shared__ unsigned cur[64], first[65];
+    const Item it = items[blockIdx.x];
+    const int n = (int)(it.e - it.b);
+    if (threadIdx.x < 64) cur[threadIdx.x] = 0u;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const VisRec r = recs[it.b + i];
+        stage[i] = r;
+        atomicAdd(&cur[sub_class(r.ij)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned a = 0;
+        for (int c = 0; c < 64; ++c) {
+            first[c] = a;
+            a += cur[c];
+        }
+        first[64] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) cur[threadIdx.x] = first[threadIdx.x];
+    if (threadIdx.x < 16) {
+        const int xp = threadIdx.x >> 1, hf = threadIdx.x & 1, c0 = xp * 8 + hf * 4;
+        FineItem f;
+        f.b = it.b + first[c0];
+        f.e = it.b + first[c0 + 4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f.o[j] = it.b + first[c0 + j + 1];
+        const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
+        f.tile = (uint32_t)((tx * 8 + xp) * (g.ngy / (kTileFine * kGroupFine)) + ty * 2 + hf);
+        f.p0 = it.p0;
+        fitems[(size_t)blockIdx.x * 16 + threadIdx.x] = f;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const VisRec r = stage[i];
+        const unsigned pos = atomicAdd(&cur[sub_class(r.ij)], 1u);
+        recs[it.b + pos] = r;
+    }
+}
+
 // ------------------------------------------------------------------------
 // kernels: gridding / degridding (the hot loops)
 // ------------------------------------------------------------------------
@@ -530,6 +597,20 @@ __device__ __forceinline__ Item load_item(const ItemSrc &src, uint32_t w, uint32
     it.e = __builtin_amdgcn_readfirstlane(raw.e);
     it.tile = __builtin_amdgcn_readfirstlane(raw.tile);
     it.p0 = __builtin_amdgcn_readfirstlane(raw.p0);
+    return it;
+}
+
+__device__ __forceinline__ Item load_fine_item(const FineItem *items, uint32_t w, uint32_t n,
+                                               uint32_t stride, uint32_t (&fo)[4]) {
+    const uint32_t i = (uint32_t)(((uint64_t)w * stride) % n);
+    const FineItem raw = items[i];
+    Item it;
+    it.b = __builtin_amdgcn_readfirstlane(raw.b);
+    it.e = __builtin_amdgcn_readfirstlane(raw.e);
+    it.tile = __builtin_amdgcn_readfirstlane(raw.tile);
+    it.p0 = __builtin_amdgcn_readfirstlane(raw.p0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fo[j] = __builtin_amdgcn_readfirstlane(raw.o[j]);
     return it;
 }
 
@@ -727,10 +808,11 @@ __device__ __forceinline__ void acc_add(float (&ar)[NQ], float (&ai)[NQ], float 
 // global float atomics (zero cells skipped), so neighbouring buckets share
 // one flush of their overlapping halos.  Records of a bucket are consumed in
 // static groups of 8 (zero-valued padding at the end of a bucket).
-template <int W, bool WS>
+template <int W, bool WS, bool FI>
 __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict__ recs,
                                                  ItemSrc src,
                                                  const unsigned *__restrict__ offs,
+                                                 const FineItem *__restrict__ fitems,
                                                  float *__restrict__ grid, int p_lo, int p_hi,
                                                  int dbg) {
     constexpr int SUB = kTileFine;
@@ -744,7 +826,10 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
     const uint32_t n_items = item_count(src);
     const uint32_t stride = item_stride(n_items);
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        const Item it = load_item(src, w_it, n_items, stride);
+        uint32_t fo[4] = {0u, 0u, 0u, 0u};
+        const Item it = FI ? load_fine_item(fitems, w_it, n_items, stride, fo)
+                           : load_item(src, w_it, n_items, stride);
+        if (FI && it.b >= it.e) continue;
         if (dbg & 4) {
             if (it.b == 0xfffffffeu) grid[0] = 1.0f;  // keep the item load live
             continue;
@@ -761,8 +846,8 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
 
         const float tap_t = (float)(lane & 7);
         for (int j = 0; j < GRP; ++j) {
-            const uint32_t rb = max(it.b, offs[key0 + j]);
-            const uint32_t re = min(it.e, offs[key0 + j + 1]);
+            const uint32_t rb = FI ? (j == 0 ? it.b : fo[j - 1]) : max(it.b, offs[key0 + j]);
+            const uint32_t re = FI ? fo[j] : min(it.e, offs[key0 + j + 1]);
             if (rb >= re) continue;
             const int jb = jbase + j * SUB;  // bucket's first cell along y
 
@@ -876,10 +961,11 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
 // exchanges per record instead of 12).  Each record belongs to exactly one
 // item, so its raw sum is added to acc[] with a plain read-modify-write; the
 // record factor wgt * exp(-2 pi i w s0) is applied by k_finalize.
-template <int W, bool WS>
+template <int W, bool WS, bool FI>
 __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restrict__ recs,
                                                    ItemSrc src,
                                                    const unsigned *__restrict__ offs,
+                                                   const FineItem *__restrict__ fitems,
                                                    const float2 *__restrict__ grid, int p_lo,
                                                    int p_hi, float2 *__restrict__ acc) {
     constexpr int SUB = kTileFine;
@@ -893,7 +979,10 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
     const uint32_t n_items = item_count(src);
     const uint32_t stride = item_stride(n_items);
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        const Item it = load_item(src, w_it, n_items, stride);
+        uint32_t fo[4] = {0u, 0u, 0u, 0u};
+        const Item it = FI ? load_fine_item(fitems, w_it, n_items, stride, fo)
+                           : load_item(src, w_it, n_items, stride);
+        if (FI && it.b >= it.e) continue;
         const int lane = threadIdx.x;
         const LaneRole<W> role(lane);
         const float ihw = g.inv_half_w, bl = g.beta_l2e;
@@ -922,8 +1011,8 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
         const float tap_t = (float)(lane & 7);
         const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
         for (int j = 0; j < GRP; ++j) {
-            const uint32_t rb = max(it.b, offs[key0 + j]);
-            const uint32_t re = min(it.e, offs[key0 + j + 1]);
+            const uint32_t rb = FI ? (j == 0 ? it.b : fo[j - 1]) : max(it.b, offs[key0 + j]);
+            const uint32_t re = FI ? fo[j] : min(it.e, offs[key0 + j + 1]);
             if (rb >= re) continue;
             const int jb = jbase + j * SUB;
 
@@ -1483,6 +1572,7 @@ struct Part {
     unsigned *hist = nullptr, *offs = nullptr, *nch = nullptr, *ioffs = nullptr;
     unsigned long long *nbad = nullptr;
     Item *items = nullptr;
+    FineItem *fitems = nullptr;  // 16 per item when sub-sorted (k_subsort)
     unsigned *meta = nullptr;  // device: see k_part_meta
     // host copies (filled by read_part_meta; synchronous plans only)
     int64_t nrec = 0, nitems = 0;
@@ -1495,6 +1585,7 @@ struct Plan {
     std::vector<Part> parts;
     bool pipelined = false;          // row parts, persistent launches, no host syncs
     bool aux_bucketing = false;      // bucketing on the auxiliary stream
+    bool subsort = false;            // 16x16 buckets re-ordered to 2x2 (register kernels)
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
     int row_lo = 0, row_hi = 0;      // grid rows (x) the visibilities reach
@@ -1734,6 +1825,13 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         pt.nvis = (pt.r1 - pt.r0) * in.nchan;
         P.parts.push_back(pt);
     }
+    // large grids: re-order the 16x16 buckets by 2x2 bucket for the register
+    // kernels (SDP_HIP_SUBSORT=0 keeps the LDS-tile kernels)
+    {
+        const char *e = std::getenv("SDP_HIP_SUBSORT");
+        P.subsort = g.sub == kTileCoarse && !P.aux_bucketing && !(e && std::atoi(e) == 0);
+        if (P.subsort) P.chunk = std::min<unsigned>(P.chunk, kSubChunk);
+    }
     P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
     return P;
 }
@@ -1914,15 +2012,59 @@ template <int W, bool WS>
 static void launch_grid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) *
                        TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
-    const void *fn = (const void *)k_grid_reg<W, WS>;
+    const void *fn = (const void *)k_grid_reg<W, WS, false>;
     const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
     if (L.blocks == 0) return;
-    k_grid_reg<W, WS><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
-                                                (float *)P.grid, p_lo, p_hi, P.g.dbg);
+    k_grid_reg<W, WS, false><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
+                                                       nullptr, (float *)P.grid, p_lo, p_hi,
+                                                       P.g.dbg);
+}
+
+// The register kernels' view of a sub-sorted coarse plan: 2x2-cell buckets
+// in groups of kGroupFine (the work items carry their bucket offsets).
+static Geo fine_view(const Geo &g) {
+    Geo f = g;
+    f.sub = kTileFine;
+    f.nty = g.ngy / kTileFine;
+    f.ntiles = (g.ngx / kTileFine) * f.nty;
+    f.grp = kGroupFine;
+    return f;
+}
+
+template <int W, bool WS>
+static void launch_grid_fine_items(const Plan &P, const Part &pt, int p_lo, int p_hi,
+                                   hipStream_t st) {
+    const size_t lds = (size_t)(WS ? W : 1) *
+                       TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
+    const auto r = chunk_items(P, pt, p_lo, p_hi);
+    const unsigned n = 16u * (r.second - r.first);
+    if (n == 0) return;
+    k_grid_reg<W, WS, true><<<n, 64, lds, st>>>(fine_view(P.g), P.recs + pt.vbase,
+                                                ItemSrc{nullptr, n, nullptr}, nullptr,
+                                                pt.fitems + 16 * (size_t)r.first, (float *)P.grid,
+                                                p_lo, p_hi, P.g.dbg);
+}
+
+template <int W, bool WS>
+static void launch_degrid_fine_items(const Plan &P, const Part &pt, int p_lo, int p_hi,
+                                     float2 *acc, hipStream_t st) {
+    const size_t lds = (size_t)(WS ? W : 1) *
+                       TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
+    const auto r = chunk_items(P, pt, p_lo, p_hi);
+    const unsigned n = 16u * (r.second - r.first);
+    if (n == 0) return;
+    k_degrid_reg<W, WS, true><<<n, 64, lds, st>>>(fine_view(P.g), P.recs + pt.vbase,
+                                                  ItemSrc{nullptr, n, nullptr}, nullptr,
+                                                  pt.fitems + 16 * (size_t)r.first, P.grid, p_lo,
+                                                  p_hi, acc + pt.vbase);
 }
 
 template <int W>
 static void launch_grid(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
+    if (P.subsort) {
+        if (P.g.do_w) return launch_grid_fine_items<W, true>(P, pt, p_lo, p_hi, st);
+        return launch_grid_fine_items<W, false>(P, pt, p_lo, p_hi, st);
+    }
     if (P.g.sub == kTileFine) {
         if (P.g.do_w) return launch_grid_reg<W, true>(P, pt, p_lo, p_hi, st);
         return launch_grid_reg<W, false>(P, pt, p_lo, p_hi, st);
@@ -1952,16 +2094,21 @@ static void launch_degrid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi,
                               hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) *
                        TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
-    const void *fn = (const void *)k_degrid_reg<W, WS>;
+    const void *fn = (const void *)k_degrid_reg<W, WS, false>;
     const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
     if (L.blocks == 0) return;
-    k_degrid_reg<W, WS><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs, P.grid,
-                                                  p_lo, p_hi, acc + pt.vbase);
+    k_degrid_reg<W, WS, false><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
+                                                         nullptr, P.grid, p_lo, p_hi,
+                                                         acc + pt.vbase);
 }
 
 template <int W>
 static void launch_degrid(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
                           hipStream_t st) {
+    if (P.subsort) {
+        if (P.g.do_w) return launch_degrid_fine_items<W, true>(P, pt, p_lo, p_hi, acc, st);
+        return launch_degrid_fine_items<W, false>(P, pt, p_lo, p_hi, acc, st);
+    }
     if (P.g.sub == kTileFine) {
         if (P.g.do_w) return launch_degrid_reg<W, true>(P, pt, p_lo, p_hi, acc, st);
         return launch_degrid_reg<W, false>(P, pt, p_lo, p_hi, acc, st);
@@ -2087,6 +2234,18 @@ static std::vector<hipEvent_t> bucket_parts(Plan &P, const Inputs &in, bool grid
     return ev;
 }
 
+// Sub-sort of every part's coarse items (synchronous plans: the item counts
+// are on the host)
+static void subsort_parts(Plan &P, hipStream_t st) {
+    for (size_t i = 0; i < P.parts.size(); ++i) {
+        Part &pt = P.parts[i];
+        if (pt.nitems == 0) continue;
+        pt.fitems = scratch<FineItem>("fitems#" + std::to_string(i), (size_t)pt.nitems * 16);
+        k_subsort<<<(unsigned)pt.nitems, 256, 0, st>>>(P.g, pt.items, P.recs + pt.vbase, pt.fitems);
+        SDP_HIP_CHECK(hipGetLastError());
+    }
+}
+
 static void release_events(std::vector<hipEvent_t> &ev) {
     for (auto e : ev) (void)hipEventDestroy(e);
     ev.clear();
@@ -2103,6 +2262,7 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     const Geo &g = P.g;
     const double *tab = phi_table(g.W, g.beta, st);
     std::vector<hipEvent_t> ev = bucket_parts(P, in, true, st);
+    if (P.subsort) subsort_parts(P, st);
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
     float tprep = 0, tgrid = 0, tfft = 0, tscr = 0;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
@@ -2167,6 +2327,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     const double *tab = phi_table(g.W, g.beta, st);
     // the bucketing runs on the aux stream under the screen + FFT
     std::vector<hipEvent_t> ev = bucket_parts(P, in, false, st);
+    if (P.subsort) subsort_parts(P, st);
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
     const int64_t nvis = in.nrow * (int64_t)in.nchan;
     if (!accumulate && nvis > 0) {

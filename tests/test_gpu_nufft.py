@@ -35,14 +35,18 @@ def _problem(seed, nrow=300, nchan=3, umax=2000.0, frac=0.45):
     return uvw, freq, ms, wgt, frac / umax
 
 
-@pytest.fixture(params=["fine", "coarse", "fine-pipelined", "fine-aux"])
+@pytest.fixture(params=["fine", "coarse", "coarse-lds", "fine-pipelined", "fine-aux"])
 def bucket(request, monkeypatch):
-    """Both gridders: 2x2-cell buckets (register gridder, the default at these
-    sizes) and 16x16-cell buckets (LDS-tile gridder used for very large grids);
-    and the pipelined plan (two row parts bucketed on the auxiliary stream,
-    persistent gridding launches) that large calls take."""
-    if request.param == "coarse":
+    """Both bucketings: 2x2-cell buckets (register kernels, the default at
+    these sizes) and 16x16-cell buckets (very large grids), whose items are
+    re-ordered to 2x2 buckets for the register kernels ("coarse") or fed to
+    the LDS-tile kernels ("coarse-lds", SDP_HIP_SUBSORT=0); and the pipelined
+    plan (two row parts bucketed on the auxiliary stream, persistent gridding
+    launches)."""
+    if request.param.startswith("coarse"):
         monkeypatch.setenv("SDP_HIP_BUCKET", "16")
+    if request.param == "coarse-lds":
+        monkeypatch.setenv("SDP_HIP_SUBSORT", "0")
     if request.param == "fine-pipelined":
         monkeypatch.setenv("SDP_HIP_PIPELINE", "2")
     if request.param == "fine-aux":  # bucketing on the auxiliary stream
@@ -62,7 +66,7 @@ def test_ms2dirty_matches_exact(dow, vdt, flip, bucket):
     out, info = kernels.ms2dirty(T(uvw), T(freq), T(ms, vdt), T(wgt), npix, 48 + 16 * dow, cell,
                                  cell * 0.9, 1e-7, dow, flip_uw=flip)
     assert info["support"] == 8
-    assert info["bucket"] == (16 if bucket == "coarse" else 2)
+    assert info["bucket"] == (16 if bucket.startswith("coarse") else 2)
     assert info["grid_launches"] == (2 if bucket == "fine-pipelined" else 1)
     assert rel_rms(out.cpu().numpy(), ex) < TOL
 
