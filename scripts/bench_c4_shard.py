@@ -20,10 +20,14 @@ ap.add_argument("--nchan", type=int, default=32, help="channels of this shard")
 ap.add_argument("--nchan-total", type=int, default=256)
 ap.add_argument("--npix", type=int, default=8192)
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--layout", choices=("interleaved", "block"), default="interleaved",
+                help="channel sharding: every 8th channel, or a contiguous 1/8 of the band")
+ap.add_argument("--rank", type=int, default=0, help="which shard (block layout: 7 = top band)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 world = a.nchan_total // a.nchan
-chans = parallel.interleaved_channels(a.nchan_total, 0, world)
+chans = (parallel.interleaved_channels(a.nchan_total, a.rank, world) if a.layout == "interleaved"
+         else np.arange(a.rank * a.nchan, (a.rank + 1) * a.nchan))
 t0 = time.perf_counter()
 obs = simulation.device_observation(a.ntimes, a.nchan, 50e6, 350e6, config="LOW", device=dev,
                                     nchan_total=a.nchan_total, channels=chans)
@@ -43,8 +47,8 @@ for it in range(a.reps + 1):
         res.append((dt, info))
 dt = float(np.mean([r[0] for r in res]))
 info = res[-1][1]
-print(json.dumps({"config": "C4 shard: SKA-LOW 512 st, %d chan of %d, %d times, %d^2 image"
-                  % (len(chans), a.nchan_total, a.ntimes, a.npix),
+print(json.dumps({"config": "C4 shard: SKA-LOW 512 st, %d chan of %d (%s, rank %d), %d times, %d^2 image"
+                  % (len(chans), a.nchan_total, a.layout, a.rank, a.ntimes, a.npix),
                   "nvis": nvis, "ms": round(dt * 1e3, 2), "Mvis_s_per_gpu": round(nvis / dt / 1e6, 1),
                   "stages_ms": {k: round(info[k], 2) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
                   "nplanes": info["nplanes"], "plane_chunk": info["plane_chunk"],
