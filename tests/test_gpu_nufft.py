@@ -232,6 +232,43 @@ def test_fft_batches_match_single_batch(fft_planes, budget, monkeypatch):
     assert rel_rms(vpart.cpu().numpy(), vfull.cpu().numpy()) < 1e-6
 
 
+@pytest.mark.parametrize("subsort", ["1", "0"])
+def test_large_grid_adjointness(subsort, monkeypatch):
+    """C4-size grid (8192^2 image, 16384^2 grid, 2.15 GB planes) on the
+    16x16-bucket path, with (register kernels) and without (LDS-tile
+    kernels) the 2x2 sub-sort: <A x, y> = <x, A^H y> and ms2dirty of the
+    predicted visibilities of a point source peaks at that source."""
+    from ska_sdp_func_python_amd import kernels
+    monkeypatch.setenv("SDP_HIP_BUCKET", "16")
+    monkeypatch.setenv("SDP_HIP_SUBSORT", subsort)
+    npix = 8192
+    uvw, freq, ms, _, _ = _problem(11, nrow=20000, nchan=4, umax=3.0e5)
+    uvw[:, 2] *= 0.02  # a handful of w planes at this cell size
+    cell = 0.45 / 3.0e5
+    rng = np.random.default_rng(12)
+    img = torch.zeros((npix, npix), dtype=torch.float64, device=dev())
+    ix = rng.integers(npix // 4, 3 * npix // 4, 64)
+    iy = rng.integers(npix // 4, 3 * npix // 4, 64)
+    img[ix, iy] = torch.as_tensor(rng.normal(size=64), device=dev())
+    d, info = kernels.ms2dirty(T(uvw), T(freq), T(ms), None, npix, npix, cell, cell, 1e-7, True)
+    assert info["bucket"] == 16 and info["ngrid_x"] == 2 * npix and info["nplanes"] >= 8
+    v, _ = kernels.dirty2ms(T(uvw), T(freq), img, None, cell, cell, 1e-7, True,
+                            vis_dtype=torch.complex128)
+    lhs = float(torch.sum(d * img))
+    rhs = float(np.real(np.vdot(v.cpu().numpy(), ms)))
+    assert abs(lhs - rhs) / abs(lhs) < 1e-5
+    # a unit point source: predicted vis have |V| = 1 (exact phasors) and
+    # the dirty image of them peaks at the source
+    pt = torch.zeros_like(img)
+    pt[int(ix[0]), int(iy[0])] = 1.0
+    vp, _ = kernels.dirty2ms(T(uvw), T(freq), pt, None, cell, cell, 1e-7, True,
+                             vis_dtype=torch.complex128)
+    assert float(torch.max(torch.abs(torch.abs(vp) - 1.0))) < 1e-5
+    dp, _ = kernels.ms2dirty(T(uvw), T(freq), vp, None, npix, npix, cell, cell, 1e-7, True)
+    k = int(torch.argmax(dp))
+    assert (k // npix, k % npix) == (int(ix[0]), int(iy[0]))
+
+
 def test_full_size_invert_matches_c_restatement():
     """C2 geometry at the full 4096^2 image (8192^2 grid, 9 w planes): the HIP
     invert of 2 of the 64 channels against oracle/wgrid_cpu.c (the C
