@@ -23,6 +23,7 @@ ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--layout", choices=("interleaved", "block"), default="interleaved",
                 help="channel sharding: every 8th channel, or a contiguous 1/8 of the band")
 ap.add_argument("--rank", type=int, default=0, help="which shard (block layout: 7 = top band)")
+ap.add_argument("--predict", action="store_true", help="also time dirty2ms (predict) of the image")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 world = a.nchan_total // a.nchan
@@ -55,3 +56,17 @@ print(json.dumps({"config": "C4 shard: SKA-LOW 512 st, %d chan of %d (%s, rank %
                   "ngrid": info["ngrid_x"], "bucket": info["bucket"], "nitems": info["nitems"],
                   "support": info["support"], "grid_launches": info["grid_launches"],
                   "gpu_mem_peak_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1)}), flush=True)
+if a.predict:
+    pres = []
+    for it in range(a.reps + 1):
+        torch.cuda.synchronize(); t0 = time.perf_counter()
+        v, pinfo = kernels.dirty2ms(obs["uvw"], obs["freq"], img, obs["wgt"], cell, cell, 1e-12, True,
+                                    flip_uw=True)
+        torch.cuda.synchronize(); pdt = time.perf_counter() - t0
+        if it > 0:
+            pres.append(pdt)
+        del v
+    pdt = float(np.mean(pres))
+    print(json.dumps({"predict_ms": round(pdt * 1e3, 2), "predict_Mvis_s_per_gpu": round(nvis / pdt / 1e6, 1),
+                      "stages_ms": {k: round(pinfo[k], 2) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")}}),
+          flush=True)
