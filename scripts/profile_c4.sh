@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 out=gpurun_out/prof_c4
 mkdir -p $out
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- \
-    python3 scripts/bench_c4_shard.py --reps 1 > $out/c4_trace.log 2>&1 || exit $?
+    python3 scripts/bench_c4_shard.py --reps 1 "$@" > $out/c4_trace.log 2>&1 || exit $?
 f=$(find $out/trace -name "run_kernel_stats.csv" | head -1)
 python3 - "$f" <<'PY'
 import csv, sys

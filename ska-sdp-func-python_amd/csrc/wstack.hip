@@ -499,16 +499,18 @@ __global__ void k_items_fill(int64_t ngroups, int grp, int groups_per_plane,
 // -- x pair major, y pair minor, so the 4 buckets of a 2 x 8-cell group are
 // consecutive -- through an LDS copy.  The item's 16 groups become register
 // gridder / degridder work items (FineItem; empty groups have b == e).  One
-// 256-thread workgroup per coarse item of <= kSubChunk records (the plan caps
-// the chunk on this path).
+// workgroup of kSubThreads per coarse item of <= kSubChunk records (the plan
+// caps the chunk on this path); the 128 KiB staging admits one workgroup per
+// CU, so it carries 16 waves.
 constexpr int kSubChunk = 4096;
+constexpr int kSubThreads = 1024;
 
 __device__ __forceinline__ int sub_class(uint32_t ij) {
     const int ic = (int)(ij & 0xffffu), jc = (int)(ij >> 16);
     return ((ic & 15) >> 1) * 8 + ((jc & 15) >> 1);
 }
 
-__global__ __launch_bounds__(256) void k_subsort(Geo g, const Item *__restrict__ items,
+__global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__restrict__ items,
                                                  VisRec *recs, FineItem *__restrict__ fitems) {
     __shared__ VisRec stage[kSubChunk];
     __shared__ unsigned cur[64], first[65];
@@ -516,7 +518,7 @@ __global__ __launch_bounds__(256) void k_subsort(Geo g, const Item *__restrict__
     const int n = (int)(it.e - it.b);
     if (threadIdx.x < 64) cur[threadIdx.x] = 0u;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += 256) {
+    for (int i = threadIdx.x; i < n; i += kSubThreads) {
         const VisRec r = recs[it.b + i];
         stage[i] = r;
         atomicAdd(&cur[sub_class(r.ij)], 1u);
@@ -545,7 +547,7 @@ __global__ __launch_bounds__(256) void k_subsort(Geo g, const Item *__restrict__
         fitems[(size_t)blockIdx.x * 16 + threadIdx.x] = f;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += 256) {
+    for (int i = threadIdx.x; i < n; i += kSubThreads) {
         const VisRec r = stage[i];
         const unsigned pos = atomicAdd(&cur[sub_class(r.ij)], 1u);
         recs[it.b + pos] = r;
@@ -2241,7 +2243,7 @@ static void subsort_parts(Plan &P, hipStream_t st) {
         Part &pt = P.parts[i];
         if (pt.nitems == 0) continue;
         pt.fitems = scratch<FineItem>("fitems#" + std::to_string(i), (size_t)pt.nitems * 16);
-        k_subsort<<<(unsigned)pt.nitems, 256, 0, st>>>(P.g, pt.items, P.recs + pt.vbase, pt.fitems);
+        k_subsort<<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(P.g, pt.items, P.recs + pt.vbase, pt.fitems);
         SDP_HIP_CHECK(hipGetLastError());
     }
 }
