@@ -2,8 +2,10 @@
  * ORACLE / TEST INFRASTRUCTURE ONLY -- never linked by the product path.
  *
  * Plain-C + OpenMP restatement of the w-stacking adjoint NUFFT (ms2dirty)
+ * and of its adjoint, the forward NUFFT (dirty2ms, at the end of this file),
  * that the reference binds through ducc0.wgridder (ducc0 0.27.0,
- * poetry.lock:305-306; call site src/ska_sdp_func_python/imaging/ng.py:240).
+ * poetry.lock:305-306; call sites src/ska_sdp_func_python/imaging/ng.py:240
+ * and ng.py:99).
  * ducc0 is not vendored under /root/reference and cannot be built or
  * installed here, so this is the CPU baseline of bench.py ("kind": "port")
  * and a second checker for the HIP path.  The algorithm is the one stated in
@@ -155,6 +157,33 @@ static void fft_bwd(const fft_plan *p, cf64 *x, cf64 *tmp) {
     }
 }
 
+/* ---------------- w-plane geometry (shared by both directions) ---------- */
+static void w_geometry(const double *uvw, const double *freq, int nchan, int64_t nrow, int npix_x,
+                       int npix_y, double pixsize_x, double pixsize_y, int W, int do_wstacking,
+                       double *s0, double *dw, double *w0, int *nplanes) {
+    double wmin = 1e300, wmax = -1e300;
+    for (int64_t r = 0; r < nrow; ++r)
+        for (int c = 0; c < nchan; ++c) {
+            double w = uvw[3 * r + 2] * freq[c] / C_LIGHT;
+            if (w < wmin) wmin = w;
+            if (w > wmax) wmax = w;
+        }
+    *s0 = 0.0;
+    *dw = 1.0;
+    *w0 = 0.0;
+    *nplanes = 1;
+    if (do_wstacking) {
+        double lmax = (npix_x / 2) * pixsize_x, mmax = (npix_y / 2) * pixsize_y;
+        double r2 = lmax * lmax + mmax * mmax;
+        if (r2 > 1.0) r2 = 1.0;
+        double tmax = 1.0 - sqrt(1.0 - r2);
+        *s0 = 0.5 * tmax;
+        *dw = tmax > 0 ? 1.0 / (2.0 * tmax) : 1.0;
+        *w0 = wmin - (0.5 * W - 0.5) * *dw;
+        *nplanes = (int)floor((wmax - *w0) / *dw - 0.5 * W) + 1 + W;
+    }
+}
+
 /* ---------------- ms2dirty ---------------------------------------------- */
 int wgrid_cpu_ms2dirty(const double *uvw, const double *freq, int nchan, int64_t nrow,
                        const float *vis /* c64 interleaved [nrow][nchan] or NULL */,
@@ -170,26 +199,10 @@ int wgrid_cpu_ms2dirty(const double *uvw, const double *freq, int nchan, int64_t
     const int ngx = 2 * npix_x, ngy = 2 * npix_y;
     const int64_t nvis = nrow * nchan;
 
-    /* visibility coordinates in wavelengths, pre-weighted values */
-    double wmin = 1e300, wmax = -1e300;
-    for (int64_t r = 0; r < nrow; ++r)
-        for (int c = 0; c < nchan; ++c) {
-            double w = uvw[3 * r + 2] * freq[c] / C_LIGHT;
-            if (w < wmin) wmin = w;
-            if (w > wmax) wmax = w;
-        }
-    double s0 = 0.0, dw = 1.0, w0 = 0.0;
-    int nplanes = 1;
-    if (do_wstacking) {
-        double lmax = (npix_x / 2) * pixsize_x, mmax = (npix_y / 2) * pixsize_y;
-        double r2 = lmax * lmax + mmax * mmax;
-        if (r2 > 1.0) r2 = 1.0;
-        double tmax = 1.0 - sqrt(1.0 - r2);
-        s0 = 0.5 * tmax;
-        dw = tmax > 0 ? 1.0 / (2.0 * tmax) : 1.0;
-        w0 = wmin - (0.5 * W - 0.5) * dw;
-        nplanes = (int)floor((wmax - w0) / dw - 0.5 * W) + 1 + W;
-    }
+    double s0, dw, w0;
+    int nplanes;
+    w_geometry(uvw, freq, nchan, nrow, npix_x, npix_y, pixsize_x, pixsize_y, W, do_wstacking, &s0,
+               &dw, &w0, &nplanes);
 
     /* per-vis records bucketed by (strip, tile column) of 32 x 32 cells;
        all w planes stay resident (like the GPU path), so each visibility's
@@ -391,6 +404,201 @@ int wgrid_cpu_ms2dirty(const double *uvw, const double *freq, int nchan, int64_t
     plan_free(&px);
     plan_free(&py);
     if (t_grid) *t_grid = tg;
+    if (t_fft) *t_fft = tf;
+    return 0;
+}
+
+/* ---------------- dirty2ms (the adjoint of ms2dirty) -------------------- */
+static void fft_fwd(const fft_plan *p, cf64 *x, cf64 *tmp) {
+    for (int i = 0; i < p->n; ++i) x[i] = conj(x[i]);
+    fft_bwd(p, x, tmp);
+    for (int i = 0; i < p->n; ++i) x[i] = conj(x[i]);
+}
+
+/* ducc0-convention dirty2ms (predict_ng's call, ng.py:99): every step of
+ * ms2dirty transposed.  The corrected image (1 / Phi in x and y; for
+ * w-stacking also 1 / (Phi_w(dw (n - 1 - s0)) n)) is, per w plane, multiplied
+ * by exp(-2 pi i w_p (n - 1 - s0)), placed on the centred grid and
+ * forward-FFT'd (columns then rows, pruned on input); all planes stay
+ * resident and each visibility interpolates its W^3 taps, times
+ * exp(-2 pi i w s0) and its weight.  vis_out: complex double [nrow][nchan];
+ * zero-weight visibilities are 0. */
+int wgrid_cpu_dirty2ms(const double *uvw, const double *freq, int nchan, int64_t nrow,
+                       const double *dirty /* [npix_x][npix_y] */, const float *wgt,
+                       int npix_x, int npix_y, double pixsize_x, double pixsize_y,
+                       double epsilon, int do_wstacking, double *vis_out, int nthreads,
+                       double *t_degrid, double *t_fft) {
+    if (npix_x % 2 || npix_y % 2) return 1;
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+    gauss_legendre();
+    const int W = kernel_support(epsilon);
+    const double beta = 2.30 * W;
+    phi_table(W, beta);
+    const int ngx = 2 * npix_x, ngy = 2 * npix_y;
+    double s0, dw, w0;
+    int nplanes;
+    w_geometry(uvw, freq, nchan, nrow, npix_x, npix_y, pixsize_x, pixsize_y, W, do_wstacking, &s0,
+               &dw, &w0, &nplanes);
+    const size_t npix = (size_t)npix_x * npix_y;
+
+    /* corrected image and each pixel's n - 1 - s0 */
+    double *img = malloc(sizeof(double) * npix), *nt = malloc(sizeof(double) * npix);
+    double *cx = malloc(sizeof(double) * npix_x), *cy = malloc(sizeof(double) * npix_y);
+    for (int x = 0; x < npix_x; ++x) cx[x] = 1.0 / es_fourier(fabs((double)(x - npix_x / 2)) / ngx, W, beta);
+    for (int y = 0; y < npix_y; ++y) cy[y] = 1.0 / es_fourier(fabs((double)(y - npix_y / 2)) / ngy, W, beta);
+#pragma omp parallel for schedule(static)
+    for (int x = 0; x < npix_x; ++x)
+        for (int y = 0; y < npix_y; ++y) {
+            const size_t k = (size_t)x * npix_y + y;
+            double v = dirty[k] * cx[x] * cy[y];
+            nt[k] = 0.0;
+            if (do_wstacking) {
+                const double l = (x - npix_x / 2) * pixsize_x, m = (y - npix_y / 2) * pixsize_y;
+                const double r2 = l * l + m * m;
+                if (r2 >= 1.0) {
+                    v = 0.0;
+                } else {
+                    const double nm1 = -r2 / (sqrt(1.0 - r2) + 1.0);
+                    nt[k] = -nm1 - s0;
+                    v /= es_fourier(fabs(dw * nt[k]), W, beta) * (nm1 + 1.0);
+                }
+            }
+            img[k] = v;
+        }
+    free(cx);
+    free(cy);
+
+    const size_t plane = (size_t)ngx * ngy;
+    float *grid = malloc(sizeof(float) * 2 * plane * nplanes); /* [plane][x][y] complex */
+    cf64 *colbuf = malloc(sizeof(cf64) * (size_t)ngx * npix_y); /* [ngx][npix_y] */
+    fft_plan px, py;
+    plan_init(&px, ngx);
+    plan_init(&py, ngy);
+    double tf = 0.0;
+    for (int p = 0; p < nplanes; ++p) {
+        const double wp = w0 + p * dw;
+        float *gp = grid + 2 * plane * (size_t)p;
+        double t1 = omp_get_wtime();
+#pragma omp parallel
+        {
+            const int nl = ngx > ngy ? ngx : ngy;
+            cf64 *line = malloc(sizeof(cf64) * nl), *tmp = malloc(sizeof(cf64) * nl);
+#pragma omp for schedule(static)
+            for (int y = 0; y < npix_y; ++y) {
+                const int Y = y - npix_y / 2;
+                memset(line, 0, sizeof(cf64) * ngx);
+                for (int x = 0; x < npix_x; ++x) {
+                    const int X = x - npix_x / 2;
+                    const size_t k = (size_t)x * npix_y + y;
+                    cf64 h = img[k];
+                    if (do_wstacking) h *= cexp(-2.0 * M_PI * I * wp * nt[k]);
+                    if ((X + Y) & 1) h = -h; /* centred-grid storage */
+                    line[(X % ngx + ngx) % ngx] = h;
+                }
+                fft_fwd(&px, line, tmp);
+                for (int i = 0; i < ngx; ++i) colbuf[(size_t)i * npix_y + y] = line[i];
+            }
+#pragma omp for schedule(static)
+            for (int i = 0; i < ngx; ++i) {
+                memset(line, 0, sizeof(cf64) * ngy);
+                for (int y = 0; y < npix_y; ++y) {
+                    const int Y = y - npix_y / 2;
+                    line[(Y % ngy + ngy) % ngy] = colbuf[(size_t)i * npix_y + y];
+                }
+                fft_fwd(&py, line, tmp);
+                float *row = gp + 2 * (size_t)i * ngy;
+                for (int j = 0; j < ngy; ++j) {
+                    row[2 * j] = (float)creal(line[j]);
+                    row[2 * j + 1] = (float)cimag(line[j]);
+                }
+            }
+            free(line);
+            free(tmp);
+        }
+        tf += omp_get_wtime() - t1;
+    }
+    free(colbuf);
+    free(img);
+    free(nt);
+
+    /* degrid: rows in parallel, a row's channels in order (neighbouring uv) */
+    const float fbeta = (float)beta, fihw = 2.0f / W;
+    const double tg0 = omp_get_wtime();
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t r = 0; r < nrow; ++r)
+        for (int c = 0; c < nchan; ++c) {
+            const int64_t k = r * nchan + c;
+            const float wt = wgt ? wgt[k] : 1.0f;
+            vis_out[2 * k] = vis_out[2 * k + 1] = 0.0;
+            if (wt == 0.0f) continue;
+            const double s = freq[c] / C_LIGHT;
+            const double a = uvw[3 * r] * s * pixsize_x * ngx;
+            const double b = uvw[3 * r + 1] * s * pixsize_y * ngy;
+            const double w = uvw[3 * r + 2] * s;
+            const double fa = floor(a - 0.5 * W), fb = floor(b - 0.5 * W);
+            const int ic = (((int)fa + 1 + ngx / 2) % ngx + ngx) % ngx;
+            const int jc = (((int)fb + 1 + ngy / 2) % ngy + ngy) % ngy;
+            const float fu = (float)(fa + 1.0 - a), fv = (float)(fb + 1.0 - b);
+            int p0 = 0;
+            float fw = 0.0f;
+            if (do_wstacking) {
+                const double pw = (w - w0) / dw, fp = floor(pw - 0.5 * W);
+                p0 = (int)fp + 1;
+                fw = (float)(fp + 1.0 - pw);
+            }
+            float ku[8], kv[8], kw[8];
+            for (int t = 0; t < W; ++t) {
+                float x = (fu + t) * fihw, y = 1.0f - x * x;
+                ku[t] = y > 0.0f ? expf(fbeta * (sqrtf(y) - 1.0f)) : 0.0f;
+                x = (fv + t) * fihw;
+                y = 1.0f - x * x;
+                kv[t] = y > 0.0f ? expf(fbeta * (sqrtf(y) - 1.0f)) : 0.0f;
+                x = (fw + t) * fihw;
+                y = 1.0f - x * x;
+                kw[t] = do_wstacking ? (y > 0.0f ? expf(fbeta * (sqrtf(y) - 1.0f)) : 0.0f)
+                                     : (t == 0 ? 1.0f : 0.0f);
+            }
+            const int nq = do_wstacking ? W : 1;
+            const int fast = jc + W <= ngy;
+            double sr = 0.0, si = 0.0;
+            for (int q = 0; q < nq; ++q) {
+                const float *pl = grid + 2 * plane * (size_t)(p0 + q);
+                float qr = 0.0f, qi = 0.0f;
+                for (int t = 0; t < W; ++t) {
+                    int gi = ic + t;
+                    if (gi >= ngx) gi -= ngx;
+                    const float *row = pl + 2 * (size_t)gi * ngy;
+                    float rr = 0.0f, ri = 0.0f;
+                    if (fast) {
+                        const float *src = row + 2 * jc;
+                        for (int tt = 0; tt < W; ++tt) {
+                            rr += kv[tt] * src[2 * tt];
+                            ri += kv[tt] * src[2 * tt + 1];
+                        }
+                    } else {
+                        for (int tt = 0; tt < W; ++tt) {
+                            int gj = jc + tt;
+                            if (gj >= ngy) gj -= ngy;
+                            rr += kv[tt] * row[2 * gj];
+                            ri += kv[tt] * row[2 * gj + 1];
+                        }
+                    }
+                    qr += ku[t] * rr;
+                    qi += ku[t] * ri;
+                }
+                sr += kw[q] * qr;
+                si += kw[q] * qi;
+            }
+            cf64 v = (sr + I * si) * (double)wt;
+            if (do_wstacking) v *= cexp(-2.0 * M_PI * I * w * s0);
+            vis_out[2 * k] = creal(v);
+            vis_out[2 * k + 1] = cimag(v);
+        }
+    const double tg = omp_get_wtime() - tg0;
+    free(grid);
+    plan_free(&px);
+    plan_free(&py);
+    if (t_degrid) *t_degrid = tg;
     if (t_fft) *t_fft = tf;
     return 0;
 }

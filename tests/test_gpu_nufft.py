@@ -297,6 +297,32 @@ def test_full_size_invert_matches_c_restatement():
     assert rel_rms(out.cpu().numpy(), ref) < 5e-6
 
 
+
+def test_full_size_predict_matches_c_restatement():
+    """The predict counterpart of the test above: HIP dirty2ms of a random
+    4096^2 image at 2 of the C2 channels against oracle/wgrid_cpu.c's dirty2ms
+    (pinned to exact sums and to the C1 fixture on the CPU)."""
+    import math
+    import wgrid_cpu
+    from ska_sdp_func_python_amd import kernels, simulation
+    fn, n_def, lat, dec = simulation.CONFIGS["MID"]
+    ha = np.linspace(-0.5, 0.5, 100) * 8.0 * math.pi / 12.0
+    uvw, _ = simulation.observe(fn(n_def, seed=1), math.radians(lat), math.radians(dec), ha)
+    uvw = uvw.reshape(-1, 3)
+    allf = np.linspace(0.95e9, 1.76e9, 64)
+    umax = float(np.max(np.abs(uvw[:, :2]))) * allf.max() / orc.C_LIGHT
+    freq = allf[[0, 63]]
+    rng = np.random.default_rng(18)
+    img = rng.normal(size=(4096, 4096))
+    wgt = rng.uniform(0.5, 1.5, (uvw.shape[0], 2)).astype(np.float32)
+    cell = 0.25 / umax
+    ref, _, _ = wgrid_cpu.dirty2ms(uvw * FLIP_UW, freq, img, wgt, cell, cell, 1e-12, True,
+                                   nthreads=16)
+    v, info = kernels.dirty2ms(T(uvw), T(freq), T(img), T(wgt), cell, cell, 1e-12, True,
+                               flip_uw=True)
+    assert info["nplanes"] >= 8 and info["ngrid_x"] == 8192
+    assert rel_rms(v.cpu().numpy(), ref) < 5e-6
+
 def _prologue_reference(vis, im, dopsf):
     """numpy restatement of invert_ng's visibility prologue (reference
     imaging/ng.py:191-204, :231-233): flagged vis -> image pol frame, flagged
