@@ -28,12 +28,17 @@ namespace stefcal {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxAnts = 1024;
-constexpr int kUnroll = 8;  // baseline batches in flight per wave (k_iter, k_residual)
+constexpr int kUnroll = 8;  // baseline batches in flight per wave (k_residual)
+#ifndef SDP_STEFCAL_STEPS
+#define SDP_STEFCAL_STEPS 8
+#endif
+constexpr int kStepsInFlight = SDP_STEFCAL_STEPS;  // 64-baseline steps in flight per wave (k_iter)
 
 enum Mode { kScalar = 0, kMatrix = 1, kNoCross = 2 };
 
 struct Dims {
     int nsolve, nants, nbl, nchan, npol, ncomp, nrec, mode;
+    size_t nd;  // dense entries per sub-solve (dense_size)
     int phase_only, refant;
     double tol, damping;
 };
@@ -66,14 +71,15 @@ __global__ void k_rowmax(Dims d, const double *__restrict__ wb, unsigned long lo
     if ((threadIdx.x & 63) == 0 && m > 0.0) atomicMax(&rowmax[s], dbits(m));
 }
 
-// x = xb / wb, w = wb / max  (masked where wb <= 0), into [s][chan][comp][bl]:
+// x = xb / wb, w = wb / max  (masked where wb <= 0), into [s][chan][comp][dense]:
 // an LDS-tiled transpose of each solve's [bl][chan*pol] block (coalesced
 // reads along chan*pol, coalesced writes along bl)
 constexpr int kTr = 32;
 __global__ __launch_bounds__(256) void k_fill(Dims d, const double2 *__restrict__ xb,
                                               const double *__restrict__ wb,
                                               const unsigned long long *__restrict__ rowmax,
-                                              float2 *x, float *w) {
+                                              const int32_t *__restrict__ dpos, float2 *x,
+                                              float *w) {
     __shared__ float2 sx[kTr][kTr + 1];
     __shared__ float sw[kTr][kTr + 1];
     const int s = blockIdx.z;
@@ -103,8 +109,9 @@ __global__ __launch_bounds__(256) void k_fill(Dims d, const double2 *__restrict_
     __syncthreads();
     for (int r = threadIdx.y; r < kTr; r += 8) {
         const int c = c0 + r, b = b0 + threadIdx.x;
-        if (b < d.nbl && c < ncc) {
-            const size_t dst = ((size_t)s * ncc + c) * d.nbl + b;
+        const int dp = b < d.nbl ? dpos[b] : -1;
+        if (dp >= 0 && c < ncc) {
+            const size_t dst = ((size_t)s * ncc + c) * d.nd + dp;
             x[dst] = sx[threadIdx.x][r];
             w[dst] = sw[threadIdx.x][r];
         }
@@ -134,124 +141,179 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
-__global__ __launch_bounds__(kThreads) void k_iter(Dims d, const int32_t *__restrict__ row_start,
-                                                   const int32_t *__restrict__ ant2,
-                                                   const float2 *__restrict__ x,
+// Dense column-block layout of a sub-solve's canonical baselines (a1 < a2):
+// block c holds antennas a2 in [64c, 64c + 64) against rows a1 in
+// [0, rows(c)), rows(c) = min(64c + 63, na - 1), row-major with 64 entries
+// per row (entry = a2 - 64c).  Entries with no baseline (a1 >= a2 inside the
+// diagonal block, flagged or absent baselines) carry weight 0.  About 12 %
+// padding at 512 stations buys a layout in which lane = a2 for a whole block:
+// the a2-side sums stay in registers and every row is one coalesced 768-B
+// read.
+__host__ __device__ __forceinline__ int dense_rows(int c, int na) {
+    return min(64 * c + 63, na - 1);
+}
+__host__ __device__ __forceinline__ size_t dense_off(int c, int na) {
+    size_t o = 0;
+    for (int k = 0; k < c; ++k) o += (size_t)dense_rows(k, na) * 64;
+    return o;
+}
+__host__ __device__ __forceinline__ size_t dense_size(int na) {
+    return dense_off((na + 63) / 64, na);
+}
+
+// canonical baseline b -> its dense entry
+__global__ void k_dense_pos(int na, int nbl, const int32_t *__restrict__ row_start,
+                            const int32_t *__restrict__ ant2, int32_t *dpos) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nbl) return;
+    int lo = 0, hi = na;  // largest a1 with row_start[a1] <= b
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (row_start[mid] <= b) lo = mid;
+        else hi = mid;
+    }
+    const int a1 = lo, a2 = ant2[b], c = a2 >> 6;
+    // not canonical (a2 <= a1) or out of range: dropped
+    dpos[b] = (a2 > a1 && a2 < na) ? (int32_t)(dense_off(c, na) + (size_t)a1 * 64 + (a2 & 63)) : -1;
+}
+
+// One 256-thread workgroup per sub-solve.  Wave w takes column blocks in
+// snake order (w, 2W-1-w, 2W+w, ...) so the triangle's block sizes balance.
+// Lane = a2: per row a1 of the block the lane adds g1 conj(x) w and |g1|^2 w
+// to its register sums (antenna a2's side) and forms g2 x w, |g2|^2 w for
+// antenna a1's side; those are summed over the 64 lanes for 8 rows at a time
+// by one reduce-scatter butterfly and added to the shared LDS sums with
+// ds_add_f64 (one per row and block; the register sums once per block).
+// Rows are loaded 8 ahead of use.
+constexpr int kRowsInFlight = 8;
+__global__ __launch_bounds__(kThreads) void k_iter(Dims d, const float2 *__restrict__ x,
                                                    const float *__restrict__ w,
                                                    const double2 *__restrict__ g, double2 *gnext,
                                                    double *gwnext, const int32_t *__restrict__ done,
                                                    unsigned long long *change) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int sub = blockIdx.x;
-    const int comp = sub % d.ncomp;
-    const int chan = (sub / d.ncomp) % d.nchan;
     const int s = sub / (d.ncomp * d.nchan);
     if (done[s]) return;
     const int na = d.nants;
-    double2 *gl = reinterpret_cast<double2 *>(lds);  // [na]
-    double2 *top = gl + na;                          // [kWaves][na]
-    double *bot = reinterpret_cast<double *>(top + (size_t)kWaves * na);  // [kWaves][na]
-    int *rs = reinterpret_cast<int *>(bot + (size_t)kWaves * na);          // [na + 1]
+    double2 *gl = reinterpret_cast<double2 *>(lds);      // [na]
+    double2 *top = gl + na;                              // [na]
+    double *bot = reinterpret_cast<double *>(top + na);  // [na]
     const size_t gbase = (size_t)sub * na;
-    const size_t xbase = (size_t)sub * d.nbl;
+    const size_t xbase = (size_t)sub * d.nd;
     for (int a = threadIdx.x; a < na; a += kThreads) {
         gl[a] = g[gbase + a];
-        for (int k = 0; k < kWaves; ++k) {
-            top[k * na + a] = make_double2(0.0, 0.0);
-            bot[k * na + a] = 0.0;
-        }
+        top[a] = make_double2(0.0, 0.0);
+        bot[a] = 0.0;
     }
-    // the CSR row offsets: staged once (each row's bounds were a dependent
-    // global load per antenna row)
-    for (int a = threadIdx.x; a <= na; a += kThreads) rs[a] = row_start[a];
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    double2 *tw = top + (size_t)wave * na;
-    double *bw = bot + (size_t)wave * na;
-    // Each wave walks antenna rows a1 = wave, wave + kWaves, ...  The next
-    // row's baselines (up to 64 * kUnroll per pass) are loaded into registers
-    // while the current row is accumulated and reduced, so a row's global
-    // load latency is hidden behind the previous row's work.
-    struct RowBuf {
-        int a2[kUnroll];
-        float2 xv[kUnroll];
-        float wv[kUnroll];
-    };
-    auto load_row = [&](int a1, int bstart, RowBuf &rb) {
-        const int b1 = a1 < na ? rs[a1 + 1] : 0;
+    constexpr int K = kRowsInFlight;
+    static_assert(K == 8, "the reduce-scatter below sums 8 rows");
+    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+    const int nblk = (na + 63) / 64;
+    for (int k = 0; k * kWaves < nblk; ++k) {
+        const int c = (k & 1) ? (k + 1) * kWaves - 1 - wave : k * kWaves + wave;
+        if (c >= nblk) continue;
+        const int a2 = 64 * c + lane;
+        const double2 g2 = a2 < na ? gl[a2] : make_double2(0.0, 0.0);
+        const double p2 = g2.x * g2.x + g2.y * g2.y;
+        double ax = 0.0, ay = 0.0, ab = 0.0;
+        const int rows = dense_rows(c, na);
+        const float2 *xr_ = x + xbase + dense_off(c, na) + lane;
+        const float *wr_ = w + xbase + dense_off(c, na) + lane;
+        if (rows <= 0) continue;
+        // rows past the block end read the last row (a valid address, no
+        // branch around the load) and are masked to weight 0
+        auto load = [&](int r0, float2 (&bx)[K], float (&bw)[K]) {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const int b = bstart + lane + 64 * u;
-            const bool ok = a1 < na && b < b1;
-            rb.a2[u] = ok ? ant2[b] : 0;
-            rb.xv[u] = ok ? x[xbase + b] : make_float2(0.0f, 0.0f);
-            rb.wv[u] = ok ? w[xbase + b] : 0.0f;
-        }
-    };
-    RowBuf cur;
-    load_row(wave, wave < na ? rs[wave] : 0, cur);
-    for (int a1 = wave; a1 < na; a1 += kWaves) {
-        const double2 g1 = gl[a1];
-        const double p1 = g1.x * g1.x + g1.y * g1.y;
-        double tr = 0.0, ti = 0.0, bs = 0.0;
-        const int bb = rs[a1], b1 = rs[a1 + 1];
-        for (int b0 = bb; b0 < b1; b0 += 64 * kUnroll) {
-            RowBuf nxt;
-            // prefetch: the rest of this row, else the next row of this wave
-            if (b0 + 64 * kUnroll < b1) load_row(a1, b0 + 64 * kUnroll, nxt);
-            else {
-                const int an = a1 + kWaves;
-                load_row(an, an < na ? rs[an] : 0, nxt);
+            for (int u = 0; u < K; ++u) {
+                const int r = min(r0 + u, rows - 1);
+                const float wl = wr_[(size_t)r * 64];
+                bx[u] = xr_[(size_t)r * 64];
+                bw[u] = r0 + u < rows ? wl : 0.0f;
             }
+        };
+        auto process = [&](int r0, const float2 (&bx)[K], const float (&bw)[K]) {
+            double pr[K], pi[K], pb[K];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                if (b0 + lane + 64 * u >= b1) break;
-                const int a2 = cur.a2[u];
-                const float2 xv = cur.xv[u];
-                const double wv = cur.wv[u];
-                const double2 g2 = gl[a2];
+            for (int u = 0; u < K; ++u) {
+                const double2 g1 = gl[min(r0 + u, na - 1)];
+                const double wv = bw[u];
+                const float2 xv = wv != 0.0 ? bx[u] : make_float2(0.0f, 0.0f);
+                const double xr = xv.x * wv, xi = xv.y * wv;
                 // antenna a2 (i = a1): x[a1,a2] = conj(x_b)
-                const double2 c1 = cmul(g1, make_double2(xv.x * wv, -xv.y * wv));
-                double2 t = tw[a2];
-                t.x += c1.x;
-                t.y += c1.y;
-                tw[a2] = t;
-                bw[a2] += p1 * wv;
+                ax += g1.x * xr + g1.y * xi;
+                ay += g1.y * xr - g1.x * xi;
+                ab += (g1.x * g1.x + g1.y * g1.y) * wv;
                 // antenna a1 (i = a2): x[a2,a1] = x_b
-                const double2 c2 = cmul(g2, make_double2(xv.x * wv, xv.y * wv));
-                tr += c2.x;
-                ti += c2.y;
-                bs += (g2.x * g2.x + g2.y * g2.y) * wv;
+                pr[u] = g2.x * xr - g2.y * xi;
+                pi[u] = g2.x * xi + g2.y * xr;
+                pb[u] = p2 * wv;
             }
-            cur = nxt;
+            // reduce-scatter over the 64 lanes: after the xor-32/16/8 halvings
+            // lane l holds row (l >> 3) & 7 summed over 8 lanes; xor 4/2/1
+            // finish it
+            double q4r[4], q4i[4], q4b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                q4r[i] = (b5 ? pr[i + 4] : pr[i]) + __shfl_xor(b5 ? pr[i] : pr[i + 4], 32);
+                q4i[i] = (b5 ? pi[i + 4] : pi[i]) + __shfl_xor(b5 ? pi[i] : pi[i + 4], 32);
+                q4b[i] = (b5 ? pb[i + 4] : pb[i]) + __shfl_xor(b5 ? pb[i] : pb[i + 4], 32);
+            }
+            double q2r[2], q2i[2], q2b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                q2r[i] = (b4 ? q4r[i + 2] : q4r[i]) + __shfl_xor(b4 ? q4r[i] : q4r[i + 2], 16);
+                q2i[i] = (b4 ? q4i[i + 2] : q4i[i]) + __shfl_xor(b4 ? q4i[i] : q4i[i + 2], 16);
+                q2b[i] = (b4 ? q4b[i + 2] : q4b[i]) + __shfl_xor(b4 ? q4b[i] : q4b[i + 2], 16);
+            }
+            double tr = (b3 ? q2r[1] : q2r[0]) + __shfl_xor(b3 ? q2r[0] : q2r[1], 8);
+            double ti = (b3 ? q2i[1] : q2i[0]) + __shfl_xor(b3 ? q2i[0] : q2i[1], 8);
+            double tb = (b3 ? q2b[1] : q2b[0]) + __shfl_xor(b3 ? q2b[0] : q2b[1], 8);
+#pragma unroll
+            for (int m = 4; m > 0; m >>= 1) {
+                tr += __shfl_xor(tr, m);
+                ti += __shfl_xor(ti, m);
+                tb += __shfl_xor(tb, m);
+            }
+            // row of lane l: bit 5 -> +4, bit 4 -> +2, bit 3 -> +1
+            const int a1 = r0 + ((lane >> 3) & 7);
+            if ((lane & 7) == 0 && a1 < rows && tb != 0.0) {
+                atomicAdd(&top[a1].x, tr);
+                atomicAdd(&top[a1].y, ti);
+                atomicAdd(&bot[a1], tb);
+            }
+        };
+        // two register buffers in ping-pong (a copy between them would wait
+        // for the prefetch it is meant to overlap)
+        float2 xa[K], xb_[K];
+        float wa[K], wb_[K];
+        // (sched_barrier: keep each prefetch issued ahead of the other
+        // buffer's arithmetic instead of sunk below it)
+        load(0, xa, wa);
+        for (int r0 = 0; r0 < rows; r0 += 2 * K) {
+            load(r0 + K, xb_, wb_);
+            __builtin_amdgcn_sched_barrier(0);
+            process(r0, xa, wa);
+            load(r0 + 2 * K, xa, wa);
+            __builtin_amdgcn_sched_barrier(0);
+            if (r0 + K < rows) process(r0 + K, xb_, wb_);
         }
-        if (bb >= b1) {  // empty row: the prefetched buffer holds the next row
-            const int an = a1 + kWaves;
-            load_row(an, an < na ? rs[an] : 0, cur);
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            tr += __shfl_xor(tr, o);
-            ti += __shfl_xor(ti, o);
-            bs += __shfl_xor(bs, o);
-        }
-        if (lane == 0) {
-            double2 t = tw[a1];
-            t.x += tr;
-            t.y += ti;
-            tw[a1] = t;
-            bw[a1] += bs;
+        if (a2 < na && ab != 0.0) {
+            atomicAdd(&top[a2].x, ax);
+            atomicAdd(&top[a2].y, ay);
+            atomicAdd(&bot[a2], ab);
         }
     }
     __syncthreads();
     // substitution (solvers.py:308-319 / :466-477), new gains into top[0]
     for (int a = threadIdx.x; a < na; a += kThreads) {
         double tx = 0.0, ty = 0.0, bb = 0.0;
-        for (int k = 0; k < kWaves; ++k) {
-            tx += top[k * na + a].x;
-            ty += top[k * na + a].y;
-            bb += bot[k * na + a];
-        }
+        tx = top[a].x;
+        ty = top[a].y;
+        bb = bot[a];
         double2 ng = bb > 0.0 ? make_double2(tx / bb, ty / bb) : make_double2(0.0, 0.0);
         if (d.phase_only) {
             const double m = sqrt(ng.x * ng.x + ng.y * ng.y);
@@ -349,9 +411,7 @@ __global__ void k_finish(Dims d, int niter, double2 *g, const int32_t *__restric
 }
 
 // residual (solvers.py:481-539): sqrt(sum w |x - g_a1 conj(g_a2)|^2 / sum w)
-__global__ __launch_bounds__(kThreads) void k_residual(Dims d, const int32_t *__restrict__ row_start,
-                                                       const int32_t *__restrict__ ant2,
-                                                       const float2 *__restrict__ x,
+__global__ __launch_bounds__(kThreads) void k_residual(Dims d, const float2 *__restrict__ x,
                                                        const float *__restrict__ w,
                                                        const double2 *__restrict__ g,
                                                        double *residual) {
@@ -359,16 +419,21 @@ __global__ __launch_bounds__(kThreads) void k_residual(Dims d, const int32_t *__
     const int sub = blockIdx.x;
     const int na = d.nants;
     const size_t gbase = (size_t)sub * na;
-    const size_t xbase = (size_t)sub * d.nbl;
+    const size_t xbase = (size_t)sub * d.nd;
     double r = 0.0, sw = 0.0;
-    for (int a1 = threadIdx.x >> 6; a1 < na; a1 += kWaves) {
-        const double2 g1 = g[gbase + a1];
-        for (int b = row_start[a1] + (threadIdx.x & 63); b < row_start[a1 + 1]; b += 64) {
-            const double2 g2 = g[gbase + ant2[b]];
-            const double mr = g1.x * g2.x + g1.y * g2.y;   // g1 conj(g2)
+    const int nblk = (na + 63) / 64;
+    for (int c = 0; c < nblk; ++c) {
+        const int a2 = 64 * c + (threadIdx.x & 63);
+        if (a2 >= na) continue;
+        const double2 g2 = g[gbase + a2];
+        const size_t off = xbase + dense_off(c, na) + (threadIdx.x & 63);
+        for (int a1 = threadIdx.x >> 6; a1 < dense_rows(c, na); a1 += kWaves) {
+            const double wv = w[off + (size_t)a1 * 64];
+            if (wv == 0.0) continue;
+            const double2 g1 = g[gbase + a1];
+            const double mr = g1.x * g2.x + g1.y * g2.y;  // g1 conj(g2)
             const double mi = g1.y * g2.x - g1.x * g2.y;
-            const float2 xv = x[xbase + b];
-            const double wv = w[xbase + b];
+            const float2 xv = x[off + (size_t)a1 * 64];
             const double er = xv.x - mr, ei = xv.y - mi;
             r += wv * (er * er + ei * ei);
             sw += wv;
@@ -419,7 +484,7 @@ static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, 
                   const double *wb, void *gain, double *gwt, double *residual,
                   int32_t *niter_out, int niter, hipStream_t st) {
     const size_t nsub = (size_t)d.nsolve * d.nchan * d.ncomp;
-    const size_t nx = nsub * d.nbl;
+    const size_t nx = nsub * d.nd;
     const size_t ng = nsub * d.nants;
     float2 *x = scratch<float2>("sc_x", std::max<size_t>(nx, 1));
     float *w = scratch<float>("sc_w", std::max<size_t>(nx, 1));
@@ -431,6 +496,10 @@ static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, 
     auto *change = scratch<unsigned long long>("sc_change", 2 * (size_t)d.nsolve);
     int32_t *done = scratch<int32_t>("sc_done", d.nsolve);
     int *ndone = scratch<int>("sc_ndone", 1);
+    int32_t *dpos = scratch<int32_t>("sc_dpos", std::max(d.nbl, 1));
+    SDP_HIP_CHECK(hipMemsetAsync(w, 0, nx * sizeof(float), st));  // padding entries: weight 0
+    if (d.nbl > 0)
+        k_dense_pos<<<(d.nbl + 255) / 256, 256, 0, st>>>(d.nants, d.nbl, row_start, ant2, dpos);
     SDP_HIP_CHECK(hipMemsetAsync(rowmax, 0, d.nsolve * sizeof(unsigned long long), st));
     SDP_HIP_CHECK(hipMemsetAsync(change, 0, 2 * (size_t)d.nsolve * sizeof(unsigned long long), st));
     SDP_HIP_CHECK(hipMemsetAsync(done, 0, d.nsolve * sizeof(int32_t), st));
@@ -443,14 +512,14 @@ static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, 
     {
         const dim3 grd((unsigned)((d.nbl + kTr - 1) / kTr),
                        (unsigned)((d.nchan * d.ncomp + kTr - 1) / kTr), (unsigned)d.nsolve);
-        k_fill<<<grd, dim3(kTr, 8), 0, st>>>(d, static_cast<const double2 *>(xb), wb, rowmax, x, w);
+        k_fill<<<grd, dim3(kTr, 8), 0, st>>>(d, static_cast<const double2 *>(xb), wb, rowmax,
+                                             dpos, x, w);
     }
     k_load_gains<<<blocks_for(ng), 256, 0, st>>>(d, static_cast<const double2 *>(gain), gwt, g,
                                                   gw);
     SDP_HIP_CHECK(hipGetLastError());
 
-    const size_t lds = (size_t)d.nants * (sizeof(double2) * (1 + kWaves) + sizeof(double) * kWaves) +
-                       (size_t)(d.nants + 1) * sizeof(int);
+    const size_t lds = (size_t)d.nants * (2 * sizeof(double2) + sizeof(double));
     if (lds > 65536)
         SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_iter,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -458,8 +527,7 @@ static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, 
     for (; it < niter; ++it) {
         unsigned long long *cur = change + (size_t)(it & 1) * d.nsolve;
         unsigned long long *nxt = change + (size_t)((it + 1) & 1) * d.nsolve;
-        k_iter<<<(unsigned)nsub, kThreads, lds, st>>>(d, row_start, ant2, x, w, g, gn, gwn, done,
-                                                     cur);
+        k_iter<<<(unsigned)nsub, kThreads, lds, st>>>(d, x, w, g, gn, gwn, done, cur);
         k_commit<<<blocks_for(ng), 256, 0, st>>>(d, it, g, gw, gn, gwn, done, cur, nxt, ndone);
         k_mark_done<<<(d.nsolve + 255) / 256, 256, 0, st>>>(d, it, done, cur, ndone);
         SDP_HIP_CHECK(hipGetLastError());
@@ -471,7 +539,7 @@ static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, 
         }
     }
     k_finish<<<blocks_for(ng), 256, 0, st>>>(d, niter, g, done, niter_out);
-    k_residual<<<(unsigned)nsub, kThreads, 0, st>>>(d, row_start, ant2, x, w, g, residual);
+    k_residual<<<(unsigned)nsub, kThreads, 0, st>>>(d, x, w, g, residual);
     k_store<<<blocks_for(ng), 256, 0, st>>>(d, g, gw, static_cast<double2 *>(gain), gwt);
     SDP_HIP_CHECK(hipGetLastError());
 }
@@ -502,6 +570,7 @@ extern "C" int sdp_hip_solve_gains(int nsolve, int nants, int nbl, const int32_t
         d.nsolve = nsolve;
         d.nants = nants;
         d.nbl = nbl;
+        d.nd = stefcal::dense_size(nants);
         d.nchan = nchan;
         d.npol = npol;
         d.mode = mode;
