@@ -9,14 +9,15 @@
 // change = max|g - g_last| over antennas AND channels (solvers.py:268, :427).
 //
 // Device layout (fp32 storage, fp64 arithmetic):
-//   x, w   [solve][chan][comp][baseline]  normalised point-source vis/weight
+//   x, w   [solve][chan][comp][dense]  normalised point-source vis/weight in
+//          the dense column-block baseline layout (dense_off below)
 //   g, gw  [solve][chan][comp][antenna]   current gains / gain weights
 // Per iteration two launches: k_iter (one 256-thread workgroup per active
-// sub-problem: baselines streamed once, per-wave partial sums in LDS -- plain
-// read-modify-write, no LDS float atomics -- then the substitution, phase
-// normalisation, refant rotation, damping and the per-row max change) and
-// k_commit (row-level convergence).  The host polls the converged-row count
-// every few iterations.
+// sub-problem: baselines streamed once with lane = station a2, register sums
+// for a2 and lane-reduced sums for a1 added to LDS with ds_add_f64, then the
+// substitution, phase normalisation, refant rotation, damping and the
+// per-row max change) and k_commit (row-level convergence).  The host polls
+// the converged-row count every few iterations.
 #include <cmath>
 #include <vector>
 
@@ -28,11 +29,6 @@ namespace stefcal {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxAnts = 1024;
-constexpr int kUnroll = 8;  // baseline batches in flight per wave (k_residual)
-#ifndef SDP_STEFCAL_STEPS
-#define SDP_STEFCAL_STEPS 8
-#endif
-constexpr int kStepsInFlight = SDP_STEFCAL_STEPS;  // 64-baseline steps in flight per wave (k_iter)
 
 enum Mode { kScalar = 0, kMatrix = 1, kNoCross = 2 };
 
@@ -137,6 +133,34 @@ __global__ void k_load_gains(Dims d, const double2 *__restrict__ gin,
     }
 }
 
+#ifndef SDP_STEFCAL_PERMLANE
+#define SDP_STEFCAL_PERMLANE 1
+#endif
+// a + b after exchanging the upper half of `a` with the lower half of `b`
+// (H = 32: wave halves, v_permlane32_swap; H = 16: odd / even 16-lane rows,
+// v_permlane16_swap): lanes with bit H clear get a[l] + a[l ^ H], lanes with
+// it set b[l] + b[l ^ H]
+template <int H>
+__device__ __forceinline__ double swap_sum(double a, double b) {
+    const unsigned alo = (unsigned)__double_as_longlong(a),
+                   ahi = (unsigned)((unsigned long long)__double_as_longlong(a) >> 32);
+    const unsigned blo = (unsigned)__double_as_longlong(b),
+                   bhi = (unsigned)((unsigned long long)__double_as_longlong(b) >> 32);
+    unsigned r0a, r0b, r1a, r1b;
+    if constexpr (H == 32) {
+        const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+        r0a = lo[0]; r0b = lo[1]; r1a = hi[0]; r1b = hi[1];
+    } else {
+        const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+        r0a = lo[0]; r0b = lo[1]; r1a = hi[0]; r1b = hi[1];
+    }
+    const double na = __longlong_as_double((long long)(((unsigned long long)r1a << 32) | r0a));
+    const double nb = __longlong_as_double((long long)(((unsigned long long)r1b << 32) | r0b));
+    return na + nb;
+}
+
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -198,17 +222,20 @@ __global__ __launch_bounds__(kThreads) void k_iter(Dims d, const float2 *__restr
     const int na = d.nants;
     double2 *gl = reinterpret_cast<double2 *>(lds);      // [na]
     double2 *top = gl + na;                              // [na]
+    double *gp = reinterpret_cast<double *>(top + na) + na;  // [na] |g|^2 (after bot)
     double *bot = reinterpret_cast<double *>(top + na);  // [na]
     const size_t gbase = (size_t)sub * na;
     const size_t xbase = (size_t)sub * d.nd;
     for (int a = threadIdx.x; a < na; a += kThreads) {
-        gl[a] = g[gbase + a];
+        const double2 ga = g[gbase + a];
+        gl[a] = ga;
+        gp[a] = ga.x * ga.x + ga.y * ga.y;
         top[a] = make_double2(0.0, 0.0);
         bot[a] = 0.0;
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: SGPR block math
     constexpr int K = kRowsInFlight;
     static_assert(K == 8, "the reduce-scatter below sums 8 rows");
     const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
@@ -221,17 +248,23 @@ __global__ __launch_bounds__(kThreads) void k_iter(Dims d, const float2 *__restr
         const double p2 = g2.x * g2.x + g2.y * g2.y;
         double ax = 0.0, ay = 0.0, ab = 0.0;
         const int rows = dense_rows(c, na);
-        const float2 *xr_ = x + xbase + dense_off(c, na) + lane;
-        const float *wr_ = w + xbase + dense_off(c, na) + lane;
-        if (rows <= 0) continue;
-        // rows past the block end read the last row (a valid address, no
-        // branch around the load) and are masked to weight 0
+        // buffer loads: the block base in the descriptor, the row offset in
+        // an SGPR, the lane offset a constant VGPR (no per-load 64-bit
+        // address arithmetic); rows past the block end read the last row and
+        // are masked to weight 0
+        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(x + xbase + dense_off(c, na)), 0, rows * 64 * (int)sizeof(float2), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(w + xbase + dense_off(c, na)), 0, rows * 64 * (int)sizeof(float), 0x00020000);
         auto load = [&](int r0, float2 (&bx)[K], float (&bw)[K]) {
 #pragma unroll
             for (int u = 0; u < K; ++u) {
                 const int r = min(r0 + u, rows - 1);
-                const float wl = wr_[(size_t)r * 64];
-                bx[u] = xr_[(size_t)r * 64];
+                const auto xv = __builtin_amdgcn_raw_buffer_load_b64(
+                    rx, lane * (int)sizeof(float2), r * 64 * (int)sizeof(float2), 0);
+                const float wl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    rw, lane * (int)sizeof(float), r * 64 * (int)sizeof(float), 0));
+                bx[u] = make_float2(__uint_as_float(xv[0]), __uint_as_float(xv[1]));
                 bw[u] = r0 + u < rows ? wl : 0.0f;
             }
         };
@@ -240,13 +273,14 @@ __global__ __launch_bounds__(kThreads) void k_iter(Dims d, const float2 *__restr
 #pragma unroll
             for (int u = 0; u < K; ++u) {
                 const double2 g1 = gl[min(r0 + u, na - 1)];
+                const double p1 = gp[min(r0 + u, na - 1)];
                 const double wv = bw[u];
                 const float2 xv = wv != 0.0 ? bx[u] : make_float2(0.0f, 0.0f);
                 const double xr = xv.x * wv, xi = xv.y * wv;
                 // antenna a2 (i = a1): x[a1,a2] = conj(x_b)
                 ax += g1.x * xr + g1.y * xi;
                 ay += g1.y * xr - g1.x * xi;
-                ab += (g1.x * g1.x + g1.y * g1.y) * wv;
+                ab += p1 * wv;
                 // antenna a1 (i = a2): x[a2,a1] = x_b
                 pr[u] = g2.x * xr - g2.y * xi;
                 pi[u] = g2.x * xi + g2.y * xr;
@@ -256,19 +290,38 @@ __global__ __launch_bounds__(kThreads) void k_iter(Dims d, const float2 *__restr
             // lane l holds row (l >> 3) & 7 summed over 8 lanes; xor 4/2/1
             // finish it
             double q4r[4], q4i[4], q4b[4];
+            double q2r[2], q2i[2], q2b[2];
+#if SDP_STEFCAL_PERMLANE
+            // the two first halvings as VALU lane swaps (gfx950
+            // v_permlane32_swap / v_permlane16_swap): after swapping the upper
+            // half of A = row i with the lower half of B = row i + 4, A + B is
+            // row i on lanes 0-31 and row i + 4 on lanes 32-63
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                q4r[i] = swap_sum<32>(pr[i], pr[i + 4]);
+                q4i[i] = swap_sum<32>(pi[i], pi[i + 4]);
+                q4b[i] = swap_sum<32>(pb[i], pb[i + 4]);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                q2r[i] = swap_sum<16>(q4r[i], q4r[i + 2]);
+                q2i[i] = swap_sum<16>(q4i[i], q4i[i + 2]);
+                q2b[i] = swap_sum<16>(q4b[i], q4b[i + 2]);
+            }
+#else
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 q4r[i] = (b5 ? pr[i + 4] : pr[i]) + __shfl_xor(b5 ? pr[i] : pr[i + 4], 32);
                 q4i[i] = (b5 ? pi[i + 4] : pi[i]) + __shfl_xor(b5 ? pi[i] : pi[i + 4], 32);
                 q4b[i] = (b5 ? pb[i + 4] : pb[i]) + __shfl_xor(b5 ? pb[i] : pb[i + 4], 32);
             }
-            double q2r[2], q2i[2], q2b[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 q2r[i] = (b4 ? q4r[i + 2] : q4r[i]) + __shfl_xor(b4 ? q4r[i] : q4r[i + 2], 16);
                 q2i[i] = (b4 ? q4i[i + 2] : q4i[i]) + __shfl_xor(b4 ? q4i[i] : q4i[i + 2], 16);
                 q2b[i] = (b4 ? q4b[i + 2] : q4b[i]) + __shfl_xor(b4 ? q4b[i] : q4b[i + 2], 16);
             }
+#endif
             double tr = (b3 ? q2r[1] : q2r[0]) + __shfl_xor(b3 ? q2r[0] : q2r[1], 8);
             double ti = (b3 ? q2i[1] : q2i[0]) + __shfl_xor(b3 ? q2i[0] : q2i[1], 8);
             double tb = (b3 ? q2b[1] : q2b[0]) + __shfl_xor(b3 ? q2b[0] : q2b[1], 8);
@@ -519,7 +572,7 @@ static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, 
                                                   gw);
     SDP_HIP_CHECK(hipGetLastError());
 
-    const size_t lds = (size_t)d.nants * (2 * sizeof(double2) + sizeof(double));
+    const size_t lds = (size_t)d.nants * (2 * sizeof(double2) + 2 * sizeof(double));
     if (lds > 65536)
         SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_iter,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
