@@ -55,4 +55,6 @@ print(json.dumps({"path": "C5 StefCal (B jones) 512 st x 256 chan x %d times" % 
                   "solves_per_s": round(nsub / t_solve, 1), "iterations_max": max(iters),
                   "iterations_median": int(np.median(iters)),
                   "max_gain_err": worst_err, "max_residual": worst_res,
-                  "cpu_estimate_h": round(nsub * 0.062 / 3600, 2)}), flush=True)
+                  # CPU port: 0.24 s per 512-station sub-solve (ref_oracle.stefcal_row,
+                  # 1 core; scripts/bench_paths.py stefcal leg)
+                  "cpu_estimate_h": round(nsub * 0.24 / 3600, 1)}), flush=True)

@@ -176,7 +176,9 @@ if "stefcal" in which:
           "value": round(nsub / t, 1), "unit": "sub-solves/s",
           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                       "note": "12 B per baseline per sub-solve iteration (c64 x + f32 w)"},
+                       "note": "12 B per baseline per sub-solve iteration (c64 x + f32 w), "
+                               "over the whole solve incl. k_fill / k_residual; k_iter alone: "
+                               "profiles/r01_stefcal_kernel_stats.txt"},
           "max_residual": float(res.max()),
           "cpu_baseline": {"value": round(1.0 / tc, 2), "unit": "sub-solves/s", "cores": 1,
                            "kind": "port",
