@@ -969,7 +969,8 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
                                                    const unsigned *__restrict__ offs,
                                                    const FineItem *__restrict__ fitems,
                                                    const float2 *__restrict__ grid, int p_lo,
-                                                   int p_hi, float2 *__restrict__ acc) {
+                                                   int p_hi, float2 *__restrict__ acc,
+                                                   float2 *__restrict__ vdirect) {
     constexpr int SUB = kTileFine;
     constexpr int GRP = kGroupFine;
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
@@ -1090,7 +1091,14 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
                         ti += __shfl_xor(ti, msk);
                     }
                     const int rec = 8 * m + ((lane >> 3) & 7);
-                    if ((lane & 7) == 0 && rec < n) {
+                    if (vdirect) {
+                        // single pass: the record factor applied here and the
+                        // visibility written in place (no acc, no k_finalize)
+                        const float cr = __shfl(my.cre, rec), ci = __shfl(my.cim, rec);
+                        const uint32_t ix = (uint32_t)__shfl((int)my.idx, rec);
+                        if ((lane & 7) == 0 && rec < n)
+                            vdirect[ix] = make_float2(cr * tr - ci * ti, cr * ti + ci * tr);
+                    } else if ((lane & 7) == 0 && rec < n) {
                         float2 *dst = acc + b0 + rec;
                         float2 a = *dst;
                         a.x += tr;
@@ -1588,6 +1596,7 @@ struct Plan {
     bool pipelined = false;          // row parts, persistent launches, no host syncs
     bool aux_bucketing = false;      // bucketing on the auxiliary stream
     bool subsort = false;            // 16x16 buckets re-ordered to 2x2 (register kernels)
+    float2 *vdirect = nullptr;       // dirty2ms: register degridders write c64 vis in place
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
     int row_lo = 0, row_hi = 0;      // grid rows (x) the visibilities reach
@@ -2058,7 +2067,7 @@ static void launch_degrid_fine_items(const Plan &P, const Part &pt, int p_lo, in
     k_degrid_reg<W, WS, true><<<n, 64, lds, st>>>(fine_view(P.g), P.recs + pt.vbase,
                                                   ItemSrc{nullptr, n, nullptr}, nullptr,
                                                   pt.fitems + 16 * (size_t)r.first, P.grid, p_lo,
-                                                  p_hi, acc + pt.vbase);
+                                                  p_hi, acc + pt.vbase, P.vdirect);
 }
 
 template <int W>
@@ -2101,7 +2110,7 @@ static void launch_degrid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi,
     if (L.blocks == 0) return;
     k_degrid_reg<W, WS, false><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
                                                          nullptr, P.grid, p_lo, p_hi,
-                                                         acc + pt.vbase);
+                                                         acc + pt.vbase, P.vdirect);
 }
 
 template <int W>
@@ -2340,8 +2349,17 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
             k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, st>>>(
                 in.nrow, in.nchan, (float2 *)vis, in.vrs, in.vcs, oc);
     }
-    float2 *acc = scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));
-    SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(nvis, 1) * sizeof(float2), st));
+    // all planes in one pass into plain contiguous c64 visibilities: the
+    // register degridders apply the record factor and write each visibility
+    // once (k_zero_vis above covers the ones with no record)
+    const bool trivial_oc = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
+    if (P.chunk_planes == g.nplanes && !accumulate && in.vis_dtype != SDP_HIP_C128 && trivial_oc &&
+        in.vcs == 1 && in.vrs == in.nchan && (P.subsort || g.sub == kTileFine) &&
+        !std::getenv("SDP_HIP_NO_DIRECT"))
+        P.vdirect = static_cast<float2 *>(vis);
+    float2 *acc = P.vdirect ? nullptr : scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));
+    if (acc)
+        SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(nvis, 1) * sizeof(float2), st));
     float tgrid = 0, tfft = 0, tscr = 0;
     bool waited = false;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
@@ -2382,7 +2400,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         }
         waited = true;
     }
-    for (size_t i = 0; i < P.parts.size(); ++i) {
+    for (size_t i = 0; i < P.parts.size() && !P.vdirect; ++i) {
         const Part &pt = P.parts[i];
         if (pt.nvis == 0) continue;
         const unsigned *ndev = P.pipelined ? pt.meta + 2 : nullptr;
