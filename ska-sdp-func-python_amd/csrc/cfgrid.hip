@@ -9,7 +9,8 @@
 // (channel, row).  Here one wave handles one (row, channel) with one lane per
 // CF tap:
 //   grid:   gd[c, p, pv-dv+iv, pu-du+iu] += conj(cf[c, p, w, dv_off, du_off, iv, iu]) * V * wt
-//           (fp64 global atomics; sumwt per block in LDS, one atomic per pol)
+//           (fp64 global atomics; sumwt per block in LDS, then one of kSlots
+//           partial sums per pol, folded by k_fold_slots)
 //   degrid: V = sum_{iv,iu} gd[c, p, window] * cf[c, p, w, dv_off, du_off, iv, iu]
 // with the reference's edge-skip rule (gridding.py:230-237, :555-563): a row
 // whose window touches pv+dv >= ny or pu+du >= nx (or < 0) is skipped.
@@ -20,6 +21,7 @@ namespace cfgrid {
 
 constexpr int kThreads = 256;
 constexpr int kMaxPol = 4;
+constexpr int kSlots = 1024;  // partial-sum slots for sumwt / skip counts (power of two)
 
 struct Shape {
     int64_t nrow;
@@ -44,8 +46,8 @@ __global__ __launch_bounds__(kThreads) void k_grid_cf(Shape s, const int32_t *__
                                                       const double2 *__restrict__ vis,
                                                       const double *__restrict__ wt,
                                                       const double2 *__restrict__ cf,
-                                                      double2 *grid, double *sumwt,
-                                                      unsigned long long *nskipped) {
+                                                      double2 *grid, double *wslots,
+                                                      unsigned long long *skslots) {
     __shared__ double s_wt[kMaxPol];
     __shared__ unsigned long long s_skip;
     if (threadIdx.x < kMaxPol) s_wt[threadIdx.x] = 0.0;
@@ -88,9 +90,43 @@ __global__ __launch_bounds__(kThreads) void k_grid_cf(Shape s, const int32_t *__
         }
     }
     __syncthreads();
-    if (threadIdx.x < s.npol && sumwt) atomicAdd(&sumwt[(size_t)imchan * s.npol + threadIdx.x],
-                                                 s_wt[threadIdx.x]);
-    if (threadIdx.x == 0 && nskipped && s_skip) atomicAdd(nskipped, s_skip);
+    // the block's weight / skip counts go to one of kSlots partial sums
+    // (one shared address per call serialised ~1M atomics), folded by
+    // k_fold_slots
+    const int slot = blockIdx.x & (kSlots - 1);
+    if (threadIdx.x < s.npol && s_wt[threadIdx.x] != 0.0)
+        atomicAdd(&wslots[((size_t)slot * s.g_nchan + imchan) * s.npol + threadIdx.x],
+                  s_wt[threadIdx.x]);
+    if (threadIdx.x == 0 && s_skip) atomicAdd(&skslots[slot], s_skip);
+}
+
+__global__ __launch_bounds__(256) void k_fold_slots(int nsum, const double *__restrict__ wslots,
+                                                    const unsigned long long *__restrict__ skslots,
+                                                    double *sumwt, unsigned long long *nskipped) {
+    // block b < nsum: sumwt entry b; block nsum: the skip count
+    const int b = blockIdx.x;
+    double sw = 0.0;
+    unsigned long long sk = 0;
+    for (int i = threadIdx.x; i < kSlots; i += 256) {
+        if (b < nsum) sw += wslots[(size_t)i * nsum + b];
+        else sk += skslots[i];
+    }
+    __shared__ double rw[256];
+    __shared__ unsigned long long rk[256];
+    rw[threadIdx.x] = sw;
+    rk[threadIdx.x] = sk;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            rw[threadIdx.x] += rw[threadIdx.x + o];
+            rk[threadIdx.x] += rk[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (b < nsum && sumwt) sumwt[b] += rw[0];
+        if (b == nsum && nskipped) *nskipped += rk[0];
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_degrid_cf(Shape s, const int32_t *__restrict__ pu,
@@ -164,11 +200,18 @@ int sdp_hip_grid_cf(int64_t nrowvis, int nchan_vis, int npol, const int32_t *pu,
         if (nrowvis == 0) return;
         SDP_REQUIRE(pu && pv && pwc && pdu && pdv && vis_to_im && vis && wt && cf && grid,
                     "null pointer argument");
+        const hipStream_t st = as_stream(stream);
+        const int nsum = g_nchan * npol;
+        double *wslots = scratch<double>("cf_wslots", (size_t)cfgrid::kSlots * nsum);
+        auto *skslots = scratch<unsigned long long>("cf_skslots", cfgrid::kSlots);
+        SDP_HIP_CHECK(hipMemsetAsync(wslots, 0, sizeof(double) * cfgrid::kSlots * nsum, st));
+        SDP_HIP_CHECK(hipMemsetAsync(skslots, 0, sizeof(unsigned long long) * cfgrid::kSlots, st));
         const dim3 blocks((unsigned)((nrowvis + 3) / 4), nchan_vis);
-        cfgrid::k_grid_cf<<<blocks, cfgrid::kThreads, 0, as_stream(stream)>>>(
+        cfgrid::k_grid_cf<<<blocks, cfgrid::kThreads, 0, st>>>(
             s, pu, pv, pwc, pdu, pdv, vis_to_im, static_cast<const double2 *>(vis), wt,
-            static_cast<const double2 *>(cf), static_cast<double2 *>(grid), sumwt,
-            reinterpret_cast<unsigned long long *>(nskipped));
+            static_cast<const double2 *>(cf), static_cast<double2 *>(grid), wslots, skslots);
+        cfgrid::k_fold_slots<<<nsum + 1, 256, 0, st>>>(
+            nsum, wslots, skslots, sumwt, reinterpret_cast<unsigned long long *>(nskipped));
         SDP_HIP_CHECK(hipGetLastError());
     });
 }

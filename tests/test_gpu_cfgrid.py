@@ -55,3 +55,35 @@ def test_centred_ffts_match_reference():
     img = dm.Image.constructor(g["a"], pf, tmpl.image_acc.wcs)
     gd2 = fft_image_to_griddata(img, dm.GridData.constructor(np.zeros_like(g["a"]), dm.WCS(4), pf))
     np.testing.assert_allclose(gd2["pixels"].data, g["fft"], rtol=1e-10, atol=1e-9)
+
+
+def test_grid_cf_weights_and_skips_many_blocks():
+    """Many workgroups (the weight / skip partial-sum slots wrap) with rows
+    on the grid edge: grid, sumwt and the skipped-sample count against the
+    restated reference loop (oracle/ref_oracle.grid_cf) and its edge rule."""
+    import torch
+    import ref_oracle as ro
+    from ska_sdp_func_python_amd import kernels
+    rng = np.random.default_rng(11)
+    nrow, nchan, npol, ny, nx, gv, gu, nw, ndv, ndu = 9000, 2, 2, 64, 48, 8, 8, 3, 4, 4
+    maps_h = {"pu": rng.integers(-2, nx + 2, (nchan, nrow)), "pv": rng.integers(-2, ny + 2, (nchan, nrow)),
+              "pwc": rng.integers(0, nw, (nchan, nrow)), "pdu": rng.integers(0, ndu, (nchan, nrow)),
+              "pdv": rng.integers(0, ndv, (nchan, nrow))}
+    vis = rng.normal(size=(nrow, nchan, npol)) + 1j * rng.normal(size=(nrow, nchan, npol))
+    wt = rng.uniform(0.5, 2.0, (nrow, nchan, npol))
+    cf = rng.normal(size=(1, npol, nw, ndv, ndu, gv, gu)) + 1j * rng.normal(size=(1, npol, nw, ndv, ndu, gv, gu))
+    v2i = np.zeros(nchan, int)
+    eg, esw = ro.grid_cf(maps_h, v2i, vis, wt, cf, (1, npol, ny, nx))
+    ok = ~((maps_h["pv"] - gv // 2 < 0) | (maps_h["pv"] + gv // 2 >= ny)
+           | (maps_h["pu"] - gu // 2 < 0) | (maps_h["pu"] + gu // 2 >= nx))
+    dev = torch.device("cuda:0")
+    T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+    maps = {k: T(v, torch.int32) for k, v in maps_h.items()}
+    grid = torch.zeros((1, npol, ny, nx), dtype=torch.complex128, device=dev)
+    sumwt = torch.zeros((1, npol), dtype=torch.float64, device=dev)
+    skipped = kernels.grid_cf(maps, T(v2i, torch.int32), T(vis, torch.complex128),
+                              T(wt, torch.float64), T(cf, torch.complex128), grid, sumwt)
+    np.testing.assert_allclose(grid.cpu().numpy(), eg, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(sumwt.cpu().numpy(), esw, rtol=1e-12)
+    assert int(skipped.item()) == int((~ok).sum()) * npol
+    assert 0 < (~ok).sum() < ok.sum()
