@@ -138,38 +138,45 @@ __global__ __launch_bounds__(kThreads) void k_degrid_cf(Shape s, const int32_t *
                                                         const double2 *__restrict__ grid,
                                                         const double2 *__restrict__ cf,
                                                         double2 *vis_out,
-                                                        unsigned long long *nskipped) {
+                                                        unsigned long long *skslots) {
+    __shared__ unsigned long long s_skip;
+    if (threadIdx.x == 0) s_skip = 0;
+    __syncthreads();
     const int chan = blockIdx.y;
     const int imchan = vis_to_im[chan];
     const int lane = threadIdx.x & 63;
     const int taps = s.gv * s.gu;
     const int dv = s.gv / 2, du = s.gu / 2;
     const int64_t row = blockIdx.x * (int64_t)(kThreads / 64) + (threadIdx.x >> 6);
-    if (row >= s.nrow) return;
-    const size_t m = (size_t)chan * s.nrow + row;
-    const int u0 = pu[m], v0 = pv[m];
-    const bool ok = window_ok(s, u0, v0);
-    if (!ok && lane == 0 && nskipped) atomicAdd(nskipped, (unsigned long long)s.npol);
-    const int iw = pwc[m], idu = pdu[m], idv = pdv[m];
-    for (int p = 0; p < s.npol; ++p) {
-        double sr = 0.0, si = 0.0;
-        if (ok) {
-            const double2 *sub = cf + cf_index(s, imchan, p, iw, idv, idu) * taps;
-            const double2 *g = grid + ((size_t)imchan * s.npol + p) * s.ny * s.nx;
-            for (int t = lane; t < taps; t += 64) {
-                const int iv = t / s.gu, iu = t - (t / s.gu) * s.gu;
-                const double2 c = sub[t];
-                const double2 a = g[(size_t)(v0 - dv + iv) * s.nx + (u0 - du + iu)];
-                sr += a.x * c.x - a.y * c.y;
-                si += a.x * c.y + a.y * c.x;
+    if (row < s.nrow) {
+        const size_t m = (size_t)chan * s.nrow + row;
+        const int u0 = pu[m], v0 = pv[m];
+        const bool ok = window_ok(s, u0, v0);
+        if (!ok && lane == 0) atomicAdd(&s_skip, (unsigned long long)s.npol);
+        const int iw = pwc[m], idu = pdu[m], idv = pdv[m];
+        for (int p = 0; p < s.npol; ++p) {
+            double sr = 0.0, si = 0.0;
+            if (ok) {
+                const double2 *sub = cf + cf_index(s, imchan, p, iw, idv, idu) * taps;
+                const double2 *g = grid + ((size_t)imchan * s.npol + p) * s.ny * s.nx;
+                for (int t = lane; t < taps; t += 64) {
+                    const int iv = t / s.gu, iu = t - (t / s.gu) * s.gu;
+                    const double2 c = sub[t];
+                    const double2 a = g[(size_t)(v0 - dv + iv) * s.nx + (u0 - du + iu)];
+                    sr += a.x * c.x - a.y * c.y;
+                    si += a.x * c.y + a.y * c.x;
+                }
+                for (int o = 32; o > 0; o >>= 1) {
+                    sr += __shfl_xor(sr, o);
+                    si += __shfl_xor(si, o);
+                }
             }
-            for (int o = 32; o > 0; o >>= 1) {
-                sr += __shfl_xor(sr, o);
-                si += __shfl_xor(si, o);
-            }
+            if (lane == 0) vis_out[((size_t)row * s.nchan + chan) * s.npol + p] = make_double2(sr, si);
         }
-        if (lane == 0) vis_out[((size_t)row * s.nchan + chan) * s.npol + p] = make_double2(sr, si);
     }
+    __syncthreads();
+    // skip counts go to kSlots partial sums, folded by k_fold_slots (nsum = 0)
+    if (threadIdx.x == 0 && s_skip) atomicAdd(&skslots[blockIdx.x & (kSlots - 1)], s_skip);
 }
 
 static Shape make_shape(int64_t nrow, int nchan, int npol, int cf_nchan, int nw, int ndv, int ndu,
@@ -229,11 +236,16 @@ int sdp_hip_degrid_cf(int64_t nrowvis, int nchan_vis, int npol, const int32_t *p
         if (nrowvis == 0) return;
         SDP_REQUIRE(pu && pv && pwc && pdu && pdv && vis_to_im && grid && cf && vis_out,
                     "null pointer argument");
+        const hipStream_t st = as_stream(stream);
+        auto *skslots = scratch<unsigned long long>("cfd_skslots", cfgrid::kSlots);
+        SDP_HIP_CHECK(hipMemsetAsync(skslots, 0, sizeof(unsigned long long) * cfgrid::kSlots, st));
         const dim3 blocks((unsigned)((nrowvis + 3) / 4), nchan_vis);
-        cfgrid::k_degrid_cf<<<blocks, cfgrid::kThreads, 0, as_stream(stream)>>>(
+        cfgrid::k_degrid_cf<<<blocks, cfgrid::kThreads, 0, st>>>(
             s, pu, pv, pwc, pdu, pdv, vis_to_im, static_cast<const double2 *>(grid),
-            static_cast<const double2 *>(cf), static_cast<double2 *>(vis_out),
-            reinterpret_cast<unsigned long long *>(nskipped));
+            static_cast<const double2 *>(cf), static_cast<double2 *>(vis_out), skslots);
+        if (nskipped)
+            cfgrid::k_fold_slots<<<1, 256, 0, st>>>(0, nullptr, skslots, nullptr,
+                                                   reinterpret_cast<unsigned long long *>(nskipped));
         SDP_HIP_CHECK(hipGetLastError());
     });
 }

@@ -87,3 +87,33 @@ def test_grid_cf_weights_and_skips_many_blocks():
     np.testing.assert_allclose(sumwt.cpu().numpy(), esw, rtol=1e-12)
     assert int(skipped.item()) == int((~ok).sum()) * npol
     assert 0 < (~ok).sum() < ok.sum()
+
+
+def test_degrid_cf_skips_many_blocks():
+    """Degridding over many workgroups with rows on the grid edge: the
+    visibilities against the restated reference loop (ref_oracle.degrid_cf;
+    skipped rows stay zero) and the skipped-sample count from the partial-sum
+    slots."""
+    import torch
+    import ref_oracle as ro
+    from ska_sdp_func_python_amd import kernels
+    rng = np.random.default_rng(12)
+    nrow, nchan, npol, ny, nx, gv, gu, nw, ndv, ndu = 9000, 2, 2, 64, 48, 8, 8, 3, 4, 4
+    maps_h = {"pu": rng.integers(-2, nx + 2, (nchan, nrow)), "pv": rng.integers(-2, ny + 2, (nchan, nrow)),
+              "pwc": rng.integers(0, nw, (nchan, nrow)), "pdu": rng.integers(0, ndu, (nchan, nrow)),
+              "pdv": rng.integers(0, ndv, (nchan, nrow))}
+    grid_h = rng.normal(size=(1, npol, ny, nx)) + 1j * rng.normal(size=(1, npol, ny, nx))
+    cf = rng.normal(size=(1, npol, nw, ndv, ndu, gv, gu)) + 1j * rng.normal(size=(1, npol, nw, ndv, ndu, gv, gu))
+    v2i = np.zeros(nchan, int)
+    ev = ro.degrid_cf(maps_h, v2i, grid_h, cf, nrow, nchan)
+    ok = ~((maps_h["pv"] - gv // 2 < 0) | (maps_h["pv"] + gv // 2 >= ny)
+           | (maps_h["pu"] - gu // 2 < 0) | (maps_h["pu"] + gu // 2 >= nx))
+    dev = torch.device("cuda:0")
+    T = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a), dtype=dt, device=dev)
+    maps = {k: T(v, torch.int32) for k, v in maps_h.items()}
+    out = torch.full((nrow, nchan, npol), 7.0 + 0j, dtype=torch.complex128, device=dev)
+    skipped = kernels.degrid_cf(maps, T(v2i, torch.int32), T(grid_h, torch.complex128),
+                                T(cf, torch.complex128), nrow, nchan, out)
+    np.testing.assert_allclose(out.cpu().numpy(), ev, rtol=1e-10, atol=1e-10)
+    assert int(skipped.item()) == int((~ok).sum()) * npol
+    assert 0 < (~ok).sum() < ok.sum()
