@@ -53,7 +53,8 @@ def load_reference(relpath, names, extra=None):
     assert not missing, missing
     ns = {"numpy": np, "log": logging.getLogger("reference"), "copy": __import__("copy"),
           "Visibility": dm.Visibility, "GainTable": dm.GainTable, "Image": dm.Image,
-          "GridData": dm.GridData}
+          "GridData": dm.GridData, "SkyCoord": dm.SkyCoord,
+          "physical_constants": __import__("types").SimpleNamespace(C_M_S=299792458.0)}
     ns.update(extra or {})
     exec(compile(ast.Module(body=defs, type_ignores=[]), relpath, "exec"), ns)
     return ns
@@ -370,6 +371,112 @@ def make_nufft_c1():
         out[f"model_w{int(dow)}"] = img
         out[f"vis_w{int(dow)}"] = orc.dirty2ms_exact(fuvw, freq, img, None, cell, cell, dow)
     save("nufft_c1.npz", uvw=uvw, freq=freq, ms=ms, wgt=wgt, cell=np.array(cell), **out)
+
+
+def _aw_reference():
+    """The reference's AW-projection wrappers (imaging/base.py:48-92, :95-155,
+    :158-259, :262-296) with the numpy helpers they call, exec'd from its own
+    sources: gridding (grid_data/gridding.py), centred FFTs
+    (fourier_transforms/fft_support.py, numpy branch), Stokes <-> pol images
+    (image/operations.py:78-195), the tangent-plane phase rotation
+    (visibility/base.py:27-125).  Data-model functions (create_griddata_from_image,
+    pixel_to_skycoord, the datamodels' stokes/pol matrix conversions) and
+    astropy's skycoord_to_lmn come from the shim (pinned in tests/test_host.py)."""
+    from ska_sdp_func_python_amd.util.coordinate_support import skycoord_to_lmn
+    PF = dm.PolarisationFrame
+
+    def conv(a, b):
+        return lambda x: dm.convert_pol_frame(x, PF(a), PF(b), polaxis=1)
+
+    fs = load_reference("fourier_transforms/fft_support.py", ["fft", "ifft"],
+                        {"pyfftw_exists": False, "pyfftw": None})
+    gr = load_reference("grid_data/gridding.py",
+                        ["convolution_mapping_visibility", "spatial_mapping",
+                         "grid_visibility_to_griddata", "degrid_visibility_from_griddata",
+                         "fft_griddata_to_image", "fft_image_to_griddata"],
+                        {"fft": fs["fft"], "ifft": fs["ifft"]})
+    ops = load_reference("image/operations.py",
+                         ["convert_stokes_to_polimage", "convert_polimage_to_stokes"],
+                         {"PolarisationFrame": PF,
+                          "convert_stokes_to_linear": conv("stokesIQUV", "linear"),
+                          "convert_stokes_to_circular": conv("stokesIQUV", "circular"),
+                          "convert_linear_to_stokes": conv("linear", "stokesIQUV"),
+                          "convert_circular_to_stokes": conv("circular", "stokesIQUV")})
+    vb = load_reference("visibility/base.py",
+                        ["calculate_visibility_phasor", "calculate_visibility_uvw_lambda",
+                         "phaserotate_visibility"],
+                        {"skycoord_to_lmn": skycoord_to_lmn})
+    extra = {"PolarisationFrame": PF, "pixel_to_skycoord": dm.pixel_to_skycoord,
+             "create_griddata_from_image": dm.create_griddata_from_image,
+             "phaserotate_visibility": vb["phaserotate_visibility"]}
+    for ns in (gr, ops):
+        extra.update({k: v for k, v in ns.items() if callable(v) and not k.startswith("__")})
+    return load_reference("imaging/base.py",
+                          ["shift_vis_to_image", "normalise_sumwt", "fill_vis_for_psf",
+                           "predict_awprojection", "invert_awprojection"], extra)
+
+
+def make_awprojection():
+    """predict_awprojection / invert_awprojection (+ PSF) with a synthetic
+    gcfcf (random positive grid correction, random oversampled w-indexed CF
+    on the image's uv cell) and the visibility phase centre offset from the
+    image's, so the tangent-plane shift of shift_vis_to_image is exercised
+    in both directions."""
+    ref = _aw_reference()
+    for tag, vpf, ipf, nchan in (("p1", "stokesI", "stokesI", 2), ("p4", "linear", "stokesIQUV", 1)):
+        rng = np.random.default_rng(41 + len(tag) + nchan)
+        npix, cell = 64, 0.004
+        freq = 1.0e8 + 2.0e6 * np.arange(nchan)
+        im_pc = dm.SkyCoord(math.radians(30.0), math.radians(-40.0))
+        vis_pc = dm.SkyCoord(math.radians(30.0) + 0.01, math.radians(-40.0) - 0.006)
+        im = dm.create_image(npix, cell, im_pc, polarisation_frame=dm.PolarisationFrame(ipf),
+                             frequency=float(freq[0]), channel_bandwidth=2e6, nchan=nchan)
+        vpf_ = dm.PolarisationFrame(vpf)
+        gd = dm.create_griddata_from_image(im, polarisation_frame=vpf_)
+        cdu, cdv = gd.attrs["grid_wcs"].wcs.cdelt[:2]
+        du = abs(cdu)
+        nw, ndv, ndu, gv, gu, dw = 3, 5, 5, 8, 8, 30.0
+        cf_wcs = dm.WCS(7, ["UU", "VV", "DUU", "DVV", "WW", "STOKES", "FREQ"],
+                        [gu // 2 + 1, gv // 2 + 1, ndu // 2 + 1, ndv // 2 + 1, nw // 2 + 1, 1, 1],
+                        [cdu, cdv, cdu / ndu, cdv / ndv, dw, 1, 2e6], [0, 0, 0, 0, 0, 1, freq[0]])
+        shape_cf = (nchan, vpf_.npol, nw, ndv, ndu, gv, gu)
+        cfp = rng.normal(size=shape_cf) + 1j * rng.normal(size=shape_cf)
+        cf = dm.ConvolutionFunction.constructor(cfp, cf_wcs, vpf_)
+        gcf = dm.create_image(npix, cell, im_pc, polarisation_frame=vpf_, frequency=float(freq[0]),
+                              channel_bandwidth=2e6, nchan=nchan)
+        gcf["pixels"].data[...] = rng.uniform(0.5, 1.5, gcf["pixels"].data.shape)
+        nt, nb = 3, 45
+        lam = 299792458.0 / freq.max()
+        uvw = np.zeros((nt, nb, 3))
+        uvw[..., :2] = rng.uniform(-29 * du, 29 * du, (nt, nb, 2)) * lam  # some rows hit the edge
+        uvw[..., 2] = rng.uniform(-1.2 * dw, 1.2 * dw, (nt, nb)) * lam
+        shape = (nt, nb, nchan, vpf_.npol)
+        vis = dm.Visibility.constructor(
+            frequency=freq, channel_bandwidth=np.full(nchan, 2e6), phasecentre=vis_pc, uvw=uvw,
+            time=np.arange(nt, dtype=float),
+            vis=rng.normal(size=shape) + 1j * rng.normal(size=shape),
+            weight=rng.uniform(0.5, 2.0, shape), flags=(rng.uniform(size=shape) < 0.05).astype(int),
+            baselines=np.stack(np.triu_indices(10, 1), 1)[:nb], polarisation_frame=vpf_,
+            imaging_weight=rng.uniform(0.5, 2.0, shape))
+        gcfcf = lambda _im: (gcf, cf)  # noqa: E731
+        dirty, sumwt = ref["invert_awprojection"](vis.copy(deep=True), im, gcfcf=gcfcf)
+        psf, psf_sumwt = ref["invert_awprojection"](vis.copy(deep=True), im, dopsf=True,
+                                                    gcfcf=gcfcf)
+        model = im.copy(deep=True)
+        model["pixels"].data[...] = rng.normal(size=model["pixels"].data.shape)
+        pv = ref["predict_awprojection"](vis.copy(deep=True), model, gcfcf=gcfcf)
+        # the reference relabels the predicted vis with the image phase centre
+        # (shift_vis_to_image, imaging/base.py:90) even on the inverse shift
+        assert pv.phasecentre.separation(im_pc).rad < 1e-12
+        save(f"awproj_{tag}.npz", uvw=uvw, freq=freq, vis=vis.vis.data, weight=vis.weight.data,
+             imaging_weight=vis.imaging_weight.data, flags=vis.flags.data,
+             vis_pc=np.array([vis_pc.ra.rad, vis_pc.dec.rad]),
+             im_pc=np.array([im_pc.ra.rad, im_pc.dec.rad]), npix=np.array(npix),
+             cell=np.array(cell), vis_pf=np.array(vpf), im_pf=np.array(ipf),
+             cf=cfp, cf_crpix=cf_wcs.wcs.crpix, cf_cdelt=cf_wcs.wcs.cdelt,
+             cf_crval=cf_wcs.wcs.crval, gcf=gcf["pixels"].data, model=model["pixels"].data,
+             dirty=dirty["pixels"].data, sumwt=sumwt, psf=psf["pixels"].data,
+             psf_sumwt=psf_sumwt, predicted=pv.vis.data)
 
 
 if __name__ == "__main__":

@@ -173,6 +173,22 @@ def test_predict_ng_c1_fixture(dow):
     assert rel_rms(pv.vis.data.reshape(-1), g[f"vis_w{dow}"].reshape(-1)) < TOL
 
 
+def test_context_2d_is_ng_without_wstacking():
+    """reference imaging/imaging.py:46-55, :87-105: context "2d" is ng with
+    do_wstacking=False -- checked against the C1 fixture's no-w-term exact
+    results through invert_visibility / predict_visibility."""
+    from ska_sdp_func_python_amd.imaging import invert_visibility, predict_visibility
+    g = golden("nufft_c1.npz")
+    vis, im = _c1_objects(g)
+    dirty, sumwt = invert_visibility(vis, im, context="2d")
+    expect = g["dirty_w0"].T / g["wgt"].sum()
+    assert rel_rms(dirty["pixels"].data[0, 0], expect) < TOL
+    assert rel_rms(dirty["pixels"].data[0, 0], g["dirty_w1"].T / g["wgt"].sum()) > 10 * TOL
+    im["pixels"].data[0, 0] = g["model_w0"].T
+    pv = predict_visibility(vis, im, context="2d")
+    assert rel_rms(pv.vis.data.reshape(-1), g["vis_w0"].reshape(-1)) < TOL
+
+
 def test_invert_predict_round_trip_point_source():
     """Reference property (tests/imaging/test_imaging.py:216-226): a unit
     point at the image centre predicts visibilities ~1."""

@@ -130,3 +130,55 @@ def test_skycoord_pixel_round_trip_and_apply_beam():
     assert out[1].flux[0, 0] == 0.0
     inv = apply_beam_to_skycomponent(comps[0], im, inverse=True)
     assert inv.flux[0, 0] == 2.0 / im["pixels"].data[0, 0, 30, 20]
+
+
+def test_unknown_imaging_context_raises():
+    """reference imaging/imaging.py:55, :105: an unknown context is a ValueError
+    (raised before any device work)."""
+    from ska_sdp_func_python_amd.imaging import invert_visibility, predict_visibility
+    with pytest.raises(ValueError, match="Unknown imaging context"):
+        invert_visibility(None, None, context="wstack-nope")
+    with pytest.raises(ValueError, match="Unknown imaging context"):
+        predict_visibility(None, None, context="")
+
+
+def test_cf_channel_map_checked_like_numpy_indexing():
+    """vis -> image channels past the GridData's / CF's channel axis raise
+    IndexError (the reference's gd[imchan], grid_data/gridding.py:226-245);
+    the check runs on the host before any launch."""
+    import torch
+    from ska_sdp_func_python_amd import kernels
+    nrow, nchan, npol = 5, 3, 1
+    maps = {k: torch.zeros((nchan, nrow), dtype=torch.int32) for k in ("pu", "pv", "pwc", "pdu", "pdv")}
+    vis = torch.zeros((nrow, nchan, npol), dtype=torch.complex128)
+    wt = torch.ones((nrow, nchan, npol), dtype=torch.float64)
+    cf = torch.zeros((2, npol, 1, 1, 1, 4, 4), dtype=torch.complex128)
+    grid = torch.zeros((2, npol, 16, 16), dtype=torch.complex128)
+    sumwt = torch.zeros((2, npol), dtype=torch.float64)
+    for bad in ([0, 1, 2], [0, -3, 1]):
+        with pytest.raises(IndexError):
+            kernels.grid_cf(maps, torch.tensor(bad, dtype=torch.int32), vis, wt, cf, grid, sumwt)
+        with pytest.raises(IndexError):
+            kernels.degrid_cf(maps, torch.tensor(bad, dtype=torch.int32), grid, cf, nrow, nchan,
+                              torch.zeros((nrow, nchan, npol), dtype=torch.complex128))
+    with pytest.raises(ValueError, match="pol axes"):
+        kernels.degrid_cf(maps, torch.zeros(nchan, dtype=torch.int32),
+                          torch.zeros((2, 2, 16, 16), dtype=torch.complex128), cf, nrow, nchan,
+                          torch.zeros((nrow, nchan, npol), dtype=torch.complex128))
+    with pytest.raises(ValueError, match="out must be"):
+        kernels.degrid_cf(maps, torch.zeros(nchan, dtype=torch.int32), grid, cf, nrow, nchan,
+                          torch.zeros((nrow, nchan, npol), dtype=torch.complex64))
+
+
+def test_epsilon_below_fp32_floor_is_reported_once(caplog):
+    import logging
+    import torch
+    from ska_sdp_func_python_amd import kernels
+    kernels._eps_warned = False
+    uvw = torch.zeros((4, 3), dtype=torch.float64)
+    with caplog.at_level(logging.WARNING, logger="func-python-logger"):
+        for _ in range(2):
+            with pytest.raises(ValueError):  # host tensors: rejected after the note
+                kernels.ms2dirty(uvw, torch.ones(1), None, None, 8, 8, 1e-3, 1e-3, 1e-12)
+    msgs = [r.getMessage() for r in caplog.records if "floor epsilon" in r.getMessage()]
+    assert len(msgs) == 1 and "1.0e-12" in msgs[0]
