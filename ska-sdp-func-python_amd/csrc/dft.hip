@@ -9,7 +9,11 @@
 // (direction cosines as fp64, fluxes as fp32 complex).  The phase is formed in
 // fp64 and reduced to turns (t - rint(t)) before the hardware v_sin_f32 /
 // v_cos_f32 (which take revolutions), so SKA-scale u ~ 1e6 wavelengths lose
-// no phase precision; the component sum accumulates in fp32.
+// no phase precision; the component sum accumulates in fp32 for complex64
+// output and in fp64 for complex128 output (the reference's dft_cpu_looped
+// sums in complex128, imaging/dft.py:265-285).
+#include <type_traits>
+
 #include "sdp_common.h"
 
 namespace sdp {
@@ -21,7 +25,7 @@ constexpr int kCompChunk = 256;
 
 __device__ __forceinline__ float2 to_f2(const double2 v) { return make_float2((float)v.x, (float)v.y); }
 __device__ __forceinline__ void put(float2 *p, float re, float im) { *p = make_float2(re, im); }
-__device__ __forceinline__ void put(double2 *p, float re, float im) { *p = make_double2(re, im); }
+__device__ __forceinline__ void put(double2 *p, double re, double im) { *p = make_double2(re, im); }
 
 template <int NPOL, class OT, bool kMetres>
 __global__ __launch_bounds__(kThreads) void k_dft(int ncomp, const double *__restrict__ dc,
@@ -50,9 +54,10 @@ __global__ __launch_bounds__(kThreads) void k_dft(int ncomp, const double *__res
             w = uvw[v * 3 + 2];
         }
     }
-    float ar[NPOL], ai[NPOL];
+    using AT = typename std::conditional<std::is_same<OT, double2>::value, double, float>::type;
+    AT ar[NPOL], ai[NPOL];
 #pragma unroll
-    for (int p = 0; p < NPOL; ++p) ar[p] = ai[p] = 0.0f;
+    for (int p = 0; p < NPOL; ++p) ar[p] = ai[p] = (AT)0;
     const bool shared_flux = fnchan == 1;
     for (int c0 = 0; c0 < ncomp; c0 += kCompChunk) {
         const int nc = min(kCompChunk, ncomp - c0);
@@ -73,9 +78,10 @@ __global__ __launch_bounds__(kThreads) void k_dft(int ncomp, const double *__res
                 const float2 f = shared_flux
                                      ? s_fl[c * NPOL + p]
                                      : to_f2(flux[((int64_t)(c0 + c) * fnchan + chan) * NPOL + p]);
-                // f * exp(-2 pi i t) = f * (cs - i sn)
-                ar[p] = fmaf(f.x, cs, fmaf(f.y, sn, ar[p]));
-                ai[p] = fmaf(f.y, cs, fmaf(-f.x, sn, ai[p]));
+                // f * exp(-2 pi i t) = f * (cs - i sn): the fp32 products
+                // summed in the accumulator's precision
+                ar[p] += (AT)(f.x * cs + f.y * sn);
+                ai[p] += (AT)(f.y * cs - f.x * sn);
             }
         }
     }

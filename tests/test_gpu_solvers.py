@@ -1,7 +1,15 @@
 """GPU parity of solve_gaintable (batched StefCal, sdp_hip_solve_gains)
 against the reference's own solve_gaintable run on the same inputs
-(tests/golden/solve_*.npz).  fp32 storage of the point-source vis in the
-kernel: gains agree to 2e-5 absolute, weights to 1e-4 relative."""
+(tests/golden/solve_*.npz).
+
+The kernel stores the normalised point-source vis / weights in fp32 and
+iterates in fp64.  A relative perturbation of 6e-8 in x moves the fixed point
+of the substitution g_j = sum_i g_i x_ij w_ij / sum_i |g_i|^2 w_ij by the same
+relative order, far below the reference's stopping tolerance tol = 1e-6, so
+the stopping iteration and the gains agree: measured max |dgain| 4.5e-8 over
+the seven fixtures, 6e-9 on 512-station C5 rows with equal iteration counts
+(scripts/gpu_stefcal_parity.py, tests/test_gpu_fullsize.py).  Asserted:
+gains to 1e-6 absolute (= tol), weights to 1e-6 relative, residuals to 1e-7."""
 
 import numpy as np
 import pytest
@@ -37,9 +45,9 @@ def test_solve_gaintable_matches_reference(case):
     out = solve_gaintable(vis, model, gain_table=gt, phase_only=bool(g["phase_only"]),
                           niter=int(g["niter"]), tol=float(g["tol"]), crosspol=bool(g["crosspol"]),
                           normalise_gains=None if norm == "None" else norm, jones_type=str(g["jones"]))
-    np.testing.assert_allclose(out["gain"].data, g["gain"], atol=2e-5)
-    np.testing.assert_allclose(out["weight"].data, g["weight"], rtol=1e-4, atol=1e-6)
-    np.testing.assert_allclose(out["residual"].data, g["residual"], rtol=2e-2, atol=2e-6)
+    np.testing.assert_allclose(out["gain"].data, g["gain"], atol=1e-6)
+    np.testing.assert_allclose(out["weight"].data, g["weight"], rtol=1e-6, atol=1e-12)
+    np.testing.assert_allclose(out["residual"].data, g["residual"], rtol=1e-5, atol=1e-7)
 
 
 def test_zero_model_raises():
@@ -112,6 +120,6 @@ def test_irregular_baselines_match_oracle(nants):
                                         np.zeros((nants, nchan, 1, 1)), niter=12, tol=0.0,
                                         phase_only=False)
         assert int(used[s]) == eu
-        np.testing.assert_allclose(gain[s].cpu().numpy(), eg, atol=2e-5)
-        np.testing.assert_allclose(gwt[s].cpu().numpy(), ew, rtol=1e-4, atol=1e-12)
-        np.testing.assert_allclose(res[s].cpu().numpy(), er, rtol=1e-3, atol=1e-6)
+        np.testing.assert_allclose(gain[s].cpu().numpy(), eg, atol=1e-6)
+        np.testing.assert_allclose(gwt[s].cpu().numpy(), ew, rtol=1e-6, atol=1e-12)
+        np.testing.assert_allclose(res[s].cpu().numpy(), er, rtol=1e-5, atol=1e-7)
