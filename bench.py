@@ -57,6 +57,16 @@ def parse():
     ap.add_argument("--cpu-chans", type=int, default=8,
                     help="channels in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_k_grid.json"))
+    ap.add_argument("--config", choices=("c2", "c4"), default="c2",
+                    help="c2: configs[1], weak scaling (default); c4: configs[3], the SKA-LOW "
+                         "256-channel band on the 8192^2 image, strong scaling")
+    ap.add_argument("--c4-batch", type=int, default=36,
+                    help="c4: max channels per streamed batch of a rank's block (a block is "
+                         "split into that many near-equal batches; 36 keeps one batch per "
+                         "rank at N = 8 and fits the 71 resident planes beside it)")
+    ap.add_argument("--emulate", default=None, metavar="RANK/WORLD",
+                    help="c4 on one GPU: run only rank RANK's block of a WORLD-way partition "
+                         "(no collective), to measure per-rank times")
     return ap.parse_args()
 
 
@@ -99,6 +109,163 @@ def cpu_baseline(args, umax, nchan_total):
                        f"{nvis_full / nvis_s:.0f}x + FFT/screen once")}
 
 
+# ---------------------------------------------------------------------------
+# C4: SKA-LOW 512 stations x 400 times x 256 channels (13.4 Gvis), 8192^2 image
+# ---------------------------------------------------------------------------
+C4_NCHAN, C4_NTIMES, C4_NPIX, C4_FLO, C4_FHI = 256, 400, 8192, 50e6, 350e6
+
+
+def run_c4(args, world, rank, local, dev, emulated=False):
+    """Strong scaling of configs[3]: the fixed 256-channel band is split into
+    `world` contiguous channel blocks balanced by the measured cost model
+    (parallel.balanced_channel_blocks); each rank streams its block through
+    one set of resident w planes in batches of --c4-batch channels
+    (kernels.ms2dirty_batch: one plane layout, one FFT pass per rank), then
+    one all-reduce of the 8192^2 fp64 image.  At N = 1 the single GPU
+    streams all 256 channels through the band's 71 planes.  Inputs: the
+    rank's uvw (52.3 M rows) resident; the batches' visibilities are resident
+    when they fit (N >= 4) and the step is timed as one bracket, else each
+    batch is generated on device between timed segments (the sum of the
+    segments, then the max over ranks, is the step time)."""
+    from ska_sdp_func_python_amd import kernels, parallel, simulation
+    freqs = np.linspace(C4_FLO, C4_FHI, C4_NCHAN)
+    blocks = parallel.balanced_channel_blocks(freqs, world)
+    lo, hi = blocks[rank]
+    nb = max(1, -(-(hi - lo) // args.c4_batch))
+    cuts = [lo + (hi - lo) * i // nb for i in range(nb + 1)]
+    batches = list(zip(cuts[:-1], cuts[1:]))
+    obs = simulation.device_observation(C4_NTIMES, 1, C4_FLO, C4_FHI, config="LOW", seed=rank,
+                                        device=dev, nchan_total=C4_NCHAN, channels=[lo])
+    uvw, nrow = obs["uvw"], obs["nrow"]
+    del obs["vis"], obs["wgt"]
+    cell = 0.25 / obs["umax"]
+    freq_all = torch.as_tensor(freqs, device=dev)
+    local_freq = freq_all[lo:hi]
+    resident = world >= 4
+    gen = torch.Generator(device=dev)
+
+    def make_vis(a, e):
+        gen.manual_seed(7919 * rank + a)
+        return torch.randn((nrow, e - a), generator=gen, device=dev, dtype=torch.complex64)
+
+    store = {(a, e): make_vis(a, e) for a, e in batches} if resident else {}
+
+    def vis_of_block(a, e):
+        return store[(a + lo, e + lo)] if resident else make_vis(a + lo, e + lo)
+
+    rel = [(a - lo, e - lo) for a, e in batches]
+    out = torch.zeros((C4_NPIX, C4_NPIX), dtype=torch.float64, device=dev)
+    nvis_rank = nrow * (hi - lo)
+    seg = {"t": 0.0}
+
+    class Seg:
+        def __enter__(self):
+            torch.cuda.synchronize(dev)
+            self.t0 = time.perf_counter()
+
+        def __exit__(self, *a):
+            torch.cuda.synchronize(dev)
+            seg["t"] += time.perf_counter() - self.t0
+            return False
+
+    dist_on = world > 1 and not emulated
+
+    def barrier():
+        if dist_on:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize(dev)
+
+    infos = []
+
+    def step(timer):
+        out.zero_()
+        parallel.invert_batched_shard(uvw, local_freq, vis_of_block, rel, C4_NPIX, cell, 1e-12,
+                                      True, flip_uw=True, out=out, timer=timer)
+
+    def reduce():
+        sw = torch.tensor([float(nrow * C4_NCHAN)], dtype=torch.float64, device=dev)
+        if dist_on:
+            dist.all_reduce(out, op=dist.ReduceOp.SUM)
+        out.div_(sw)
+
+    kernels.set_stage_timing(False)
+    for _ in range(args.warmup):
+        step(None)
+        reduce()
+    barrier()
+    if resident:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(None)
+            reduce()
+        barrier()
+        elapsed = time.perf_counter() - t0
+    else:
+        for _ in range(args.steps):
+            step(Seg)
+            barrier()
+            with Seg():
+                reduce()
+        barrier()
+        elapsed = seg["t"]
+    # one extra, untimed pass with stage timing for the kernel breakdown
+    kernels.set_stage_timing(True)
+    orig = kernels.ms2dirty_batch
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        infos.append(r[1])
+        return r
+
+    kernels.ms2dirty_batch = spy
+    step(None)
+    kernels.ms2dirty_batch = orig
+    kernels.set_stage_timing(False)
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = elapsed / args.steps * 1e3
+    nvis_total = nrow * C4_NCHAN
+    if emulated:
+        print(json.dumps({"emulated_rank": rank, "world": world, "block": blocks[rank],
+                          "ms_per_step": round(ms_step, 3), "nvis_rank": nvis_rank,
+                          "model_ms": round(parallel.c4_block_cost(freqs[lo:hi]), 1),
+                          "note": "rank's block only; no all-reduce"}), flush=True)
+        return
+    value = nvis_total / (elapsed / args.steps) / 1e6
+    info = infos[-1]
+    ms_grid = float(sum(i["ms_grid"] for i in infos))
+    alg = sum(nrow * (e - a) * (8 + 24.0 / (e - a)) for a, e in batches) + \
+        len(batches) * info["nplanes"] * info["ngrid_x"] * info["ngrid_y"] * 8
+    achieved = alg / (ms_grid * 1e-3) / 1e9 if ms_grid > 0 else None
+    model = [round(parallel.c4_block_cost(freqs[a:e]), 1) for a, e in blocks]
+    if rank == 0 and not emulated:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "Mvis/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded SKA-LOW-like layout, N(0,1) c64 vis, unit weights, "
+                    "generated on device)",
+            "config": {"workload": "C4: SKA-LOW 512 stations x 400 times x 256 chan (50-350 MHz) "
+                                   "= 13.4 Gvis, 8192^2 image, 16384^2 w-stack grid",
+                       "nvis_total": nvis_total, "npix": C4_NPIX, "cell_rad": cell,
+                       "channel_blocks": blocks, "model_ms_per_rank": model,
+                       "rank0_batches": len(batches), "inputs_resident": resident,
+                       "support": info["support"], "nplanes_rank0": info["nplanes"],
+                       "parallelism": f"channel blocks x{world}, streamed batches, 1 all-reduce"},
+            "stages_ms_rank0": {k: round(float(sum(i[k] for i in infos)), 3)
+                                for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": None, "kernel": f"k_grid_reg<{info['support']},true> (sub-sorted)",
+                         "kernel_ms_rank0": round(ms_grid, 3)},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,6 +277,15 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.config == "c4":
+        if args.emulate and world == 1:
+            er, ew = (int(x) for x in args.emulate.split("/"))
+            run_c4(args, ew, er, local, dev, emulated=True)
+        else:
+            run_c4(args, world, rank, local, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from ska_sdp_func_python_amd import kernels, parallel, simulation
 

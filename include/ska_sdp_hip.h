@@ -40,6 +40,8 @@ extern "C" {
 /* ---- flags for the NUFFT pair ------------------------------------------ */
 #define SDP_HIP_FLIP_UW 1u    /* negate u and w on the fly (RASCIL, ng.py:210-213) */
 #define SDP_HIP_ACCUMULATE 2u /* add into the output instead of overwriting      */
+#define SDP_HIP_BATCH_FIRST 4u /* sdp_hip_ms2dirty_batch: first batch (zero the planes) */
+#define SDP_HIP_BATCH_LAST 8u  /* sdp_hip_ms2dirty_batch: last batch (FFT + screens)    */
 
 /* Diagnostics filled by the NUFFT entry points (may be NULL). */
 typedef struct sdp_hip_wgrid_info {
@@ -94,6 +96,35 @@ int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride,
                      int64_t dirty_stride_y, void *stream,
                      sdp_hip_wgrid_info *info, char *errbuf,
                      size_t errbuf_len);
+
+/*
+ * sdp_hip_ms2dirty_batch -- sdp_hip_ms2dirty over a sequence of visibility
+ * batches that share one w-plane layout and one set of resident uv planes
+ * (a band too large for one call, e.g. the 13.4 Gvis of C4 on fewer than 8
+ * GPUs, streamed through the device channel block by channel block).  Every
+ * call of a sequence passes the same image geometry, epsilon, do_wstacking,
+ * FLIP_UW and `bounds`; the first carries SDP_HIP_BATCH_FIRST (planes
+ * zeroed), the last SDP_HIP_BATCH_LAST (FFT, w-screens, grid correction into
+ * `dirty`, which may be NULL before).  The result equals one sdp_hip_ms2dirty
+ * call over all batches with that plane layout.
+ * bounds   host {min w, max w, max|u|, max|v|} over ALL batches in metres
+ *          (uvw as given, before FLIP_UW) and {min freq, max freq} over all
+ *          batches' frequencies (6 doubles)
+ * Replaces the reference's per-(pol, chan) ducc0 loop as a streaming form of
+ * ms2dirty (ng.py:259-289); the planes must all fit on the device.
+ */
+int sdp_hip_ms2dirty_batch(const double *uvw, int64_t uvw_row_stride,
+                           const double *freq, int nchan, int64_t nrow,
+                           const void *vis, int vis_dtype,
+                           int64_t vis_row_stride, int64_t vis_chan_stride,
+                           const float *wgt, int64_t wgt_row_stride,
+                           int64_t wgt_chan_stride, int npix_x, int npix_y,
+                           double pixsize_x, double pixsize_y, double epsilon,
+                           int do_wstacking, unsigned flags,
+                           const double *bounds, double *dirty,
+                           int64_t dirty_stride_x, int64_t dirty_stride_y,
+                           void *stream, sdp_hip_wgrid_info *info,
+                           char *errbuf, size_t errbuf_len);
 
 /*
  * sdp_hip_ms2dirty_vis -- sdp_hip_ms2dirty with the visibility-side prologue

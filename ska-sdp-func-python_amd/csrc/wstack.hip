@@ -1624,6 +1624,10 @@ struct Inputs {
     int do_w;
     unsigned flags;
     VisExtra x{};
+    // batched invert (sdp_hip_ms2dirty_batch): host {min w, max w, max |u|,
+    // max |v|} in metres (uvw as given, before FLIP_UW) and {fmin, fmax} of
+    // every batch of the sequence, so all batches share one plane layout
+    const double *bounds = nullptr;
 };
 
 // Bytes of w planes kept resident per pass: SDP_HIP_GRID_BUDGET_GB if set,
@@ -1726,9 +1730,19 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.nrow = in.nrow;
     g.dbg = std::getenv("SDP_HIP_DBG") ? std::atoi(std::getenv("SDP_HIP_DBG")) : 0;
 
-    // uvw and frequency extremes (device) -> host
+    // uvw and frequency extremes (device) -> host, or the batch sequence's
     double *hb = pinned_host<double>(0, 6);
-    {
+    if (in.bounds) {
+        const double *b = in.bounds;
+        SDP_REQUIRE(b[0] <= b[1] && b[2] >= 0 && b[3] >= 0 && b[4] > 0 && b[4] <= b[5],
+                    "bounds must be {wmin <= wmax, umax >= 0, vmax >= 0, 0 < fmin <= fmax}");
+        hb[0] = g.su > 0 ? b[0] : -b[1];  // extremes of su * w
+        hb[1] = g.su > 0 ? b[1] : -b[0];
+        hb[2] = b[2];
+        hb[3] = b[3];
+        hb[4] = b[4];
+        hb[5] = b[5];
+    } else {
         auto *part = scratch<double>("bounds_part", 4 * kBoundsBlocks);
         auto *bnd = scratch<double>("bounds", 6);
         const int nb = (int)std::max<int64_t>(
@@ -1741,8 +1755,9 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     const double fmin_ = hb[4], fmax_ = hb[5];
     SDP_REQUIRE(fmin_ > 0, "frequencies must be positive");
     const double slo = fmin_ / kCLight, shi = fmax_ / kCLight;
-    const double wmin = in.nrow > 0 ? std::min(hb[0] * slo, hb[0] * shi) : 0.0;
-    const double wmax = in.nrow > 0 ? std::max(hb[1] * slo, hb[1] * shi) : 0.0;
+    const bool any = in.nrow > 0 || in.bounds;
+    const double wmin = any ? std::min(hb[0] * slo, hb[0] * shi) : 0.0;
+    const double wmax = any ? std::max(hb[1] * slo, hb[1] * shi) : 0.0;
     const double umax = hb[2] * shi, vmax = hb[3] * shi;
     SDP_REQUIRE(std::isfinite(wmin) && std::isfinite(wmax) && std::isfinite(umax) &&
                     std::isfinite(vmax),
@@ -2271,6 +2286,15 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     tm.mark();
     Plan P = plan_geometry(in, true, st);
     const Geo &g = P.g;
+    // batched invert: planes zeroed by the first batch, FFT + screens by the
+    // last; in between they stay resident in the workspace
+    const bool batched = in.bounds != nullptr;
+    const bool first = !batched || (in.flags & SDP_HIP_BATCH_FIRST);
+    const bool last = !batched || (in.flags & SDP_HIP_BATCH_LAST);
+    if (batched) {
+        SDP_REQUIRE(P.chunk_planes == g.nplanes,
+                    "batched invert: the w planes do not all fit in device memory");
+    }
     const double *tab = phi_table(g.W, g.beta, st);
     std::vector<hipEvent_t> ev = bucket_parts(P, in, true, st);
     if (P.subsort) subsort_parts(P, st);
@@ -2279,7 +2303,7 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
-        zero_band(P, np, st);
+        if (first) zero_band(P, np, st);
         for (size_t i = 0; i < P.parts.size(); ++i) {
             if (!ev.empty()) SDP_HIP_CHECK(hipStreamWaitEvent(st, ev[i], 0));
             StageTimer tg(st);
@@ -2291,7 +2315,7 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
             tg.mark();
             tgrid += tg.ms(0, 1);
         }
-        for (int sb = 0; sb < np; sb += P.fft_planes) {
+        for (int sb = 0; last && sb < np; sb += P.fft_planes) {
             const int nb = std::min(P.fft_planes, np - sb);
             StageTimer t2(st);
             t2.mark();
@@ -2471,6 +2495,30 @@ int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride, const double *fr
                                 vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
                                 npix_x,      npix_y,          pixsize_x,      pixsize_y,
                                 epsilon,     do_wstacking,    flags};
+        wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
+    });
+}
+
+int sdp_hip_ms2dirty_batch(const double *uvw, int64_t uvw_row_stride, const double *freq,
+                           int nchan, int64_t nrow, const void *vis, int vis_dtype,
+                           int64_t vis_row_stride, int64_t vis_chan_stride, const float *wgt,
+                           int64_t wgt_row_stride, int64_t wgt_chan_stride, int npix_x,
+                           int npix_y, double pixsize_x, double pixsize_y, double epsilon,
+                           int do_wstacking, unsigned flags, const double *bounds,
+                           double *dirty, int64_t dirty_stride_x, int64_t dirty_stride_y,
+                           void *stream, sdp_hip_wgrid_info *info, char *errbuf,
+                           size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(freq != nullptr && (uvw != nullptr || nrow == 0) && bounds != nullptr,
+                    "null pointer argument");
+        SDP_REQUIRE(dirty != nullptr || !(flags & SDP_HIP_BATCH_LAST),
+                    "the last batch needs the dirty image");
+        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                          nrow,        vis,             vis_dtype,      vis_row_stride,
+                          vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
+                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                          epsilon,     do_wstacking,    flags};
+        in.bounds = bounds;
         wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
     });
 }

@@ -27,6 +27,8 @@ SDP_HIP_C128 = 4
 
 SDP_HIP_FLIP_UW = 1
 SDP_HIP_ACCUMULATE = 2
+SDP_HIP_BATCH_FIRST = 4
+SDP_HIP_BATCH_LAST = 8
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
@@ -73,6 +75,14 @@ SIGNATURES = {
         c_vp, c_int, c_i64, c_i64,                # vis, dtype, strides
         c_vp, c_i64, c_i64,                       # wgt, strides
         c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,
+        c_vp, c_i64, c_i64,                       # dirty, strides
+        c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
+    "sdp_hip_ms2dirty_batch": [
+        c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
+        c_vp, c_int, c_i64, c_i64,                # vis, dtype, strides
+        c_vp, c_i64, c_i64,                       # wgt, strides
+        c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,
+        c_vp,                                     # bounds (host, 6 doubles)
         c_vp, c_i64, c_i64,                       # dirty, strides
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_ms2dirty_vis": [

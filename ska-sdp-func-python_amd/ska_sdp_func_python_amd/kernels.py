@@ -108,6 +108,70 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
     return out, info.as_dict()
 
 
+def uvw_bounds(uvw, freq):
+    """Host {min w, max w, max|u|, max|v|, min f, max f} of device arrays uvw
+    [nrow, 3] (metres) and freq: one batch's contribution to the bounds of
+    an ms2dirty_batch sequence (combine with merge_bounds)."""
+    _check_uvw(uvw)
+    b = torch.stack([uvw[:, 2].min(), uvw[:, 2].max(), uvw[:, 0].abs().max(),
+                     uvw[:, 1].abs().max(), freq.min().double(), freq.max().double()])
+    return [float(x) for x in b.cpu()]
+
+
+def merge_bounds(*bs):
+    return [min(b[0] for b in bs), max(b[1] for b in bs), max(b[2] for b in bs),
+            max(b[3] for b in bs), min(b[4] for b in bs), max(b[5] for b in bs)]
+
+
+def ms2dirty_batch(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y, bounds,
+                   first, last, epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
+                   out_strides=None, accumulate=False):
+    """One batch of a batched invert (sdp_hip_ms2dirty_batch): the batch is
+    gridded into the resident w planes shared by the whole sequence; the
+    ``first`` batch zeroes them, the ``last`` runs the FFT and w-screens into
+    ``out`` (allocated if None; earlier batches return None).  ``bounds``:
+    merge_bounds over every batch of the sequence."""
+    _eps_note(epsilon)
+    _check_uvw(uvw)
+    dev = uvw.device
+    freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
+    nrow, nchan = uvw.shape[0], freq.shape[0]
+    if vis is not None:
+        _on_gpu(vis, "vis")
+        if vis.dtype not in (torch.complex64, torch.complex128) or tuple(vis.shape) != (nrow, nchan):
+            raise ValueError("vis must be complex [nrow, nchan]")
+    if wgt is not None:
+        _on_gpu(wgt, "wgt")
+        if wgt.dtype != torch.float32 or tuple(wgt.shape) != (nrow, nchan):
+            raise ValueError("wgt must be float32 [nrow, nchan]")
+    if last:
+        if out is None:
+            out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=dev)
+            out_strides = (npix_y, 1)
+        elif out_strides is None:
+            out_strides = out.stride()
+        _on_gpu(out, "out")
+        if out.dtype != torch.float64:
+            raise ValueError("dirty output must be float64")
+    if len(bounds) != 6:
+        raise ValueError("bounds: {wmin, wmax, umax, vmax, fmin, fmax}")
+    bbuf = (ctypes.c_double * 6)(*[float(x) for x in bounds])
+    flags = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+             | (_lib.SDP_HIP_BATCH_FIRST if first else 0) | (_lib.SDP_HIP_BATCH_LAST if last else 0))
+    info = _lib.WGridInfo()
+    _lib.call(
+        "sdp_hip_ms2dirty_batch",
+        _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
+        _ptr(vis), _DT_CODE[vis.dtype] if vis is not None else _lib.SDP_HIP_C64,
+        vis.stride(0) if vis is not None else 0, vis.stride(1) if vis is not None else 0,
+        _ptr(wgt), wgt.stride(0) if wgt is not None else 0, wgt.stride(1) if wgt is not None else 0,
+        int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
+        int(bool(do_wstacking)), flags, ctypes.cast(bbuf, ctypes.c_void_p),
+        _ptr(out if last else None), int(out_strides[0]) if last else 0,
+        int(out_strides[1]) if last else 0, _stream(dev), ctypes.byref(info))
+    return (out if last else None), info.as_dict()
+
+
 def _host3(v):
     """(l, m, n-1) as a host double[3] for the C ABI, or NULL."""
     if v is None:

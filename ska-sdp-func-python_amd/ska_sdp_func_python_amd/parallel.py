@@ -27,6 +27,99 @@ def interleaved_channels(nchan_total, rank, world):
     return np.arange(rank, nchan_total, world)
 
 
+# Cost model of one rank's invert of a contiguous channel block of the C4
+# band (SKA-LOW 512 stations x 400 times, 8192^2 image, 16384^2 grid),
+# fitted to the per-block stage times measured on one MI355X
+# (profiles/r02_c4_blocks.jsonl): bucketing + gridding per channel (higher in
+# the compact low band, whose uv core concentrates the histogram atomics)
+# plus FFT + w-screen per resident w plane, the plane count growing with the
+# block's top frequency (w range in wavelengths ~ f_hi).
+C4_CHAN_COST = ((68.75e6, 8.09), (106.25e6, 6.67), (143.75e6, 6.47), (181.25e6, 6.39),
+                (218.75e6, 6.39), (256.25e6, 6.39), (293.75e6, 6.39), (331.25e6, 6.82))
+C4_PLANE_MS = 1.58
+C4_PLANES = (0.179e-6, 8.33)  # nplanes ~ a f_hi + b
+
+
+def c4_block_cost(freqs):
+    """Modelled invert time (ms) of one rank holding the channels `freqs`
+    (one shared plane layout, one FFT pass)."""
+    f = np.asarray(freqs, dtype=float)
+    if f.size == 0:
+        return 0.0
+    xs, ys = zip(*C4_CHAN_COST)
+    per_chan = float(np.interp(f, xs, ys).sum())
+    return per_chan + C4_PLANE_MS * (C4_PLANES[0] * float(f.max()) + C4_PLANES[1])
+
+
+def balanced_channel_blocks(freqs, world, cost=c4_block_cost):
+    """Contiguous channel blocks [(lo, hi)] for `world` ranks whose modelled
+    costs are as equal as possible (minimise the maximum: bisection on the
+    target with a greedy sweep).  Contiguous blocks keep each rank's w range
+    (hence its plane count) small; the cost model moves channels from the
+    high band, which carries the most w planes, to the low band."""
+    n = len(freqs)
+    if world <= 1:
+        return [(0, n)]
+
+    def sweep(target):
+        blocks, lo = [], 0
+        for r in range(world):
+            hi = lo
+            while hi < n and (hi == lo or cost(freqs[lo:hi + 1]) <= target) and \
+                    n - (hi + 1) >= world - r - 1:
+                hi += 1
+            if r == world - 1:
+                hi = n
+            blocks.append((lo, hi))
+            lo = hi
+        return blocks
+
+    lo_t, hi_t = 0.0, cost(freqs)
+    for _ in range(60):
+        mid = 0.5 * (lo_t + hi_t)
+        b = sweep(mid)
+        if max(cost(freqs[a:e]) for a, e in b) <= mid:
+            hi_t = mid
+        else:
+            lo_t = mid
+    return sweep(hi_t)
+
+
+def invert_batched_shard(uvw, freq, vis_of_block, blocks, npix, cell, epsilon=1e-7,
+                         do_wstacking=True, flip_uw=True, out=None, timer=None):
+    """Invert one rank's channels as a sequence of channel blocks streamed
+    through shared resident w planes (kernels.ms2dirty_batch: one plane
+    layout from the merged bounds, one FFT pass).  ``vis_of_block(a, e)``
+    returns the [nrow, e - a] device visibilities of channels a..e (generated
+    or loaded on demand); ``timer`` (optional) is a context-manager factory
+    wrapped around each device call so the caller can exclude the input
+    staging from its timing.  Unit weights.  Returns the dirty image in
+    RASCIL [y, x] order (unnormalised) accumulated into ``out``."""
+    from . import kernels
+    dev = uvw.device
+    if out is None:
+        out = torch.zeros((npix, npix), dtype=torch.float64, device=dev)
+    b = kernels.merge_bounds(*[kernels.uvw_bounds(uvw, freq[a:e]) for a, e in blocks])
+    for i, (a, e) in enumerate(blocks):
+        vis = vis_of_block(a, e)
+        ctx = timer() if timer else _nullctx()
+        with ctx:
+            kernels.ms2dirty_batch(uvw, freq[a:e], vis, None, npix, npix, cell, cell, b,
+                                   first=i == 0, last=i == len(blocks) - 1, epsilon=epsilon,
+                                   do_wstacking=do_wstacking, flip_uw=flip_uw, out=out,
+                                   out_strides=(1, npix), accumulate=True)
+        del vis
+    return out
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def _gridder():
     from . import kernels
     return kernels.ms2dirty

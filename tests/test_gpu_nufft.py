@@ -508,3 +508,33 @@ def test_fused_phase_shift_invert_and_predict(device):
     got = out.vis.data.cpu().numpy() if device else out.vis.data
     assert rel_rms(got[..., 0], pred) < TOL
     assert out.phasecentre.separation(ipc).rad < 1e-12
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_batched_invert_equals_single_call(flip, monkeypatch):
+    """sdp_hip_ms2dirty_batch: three channel blocks gridded into shared
+    resident planes and transformed once equal one ms2dirty over all the
+    channels (same plane layout from the merged bounds); a plane layout that
+    does not fit the device is refused."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(21, nrow=4000, nchan=6, umax=6000.0)
+    U, F, M, Wt = T(uvw), T(freq), T(ms), T(wgt)
+    full, info = kernels.ms2dirty(U, F, M, Wt, 256, 192, cell, cell, 1e-7, True, flip_uw=flip)
+    blocks = [(0, 2), (2, 3), (3, 6)]
+    b = kernels.merge_bounds(*[kernels.uvw_bounds(U, F[a:e]) for a, e in blocks])
+    out = None
+    for i, (a, e) in enumerate(blocks):
+        out, binfo = kernels.ms2dirty_batch(U, F[a:e], M[:, a:e].contiguous(),
+                                            Wt[:, a:e].contiguous(), 256, 192, cell, cell, b,
+                                            first=i == 0, last=i == len(blocks) - 1,
+                                            epsilon=1e-7, flip_uw=flip)
+        assert (out is None) == (i < len(blocks) - 1)
+        assert binfo["nplanes"] == info["nplanes"] and binfo["w0"] == info["w0"]
+    assert rel_rms(out.cpu().numpy(), full.cpu().numpy()) < 1e-6
+    exact = orc.ms2dirty_exact(uvw * (FLIP_UW if flip else 1.0), freq, ms, wgt, 256, 192, cell,
+                               cell, True)
+    assert rel_rms(out.cpu().numpy(), exact) < TOL
+    monkeypatch.setenv("SDP_HIP_GRID_BUDGET_GB", "0.0001")
+    with pytest.raises(ValueError, match="do not all fit"):
+        kernels.ms2dirty_batch(U, F[:2], M[:, :2].contiguous(), None, 256, 192, cell, cell, b,
+                               first=True, last=False, epsilon=1e-7)

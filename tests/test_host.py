@@ -182,3 +182,16 @@ def test_epsilon_below_fp32_floor_is_reported_once(caplog):
                 kernels.ms2dirty(uvw, torch.ones(1), None, None, 8, 8, 1e-3, 1e-3, 1e-12)
     msgs = [r.getMessage() for r in caplog.records if "floor epsilon" in r.getMessage()]
     assert len(msgs) == 1 and "1.0e-12" in msgs[0]
+
+
+def test_balanced_channel_blocks_cover_and_balance():
+    """The C4 strong-scaling partition: contiguous, covering, and within 3 % of
+    the mean modelled cost at 2/4/8 ranks (parallel.balanced_channel_blocks)."""
+    from ska_sdp_func_python_amd import parallel
+    f = np.linspace(50e6, 350e6, 256)
+    for world in (1, 2, 3, 4, 8):
+        b = parallel.balanced_channel_blocks(f, world)
+        assert len(b) == world and b[0][0] == 0 and b[-1][1] == 256
+        assert all(b[i][1] == b[i + 1][0] and b[i][0] < b[i][1] for i in range(world - 1))
+        c = [parallel.c4_block_cost(f[a:e]) for a, e in b]
+        assert max(c) <= 1.03 * (sum(c) / world)
