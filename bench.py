@@ -259,7 +259,7 @@ def run_c4(args, world, rank, local, dev, emulated=False):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": None, "kernel": f"k_grid_reg<{info['support']},true> (sub-sorted)",
+                         "traffic": None, "kernel": f"k_grid_mfma<{info['support']},true,true> (sub-sorted cells)",
                          "kernel_ms_rank0": round(ms_grid, 3)},
             "cpu_baseline": None,
         }
@@ -348,7 +348,8 @@ def main():
             traffic = json.load(f).get("bytes_per_launch")
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": (f"k_grid_reg<{info['support']},true>" if info["bucket"] == 2
+            "kernel": (f"k_grid_mfma<{info['support']},true,false>" if info["bucket"] == 1
+                       else f"k_grid_reg<{info['support']},true>" if info["bucket"] == 2
                        else f"k_grid_lds<{info['support']},true,2>"), "kernel_ms": round(ms_grid / launches, 4),
             "alg_bytes_per_launch": int(alg_bytes / launches),
             # the gridder is VALU-issue bound: the same kernel against the

@@ -47,6 +47,13 @@ constexpr double kCLight = 299792458.0;
 constexpr int kTileCoarse = 16;  // bucket edge (cells) of the LDS-tile gridder
 constexpr int kTileFine = 2;     // bucket edge (cells) of the register gridder
 constexpr int kGroupFine = 4;    // fine buckets per work-item group (along y)
+// invert on MFMA (k_grid_mfma): one-cell buckets ordered x-pair major
+// (key tile = ((ic >> 1) * ngy + jc) * 2 + (ic & 1)), so a bucket's records
+// share their footprint origin and 16 consecutive buckets form the same
+// 2 x 8-cell work-item region as kGroupFine 2x2-cell buckets
+constexpr int kTileCell = 1;
+constexpr int kGroupCell = 16;
+constexpr int64_t kMaxCellKeys = (int64_t)1 << 28;
 constexpr int kGridAlign = 16;   // padded grid edges are multiples of this
 // fine buckets are used while the dense (p0, 2x2-cell) histogram stays small
 constexpr int64_t kMaxFineKeys = (int64_t)1 << 27;
@@ -91,7 +98,7 @@ struct Item {
 // [b, e) ordered by bucket, bucket j of the group ending at o[j] (k_subsort)
 struct FineItem {
     uint32_t b, e, tile, p0;
-    uint32_t o[4];
+    uint32_t o[16];  // end of bucket j of the group (2x2 buckets: j < 4; cells: j < 16)
 };
 
 // ------------------------------------------------------------------------
@@ -164,7 +171,8 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
 
 // p0-major bucket keys: the items of a range of first planes are contiguous.
 __device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c) {
-    const int tile = (c.ic0 / g.sub) * g.nty + (c.jc0 / g.sub);
+    const int tile = g.sub == kTileCell ? ((c.ic0 >> 1) * g.ngy + c.jc0) * 2 + (c.ic0 & 1)
+                                        : (c.ic0 / g.sub) * g.nty + (c.jc0 / g.sub);
     return (unsigned)c.p0 * (unsigned)g.ntiles + (unsigned)tile;
 }
 
@@ -505,51 +513,61 @@ __global__ void k_items_fill(int64_t ngroups, int grp, int groups_per_plane,
 constexpr int kSubChunk = 4096;
 constexpr int kSubThreads = 1024;
 
+// class of a record inside its 16x16-cell item: 2x2 bucket (x pair major,
+// y pair minor; 64 classes) or, for the MFMA gridder, one cell in the
+// x-pair-major order of kTileCell keys (256 classes)
+template <bool CELLS>
 __device__ __forceinline__ int sub_class(uint32_t ij) {
     const int ic = (int)(ij & 0xffffu), jc = (int)(ij >> 16);
+    if (CELLS) return ((ic & 15) >> 1) * 32 + (jc & 15) * 2 + (ic & 1);
     return ((ic & 15) >> 1) * 8 + ((jc & 15) >> 1);
 }
 
+template <bool CELLS>
 __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__restrict__ items,
                                                  VisRec *recs, FineItem *__restrict__ fitems) {
+    constexpr int NC = CELLS ? 256 : 64;  // classes
+    constexpr int PG = NC / 16;           // classes per fine group
     __shared__ VisRec stage[kSubChunk];
-    __shared__ unsigned cur[64], first[65];
+    __shared__ unsigned cur[NC], first[NC + 1];
     const Item it = items[blockIdx.x];
     const int n = (int)(it.e - it.b);
-    if (threadIdx.x < 64) cur[threadIdx.x] = 0u;
+    for (int c = threadIdx.x; c < NC; c += kSubThreads) cur[c] = 0u;
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += kSubThreads) {
         const VisRec r = recs[it.b + i];
         stage[i] = r;
-        atomicAdd(&cur[sub_class(r.ij)], 1u);
+        atomicAdd(&cur[sub_class<CELLS>(r.ij)], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned a = 0;
-        for (int c = 0; c < 64; ++c) {
+        for (int c = 0; c < NC; ++c) {
             first[c] = a;
             a += cur[c];
         }
-        first[64] = a;
+        first[NC] = a;
     }
     __syncthreads();
-    if (threadIdx.x < 64) cur[threadIdx.x] = first[threadIdx.x];
+    for (int c = threadIdx.x; c < NC; c += kSubThreads) cur[c] = first[c];
     if (threadIdx.x < 16) {
-        const int xp = threadIdx.x >> 1, hf = threadIdx.x & 1, c0 = xp * 8 + hf * 4;
+        // fine group gi = 2 * (x pair) + (y half): a 2 x 8-cell region
+        const int gi = threadIdx.x, xp = gi >> 1, hf = gi & 1;
+        const int c0 = CELLS ? gi * PG : xp * 8 + hf * 4;
         FineItem f;
         f.b = it.b + first[c0];
-        f.e = it.b + first[c0 + 4];
+        f.e = it.b + first[c0 + PG];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) f.o[j] = it.b + first[c0 + j + 1];
+        for (int j = 0; j < 16; ++j) f.o[j] = it.b + first[c0 + min(j + 1, PG)];
         const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
-        f.tile = (uint32_t)((tx * 8 + xp) * (g.ngy / (kTileFine * kGroupFine)) + ty * 2 + hf);
+        f.tile = (uint32_t)((tx * 8 + xp) * (g.ngy / 8) + ty * 2 + hf);
         f.p0 = it.p0;
         fitems[(size_t)blockIdx.x * 16 + threadIdx.x] = f;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += kSubThreads) {
         const VisRec r = stage[i];
-        const unsigned pos = atomicAdd(&cur[sub_class(r.ij)], 1u);
+        const unsigned pos = atomicAdd(&cur[sub_class<CELLS>(r.ij)], 1u);
         recs[it.b + pos] = r;
     }
 }
@@ -602,8 +620,9 @@ __device__ __forceinline__ Item load_item(const ItemSrc &src, uint32_t w, uint32
     return it;
 }
 
+template <int NO>
 __device__ __forceinline__ Item load_fine_item(const FineItem *items, uint32_t w, uint32_t n,
-                                               uint32_t stride, uint32_t (&fo)[4]) {
+                                               uint32_t stride, uint32_t (&fo)[NO]) {
     const uint32_t i = (uint32_t)(((uint64_t)w * stride) % n);
     const FineItem raw = items[i];
     Item it;
@@ -612,7 +631,7 @@ __device__ __forceinline__ Item load_fine_item(const FineItem *items, uint32_t w
     it.tile = __builtin_amdgcn_readfirstlane(raw.tile);
     it.p0 = __builtin_amdgcn_readfirstlane(raw.p0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fo[j] = __builtin_amdgcn_readfirstlane(raw.o[j]);
+    for (int j = 0; j < NO; ++j) fo[j] = __builtin_amdgcn_readfirstlane(raw.o[j]);
     return it;
 }
 
@@ -948,6 +967,214 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
                         atomicAdd(dst, val);
                     }
                 }
+            }
+        }
+    }
+}
+
+// MFMA gridder (invert): one wave per work item = a chunk of the records of
+// a 2 x 8-cell region (16 one-cell buckets, same first plane p0; records
+// ordered by cell).  All records of a cell share their footprint origin, so
+// a cell's contribution to its W x W x W footprint is one GEMM
+//     C[(kx, ky), (q, re/im)] += sum_r  tu_r[kx] tv_r[ky] * tw_r[q] c_r
+// with A = the separable (u, v) taps (64 rows) and B = the w taps x value
+// (8 planes x re/im = 16 columns), K = records: v_mfma_f32_16x16x4_f32
+// (exact fp32 multiply-adds), 4 M-tiles of 16 taps, 4 records per K-step.
+//
+// Records stream through the wave 64 at a time (one per lane, one coalesced
+// 2 KiB load, the next batch prefetched while this one is consumed).  Inside
+// a batch the cell runs are found with ballots; a run is consumed in K-steps
+// of 4 records (lanes k0..k0+3; the tail K-step of a run carries zero
+// values).  In a K-step, lane l gathers the fields of record k0 + (l >> 4)
+// (ds_bpermute) and evaluates its 1-D taps (l & 7) for u, v and w; the MFMA
+// operands are those taps permuted inside the 16-lane record group:
+// A[row][k] = tu[2t + (row >> 3)] tv[row & 7], B[k][col] = tw[col >> 1] x
+// (re | im of c).  When the cell changes, the four 16 x 16 accumulators are
+// added into the region's (2+W-1) x (8+W-1) x W LDS tile, which is flushed
+// once per item with global float atomics (zero cells skipped), exactly as
+// k_grid_reg.  Per record: one MFMA, ~8 VALU, 2.5 ds_bpermute -- versus 24
+// VALU, 7.6 SALU and 4 LDS instructions in k_grid_reg.
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bperm(int byte_addr, float v) {
+    return __builtin_bit_cast(float,
+                              __builtin_amdgcn_ds_bpermute(byte_addr, __builtin_bit_cast(int, v)));
+}
+
+// ES kernel for the MFMA gridder's taps: x = fu*ihw + t*ihw by one fma; for
+// W = 8 every tap of the footprint lies inside the support (|x| <= 1), so
+// no range select (the max() only guards rounding below zero)
+template <int W>
+__device__ __forceinline__ float es_tap(float f, float tihw, float ihw, float bl) {
+    const float x = fmaf(f, ihw, tihw);
+    const float y = fmaf(-x, x, 1.0f);
+    const float e = __builtin_amdgcn_exp2f(fmaf(bl, __builtin_amdgcn_sqrtf(fmaxf(y, 0.0f)), -bl));
+    return W == 8 ? e : (y > 0.0f ? e : 0.0f);
+}
+
+template <int W, bool WS, bool FI>
+__global__ __launch_bounds__(64) void k_grid_mfma(Geo g, const VisRec *__restrict__ recs,
+                                                  ItemSrc src, const unsigned *__restrict__ offs,
+                                                  const FineItem *__restrict__ fitems,
+                                                  float *__restrict__ grid, int p_lo, int p_hi) {
+    static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
+    // LDS: the region tile (W planes x RX x RY complex) + the staged batch
+    // (64 records: fu fv fw - | cre cim - - as two float4 rows per record)
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
+    constexpr int NQ = WS ? W : 1;
+    float4 *const stage = reinterpret_cast<float4 *>(tile + NQ * PS);  // [64][2]
+    (void)offs;
+    const uint32_t n_items = item_count(src);
+    const uint32_t stride = item_stride(n_items);
+    const int lane = threadIdx.x;
+    const float ihw = g.inv_half_w, bl = g.beta_l2e;
+    const float tihw = (float)(lane & 7) * ihw;
+    const int grp16 = lane & ~15;
+    const int srcA = (grp16 | ((lane >> 3) & 1)) << 2;  // + 8 t bytes: tu tap 2t + (row >> 3)
+    const int srcB = (grp16 | ((lane & 15) >> 1)) << 2;   // tw tap q = col >> 1
+    const bool col_im = lane & 1;
+    // accumulator element i of M-tile t: tap (2t + (lane >> 5), 4 ((lane >> 4) & 1) + i),
+    // column (q, re/im) = ((lane & 15) >> 1, lane & 1)
+    const int cq = (lane & 15) >> 1;
+    const int ckx = lane >> 5, cky = 4 * ((lane >> 4) & 1);
+    float *const ftile = reinterpret_cast<float *>(tile);
+
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        Item it;
+        if (FI) {
+            uint32_t fo[1];
+            it = load_fine_item<1>(fitems, w_it, n_items, stride, fo);
+            if (it.b >= it.e) continue;
+        } else {
+            it = load_item(src, w_it, n_items, stride);
+        }
+        const int ntg = g.ngy / 8;
+        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
+        const int ibase = sx * 2, jbase = sg * 8;
+
+        __syncthreads();
+        for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
+
+        floatx4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+        int cur = -1;  // cell of the accumulators (wave-uniform)
+        auto flush_cell = [&]() {
+            const int xo = cur & 1, yo = cur >> 1;
+            if (cq < NQ) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int kx = 2 * t + ckx;
+                    if (kx >= W) continue;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int ky = cky + i;
+                        if (ky >= W) continue;
+                        float *d = ftile + ((cq * RX + xo + kx) * RY + yo + ky) * 2 + (col_im ? 1 : 0);
+                        *d += acc[t][i];
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+        };
+        // one K-step: records k0 .. k0+3 of the staged batch (lane >> 4 picks
+        // the record), valid below `rend`; operands A[t], B
+        auto prep = [&](int k0, int rend, float (&A)[4], float &B) {
+            const int kl = k0 + (lane >> 4);
+            const float4 h = stage[2 * min(kl, 63)];      // fu fv fw -
+            const float4 c = stage[2 * min(kl, 63) + 1];  // cre cim - -
+            const float tu = es_tap<W>(h.x, tihw, ihw, bl);
+            const float tv = es_tap<W>(h.y, tihw, ihw, bl);
+            const float tw = WS ? es_tap<W>(h.z, tihw, ihw, bl) : ((lane & 7) == 0 ? 1.0f : 0.0f);
+            const float keep = kl < rend ? 1.0f : 0.0f;
+            B = bperm(srcB, tw) * (col_im ? c.y : c.x) * keep;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) A[t] = bperm(srcA + 8 * t, tu) * tv;
+        };
+
+        // batch = 64 records, lane l holds record b0 + l (staged in LDS); the
+        // next batch is loaded before this one is consumed
+        VisRec nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
+        for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+            const VisRec my = nx;
+            if (b0 + 64 < it.e) nx = recs[min(b0 + 64 + (uint32_t)lane, it.e - 1)];
+            const int nb = (int)min(64u, it.e - b0);
+            const bool live = lane < nb;
+            const int cj = live ? ((int)(my.ij >> 16) - jbase) * 2 + ((int)(my.ij & 0xffffu) - ibase)
+                                : 16;
+            __syncthreads();  // previous batch's stage reads
+            stage[2 * lane] = make_float4(my.fu, my.fv, my.fw, 0.0f);
+            stage[2 * lane + 1] = make_float4(live ? my.cre : 0.0f, live ? my.cim : 0.0f, 0.0f, 0.0f);
+            __syncthreads();
+            // run starts: lane 0, and every lane whose cell differs from the previous lane's
+            const int prev = __shfl_up(cj, 1);
+            uint64_t starts = __ballot(live && (lane == 0 || prev != cj));
+            while (starts) {
+                const int pos = __builtin_ctzll(starts);
+                starts &= starts - 1;
+                const int rend = starts ? __builtin_ctzll(starts) : nb;
+                const int cell = __builtin_amdgcn_readlane(cj, pos);
+                if (cell != cur) {
+                    if (cur >= 0) flush_cell();
+                    cur = cell;
+                }
+                int k0 = pos;
+                for (; k0 + 4 < rend; k0 += 8) {  // two K-steps
+                    float A0[4], A1[4], B0, B1;
+                    prep(k0, rend, A0, B0);
+                    prep(k0 + 4, rend, A1, B1);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[t], B0, acc[t], 0, 0, 0);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[t], B1, acc[t], 0, 0, 0);
+                }
+                if (k0 < rend) {  // last K-step of the run
+                    float A0[4], B0;
+                    prep(k0, rend, A0, B0);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[t], B0, acc[t], 0, 0, 0);
+                }
+            }
+        }
+        if (cur >= 0) flush_cell();
+        __syncthreads();
+
+        // flush: float f = i0 + lane of each plane's RX x RY complex cells,
+        // buffer atomics off a per-plane descriptor (32-bit offsets), the
+        // cell index advanced incrementally; zero floats are skipped
+        constexpr int FPP = RX * RY * 2;
+        const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
+        int xl = (lane >> 1) / RY, yl = (lane >> 1) - xl * RY;
+#pragma unroll
+        for (int i0 = 0; i0 < FPP; i0 += 64) {
+            const int f = i0 + lane;
+            if (f >= FPP) break;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            const int voff = ((gx * g.ngy + gy) * 2 + (f & 1)) * (int)sizeof(float);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int p = (int)it.p0 + q;
+                const float val = ftile[q * PS * 2 + f];
+                if (p >= p_lo && p < p_hi && val != 0.0f) {
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)), 0,
+                        (int)plane_bytes, 0x00020000);
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, rs, voff, 0, 0);
+                }
+            }
+            yl += 32 % RY;
+            xl += 32 / RY;
+            if (yl >= RY) {
+                yl -= RY;
+                ++xl;
             }
         }
     }
@@ -1596,6 +1823,7 @@ struct Plan {
     bool pipelined = false;          // row parts, persistent launches, no host syncs
     bool aux_bucketing = false;      // bucketing on the auxiliary stream
     bool subsort = false;            // 16x16 buckets re-ordered to 2x2 (register kernels)
+    bool cells = false;              // invert on k_grid_mfma: one-cell buckets / sub-sort
     float2 *vdirect = nullptr;       // dirty2ms: register degridders write c64 vis in place
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
@@ -1783,18 +2011,25 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         g.nplanes = 1;
         g.nps = 1;
     }
-    // bucket granularity: 2x2-cell buckets feed the register gridder while
-    // the dense (first plane, bucket) histogram stays below kMaxFineKeys,
-    // else 16x16-cell buckets and the LDS-tile gridder
+    // bucket granularity.  Invert: one-cell buckets for the MFMA gridder
+    // while the dense (first plane, cell) histogram stays below kMaxCellKeys
+    // (SDP_HIP_MFMA=0: the register gridder's 2x2-cell buckets).  Predict:
+    // 2x2-cell buckets for the register degridder below kMaxFineKeys.  Else
+    // 16x16-cell buckets (sub-sorted to cells / 2x2 buckets below, or the
+    // LDS-tile kernels).
     {
         const char *e = std::getenv("SDP_HIP_BUCKET");
+        const char *m = std::getenv("SDP_HIP_MFMA");
+        P.cells = grid_mode && !(m && std::atoi(m) == 0);
+        const int64_t cell = (int64_t)g.ngx * g.ngy * g.nps;
         const int64_t fine = (int64_t)(g.ngx / kTileFine) * (g.ngy / kTileFine) * g.nps;
-        g.sub = fine <= kMaxFineKeys ? kTileFine : kTileCoarse;
+        if (P.cells) g.sub = cell <= kMaxCellKeys ? kTileCell : kTileCoarse;
+        else g.sub = fine <= kMaxFineKeys ? kTileFine : kTileCoarse;
         if (e && std::atoi(e) == kTileCoarse) g.sub = kTileCoarse;
     }
     g.nty = g.ngy / g.sub;
     g.ntiles = (g.ngx / g.sub) * g.nty;
-    g.grp = g.sub == kTileFine ? kGroupFine : 1;  // nty is a multiple of kGridAlign / sub
+    g.grp = g.sub == kTileCell ? kGroupCell : (g.sub == kTileFine ? kGroupFine : 1);
     SDP_REQUIRE((double)g.ntiles * g.nps < 4.0e9, "too many (plane, tile) buckets");
 
     // grid rows reached by any footprint (centred storage)
@@ -1840,7 +2075,8 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // part split
     const char *pe = std::getenv("SDP_HIP_PIPELINE");
     const int pmode = pe ? std::atoi(pe) : 0;
-    P.pipelined = pmode == 2 && g.sub == kTileFine && P.chunk_planes == g.nplanes && in.nrow >= 2;
+    P.pipelined = pmode == 2 && (g.sub == kTileFine || g.sub == kTileCell) &&
+                  P.chunk_planes == g.nplanes && in.nrow >= 2;
     P.aux_bucketing = P.pipelined || (pmode == 1 && !grid_mode);
     const int nparts = P.pipelined ? kPipelineParts : 1;
     for (int i = 0; i < nparts; ++i) {
@@ -2085,8 +2321,33 @@ static void launch_degrid_fine_items(const Plan &P, const Part &pt, int p_lo, in
                                                   p_hi, acc + pt.vbase, P.vdirect);
 }
 
+template <int W, bool WS>
+static void launch_grid_mfma(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
+    const size_t lds = (size_t)(WS ? W : 1) * (2 + W - 1) * (8 + W - 1) * sizeof(float2) +
+                       128 * sizeof(float4);
+    if (P.subsort) {
+        const auto r = chunk_items(P, pt, p_lo, p_hi);
+        const unsigned n = 16u * (r.second - r.first);
+        if (n == 0) return;
+        k_grid_mfma<W, WS, true><<<n, 64, lds, st>>>(P.g, P.recs + pt.vbase,
+                                                     ItemSrc{nullptr, n, nullptr}, nullptr,
+                                                     pt.fitems + 16 * (size_t)r.first,
+                                                     (float *)P.grid, p_lo, p_hi);
+        return;
+    }
+    const void *fn = (const void *)k_grid_mfma<W, WS, false>;
+    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
+    if (L.blocks == 0) return;
+    k_grid_mfma<W, WS, false><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
+                                                        nullptr, (float *)P.grid, p_lo, p_hi);
+}
+
 template <int W>
 static void launch_grid(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
+    if (P.cells && (P.subsort || P.g.sub == kTileCell)) {
+        if (P.g.do_w) return launch_grid_mfma<W, true>(P, pt, p_lo, p_hi, st);
+        return launch_grid_mfma<W, false>(P, pt, p_lo, p_hi, st);
+    }
     if (P.subsort) {
         if (P.g.do_w) return launch_grid_fine_items<W, true>(P, pt, p_lo, p_hi, st);
         return launch_grid_fine_items<W, false>(P, pt, p_lo, p_hi, st);
@@ -2267,7 +2528,12 @@ static void subsort_parts(Plan &P, hipStream_t st) {
         Part &pt = P.parts[i];
         if (pt.nitems == 0) continue;
         pt.fitems = scratch<FineItem>("fitems#" + std::to_string(i), (size_t)pt.nitems * 16);
-        k_subsort<<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(P.g, pt.items, P.recs + pt.vbase, pt.fitems);
+        if (P.cells)
+            k_subsort<true><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(
+                P.g, pt.items, P.recs + pt.vbase, pt.fitems);
+        else
+            k_subsort<false><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(
+                P.g, pt.items, P.recs + pt.vbase, pt.fitems);
         SDP_HIP_CHECK(hipGetLastError());
     }
 }

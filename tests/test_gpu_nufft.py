@@ -35,14 +35,19 @@ def _problem(seed, nrow=300, nchan=3, umax=2000.0, frac=0.45):
     return uvw, freq, ms, wgt, frac / umax
 
 
-@pytest.fixture(params=["fine", "coarse", "coarse-lds", "fine-pipelined", "fine-aux"])
+@pytest.fixture(params=["fine", "fine-reg", "coarse", "coarse-reg", "coarse-lds", "fine-pipelined",
+                        "fine-aux"])
 def bucket(request, monkeypatch):
-    """Both bucketings: 2x2-cell buckets (register kernels, the default at
-    these sizes) and 16x16-cell buckets (very large grids), whose items are
-    re-ordered to 2x2 buckets for the register kernels ("coarse") or fed to
-    the LDS-tile kernels ("coarse-lds", SDP_HIP_SUBSORT=0); and the pipelined
-    plan (two row parts bucketed on the auxiliary stream, persistent gridding
+    """Every bucketing: one-cell buckets for the MFMA gridder (invert) and
+    2x2-cell buckets for the register degridder (predict), the default at
+    these sizes; 2x2-cell buckets for the register gridder ("fine-reg",
+    SDP_HIP_MFMA=0); 16x16-cell buckets (very large grids), whose items are
+    re-ordered to cells / 2x2 buckets ("coarse", "coarse-reg") or fed to the
+    LDS-tile kernels ("coarse-lds", SDP_HIP_SUBSORT=0); and the pipelined plan
+    (two row parts bucketed on the auxiliary stream, persistent gridding
     launches)."""
+    if request.param.endswith("-reg"):
+        monkeypatch.setenv("SDP_HIP_MFMA", "0")
     if request.param.startswith("coarse"):
         monkeypatch.setenv("SDP_HIP_BUCKET", "16")
     if request.param == "coarse-lds":
@@ -66,7 +71,8 @@ def test_ms2dirty_matches_exact(dow, vdt, flip, bucket):
     out, info = kernels.ms2dirty(T(uvw), T(freq), T(ms, vdt), T(wgt), npix, 48 + 16 * dow, cell,
                                  cell * 0.9, 1e-7, dow, flip_uw=flip)
     assert info["support"] == 8
-    assert info["bucket"] == (16 if bucket.startswith("coarse") else 2)
+    assert info["bucket"] == (16 if bucket.startswith("coarse") else
+                              (2 if bucket == "fine-reg" else 1))
     assert info["grid_launches"] == (2 if bucket == "fine-pipelined" else 1)
     assert rel_rms(out.cpu().numpy(), ex) < TOL
 
