@@ -1013,7 +1013,7 @@ __device__ __forceinline__ float es_tap(float f, float tihw, float ihw, float bl
 }
 
 template <int W, bool WS, bool FI>
-__global__ __launch_bounds__(64) void k_grid_mfma(Geo g, const VisRec *__restrict__ recs,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma(Geo g, const VisRec *__restrict__ recs,
                                                   ItemSrc src, const unsigned *__restrict__ offs,
                                                   const FineItem *__restrict__ fitems,
                                                   float *__restrict__ grid, int p_lo, int p_hi) {
@@ -1080,18 +1080,40 @@ __global__ __launch_bounds__(64) void k_grid_mfma(Geo g, const VisRec *__restric
             for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
         };
         // one K-step: records k0 .. k0+3 of the staged batch (lane >> 4 picks
-        // the record), valid below `rend`; operands A[t], B
-        auto prep = [&](int k0, int rend, float (&A)[4], float &B) {
+        // the record), valid below `rend`.  Phase 1 (taps): the three 1-D
+        // taps (lane & 7) of the record and its value; phase 2 (gather): the
+        // 5 operand values from the record group's lanes; phase 3: A, B.
+        // Two K-steps are interleaved phase by phase (sched_barrier keeps
+        // every ds_bpermute of both in flight before the first use).
+        struct Taps {
+            float tu, tv, tw, cv;
+        };
+        auto taps = [&](int k0, int rend) {
             const int kl = k0 + (lane >> 4);
             const float4 h = stage[2 * min(kl, 63)];      // fu fv fw -
             const float4 c = stage[2 * min(kl, 63) + 1];  // cre cim - -
-            const float tu = es_tap<W>(h.x, tihw, ihw, bl);
-            const float tv = es_tap<W>(h.y, tihw, ihw, bl);
-            const float tw = WS ? es_tap<W>(h.z, tihw, ihw, bl) : ((lane & 7) == 0 ? 1.0f : 0.0f);
-            const float keep = kl < rend ? 1.0f : 0.0f;
-            B = bperm(srcB, tw) * (col_im ? c.y : c.x) * keep;
+            Taps r;
+            r.tu = es_tap<W>(h.x, tihw, ihw, bl);
+            r.tv = es_tap<W>(h.y, tihw, ihw, bl);
+            r.tw = WS ? es_tap<W>(h.z, tihw, ihw, bl) : ((lane & 7) == 0 ? 1.0f : 0.0f);
+            r.cv = (col_im ? c.y : c.x) * (kl < rend ? 1.0f : 0.0f);
+            return r;
+        };
+        struct Ops {
+            float u[4], w;
+        };
+        auto gather = [&](const Taps &r) {
+            Ops o;
+            o.w = bperm(srcB, r.tw);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) A[t] = bperm(srcA + 8 * t, tu) * tv;
+            for (int t = 0; t < 4; ++t) o.u[t] = bperm(srcA + 8 * t, r.tu);
+            return o;
+        };
+        auto mfma4 = [&](const Taps &r, const Ops &o) {
+            const float bop = o.w * r.cv;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.u[t] * r.tv, bop, acc[t], 0, 0, 0);
         };
 
         // batch = 64 records, lane l holds record b0 + l (staged in LDS); the
@@ -1122,22 +1144,19 @@ __global__ __launch_bounds__(64) void k_grid_mfma(Geo g, const VisRec *__restric
                 }
                 int k0 = pos;
                 for (; k0 + 4 < rend; k0 += 8) {  // two K-steps
-                    float A0[4], A1[4], B0, B1;
-                    prep(k0, rend, A0, B0);
-                    prep(k0 + 4, rend, A1, B1);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[t], B0, acc[t], 0, 0, 0);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[t], B1, acc[t], 0, 0, 0);
+                    const Taps r0 = taps(k0, rend), r1 = taps(k0 + 4, rend);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const Ops o0 = gather(r0), o1 = gather(r1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mfma4(r0, o0);
+                    mfma4(r1, o1);
                 }
                 if (k0 < rend) {  // last K-step of the run
-                    float A0[4], B0;
-                    prep(k0, rend, A0, B0);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[t], B0, acc[t], 0, 0, 0);
+                    const Taps r0 = taps(k0, rend);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const Ops o0 = gather(r0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mfma4(r0, o0);
                 }
             }
         }
