@@ -10,6 +10,13 @@ nchan = int(os.environ.get("SWEEP_NCHAN", "64"))
 obs = simulation.device_observation(100, nchan, 0.95e9, 1.76e9, device=dev, nchan_total=64,
                                     channels=np.arange(nchan) if nchan < 64 else None)
 cell = 0.25 / obs["umax"]
+if os.environ.get("SWEEP_BLMAJOR") == "1":
+    # rows [time][baseline] -> [baseline][time] (experiment: traversal order)
+    nbl = 197 * 196 // 2
+    nt = obs["nrow"] // nbl
+    perm = torch.arange(obs["nrow"], device=dev).reshape(nt, nbl).t().reshape(-1)
+    for k in ("uvw", "vis", "wgt"):
+        obs[k] = obs[k][perm].contiguous()
 npix = 4096
 knob = sys.argv[1] if len(sys.argv) > 1 else "SDP_HIP_GRID_WAVES"
 vals = sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "2", "4"]

@@ -72,7 +72,11 @@ struct Geo {
     double px, py;
     int do_w, nplanes, nps;  // nps = number of distinct first planes
     double w0, dw, s0;
-    int sub, nty, ntiles;  // bucket edge in cells, buckets per grid column, buckets
+    int sub, nty, ntiles;  // bucket edge in cells, buckets per window column, buckets
+    // bucket window: the footprint origins of all visibilities lie in cells
+    // [wx0, wx0 + wnx) x [wy0, wy0 + wny) (16-aligned), so only the window's
+    // buckets are histogrammed, scanned and itemised
+    int wx0, wy0, wnx, wny;
     int grp;               // consecutive buckets (along y) per work-item group
     int dbg;               // experiment knobs (SDP_HIP_DBG)
     double su;  // sign applied to u and w (-1 with SDP_HIP_FLIP_UW)
@@ -104,6 +108,11 @@ struct FineItem {
 // ------------------------------------------------------------------------
 // device helpers
 // ------------------------------------------------------------------------
+static int env_int(const char *name, int dflt) {
+    const char *e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
+
 __device__ __forceinline__ unsigned long long ord_enc(double d) {
     long long i = __double_as_longlong(d);
     return i < 0 ? ~(unsigned long long)i : ((unsigned long long)i | 0x8000000000000000ull);
@@ -171,8 +180,9 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
 
 // p0-major bucket keys: the items of a range of first planes are contiguous.
 __device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c) {
-    const int tile = g.sub == kTileCell ? ((c.ic0 >> 1) * g.ngy + c.jc0) * 2 + (c.ic0 & 1)
-                                        : (c.ic0 / g.sub) * g.nty + (c.jc0 / g.sub);
+    const int ic = c.ic0 - g.wx0, jc = c.jc0 - g.wy0;
+    const int tile = g.sub == kTileCell ? ((ic >> 1) * g.nty + jc) * 2 + (ic & 1)
+                                        : (ic / g.sub) * g.nty + (jc / g.sub);
     return (unsigned)c.p0 * (unsigned)g.ntiles + (unsigned)tile;
 }
 
@@ -348,7 +358,7 @@ __device__ __forceinline__ float2 load_vis(const double2 *p) {
 
 // Two passes over the visibilities.  Rank pass (kScatter = false): fp64
 // coordinates -> bucket key, and the visibility's rank inside its bucket
-// from a run-aggregated atomicAdd on the histogram; (key, rank) is stored.
+// from a run-aggregated atomicAdd on the histogram; the rank is stored.
 // Scatter pass: position = offs[key] + rank -- no atomics -- and the 32-byte
 // record is written there.  Invalid visibilities carry key 0xffffffff.
 template <class VT>
@@ -381,7 +391,7 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
                          int64_t uvw_rs, const double *__restrict__ freq,
                          const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
                          const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x,
-                         double *sw_slots, unsigned *counter, uint2 *__restrict__ kr,
+                         double *sw_slots, unsigned *counter, unsigned *__restrict__ rk,
                          VisRec *__restrict__ recs, unsigned long long *nbad) {
     // v indexes the part's visibilities (rows row0...); vg the call's
     const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -392,11 +402,11 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
     float wt = 1.0f;
     Coord c;
     c.ok = false;
-    uint2 mine = make_uint2(0xffffffffu, 0u);
+    unsigned mine = 0xffffffffu;  // rank in the bucket (0xffffffff: not gridded)
     if (kScatter) {
         if (!valid) return;
-        mine = kr[v];
-        if (mine.x == 0xffffffffu) return;
+        mine = rk[v];
+        if (mine == 0xffffffffu) return;
         row = vg / g.nchan;
         chan = (int)(vg - row * g.nchan);
         wt = (float)eff_weight(wgt, wrs, wcs, x, row, chan);
@@ -419,7 +429,8 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
         }
         const unsigned key = valid ? coord_key(g, c) : 0xffffffffu;
         const unsigned rank = (g.dbg & 8) ? 0u : run_reserve<true>(key, valid, counter);
-        if (v < nvis) kr[v] = make_uint2(key, rank);
+        // only the rank is kept: the scatter pass recomputes the key
+        if (v < nvis) rk[v] = valid ? rank : 0xffffffffu;
         if (sw_slots) {
             // weight sum: wave reduction, one atomic per wave into a slot
 #pragma unroll
@@ -431,7 +442,7 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
         }
         return;
     }
-    const unsigned pos = (g.dbg & 16) ? (unsigned)v : counter[mine.x] + mine.y;
+    const unsigned pos = (g.dbg & 16) ? (unsigned)v : counter[coord_key(g, c)] + mine;
     float cr = wt, ci = 0.0f;
     if (kGrid) {
         const float2 xv = vis ? eff_vis(vis, vrs, vcs, x, row, chan) : make_float2(1.0f, 0.0f);
@@ -560,7 +571,7 @@ __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__re
 #pragma unroll
         for (int j = 0; j < 16; ++j) f.o[j] = it.b + first[c0 + min(j + 1, PG)];
         const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
-        f.tile = (uint32_t)((tx * 8 + xp) * (g.ngy / 8) + ty * 2 + hf);
+        f.tile = (uint32_t)((tx * 8 + xp) * (g.wny / 8) + ty * 2 + hf);
         f.p0 = it.p0;
         fitems[(size_t)blockIdx.x * 16 + threadIdx.x] = f;
     }
@@ -738,7 +749,8 @@ __global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__re
         const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
         const LaneRole<W> role(lane);
         const float ihw = g.inv_half_w, bl = g.beta_l2e;
-        const int lane_off = role.kx * kPitch + role.ky - (tx * kTile) * kPitch - ty * kTile;
+        const int lane_off = role.kx * kPitch + role.ky - (g.wx0 + tx * kTile) * kPitch -
+                             (g.wy0 + ty * kTile);
         const int q0 = wv * NQW;
         float2 *const wtile = tile + q0 * PS;
 
@@ -794,9 +806,9 @@ __global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__re
             const int xl = rem / R, yl = rem - (rem / R) * R;
             const float2 val = tile[q * PS + xl * kPitch + yl];
             if (val.x != 0.0f || val.y != 0.0f) {
-                int gx = tx * kTile + xl;
+                int gx = g.wx0 + tx * kTile + xl;
                 if (gx >= g.ngx) gx -= g.ngx;
-                int gy = ty * kTile + yl;
+                int gy = g.wy0 + ty * kTile + yl;
                 if (gy >= g.ngy) gy -= g.ngy;
                 float *dst =
                     grid + ((int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy) * 2;
@@ -860,7 +872,7 @@ __global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict
         const float ihw = g.inv_half_w, bl = g.beta_l2e;
         const int ntg = g.nty / GRP;
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-        const int ibase = sx * SUB, jbase = sg * GRP * SUB;
+        const int ibase = g.wx0 + sx * SUB, jbase = g.wy0 + sg * GRP * SUB;
         const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
 
         for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
@@ -1049,9 +1061,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         } else {
             it = load_item(src, w_it, n_items, stride);
         }
-        const int ntg = g.ngy / 8;
+        const int ntg = FI ? g.wny / 8 : g.nty / 8;  // groups per x pair
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-        const int ibase = sx * 2, jbase = sg * 8;
+        const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
         __syncthreads();
         for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
@@ -1237,7 +1249,7 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
         const float ihw = g.inv_half_w, bl = g.beta_l2e;
         const int ntg = g.nty / GRP;
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-        const int ibase = sx * SUB, jbase = sg * GRP * SUB;
+        const int ibase = g.wx0 + sx * SUB, jbase = g.wy0 + sg * GRP * SUB;
         const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
         const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
 
@@ -1376,7 +1388,7 @@ __global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__
         const Item it = load_item(src, w_it, n_items, stride);
         const int ntg = g.nty / g.grp;
         const int tx = (int)it.tile / ntg, tg = (int)it.tile - tx * ntg;
-        const int ibase = tx * SX, jbase = tg * SY;
+        const int ibase = g.wx0 + tx * SX, jbase = g.wy0 + tg * SY;
         const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
         const int lane = threadIdx.x;
         for (int i = lane; i < NQ * RX * RY; i += 64) {
@@ -2030,6 +2042,28 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         g.nplanes = 1;
         g.nps = 1;
     }
+    // bucket window (origins only: the footprints' halo may leave it)
+    {
+        const double amax = umax * in.px * g.ngx, bmax = vmax * in.py * g.ngy;
+        auto window = [&](double m, int ng, int &w0, int &wn) {
+            const int reach = (int)std::ceil(m + 0.5 * g.W) + 2;
+            int lo = (ng / 2 - reach) & ~(kGridAlign - 1);
+            int hi = ((ng / 2 + reach + kGridAlign - 1) / kGridAlign) * kGridAlign;
+            if (lo <= 0 || hi >= ng || env_int("SDP_HIP_NO_WINDOW", 0)) {
+                lo = 0;
+                hi = ng;
+            }
+            w0 = lo;
+            wn = hi - lo;
+        };
+        // x (rows) only: the y stride stays ngy, since a compacted y range
+        // packs the hot histogram counters of the uv core closer together
+        // and measured 2x slower count-pass atomics on C2
+        (void)bmax;
+        window(amax, g.ngx, g.wx0, g.wnx);
+        g.wy0 = 0;
+        g.wny = g.ngy;
+    }
     // bucket granularity.  Invert: one-cell buckets for the MFMA gridder
     // while the dense (first plane, cell) histogram stays below kMaxCellKeys
     // (SDP_HIP_MFMA=0: the register gridder's 2x2-cell buckets).  Predict:
@@ -2040,14 +2074,14 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         const char *e = std::getenv("SDP_HIP_BUCKET");
         const char *m = std::getenv("SDP_HIP_MFMA");
         P.cells = grid_mode && !(m && std::atoi(m) == 0);
-        const int64_t cell = (int64_t)g.ngx * g.ngy * g.nps;
-        const int64_t fine = (int64_t)(g.ngx / kTileFine) * (g.ngy / kTileFine) * g.nps;
+        const int64_t cell = (int64_t)g.wnx * g.wny * g.nps;
+        const int64_t fine = (int64_t)(g.wnx / kTileFine) * (g.wny / kTileFine) * g.nps;
         if (P.cells) g.sub = cell <= kMaxCellKeys ? kTileCell : kTileCoarse;
         else g.sub = fine <= kMaxFineKeys ? kTileFine : kTileCoarse;
         if (e && std::atoi(e) == kTileCoarse) g.sub = kTileCoarse;
     }
-    g.nty = g.ngy / g.sub;
-    g.ntiles = (g.ngx / g.sub) * g.nty;
+    g.nty = g.wny / g.sub;
+    g.ntiles = (g.wnx / g.sub) * g.nty;
     g.grp = g.sub == kTileCell ? kGroupCell : (g.sub == kTileFine ? kGroupFine : 1);
     SDP_REQUIRE((double)g.ntiles * g.nps < 4.0e9, "too many (plane, tile) buckets");
 
@@ -2075,7 +2109,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     P.fft_planes = std::min(P.fft_planes, g.nplanes);
     const int64_t nvis_all = in.nrow * (int64_t)in.nchan;
     const size_t need_other =
-        (size_t)nvis_all * (sizeof(VisRec) + sizeof(uint2) + (grid_mode ? 0 : sizeof(float2))) +
+        (size_t)nvis_all * (sizeof(VisRec) + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2))) +
         (size_t)g.ntiles * g.nps * 2 * sizeof(unsigned) + (size_t)P.fft_planes * spec_plane;
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
     P.chunk_planes = std::min(cp, g.nplanes);
@@ -2134,7 +2168,7 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     pt.meta = scratch<unsigned>("meta" + sfx, g.nps + 5);
     const int64_t icap = std::min<int64_t>(ngroups, pt.nvis) + pt.nvis / P.chunk + 1;
     pt.items = scratch<Item>("items" + sfx, icap);
-    uint2 *kr = scratch<uint2>("key_rank", std::max<int64_t>(in.nrow * (int64_t)in.nchan, 1)) +
+    unsigned *kr = scratch<unsigned>("key_rank", std::max<int64_t>(in.nrow * (int64_t)in.nchan, 1)) +
                 pt.vbase;
     VisRec *recs = P.recs + pt.vbase;
     SDP_HIP_CHECK(hipMemsetAsync(pt.hist, 0, (nkeys + 1) * sizeof(unsigned), st));
@@ -2306,8 +2340,8 @@ static void launch_grid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi, h
 static Geo fine_view(const Geo &g) {
     Geo f = g;
     f.sub = kTileFine;
-    f.nty = g.ngy / kTileFine;
-    f.ntiles = (g.ngx / kTileFine) * f.nty;
+    f.nty = g.wny / kTileFine;
+    f.ntiles = (g.wnx / kTileFine) * f.nty;
     f.grp = kGroupFine;
     return f;
 }
