@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--npix", type=int, default=NPIX)
     ap.add_argument("--cpu-chans", type=int, default=8,
                     help="channels in the cpu_baseline sample (0 = skip)")
+    ap.add_argument("--no-api", action="store_true",
+                    help="skip the invert_ng API (device / host Visibility) timings")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_k_grid.json"))
     ap.add_argument("--config", choices=("c2", "c4"), default="c2",
                     help="c2: configs[1], weak scaling (default); c4: configs[3], the SKA-LOW "
@@ -71,10 +73,14 @@ def parse():
 
 
 def cpu_baseline(args, umax, nchan_total):
-    """oracle/wgrid_cpu.c on a bounded C2 sample (8 channels of the 64 by default):
-    the sample's gridding time is scaled to the full visibility count and its
-    per-plane FFT + w-screen time is counted once (the full job has the same
-    planes), giving the CPU's full-C2 invert rate."""
+    """oracle/wgrid_cpu.c on bounded C2 samples: the sample's gridding time is
+    scaled to the full visibility count and its per-plane FFT + w-screen time
+    counted once (the full job has the same planes), giving the CPU's full-C2
+    invert rate.  `value`: matched precision (fp32 taps and planes, W = 8,
+    what the GPU computes) on all host cores the process may use (<= 16).
+    `variants`: the same at the reference's default 4 threads (ng.py:58), and
+    the reference's precision (epsilon 1e-12 -> W = 13, fp64 taps and planes,
+    double_precision_accumulation=True, ng.py:240-256) at both thread counts."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import wgrid_cpu
     from ska_sdp_func_python_amd import simulation
@@ -82,31 +88,97 @@ def cpu_baseline(args, umax, nchan_total):
     en = fn(n_def, seed=1)
     ha = np.linspace(-0.5, 0.5, args.ntimes) * 8.0 * math.pi / 12.0
     uvw, _ = simulation.observe(en, math.radians(lat), math.radians(dec), ha)
-    uvw = uvw.reshape(-1, 3)
+    uvw = uvw.reshape(-1, 3) * np.array([-1.0, 1.0, -1.0])
     allf = np.linspace(F_LO, F_HI, nchan_total)
-    chans = np.linspace(0, nchan_total - 1, args.cpu_chans).round().astype(int)
-    freq = allf[chans]
-    rng = np.random.default_rng(2)
-    ms = (rng.normal(size=(uvw.shape[0], len(freq)))
-          + 1j * rng.normal(size=(uvw.shape[0], len(freq)))).astype(np.complex64)
-    wgt = np.ones(ms.shape, np.float32)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    threads = min(threads, len(os.sched_getaffinity(0)))
     cell = 0.25 / umax
-    t0 = time.perf_counter()
-    _, tg, tf = wgrid_cpu.ms2dirty(uvw, freq, ms, wgt, args.npix, args.npix, cell, cell,
-                                   EPS_REQUESTED, True, nthreads=threads)
-    wall = time.perf_counter() - t0
-    nvis_s = ms.size
+    allcores = min(16, len(os.sched_getaffinity(0)))
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        allcores = min(allcores, env)
     nvis_full = uvw.shape[0] * args.nchan
-    t_full = (wall - tf) * nvis_full / nvis_s + tf
-    return {"value": round(nvis_full / t_full / 1e6, 4), "unit": "Mvis/s", "cores": threads,
-            "kind": "port",
-            "sample": (f"oracle/wgrid_cpu.c (C+OpenMP w-stacking restatement; ducc0 absent) on "
-                       f"{len(freq)} of {args.nchan} C2 channels ({nvis_s / 1e6:.2f} Mvis, "
-                       f"{args.npix}^2 image, same planes): {wall:.1f} s wall, of which "
-                       f"{tf:.1f} s FFT+screen; full-job rate = gridding scaled by "
-                       f"{nvis_full / nvis_s:.0f}x + FFT/screen once")}
+
+    def run(nch, threads, precision):
+        chans = np.linspace(0, nchan_total - 1, nch).round().astype(int)
+        freq = allf[chans]
+        rng = np.random.default_rng(2)
+        ms = (rng.normal(size=(uvw.shape[0], nch))
+              + 1j * rng.normal(size=(uvw.shape[0], nch))).astype(np.complex64)
+        wgt = np.ones(ms.shape, np.float32)
+        info = {}
+        t0 = time.perf_counter()
+        _, tg, tf = wgrid_cpu.ms2dirty(uvw, freq, ms, wgt, args.npix, args.npix, cell, cell,
+                                       EPS_REQUESTED, True, nthreads=threads, precision=precision,
+                                       info=info)
+        wall = time.perf_counter() - t0
+        t_full = (wall - tf) * nvis_full / ms.size + tf
+        return {"value": round(nvis_full / t_full / 1e6, 4), "cores": threads,
+                "precision": precision, "support": info["support"], "nplanes": info["nplanes"],
+                "sample": f"{nch} of {args.nchan} channels ({ms.size / 1e6:.2f} Mvis): {wall:.1f} s "
+                          f"wall, {tf:.1f} s FFT+screen"}
+
+    main = run(args.cpu_chans, allcores, "single")
+    variants = [run(max(1, args.cpu_chans // 2), 4, "single"),
+                run(max(1, args.cpu_chans // 2), allcores, "double"),
+                run(max(1, args.cpu_chans // 4), 4, "double")]
+    return {"value": main["value"], "unit": "Mvis/s", "cores": allcores, "kind": "port",
+            "sample": ("oracle/wgrid_cpu.c (C+OpenMP w-stacking restatement, load-balanced "
+                       "tile tasks; ducc0 absent), matched precision (fp32, W=8) on "
+                       + main["sample"] + "; full-job rate = gridding scaled to all "
+                       f"{nvis_full / 1e6:.1f} Mvis + FFT/screen once"),
+            "variants": variants}
+
+
+def api_rates(args, obs, cell):
+    """invert_ng through the reference-shaped API (datamodels-shim Visibility
+    with the datamodels' dtypes: vis c128, weights f64, flags int64) on the
+    bench workload: device-resident arrays, and host numpy arrays copied to
+    the device inside the call (PCIe-inclusive; never the headline value)."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import invert_ng
+    dev = obs["uvw"].device
+    nrow, nchan = obs["nrow"], obs["vis"].shape[1]
+    nb = 197 * 196 // 2
+    nt = nrow // nb
+    shape = (nt, nb, nchan, 1)
+    pc = dm.SkyCoord(0.0, math.radians(-45.0))
+    freq = obs["freq"].cpu().numpy()
+
+    def make(arrs):
+        return dm.Visibility.constructor(
+            frequency=freq, channel_bandwidth=np.full(nchan, 1e6), phasecentre=pc,
+            uvw=arrs["uvw"], time=np.arange(nt, dtype=float), vis=arrs["vis"],
+            weight=arrs["w"], imaging_weight=arrs["w"], flags=arrs["f"],
+            baselines=np.stack(np.triu_indices(197, 1), 1), polarisation_frame=dm.PolarisationFrame("stokesI"))
+
+    d = {"uvw": obs["uvw"].reshape(nt, nb, 3),
+         "vis": obs["vis"].to(torch.complex128).reshape(shape),
+         "w": torch.ones(shape, dtype=torch.float64, device=dev),
+         "f": torch.zeros(shape, dtype=torch.int64, device=dev)}
+    model = dm.create_image(args.npix, cell, pc, frequency=float(freq.mean()),
+                            channel_bandwidth=float(2 * (freq.max() - freq.min()) + 1e6), nchan=1)
+
+    def timed(bvis, reps=2):
+        invert_ng(bvis, model, epsilon=EPS_REQUESTED)
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            invert_ng(bvis, model, epsilon=EPS_REQUESTED)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    t_dev = timed(make(d))
+    h = {k: v.cpu().numpy() for k, v in d.items()}
+    del d
+    torch.cuda.empty_cache()
+    t_host = timed(make(h))
+    nvis = nrow * nchan
+    return {"invert_ng_device_visibility_ms": round(t_dev * 1e3, 2),
+            "invert_ng_host_visibility_ms": round(t_host * 1e3, 2),
+            "host_visibility_Mvis_s": round(nvis / t_host / 1e6, 1),
+            "note": "reference-shaped invert_ng on a c128/f64/int64 Visibility; the host "
+                    "figure includes the H2D copies of ~5 GB (PCIe-inclusive) and the image D2H"}
 
 
 # ---------------------------------------------------------------------------
@@ -359,6 +431,9 @@ def main():
                         "frac": round(nvis_rank * 4 * info["support"] ** 3 / (ms_grid * 1e-3) / 1e12
                                       / FP32_PEAK_TFLOPS, 4)}}
 
+    api = None
+    if rank == 0 and world == 1 and not args.no_api:
+        api = api_rates(args, obs, cell)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_chans > 0:
         cpu = cpu_baseline(args, obs["umax"], nchan_total)
@@ -380,6 +455,7 @@ def main():
                           for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "api": api,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
