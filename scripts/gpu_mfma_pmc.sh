@@ -9,7 +9,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_
            "SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_TRANS_F32 GRBM_GUI_ACTIVE" \
            "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_MISC SQ_WAIT_ANY SQ_INSTS_BRANCH" ; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex "k_grid" --output-format csv -d $out/p$i -o run -- \
+  timeout -s KILL 120 rocprofv3 --pmc $set --kernel-include-regex "${KRX:-k_grid}" --output-format csv -d $out/p$i -o run -- \
       python3 scripts/gpu_sweep.py SDP_HIP_DBG ${DBG:-0} > $out/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $out/p$i.log; }
 done
 python3 - "$out" <<'PY'

@@ -93,6 +93,23 @@ struct __attribute__((aligned(32))) VisRec {
 };
 static_assert(sizeof(VisRec) == 32, "record layout");
 
+// 16-byte record of the 4-padded invert (k_grid_mfma_pad): the value and the
+// footprint offsets as fixed-point fractions, e = (1 - W/2) - f in [0, 1):
+// u in lo[0:21), v in lo[21:32) | hi[0:10), w in hi[10:32) (steps of 2^-21,
+// 2^-21, 2^-22 cells / planes, i.e. rounding errors <= 2.4e-7 / 1.2e-7 --
+// fp32 offsets near 3.5 round to 1.2e-7).  The cell and the first plane are
+// those of the record's bucket, so the record does not carry them.
+struct __attribute__((aligned(16))) RecC {
+    float cre, cim;
+    uint32_t lo, hi;
+};
+static_assert(sizeof(RecC) == 16, "record layout");
+
+__device__ __forceinline__ uint32_t fix_frac(double e, int bits) {
+    const double q = floor(e * (double)(1u << bits) + 0.5);
+    return (uint32_t)fmin(fmax(q, 0.0), (double)((1u << bits) - 1u));
+}
+
 struct Item {
     uint32_t b, e, tile, p0;
 };
@@ -144,6 +161,7 @@ __device__ __forceinline__ double phi_lookup(const double *__restrict__ tab, dou
 struct Coord {
     int ic0, jc0, p0;
     float fu, fv, fw;
+    double du, dv, dw;  // the same offsets in fp64 (RecC encoding)
     double w;  // w in wavelengths (sign applied)
     bool ok;
 };
@@ -160,8 +178,10 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
     c.ok = fabs(a) < (double)g.ngx && fabs(b) < (double)g.ngy;
     if (!c.ok) return c;
     const double fa = floor(a - 0.5 * g.W), fb = floor(b - 0.5 * g.W);
-    c.fu = (float)(fa + 1.0 - a);
-    c.fv = (float)(fb + 1.0 - b);
+    c.du = fa + 1.0 - a;
+    c.dv = fb + 1.0 - b;
+    c.fu = (float)c.du;
+    c.fv = (float)c.dv;
     const int ic = ((int)fa + 1 + g.ngx / 2) % g.ngx;
     const int jc = ((int)fb + 1 + g.ngy / 2) % g.ngy;
     c.ic0 = ic < 0 ? ic + g.ngx : ic;
@@ -169,11 +189,13 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
     if (g.do_w) {
         const double pw = (c.w - g.w0) / g.dw;
         const double fp = floor(pw - 0.5 * g.W);
-        c.fw = (float)(fp + 1.0 - pw);
+        c.dw = fp + 1.0 - pw;
+        c.fw = (float)c.dw;
         c.p0 = min(max((int)fp + 1, 0), g.nps - 1);
     } else {
         c.p0 = 0;
         c.fw = 0.0f;
+        c.dw = 0.0;
     }
     return c;
 }
@@ -266,13 +288,14 @@ __global__ __launch_bounds__(256) void k_bounds_final(int nblocks, const double 
 // {nbad lo, nbad hi, nrec, nitems, first item of each first-plane value
 // [nps + 1]}; meta[3] is also the item count persistent launches read
 __global__ void k_part_meta(const unsigned long long *__restrict__ nbad,
-                            const unsigned *__restrict__ nrec, const unsigned *__restrict__ ioffs,
-                            int groups_per_plane, int nps, unsigned *__restrict__ meta) {
+                            const unsigned *__restrict__ nrec, const unsigned *__restrict__ npad,
+                            const unsigned *__restrict__ ioffs, int groups_per_plane, int nps,
+                            unsigned *__restrict__ meta) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0) {
         meta[0] = (unsigned)(*nbad & 0xffffffffull);
         meta[1] = (unsigned)(*nbad >> 32);
-        meta[2] = *nrec;
+        meta[2] = *nrec - (npad ? *npad : 0u);  // gridded visibilities (pads excluded)
         meta[3] = ioffs[(size_t)nps * groups_per_plane];
     }
     if (k <= nps) meta[4 + k] = ioffs[(size_t)k * groups_per_plane];
@@ -386,7 +409,7 @@ __device__ __forceinline__ float2 eff_vis(const VT *vis, int64_t vrs, int64_t vc
     return make_float2((float)re, (float)im);
 }
 
-template <class VT, bool kScatter, bool kGrid>
+template <class VT, bool kScatter, bool kGrid, bool kCompact = false>
 __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__restrict__ uvw,
                          int64_t uvw_rs, const double *__restrict__ freq,
                          const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
@@ -463,6 +486,19 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
         cr = r_;
         ci = i_;
     }
+    if (kCompact) {
+        // RecC: offsets as fractions of (1 - W/2) - offset (do_w off: w = 0)
+        const double base = 1.0 - 0.5 * g.W;
+        const uint32_t qu = fix_frac(base - c.du, 21), qv = fix_frac(base - c.dv, 21);
+        const uint32_t qw = g.do_w ? fix_frac(base - c.dw, 22) : 0u;
+        RecC rc;
+        rc.cre = cr;
+        rc.cim = ci;
+        rc.lo = qu | (qv << 21);
+        rc.hi = (qv >> 11) | (qw << 10);
+        reinterpret_cast<RecC *>(recs)[pos] = rc;
+        return;
+    }
     VisRec rec;
     rec.cre = cr;
     rec.cim = ci;
@@ -511,6 +547,59 @@ __global__ void k_items_fill(int64_t ngroups, int grp, int groups_per_plane,
         items[o++] = x;
     }
 }
+
+// 4-padding of the one-cell buckets for k_grid_mfma_pad: key k's records
+// fill [offs[k], offs[k] + hist[k]) of a slot range rounded up to a multiple
+// of 4 (the scan ran over the rounded counts); the remaining slots get
+// zero-valued RecC records.  Per block the pad count is added into one of
+// kSumSlots slots (k_sum_pads folds them).
+__global__ __launch_bounds__(256) void k_pad_cells(unsigned nkeys,
+                                                   const unsigned *__restrict__ hist,
+                                                   const unsigned *__restrict__ offs,
+                                                   RecC *__restrict__ recs,
+                                                   unsigned *__restrict__ pad_slots) {
+    __shared__ unsigned red[4];
+    const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned npad = 0;
+    if (k < nkeys) {
+        const unsigned n = hist[k];
+        if (n & 3u) {
+            npad = 4u - (n & 3u);
+            const unsigned base = offs[k] + n;
+            RecC r;
+            r.cre = r.cim = 0.0f;
+            r.lo = r.hi = 0u;  // offsets 1 - W/2: in range, finite taps
+            for (unsigned i = 0; i < npad; ++i) recs[base + i] = r;
+        }
+    }
+    unsigned s = npad;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = red[0] + red[1] + red[2] + red[3];
+        if (t) atomicAdd(&pad_slots[blockIdx.x & (kSumSlots - 1)], t);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sum_pads(const unsigned *__restrict__ slots,
+                                                  unsigned *out) {
+    __shared__ unsigned red[4];
+    unsigned s = 0;
+    for (int i = threadIdx.x; i < kSumSlots; i += 256) s += slots[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = red[0] + red[1] + red[2] + red[3];
+}
+
+struct Round4 {
+    __host__ __device__ __forceinline__ unsigned operator()(unsigned n) const {
+        return (n + 3u) & ~3u;
+    }
+};
 
 // Large grids: the dense 2x2-cell histogram would be too large (C4: 70
 // planes of 8192^2 buckets), so visibilities are bucketed by 16x16 cells and
@@ -1211,6 +1300,223 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     }
 }
 
+// MFMA gridder on 4-padded cells (invert, one-cell buckets): the bucketing
+// rounds every cell's record count up to a multiple of 4 with zero-valued
+// pad records (k_pad_cells), so every K-step of 4 consecutive records
+// belongs to one cell and no K-step straddles a batch or an item.  Same GEMM
+// and region tile as k_grid_mfma; what changes is the work per K-step:
+//  * per batch of 64 records, the 64 x 3 x 8 one-dimensional taps are
+//    evaluated once with every lane busy (lane l: tap l & 7 of records
+//    8m + (l >> 3), 24 ES evaluations) into an LDS tap block of one
+//    kTapRec-float row per record: tu in h-major order (tu[2t + h] at
+//    4h + t, so a lane's four A taps are one ds_read_b128), tv, tw, value;
+//  * the 16 K-steps of a batch are unrolled with compile-time LDS offsets,
+//    the operands of K-step j + 1 read before the MFMAs of K-step j issue:
+//    per K-step 4 LDS reads, 5 multiplies, 4 MFMAs and a cell-change bit
+//    test -- no run bookkeeping, no masking.
+constexpr int kTapRec = 28;    // floats per record row of the tap block (16-B multiple)
+constexpr int kTapBatch = 16;  // records per tap block (half a 64-record load: LDS, occupancy)
+
+template <int W, bool WS>
+constexpr int mfma_tile_f2() {  // region tile, rounded to 16 B
+    return (((WS ? W : 1) * (2 + W - 1) * (8 + W - 1)) + 1) & ~1;
+}
+
+template <int W, bool WS>
+constexpr size_t grid_mfma_pad_lds() {
+    return (size_t)mfma_tile_f2<W, WS>() * sizeof(float2) + kTapBatch * sizeof(float4) +
+           (size_t)kTapBatch * kTapRec * sizeof(float);
+}
+
+template <int W, bool WS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma_pad(
+    Geo g, const RecC *__restrict__ recs, ItemSrc src, const unsigned *__restrict__ offs,
+    float *__restrict__ grid, int p_lo, int p_hi) {
+    static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
+    constexpr int NQ = WS ? W : 1;
+    float4 *const stage = reinterpret_cast<float4 *>(tile + mfma_tile_f2<W, WS>());  // fu fv fw -
+    float *const blk = reinterpret_cast<float *>(stage + kTapBatch);  // [kTapBatch][kTapRec]
+    const uint32_t n_items = item_count(src);
+    const uint32_t stride = item_stride(n_items);
+    const int lane = threadIdx.x;
+    const float ihw = g.inv_half_w, bl = g.beta_l2e;
+    const float fbase = 1.0f - 0.5f * (float)W;  // RecC offset origin
+    // tap phase: tap t = lane & 7 of records 8m + (lane >> 3)
+    const int tt = lane & 7;
+    const float tihw = (float)tt * ihw;
+    float *const tap_dst = blk + (lane >> 3) * kTapRec;
+    const int wu = (tt & 1) * 4 + (tt >> 1), wv = 8 + tt, ww = 16 + tt;
+    // K-step j: record 4j + (lane >> 4); A row lane & 15 = (tu h, tv tap),
+    // B column lane & 15 = (tw tap, re / im)
+    const float *const kA = blk + (lane >> 4) * kTapRec + ((lane >> 3) & 1) * 4;
+    const float *const kV = blk + (lane >> 4) * kTapRec + 8 + (lane & 7);
+    const float *const kW = blk + (lane >> 4) * kTapRec + 16 + ((lane & 15) >> 1);
+    const float *const kC = blk + (lane >> 4) * kTapRec + 24 + (lane & 1);
+    const bool col_im = lane & 1;
+    // accumulator element i of M-tile t: tap (2t + (lane >> 5), 4 ((lane >> 4) & 1) + i),
+    // column (q, re/im) = ((lane & 15) >> 1, lane & 1)
+    const int cq = (lane & 15) >> 1;
+    const int ckx = lane >> 5, cky = 4 * ((lane >> 4) & 1);
+    float *const ftile = reinterpret_cast<float *>(tile);
+
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        const Item it = load_item(src, w_it, n_items, stride);
+        const int ntg = g.nty / 8;  // groups per x pair
+        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
+        const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
+        // the group's 16 cell buckets end at ob[1..16] (record indices)
+        const unsigned *ob = offs + ((size_t)it.p0 * g.ntiles + (size_t)it.tile * kGroupCell);
+        uint32_t bnd[kGroupCell - 1];
+#pragma unroll
+        for (int c = 0; c < kGroupCell - 1; ++c)
+            bnd[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
+
+        __syncthreads();
+        for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
+
+        floatx4 acc[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+        int cur = -1;  // cell of the accumulators (wave-uniform)
+        auto flush_cell = [&]() {
+            const int xo = cur & 1, yo = cur >> 1;
+            if (cq < NQ) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int kx = 2 * t + ckx;
+                    if (kx >= W) continue;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int ky = cky + i;
+                        if (ky >= W) continue;
+                        float *d = ftile + ((cq * RX + xo + kx) * RY + yo + ky) * 2 + (col_im ? 1 : 0);
+                        *d += acc[t][i];
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+        };
+        struct Ops {
+            floatx4 a;
+            float v, w, c;
+        };
+        auto kload = [&](int j) {
+            Ops o;
+            o.a = *reinterpret_cast<const floatx4 *>(kA + 4 * j * kTapRec);
+            o.v = kV[4 * j * kTapRec];
+            o.w = kW[4 * j * kTapRec];
+            o.c = kC[4 * j * kTapRec];
+            return o;
+        };
+        auto kmfma = [&](const Ops &o) {
+            const float b = o.w * o.c;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a[t] * o.v, b, acc[t], 0, 0, 0);
+        };
+
+        RecC nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
+        for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+            const RecC my = nx;
+            if (b0 + 64 < it.e) nx = recs[min(b0 + 64 + (uint32_t)lane, it.e - 1)];
+            const int nb = (int)min(64u, it.e - b0);  // a multiple of 4
+            // cell (x-pair-major index in the group) of the lane's record
+            const uint32_t ri = b0 + (uint32_t)lane;
+            int cj = 0;
+#pragma unroll
+            for (int c = 0; c < kGroupCell - 1; ++c) cj += ri >= bnd[c] ? 1 : 0;
+            const float fu = fbase - (float)(my.lo & 0x1fffffu) * 0x1p-21f;
+            const float fv = fbase - (float)((my.lo >> 21) | ((my.hi & 0x3ffu) << 11)) * 0x1p-21f;
+            const float fw = fbase - (float)(my.hi >> 10) * 0x1p-22f;
+            // K-steps whose cell differs from the previous K-step's (bit 4j)
+            const int prev = __shfl_up(cj, 4);
+            uint64_t chg = __ballot((lane & 3) == 0 && lane >= 4 && prev != cj);
+            if (__builtin_amdgcn_readfirstlane(cj) != cur) chg |= 1ull;
+            // two halves of kTapBatch records: taps, then their K-steps
+            for (int h = 0; h < 64 / kTapBatch; ++h) {
+                const int nbh = min(kTapBatch, nb - kTapBatch * h);
+                if (nbh <= 0) break;
+                __syncthreads();  // previous half's tap block reads
+                if (lane / kTapBatch == h) {
+                    const int r = lane % kTapBatch;
+                    stage[r] = make_float4(fu, fv, fw, 0.0f);
+                    *reinterpret_cast<float2 *>(blk + r * kTapRec + 24) =
+                        make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
+                }
+                __syncthreads();
+#pragma unroll
+                for (int m = 0; m < kTapBatch / 8; ++m) {
+                    const float4 f = stage[8 * m + (lane >> 3)];
+                    float *d = tap_dst + 8 * m * kTapRec;
+                    d[wu] = es_tap<W>(f.x, tihw, ihw, bl);
+                    d[wv] = es_tap<W>(f.y, tihw, ihw, bl);
+                    d[ww] = WS ? es_tap<W>(f.z, tihw, ihw, bl) : (tt == 0 ? 1.0f : 0.0f);
+                }
+                __syncthreads();
+                // segments of K-steps of one cell; inside a segment the operands
+                // of K-step j + 1 are read before the MFMAs of K-step j issue
+                const uint64_t hchg = chg >> (kTapBatch * h);
+                const int nk = nbh >> 2;
+                int j = 0;
+                while (j < nk) {
+                    if ((hchg >> (4 * j)) & 1ull) {
+                        if (cur >= 0) flush_cell();
+                        cur = __builtin_amdgcn_readlane(cj, kTapBatch * h + 4 * j);
+                    }
+                    const uint64_t rest = hchg & ~((2ull << (4 * j)) - 1ull);
+                    const int je = rest ? min(nk, (int)(__builtin_ctzll(rest) >> 2)) : nk;
+                    Ops o = kload(j);
+                    for (++j; j < je; ++j) {
+                        const Ops on = kload(j);
+                        kmfma(o);
+                        o = on;
+                    }
+                    kmfma(o);
+                }
+            }
+        }
+        if (cur >= 0) flush_cell();
+        __syncthreads();
+
+        // flush: float f = i0 + lane of each plane's RX x RY complex cells,
+        // buffer atomics off a per-plane descriptor (32-bit offsets), the
+        // cell index advanced incrementally; zero floats are skipped
+        constexpr int FPP = RX * RY * 2;
+        const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
+        int xl = (lane >> 1) / RY, yl = (lane >> 1) - xl * RY;
+#pragma unroll
+        for (int i0 = 0; i0 < FPP; i0 += 64) {
+            const int f = i0 + lane;
+            if (f >= FPP) break;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            const int voff = ((gx * g.ngy + gy) * 2 + (f & 1)) * (int)sizeof(float);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int p = (int)it.p0 + q;
+                const float val = ftile[q * PS * 2 + f];
+                if (p >= p_lo && p < p_hi && val != 0.0f) {
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)), 0,
+                        (int)plane_bytes, 0x00020000);
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, rs, voff, 0, 0);
+                }
+            }
+            yl += 32 % RY;
+            xl += 32 / RY;
+            if (yl >= RY) {
+                yl -= RY;
+                ++xl;
+            }
+        }
+    }
+}
+
 // Register degridder (mirror of k_grid_reg): one wave per work item = a
 // chunk of a group of kGroupFine consecutive 2x2-cell buckets.  The group's
 // (2+W-1) x (8+W-1) x W region is staged in LDS once; per bucket, lane
@@ -1839,6 +2145,7 @@ struct Part {
     int64_t r0 = 0, r1 = 0, vbase = 0, nvis = 0;
     unsigned *hist = nullptr, *offs = nullptr, *nch = nullptr, *ioffs = nullptr;
     unsigned long long *nbad = nullptr;
+    unsigned *npad = nullptr;  // pad records of a 4-padded plan (device)
     Item *items = nullptr;
     FineItem *fitems = nullptr;  // 16 per item when sub-sorted (k_subsort)
     unsigned *meta = nullptr;  // device: see k_part_meta
@@ -1855,6 +2162,7 @@ struct Plan {
     bool aux_bucketing = false;      // bucketing on the auxiliary stream
     bool subsort = false;            // 16x16 buckets re-ordered to 2x2 (register kernels)
     bool cells = false;              // invert on k_grid_mfma: one-cell buckets / sub-sort
+    bool pad4 = false;               // one-cell buckets padded to 4 records (k_grid_mfma_pad)
     float2 *vdirect = nullptr;       // dirty2ms: register degridders write c64 vis in place
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
@@ -2147,6 +2455,12 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         P.subsort = g.sub == kTileCoarse && !P.aux_bucketing && !(e && std::atoi(e) == 0);
         if (P.subsort) P.chunk = std::min<unsigned>(P.chunk, kSubChunk);
     }
+    // one-cell buckets padded to multiples of 4 records (k_grid_mfma_pad);
+    // SDP_HIP_PAD4=0 keeps the unpadded run-walking k_grid_mfma.  The padded
+    // record count is read back before the scatter (one host sync), so the
+    // host-sync-free pipelined plans stay unpadded.
+    P.pad4 = P.cells && g.sub == kTileCell && !P.aux_bucketing && env_int("SDP_HIP_PAD4", 1) != 0;
+    P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
     P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
     return P;
 }
@@ -2170,7 +2484,6 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     pt.items = scratch<Item>("items" + sfx, icap);
     unsigned *kr = scratch<unsigned>("key_rank", std::max<int64_t>(in.nrow * (int64_t)in.nchan, 1)) +
                 pt.vbase;
-    VisRec *recs = P.recs + pt.vbase;
     SDP_HIP_CHECK(hipMemsetAsync(pt.hist, 0, (nkeys + 1) * sizeof(unsigned), st));
     SDP_HIP_CHECK(hipMemsetAsync(pt.nbad, 0, sizeof(unsigned long long), st));
     SDP_HIP_CHECK(hipMemsetAsync(pt.nch + ngroups, 0, sizeof(unsigned), st));
@@ -2179,10 +2492,14 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
     auto launch_bucket = [&](auto scatter_tag, unsigned *counter) {
         constexpr bool S = decltype(scatter_tag)::value;
-        VisRec *out = S ? recs : nullptr;
+        VisRec *out = S ? P.recs + pt.vbase : nullptr;
         double *sl = S ? nullptr : slots;
         if (in.vis_dtype == SDP_HIP_C128) {
-            if (grid_mode)
+            if (grid_mode && S && P.pad4)  // 16-byte RecC records
+                k_bucket<double2, S, true, true><<<nb, 256, 0, st>>>(
+                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
+                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
+            else if (grid_mode)
                 k_bucket<double2, S, true><<<nb, 256, 0, st>>>(
                     g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
                     in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
@@ -2191,7 +2508,11 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
                     g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
                     in.wcs, in.x, sl, counter, kr, out, pt.nbad);
         } else {
-            if (grid_mode)
+            if (grid_mode && S && P.pad4)  // 16-byte RecC records
+                k_bucket<float2, S, true, true><<<nb, 256, 0, st>>>(
+                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
+                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
+            else if (grid_mode)
                 k_bucket<float2, S, true><<<nb, 256, 0, st>>>(
                     g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
                     in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
@@ -2207,9 +2528,39 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
                                                    (int)(nkeys + 1), st));
     void *tmp = scratch<char>("scan_tmp" + sfx, tmp_bytes + 16);
     size_t tb = tmp_bytes + 16;
-    SDP_HIP_CHECK(
-        hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.hist, pt.offs, (int)(nkeys + 1), st));
+    if (P.pad4) {
+        // scan of the counts rounded up to 4, then the padded total sizes
+        // the record array (one host sync)
+        hipcub::TransformInputIterator<unsigned, Round4, const unsigned *> r4(pt.hist, Round4{});
+        size_t need = 0;
+        SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, r4, pt.offs,
+                                                       (int)(nkeys + 1), st));
+        if (need > tmp_bytes) {
+            tmp_bytes = need;
+            tmp = scratch<char>("scan_tmp" + sfx, tmp_bytes + 16);
+        }
+        tb = tmp_bytes + 16;
+        SDP_HIP_CHECK(
+            hipcub::DeviceScan::ExclusiveSum(tmp, tb, r4, pt.offs, (int)(nkeys + 1), st));
+        unsigned *htot = pinned_host<unsigned>(48, 1);
+        SDP_HIP_CHECK(hipMemcpyAsync(htot, pt.offs + nkeys, sizeof(unsigned),
+                                     hipMemcpyDeviceToHost, st));
+        SDP_HIP_CHECK(hipStreamSynchronize(st));
+        SDP_REQUIRE(P.parts.size() == 1, "4-padded bucketing runs on one part");
+        P.recs = scratch<VisRec>("recs", ((int64_t)*htot + 1) / 2 + 1);  // RecC records
+    } else {
+        SDP_HIP_CHECK(
+            hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.hist, pt.offs, (int)(nkeys + 1), st));
+    }
     if (pt.nvis > 0) launch_bucket(std::true_type{}, pt.offs);
+    if (P.pad4) {
+        unsigned *pslots = scratch<unsigned>("pad_slots", kSumSlots);
+        pt.npad = scratch<unsigned>("npad" + sfx, 1);
+        SDP_HIP_CHECK(hipMemsetAsync(pslots, 0, kSumSlots * sizeof(unsigned), st));
+        k_pad_cells<<<grid1d((int64_t)nkeys, 256), 256, 0, st>>>(
+            (unsigned)nkeys, pt.hist, pt.offs, reinterpret_cast<RecC *>(P.recs), pslots);
+        k_sum_pads<<<1, 256, 0, st>>>(pslots, pt.npad);
+    }
 
     // work items (p0-major, so a first-plane range is a contiguous item range)
     k_items_count<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, pt.offs, P.chunk, pt.nch);
@@ -2218,7 +2569,7 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
         hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.nch, pt.ioffs, (int)(ngroups + 1), st));
     k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, gpp, pt.offs, pt.ioffs,
                                                        P.chunk, pt.items);
-    k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys, pt.ioffs, gpp,
+    k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys, pt.npad, pt.ioffs, gpp,
                                                       g.nps, pt.meta);
     SDP_HIP_CHECK(hipGetLastError());
 }
@@ -2391,12 +2742,31 @@ static void launch_grid_mfma(const Plan &P, const Part &pt, int p_lo, int p_hi, 
     const void *fn = (const void *)k_grid_mfma<W, WS, false>;
     const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
     if (L.blocks == 0) return;
+    // SDP_HIP_DBG & 32 (timing experiment): an empty plane range skips the flush
+    const int ph = (P.g.dbg & 32) ? p_lo : p_hi;
     k_grid_mfma<W, WS, false><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
-                                                        nullptr, (float *)P.grid, p_lo, p_hi);
+                                                        nullptr, (float *)P.grid, p_lo, ph);
+}
+
+template <int W, bool WS>
+static void launch_grid_mfma_pad(const Plan &P, const Part &pt, int p_lo, int p_hi,
+                                 hipStream_t st) {
+    constexpr size_t lds = grid_mfma_pad_lds<W, WS>();
+    const void *fn = (const void *)k_grid_mfma_pad<W, WS>;
+    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
+    if (L.blocks == 0) return;
+    const int ph = (P.g.dbg & 32) ? p_lo : p_hi;  // SDP_HIP_DBG & 32: no flush (timing)
+    k_grid_mfma_pad<W, WS><<<L.blocks, 64, lds, st>>>(
+        P.g, reinterpret_cast<const RecC *>(P.recs) + pt.vbase, L.src, pt.offs, (float *)P.grid,
+        p_lo, ph);
 }
 
 template <int W>
 static void launch_grid(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
+    if (P.pad4) {
+        if (P.g.do_w) return launch_grid_mfma_pad<W, true>(P, pt, p_lo, p_hi, st);
+        return launch_grid_mfma_pad<W, false>(P, pt, p_lo, p_hi, st);
+    }
     if (P.cells && (P.subsort || P.g.sub == kTileCell)) {
         if (P.g.do_w) return launch_grid_mfma<W, true>(P, pt, p_lo, p_hi, st);
         return launch_grid_mfma<W, false>(P, pt, p_lo, p_hi, st);
