@@ -42,6 +42,18 @@ extern "C" {
 #define SDP_HIP_ACCUMULATE 2u /* add into the output instead of overwriting      */
 #define SDP_HIP_BATCH_FIRST 4u /* sdp_hip_ms2dirty_batch: first batch (zero the planes) */
 #define SDP_HIP_BATCH_LAST 8u  /* sdp_hip_ms2dirty_batch: last batch (FFT + screens)    */
+/* sdp_hip_ms2dirty / _vis: bucket every in-grid visibility (zero weights too,
+ * they add exact zeros; info.nvis_used then counts them) and keep the
+ * bucketing on the device for following SDP_HIP_REUSE_BUCKETS calls */
+#define SDP_HIP_KEEP_BUCKETS 16u
+/* sdp_hip_ms2dirty / _vis: reuse the kept bucketing (invert_ng's other
+ * polarisations): the same uvw and freq arrays, unchanged, and the same nrow,
+ * nchan, image geometry, epsilon, do_wstacking and FLIP_UW as the keeping
+ * call; only the visibilities, weights, flags and pol differ.  Only the value
+ * pass, gridding and FFT run.  Any other wstack call (or a workspace release)
+ * in between drops the kept bucketing: the call then fails with
+ * SDP_HIP_ERR_INVALID_ARG. */
+#define SDP_HIP_REUSE_BUCKETS 32u
 
 /* Diagnostics filled by the NUFFT entry points (may be NULL). */
 typedef struct sdp_hip_wgrid_info {

@@ -77,6 +77,7 @@ class Workspace {
         auto &b = bufs_[{dev, name}];
         if (b.bytes < bytes) {
             if (b.ptr) {
+                ++gen_;  // an existing buffer moves
                 SDP_HIP_CHECK(hipDeviceSynchronize());
                 SDP_HIP_CHECK(hipFree(b.ptr));
                 b.ptr = nullptr;
@@ -110,8 +111,15 @@ class Workspace {
         auto it = bufs_.find({dev, name});
         return it == bufs_.end() ? 0 : it->second.bytes;
     }
+    // bumped whenever a buffer handed out before is freed (regrowth, release):
+    // pointers kept across calls are valid while it is unchanged
+    uint64_t generation() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return gen_;
+    }
     void release() {
         std::lock_guard<std::mutex> lk(mu_);
+        ++gen_;
         if (!bufs_.empty()) (void)hipDeviceSynchronize();
         for (auto &kv : bufs_)
             if (kv.second.ptr) (void)hipFree(kv.second.ptr);
@@ -124,6 +132,7 @@ class Workspace {
         size_t bytes = 0;
     };
     std::mutex mu_;
+    uint64_t gen_ = 0;
     std::map<std::pair<int, std::string>, Buf> bufs_;
 };
 

@@ -342,6 +342,9 @@ struct VisExtra {
     // (vis * conj(phasor)) and exp(-2 pi i d) for predict (vis * phasor)
     bool shift = false;
     double sl = 0.0, sm = 0.0, sn = 0.0;
+    // SDP_HIP_KEEP_BUCKETS: every in-grid visibility is bucketed (zero
+    // weights add exact zeros), so the bucketing holds for any weights
+    bool all = false;
 };
 
 constexpr int kSumSlots = 1024;
@@ -427,12 +430,26 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
     c.ok = false;
     unsigned mine = 0xffffffffu;  // rank in the bucket (0xffffffff: not gridded)
     if (kScatter) {
+        double wd = 0.0;
+        if (valid) {
+            row = vg / g.nchan;
+            chan = (int)(vg - row * g.nchan);
+            wd = eff_weight(wgt, wrs, wcs, x, row, chan);
+            wt = (float)wd;
+        }
+        if (sw_slots) {
+            // weight sum of a reused bucketing (SDP_HIP_REUSE_BUCKETS): the
+            // count pass did not run, so the value pass sums the weights
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) wd += __shfl_xor(wd, o, 64);
+            if ((threadIdx.x & 63) == 0 && wd != 0.0)
+                atomicAdd(&sw_slots[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) &
+                                    (kSumSlots - 1)],
+                          wd);
+        }
         if (!valid) return;
         mine = rk[v];
         if (mine == 0xffffffffu) return;
-        row = vg / g.nchan;
-        chan = (int)(vg - row * g.nchan);
-        wt = (float)eff_weight(wgt, wrs, wcs, x, row, chan);
         c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
     } else {
         double wd = 0.0;
@@ -441,7 +458,7 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
             chan = (int)(vg - row * g.nchan);
             wd = eff_weight(wgt, wrs, wcs, x, row, chan);
             wt = (float)wd;
-            valid = (wt != 0.0f);
+            valid = x.all || (wt != 0.0f);
             if (valid) {
                 c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
                 if (!c.ok) {
@@ -2269,6 +2286,70 @@ static float2 *band_input(const Plan &P, hipStream_t st) {
     return buf;
 }
 
+// Bucketing kept by an SDP_HIP_KEEP_BUCKETS invert for SDP_HIP_REUSE_BUCKETS
+// calls (invert_ng's other polarisations): the plan (its scratch pointers and
+// host metadata), the workspace generation it is valid under, and the
+// arguments the bucketing depends on.  Every fresh plan drops it.
+struct KeptBuckets {
+    bool valid = false;
+    uint64_t gen = 0;
+    const double *uvw = nullptr, *freq = nullptr;
+    int64_t uvw_rs = 0, nrow = 0;
+    int nchan = 0, nx = 0, ny = 0, do_w = 0;
+    double px = 0, py = 0, eps = 0;
+    unsigned flip = 0;
+    Plan P;
+};
+
+static std::mutex g_kept_mu;
+static std::map<int, KeptBuckets> g_kept;
+
+static KeptBuckets &kept_buckets() {
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    return g_kept[dev];
+}
+
+static void drop_kept_buckets() {
+    std::lock_guard<std::mutex> lk(g_kept_mu);
+    kept_buckets().valid = false;
+}
+
+static void keep_buckets(const Plan &P, const Inputs &in) {
+    std::lock_guard<std::mutex> lk(g_kept_mu);
+    KeptBuckets &k = kept_buckets();
+    k.valid = true;
+    k.gen = Workspace::get().generation();
+    k.uvw = in.uvw;
+    k.freq = in.freq;
+    k.uvw_rs = in.uvw_rs;
+    k.nrow = in.nrow;
+    k.nchan = in.nchan;
+    k.nx = in.nx;
+    k.ny = in.ny;
+    k.do_w = in.do_w;
+    k.px = in.px;
+    k.py = in.py;
+    k.eps = in.eps;
+    k.flip = in.flags & SDP_HIP_FLIP_UW;
+    k.P = P;
+}
+
+static Plan reuse_buckets(const Inputs &in) {
+    std::lock_guard<std::mutex> lk(g_kept_mu);
+    const KeptBuckets &k = kept_buckets();
+    SDP_REQUIRE(k.valid && k.gen == Workspace::get().generation(),
+                "SDP_HIP_REUSE_BUCKETS: no kept bucketing (another wstack call or a workspace "
+                "release came in between)");
+    SDP_REQUIRE(k.uvw == in.uvw && k.freq == in.freq && k.uvw_rs == in.uvw_rs &&
+                    k.nrow == in.nrow && k.nchan == in.nchan && k.nx == in.nx &&
+                    k.ny == in.ny && k.do_w == in.do_w && k.px == in.px && k.py == in.py &&
+                    k.eps == in.eps && k.flip == (in.flags & SDP_HIP_FLIP_UW),
+                "SDP_HIP_REUSE_BUCKETS: uvw, freq and the geometry must be those of the "
+                "SDP_HIP_KEEP_BUCKETS call");
+    return k.P;
+}
+
 // Geometry shared by both directions: kernel, padded grid, w planes, bucket
 // granularity, row band, plane chunking, part split.  One host sync (uvw and
 // frequency extremes).
@@ -2279,6 +2360,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     SDP_REQUIRE(in.nchan > 0 && in.nrow >= 0, "nchan must be positive");
     SDP_REQUIRE(in.nrow * (int64_t)in.nchan < (int64_t)0xffffffffll,
                 "more than 2^32 visibilities per call");
+    drop_kept_buckets();  // a fresh plan re-uses the bucketing scratch
     Plan P;
     Geo &g = P.g;
     g.W = kernel_support(in.eps);
@@ -2437,7 +2519,8 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     const char *pe = std::getenv("SDP_HIP_PIPELINE");
     const int pmode = pe ? std::atoi(pe) : 0;
     P.pipelined = pmode == 2 && (g.sub == kTileFine || g.sub == kTileCell) &&
-                  P.chunk_planes == g.nplanes && in.nrow >= 2;
+                  P.chunk_planes == g.nplanes && in.nrow >= 2 &&
+                  !(in.flags & SDP_HIP_KEEP_BUCKETS);
     P.aux_bucketing = P.pipelined || (pmode == 1 && !grid_mode);
     const int nparts = P.pipelined ? kPipelineParts : 1;
     for (int i = 0; i < nparts; ++i) {
@@ -2467,7 +2550,8 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
 
 // Bucketing of one part on stream `st` (no host sync): histogram with ranks,
 // scan, scatter of the 32-byte records, work items, part metadata.
-static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipStream_t st) {
+static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipStream_t st,
+                        bool values_only = false) {
     const Geo &g = P.g;
     Part &pt = P.parts[ip];
     const std::string sfx = "#" + std::to_string(ip);
@@ -2484,16 +2568,19 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     pt.items = scratch<Item>("items" + sfx, icap);
     unsigned *kr = scratch<unsigned>("key_rank", std::max<int64_t>(in.nrow * (int64_t)in.nchan, 1)) +
                 pt.vbase;
-    SDP_HIP_CHECK(hipMemsetAsync(pt.hist, 0, (nkeys + 1) * sizeof(unsigned), st));
-    SDP_HIP_CHECK(hipMemsetAsync(pt.nbad, 0, sizeof(unsigned long long), st));
-    SDP_HIP_CHECK(hipMemsetAsync(pt.nch + ngroups, 0, sizeof(unsigned), st));
+    if (!values_only) SDP_HIP_CHECK(hipMemsetAsync(pt.hist, 0, (nkeys + 1) * sizeof(unsigned), st));
+    if (!values_only) {
+        SDP_HIP_CHECK(hipMemsetAsync(pt.nbad, 0, sizeof(unsigned long long), st));
+        SDP_HIP_CHECK(hipMemsetAsync(pt.nch + ngroups, 0, sizeof(unsigned), st));
+    }
 
     const unsigned nb = grid1d(std::max<int64_t>(pt.nvis, 1), 256);
     double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
+    // weight sums: in the count pass, or in the value pass of a reused plan
     auto launch_bucket = [&](auto scatter_tag, unsigned *counter) {
         constexpr bool S = decltype(scatter_tag)::value;
         VisRec *out = S ? P.recs + pt.vbase : nullptr;
-        double *sl = S ? nullptr : slots;
+        double *sl = S == values_only ? slots : nullptr;
         if (in.vis_dtype == SDP_HIP_C128) {
             if (grid_mode && S && P.pad4)  // 16-byte RecC records
                 k_bucket<double2, S, true, true><<<nb, 256, 0, st>>>(
@@ -2522,6 +2609,11 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
                     in.wcs, in.x, sl, counter, kr, out, pt.nbad);
         }
     };
+    if (values_only) {  // SDP_HIP_REUSE_BUCKETS: keys, ranks, offsets, items kept
+        if (pt.nvis > 0) launch_bucket(std::true_type{}, pt.offs);
+        SDP_HIP_CHECK(hipGetLastError());
+        return;
+    }
     if (pt.nvis > 0) launch_bucket(std::false_type{}, pt.hist);
     size_t tmp_bytes = 0;
     SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, pt.hist, pt.offs,
@@ -2973,7 +3065,13 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
                 "vis must be complex64 or complex128");
     StageTimer tm(st);
     tm.mark();
-    Plan P = plan_geometry(in, true, st);
+    const bool keep = in.flags & SDP_HIP_KEEP_BUCKETS, reuse = in.flags & SDP_HIP_REUSE_BUCKETS;
+    SDP_REQUIRE(!(keep && reuse), "SDP_HIP_KEEP_BUCKETS and SDP_HIP_REUSE_BUCKETS exclude each other");
+    SDP_REQUIRE(in.bounds == nullptr || !(keep || reuse),
+                "batched inverts do not keep or reuse bucketings");
+    Inputs inx = in;
+    inx.x.all = keep;
+    Plan P = reuse ? reuse_buckets(in) : plan_geometry(inx, true, st);
     const Geo &g = P.g;
     // batched invert: planes zeroed by the first batch, FFT + screens by the
     // last; in between they stay resident in the workspace
@@ -2985,8 +3083,18 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
                     "batched invert: the w planes do not all fit in device memory");
     }
     const double *tab = phi_table(g.W, g.beta, st);
-    std::vector<hipEvent_t> ev = bucket_parts(P, in, true, st);
+    std::vector<hipEvent_t> ev;
+    if (reuse) {
+        // value pass only (weight sums included), then the kept sub-sort
+        double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
+        if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
+        for (size_t i = 0; i < P.parts.size(); ++i) bucket_part(P, (int)i, inx, true, st, true);
+        if (slots) k_sum_slots<<<1, 64, 0, st>>>(slots, in.x.sumwt);
+    } else {
+        ev = bucket_parts(P, inx, true, st);
+    }
     if (P.subsort) subsort_parts(P, st);
+    if (keep) keep_buckets(P, in);
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
     float tprep = 0, tgrid = 0, tfft = 0, tscr = 0;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {

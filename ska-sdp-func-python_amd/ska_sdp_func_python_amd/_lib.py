@@ -29,6 +29,8 @@ SDP_HIP_FLIP_UW = 1
 SDP_HIP_ACCUMULATE = 2
 SDP_HIP_BATCH_FIRST = 4
 SDP_HIP_BATCH_LAST = 8
+SDP_HIP_KEEP_BUCKETS = 16
+SDP_HIP_REUSE_BUCKETS = 32
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int

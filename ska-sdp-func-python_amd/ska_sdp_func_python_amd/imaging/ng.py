@@ -168,6 +168,10 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     vis_to_im = _vis_to_im(model, freq)
     mfs = nchan == 1 and vnchan > 1
 
+    # the image pols of one channel range share one bucketing: the first pol
+    # keeps it, the others only re-run the value pass (SDP_HIP_REUSE_BUCKETS)
+    share = npol > 1 and not dopsf
+
     def grid_pol(pol, chans, ichan):
         sw = sumwt_d[ichan, pol:pol + 1]
         if dopsf and pol != 0:
@@ -181,7 +185,8 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
             uvw, freq_t[chans], None if dopsf else ms[:, chans, :], pol, wgt[:, chans, pol],
             flags[:, chans, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
             do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
-            accumulate=True, sumwt=sw, shift_lmn=lmn)
+            accumulate=True, sumwt=sw, shift_lmn=lmn, keep_buckets=share and pol == 0,
+            reuse_buckets=share and pol > 0)
         if verbosity:
             log.info("invert_ng: %s", info)
 
@@ -189,8 +194,10 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
         for pol in range(npol):
             grid_pol(pol, slice(0, vnchan), 0)
     else:
-        for pol in range(npol):
-            for vchan in range(vnchan):
+        # channel-major (the reference loops pol-major, ng.py:259-289; each
+        # (pol, chan) image is independent, so the order does not matter)
+        for vchan in range(vnchan):
+            for pol in range(npol):
                 grid_pol(pol, slice(vchan, vchan + 1), int(vis_to_im[vchan]))
     sumwt = sumwt_d.cpu().numpy()
 

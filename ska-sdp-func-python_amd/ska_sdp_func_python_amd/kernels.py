@@ -184,14 +184,20 @@ _FLAG_DT = {torch.int64: 8, torch.int32: 4, torch.int8: 1, torch.uint8: 1, torch
 
 def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_x, pixsize_y,
                  epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None, out_strides=None,
-                 accumulate=False, sumwt=None, shift_lmn=None):
+                 accumulate=False, sumwt=None, shift_lmn=None, keep_buckets=False,
+                 reuse_buckets=False):
     """ms2dirty with invert_ng's visibility prologue fused in
     (sdp_hip_ms2dirty_vis): ``vis`` [nrow, nchan, npol_vis] complex (any
     strides, read in place; None = unit visibilities), ``flags`` the same
     shape (integer / bool, or None), ``wgt`` [nrow, nchan] f32/f64 weights of
     image pol ``pol``, ``coef`` the conversion-matrix row for that pol
     (complex [npol_vis]) or None for no conversion, ``sumwt`` a one-element
-    f64 device view that receives += the masked weight sum."""
+    f64 device view that receives += the masked weight sum.
+
+    ``keep_buckets`` buckets every in-grid visibility and keeps the bucketing
+    on the device; a following call with ``reuse_buckets`` and the same uvw,
+    freq and geometry (another image pol) runs only the value pass, gridding
+    and FFT (SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS)."""
     _eps_note(epsilon)
     _check_uvw(uvw)
     dev = uvw.device
@@ -232,6 +238,8 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
     if sumwt is not None and (sumwt.dtype != torch.float64 or not sumwt.is_cuda):
         raise ValueError("sumwt must be a float64 device tensor")
     bits = (_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+    bits |= (_lib.SDP_HIP_KEEP_BUCKETS if keep_buckets else 0) | \
+        (_lib.SDP_HIP_REUSE_BUCKETS if reuse_buckets else 0)
     info = _lib.WGridInfo()
     _lib.call(
         "sdp_hip_ms2dirty_vis",

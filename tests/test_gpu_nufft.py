@@ -416,6 +416,55 @@ def test_invert_ng_fused_prologue(pf, ipf, mfs, dopsf, device):
     np.testing.assert_allclose(sumwt, exp_sw, rtol=1e-6 if device else 1e-12)
 
 
+def test_shared_bucketing_across_pols():
+    """SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS (invert_ng's image pols):
+    pol 0 keeps its bucketing, pols 1-3 -- different weights and flags, pol 0
+    zero where the others are not -- re-run only the value pass.  Each image
+    and weight sum equals an independent call (1e-6 relative RMS: the order
+    of the fp32 sums inside a cell differs; sumwt 1e-12); a reuse after
+    another wstack call, or with other uvw, is refused."""
+    from ska_sdp_func_python_amd import kernels
+    rng = np.random.default_rng(71)
+    nrow, nchan, npol, npix = 6000, 8, 4, 256
+    freq = np.linspace(1.0e9, 1.2e9, nchan)
+    umax = 3000.0
+    uvw_h = rng.uniform(-1, 1, (nrow, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw_h[:, 2] *= 0.3
+    dev = "cuda"
+    uvw = torch.as_tensor(uvw_h, device=dev)
+    freq_t = torch.as_tensor(freq, device=dev)
+    vis = torch.as_tensor(rng.normal(size=(nrow, nchan, npol)) +
+                          1j * rng.normal(size=(nrow, nchan, npol)), device=dev).to(torch.complex64)
+    flags = torch.as_tensor(rng.uniform(size=(nrow, nchan, npol)) < 0.2, device=dev).to(torch.int32)
+    wgt = torch.as_tensor(rng.uniform(0.5, 2.0, (nrow, nchan, npol)), device=dev)
+    wgt[: nrow // 3, :, 0] = 0.0  # pol 0 drops rows the other pols grid
+    cell = 0.35 / umax
+    args = (npix, npix, cell, cell, 1e-5, True)
+
+    def run(pol, **kw):
+        sw = torch.zeros(1, dtype=torch.float64, device=dev)
+        out, info = kernels.ms2dirty_vis(uvw, freq_t, vis, pol, wgt[:, :, pol].contiguous(), flags,
+                                         None, *args, flip_uw=True, sumwt=sw, **kw)
+        return out.cpu().numpy(), float(sw.cpu()), info
+
+    ind = [run(p) for p in range(npol)]
+    shared = [run(0, keep_buckets=True)] + [run(p, reuse_buckets=True) for p in range(1, npol)]
+    for p in range(npol):
+        assert rel_rms(shared[p][0], ind[p][0]) < 1e-6, p
+        assert abs(shared[p][1] - ind[p][1]) <= 1e-12 * abs(ind[p][1])
+    assert shared[0][2]["nvis_used"] == nrow * nchan  # zero weights bucketed too
+    # any other wstack call drops the kept bucketing
+    kernels.dirty2ms(uvw, freq_t, torch.zeros((npix, npix), dtype=torch.float64, device=dev),
+                     None, cell, cell, 1e-5, True, flip_uw=True)
+    with pytest.raises(ValueError, match="no kept bucketing"):
+        run(1, reuse_buckets=True)
+    run(0, keep_buckets=True)
+    uvw2 = uvw.clone()
+    with pytest.raises(ValueError, match="must be those of"):
+        kernels.ms2dirty_vis(uvw2, freq_t, vis, 1, wgt[:, :, 1].contiguous(), flags, None, *args,
+                             flip_uw=True, reuse_buckets=True)
+
+
 @pytest.mark.parametrize("ipf,pf", [("stokesI", "stokesI"), ("stokesIQUV", "linear"),
                                     ("stokesIQUV", "circular"), ("linear", "linear")])
 @pytest.mark.parametrize("mfs", [True, False])
