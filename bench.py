@@ -420,12 +420,13 @@ def main():
             traffic = json.load(f).get("bytes_per_launch")
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": (f"k_grid_mfma<{info['support']},true,false>" if info["bucket"] == 1
+            "kernel": (f"k_grid_mfma_pad<{info['support']},true>" if info["bucket"] == 1
                        else f"k_grid_reg<{info['support']},true>" if info["bucket"] == 2
                        else f"k_grid_lds<{info['support']},true,2>"), "kernel_ms": round(ms_grid / launches, 4),
             "alg_bytes_per_launch": int(alg_bytes / launches),
-            # the gridder is VALU-issue bound: the same kernel against the
-            # fp32 vector peak (4 W^3 flops per visibility)
+            # the gridder's work is fp32 MFMA (v_mfma_f32_16x16x4_f32): the
+            # same kernel against the fp32 matrix peak (= the fp32 vector peak
+            # on gfx950), 4 W^3 flops per visibility
             "compute": {"achieved": round(nvis_rank * 4 * info["support"] ** 3 / (ms_grid * 1e-3) / 1e12, 2),
                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(nvis_rank * 4 * info["support"] ** 3 / (ms_grid * 1e-3) / 1e12
