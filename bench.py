@@ -62,9 +62,9 @@ def parse():
     ap.add_argument("--config", choices=("c2", "c4"), default="c2",
                     help="c2: configs[1], weak scaling (default); c4: configs[3], the SKA-LOW "
                          "256-channel band on the 8192^2 image, strong scaling")
-    ap.add_argument("--c4-batch", type=int, default=36,
+    ap.add_argument("--c4-batch", type=int, default=40,
                     help="c4: max channels per streamed batch of a rank's block (a block is "
-                         "split into that many near-equal batches; 36 keeps one batch per "
+                         "split into that many near-equal batches; 40 keeps one batch per "
                          "rank at N = 8 and fits the 71 resident planes beside it)")
     ap.add_argument("--emulate", default=None, metavar="RANK/WORLD",
                     help="c4 on one GPU: run only rank RANK's block of a WORLD-way partition "

@@ -7,11 +7,11 @@ mkdir -p gpurun_out
 tag=${1:-r02}
 out=gpurun_out/${tag}_c4_scaling.jsonl
 : > $out
-timeout -k 10 300 python -u bench.py --config c4 --steps 2 --warmup 1 > gpurun_out/${tag}_c4_n1.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --config c4 --steps 2 --warmup 1 ${C4ARGS} > gpurun_out/${tag}_c4_n1.log 2>&1 || exit $?
 grep '^{' gpurun_out/${tag}_c4_n1.log >> $out
 for w in ${WORLDS:-8 4 2}; do
   for ((r = 0; r < w; r++)); do
-    timeout -k 10 300 python -u bench.py --config c4 --steps 2 --warmup 1 --emulate $r/$w > gpurun_out/${tag}_c4_e${r}_${w}.log 2>&1 || exit $?
+    timeout -k 10 300 python -u bench.py --config c4 --steps 2 --warmup 1 ${C4ARGS} --emulate $r/$w > gpurun_out/${tag}_c4_e${r}_${w}.log 2>&1 || exit $?
     grep '^{' gpurun_out/${tag}_c4_e${r}_${w}.log >> $out
   done
 done

@@ -78,6 +78,11 @@ struct Geo {
     // buckets are histogrammed, scanned and itemised
     int wx0, wy0, wnx, wny;
     int grp;               // consecutive buckets (along y) per work-item group
+    // keys per bucket (16x16-cell buckets: a power of 2 > 1): the count pass
+    // spreads a bucket's histogram counter over `salt` adjacent counters by
+    // row, so the uv core's hot buckets take several memory-side atomic
+    // streams; the sub-buckets are adjacent, so the bucket stays contiguous
+    int salt;
     int dbg;               // experiment knobs (SDP_HIP_DBG)
     double su;  // sign applied to u and w (-1 with SDP_HIP_FLIP_UW)
     int nchan;
@@ -201,11 +206,12 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
 }
 
 // p0-major bucket keys: the items of a range of first planes are contiguous.
-__device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c) {
+__device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c, int64_t row) {
     const int ic = c.ic0 - g.wx0, jc = c.jc0 - g.wy0;
     const int tile = g.sub == kTileCell ? ((ic >> 1) * g.nty + jc) * 2 + (ic & 1)
                                         : (ic / g.sub) * g.nty + (jc / g.sub);
-    return (unsigned)c.p0 * (unsigned)g.ntiles + (unsigned)tile;
+    return ((unsigned)c.p0 * (unsigned)g.ntiles + (unsigned)tile) * (unsigned)g.salt +
+           ((unsigned)row & (unsigned)(g.salt - 1));
 }
 
 // ------------------------------------------------------------------------
@@ -467,7 +473,7 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
                 }
             }
         }
-        const unsigned key = valid ? coord_key(g, c) : 0xffffffffu;
+        const unsigned key = valid ? coord_key(g, c, row) : 0xffffffffu;
         const unsigned rank = (g.dbg & 8) ? 0u : run_reserve<true>(key, valid, counter);
         // only the rank is kept: the scatter pass recomputes the key
         if (v < nvis) rk[v] = valid ? rank : 0xffffffffu;
@@ -482,7 +488,7 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
         }
         return;
     }
-    const unsigned pos = (g.dbg & 16) ? (unsigned)v : counter[coord_key(g, c)] + mine;
+    const unsigned pos = (g.dbg & 16) ? (unsigned)v : counter[coord_key(g, c, row)] + mine;
     float cr = wt, ci = 0.0f;
     if (kGrid) {
         const float2 xv = vis ? eff_vis(vis, vrs, vcs, x, row, chan) : make_float2(1.0f, 0.0f);
@@ -2473,7 +2479,13 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.nty = g.wny / g.sub;
     g.ntiles = (g.wnx / g.sub) * g.nty;
     g.grp = g.sub == kTileCell ? kGroupCell : (g.sub == kTileFine ? kGroupFine : 1);
-    SDP_REQUIRE((double)g.ntiles * g.nps < 4.0e9, "too many (plane, tile) buckets");
+    g.salt = 1;
+    if (g.sub == kTileCoarse) {
+        const int sv = env_int("SDP_HIP_SALT", 4);
+        g.salt = (sv >= 1 && sv <= 64 && (sv & (sv - 1)) == 0) ? sv : 4;
+        while (g.salt > 1 && (double)g.ntiles * g.nps * g.salt >= 1.0e9) g.salt >>= 1;
+    }
+    SDP_REQUIRE((double)g.ntiles * g.nps * g.salt < 4.0e9, "too many (plane, tile) buckets");
 
     // grid rows reached by any footprint (centred storage)
     {
@@ -2500,7 +2512,8 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     const int64_t nvis_all = in.nrow * (int64_t)in.nchan;
     const size_t need_other =
         (size_t)nvis_all * (sizeof(VisRec) + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2))) +
-        (size_t)g.ntiles * g.nps * 2 * sizeof(unsigned) + (size_t)P.fft_planes * spec_plane;
+        (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned) +
+        (size_t)P.fft_planes * spec_plane;
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
     P.chunk_planes = std::min(cp, g.nplanes);
     P.fft_planes = std::min(P.fft_planes, P.chunk_planes);
@@ -2555,8 +2568,9 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     const Geo &g = P.g;
     Part &pt = P.parts[ip];
     const std::string sfx = "#" + std::to_string(ip);
-    const size_t nkeys = (size_t)g.ntiles * g.nps;
-    const int64_t ngroups = (int64_t)nkeys / g.grp;
+    const size_t nkeys = (size_t)g.ntiles * g.nps * g.salt;
+    const int kpg = g.grp * g.salt;  // keys per work-item group
+    const int64_t ngroups = (int64_t)nkeys / kpg;
     const int gpp = g.ntiles / g.grp;  // groups per first-plane value
     pt.hist = scratch<unsigned>("hist" + sfx, nkeys + 1);
     pt.offs = scratch<unsigned>("offs" + sfx, nkeys + 1);
@@ -2655,11 +2669,11 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     }
 
     // work items (p0-major, so a first-plane range is a contiguous item range)
-    k_items_count<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, pt.offs, P.chunk, pt.nch);
+    k_items_count<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, kpg, pt.offs, P.chunk, pt.nch);
     tb = tmp_bytes + 16;
     SDP_HIP_CHECK(
         hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.nch, pt.ioffs, (int)(ngroups + 1), st));
-    k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, g.grp, gpp, pt.offs, pt.ioffs,
+    k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, kpg, gpp, pt.offs, pt.ioffs,
                                                        P.chunk, pt.items);
     k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys, pt.npad, pt.ioffs, gpp,
                                                       g.nps, pt.meta);

@@ -28,27 +28,39 @@ def interleaved_channels(nchan_total, rank, world):
 
 
 # Cost model of one rank's invert of a contiguous channel block of the C4
-# band (SKA-LOW 512 stations x 400 times, 8192^2 image, 16384^2 grid),
-# fitted to the per-block stage times measured on one MI355X
-# (profiles/r02_c4_blocks.jsonl): bucketing + gridding per channel (higher in
-# the compact low band, whose uv core concentrates the histogram atomics)
-# plus FFT + w-screen per resident w plane, the plane count growing with the
-# block's top frequency (w range in wavelengths ~ f_hi).
-C4_CHAN_COST = ((68.75e6, 8.09), (106.25e6, 6.67), (143.75e6, 6.47), (181.25e6, 6.39),
-                (218.75e6, 6.39), (256.25e6, 6.39), (293.75e6, 6.39), (331.25e6, 6.82))
-C4_PLANE_MS = 1.58
+# band (SKA-LOW 512 stations x 400 times, 8192^2 image, 16384^2 grid): a
+# least-squares fit (non-negative) to the per-rank times of the 1-, 2-, 4-
+# and 8-way partitions measured on one MI355X
+# (profiles/r02_c4_scaling_salt4.jsonl, bench.py --config c4 --emulate),
+# within 4 % of every measurement:
+#   * bucketing + gridding per channel (52.3 Mvis each), piecewise linear in
+#     frequency -- highest in the compact low band, whose uv core
+#     concentrates the histogram atomics;
+#   * 48.8 ms per batch beyond the first (a block streams in batches of at
+#     most C4_MAX_BATCH channels: plan, bucket histogram, sub-sort items);
+#   * 2.34 ms per resident w plane (zeroing, FFT, w-screen), the plane
+#     count growing with the block's top frequency (w range ~ f_hi);
+#   * 4.2 ms fixed.
+C4_CHAN_COST = ((50e6, 7.49), (110e6, 4.14), (170e6, 4.76), (230e6, 4.19), (290e6, 4.82),
+                (350e6, 4.77))
+C4_BATCH_MS = 48.8
+C4_MAX_BATCH = 40
+C4_PLANE_MS = 2.34
+C4_FIXED_MS = 4.2
 C4_PLANES = (0.179e-6, 8.33)  # nplanes ~ a f_hi + b
 
 
-def c4_block_cost(freqs):
+def c4_block_cost(freqs, max_batch=C4_MAX_BATCH):
     """Modelled invert time (ms) of one rank holding the channels `freqs`
-    (one shared plane layout, one FFT pass)."""
+    (one shared plane layout, one FFT pass, batches of <= max_batch)."""
     f = np.asarray(freqs, dtype=float)
     if f.size == 0:
         return 0.0
     xs, ys = zip(*C4_CHAN_COST)
     per_chan = float(np.interp(f, xs, ys).sum())
-    return per_chan + C4_PLANE_MS * (C4_PLANES[0] * float(f.max()) + C4_PLANES[1])
+    batches = -(-f.size // max_batch)
+    return (C4_FIXED_MS + per_chan + C4_BATCH_MS * (batches - 1) +
+            C4_PLANE_MS * (C4_PLANES[0] * float(f.max()) + C4_PLANES[1]))
 
 
 def balanced_channel_blocks(freqs, world, cost=c4_block_cost):
