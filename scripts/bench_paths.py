@@ -248,7 +248,7 @@ if "cfgrid" in which:
           "value": round(nrow / t / 1e6, 1), "unit": "Mvis/s",
           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                       "note": "inputs + 16 B of fp64 atomic adds per tap"},
+                       "note": "the per-tap algorithm's bytes: inputs + 16 B (one complex add) per tap; the LDS tile turns the adds into one fp64 atomic per touched cell per work item"},
           "cpu_baseline": {"value": round(ns / tc / 1e6, 4), "unit": "Mvis/s", "cores": 1,
                            "kind": "port",
                            "sample": f"ref_oracle.grid_cf (the reference's per-visibility loop), "

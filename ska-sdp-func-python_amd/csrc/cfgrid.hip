@@ -6,14 +6,23 @@
 //
 // The Python layer evaluates the reference's WCS mappings (spatial_mapping,
 // gridding.py:60-157) into integer grid / sub-sample / w-plane indices per
-// (channel, row).  Here one wave handles one (row, channel) with one lane per
-// CF tap:
-//   grid:   gd[c, p, pv-dv+iv, pu-du+iu] += conj(cf[c, p, w, dv_off, du_off, iv, iu]) * V * wt
-//           (fp64 global atomics; sumwt per block in LDS, then one of kSlots
-//           partial sums per pol, folded by k_fold_slots)
-//   degrid: V = sum_{iv,iu} gd[c, p, window] * cf[c, p, w, dv_off, du_off, iv, iu]
+// (channel, row).  Gridding,
+//   gd[c, p, pv-dv+iv, pu-du+iu] += conj(cf[c, p, w, dv_off, du_off, iv, iu]) * V * wt,
+// runs on (row, channel) entries sorted by 16x16-pixel tile of their centre
+// pixel (k_cf_count: rank by atomic, hipcub scan, k_cf_scatter), split into
+// work items of <= kChunk entries; one wave per (item, pol) accumulates its
+// entries' footprints in an LDS tile of (16+gv-1) x (16+gu-1) fp64 complex
+// cells (plain read-modify-write: one lane per tap, in-order LDS per wave)
+// and flushes it once with fp64 global atomics, zero cells skipped -- one
+// global add per touched cell per item instead of one per tap per entry.
+// sumwt per block in LDS, then one of kSlots partial sums per pol, folded
+// by k_fold_slots.  Supports too large for the LDS tile use k_grid_cf (one
+// wave per entry, fp64 atomics per tap).  Degridding:
+//   V = sum_{iv,iu} gd[c, p, window] * cf[c, p, w, dv_off, du_off, iv, iu]
 // with the reference's edge-skip rule (gridding.py:230-237, :555-563): a row
 // whose window touches pv+dv >= ny or pu+du >= nx (or < 0) is skipped.
+#include <hipcub/hipcub.hpp>
+
 #include "sdp_common.h"
 
 namespace sdp {
@@ -98,6 +107,181 @@ __global__ __launch_bounds__(kThreads) void k_grid_cf(Shape s, const int32_t *__
         atomicAdd(&wslots[((size_t)slot * s.g_nchan + imchan) * s.npol + threadIdx.x],
                   s_wt[threadIdx.x]);
     if (threadIdx.x == 0 && s_skip) atomicAdd(&skslots[slot], s_skip);
+}
+
+// ---- sorted / LDS-tile gridding -----------------------------------------
+constexpr int kTile = 16;            // tile edge (pixels) of the entry sort
+constexpr unsigned kChunk = 256;     // max entries per work item
+constexpr size_t kMaxTileLds = 64 * 1024;
+
+struct CfItem {
+    uint32_t b, e, key, pad;
+};
+
+// Count pass, one thread per (row, chan) entry (blockIdx.y = chan): the
+// edge-skip rule, the weight sums (per block in LDS, then slots) and the
+// entry's rank in its (image channel, tile) bucket
+__global__ __launch_bounds__(kThreads) void k_cf_count(Shape s, int ntx, int ntiles,
+                                                       const int32_t *__restrict__ pu,
+                                                       const int32_t *__restrict__ pv,
+                                                       const int32_t *__restrict__ vis_to_im,
+                                                       const double *__restrict__ wt,
+                                                       unsigned *cnt, unsigned *__restrict__ rk,
+                                                       double *wslots,
+                                                       unsigned long long *skslots) {
+    __shared__ double s_wt[kMaxPol];
+    __shared__ unsigned long long s_skip;
+    if (threadIdx.x < kMaxPol) s_wt[threadIdx.x] = 0.0;
+    if (threadIdx.x == 0) s_skip = 0;
+    __syncthreads();
+    const int chan = blockIdx.y;
+    const int imchan = vis_to_im[chan];
+    const int64_t row = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+    bool ok = false;
+    if (row < s.nrow) {
+        const size_t m = (size_t)chan * s.nrow + row;
+        const int u0 = pu[m], v0 = pv[m];
+        ok = window_ok(s, u0, v0);
+        if (!ok) {
+            atomicAdd(&s_skip, (unsigned long long)s.npol);
+            rk[m] = 0xffffffffu;
+        } else {
+            const unsigned key = (unsigned)imchan * (unsigned)ntiles +
+                                 (unsigned)((v0 / kTile) * ntx + u0 / kTile);
+            rk[m] = atomicAdd(&cnt[key], 1u);
+        }
+    }
+    // weight sums: wave reduction, one LDS add per wave and pol
+    for (int p = 0; p < s.npol; ++p) {
+        double w = ok ? wt[((size_t)row * s.nchan + chan) * s.npol + p] : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o, 64);
+        if ((threadIdx.x & 63) == 0 && w != 0.0) atomicAdd(&s_wt[p], w);
+    }
+    __syncthreads();
+    const int slot = (blockIdx.x + blockIdx.y * gridDim.x) & (kSlots - 1);
+    if (threadIdx.x < s.npol && s_wt[threadIdx.x] != 0.0)
+        atomicAdd(&wslots[((size_t)slot * s.g_nchan + imchan) * s.npol + threadIdx.x],
+                  s_wt[threadIdx.x]);
+    if (threadIdx.x == 0 && s_skip) atomicAdd(&skslots[slot], s_skip);
+}
+
+__global__ __launch_bounds__(kThreads) void k_cf_scatter(Shape s, int ntx, int ntiles,
+                                                         const int32_t *__restrict__ pu,
+                                                         const int32_t *__restrict__ pv,
+                                                         const int32_t *__restrict__ vis_to_im,
+                                                         const unsigned *__restrict__ offs,
+                                                         const unsigned *__restrict__ rk,
+                                                         uint32_t *__restrict__ order) {
+    const int chan = blockIdx.y;
+    const int64_t row = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+    if (row >= s.nrow) return;
+    const size_t m = (size_t)chan * s.nrow + row;
+    const unsigned r = rk[m];
+    if (r == 0xffffffffu) return;
+    const int u0 = pu[m], v0 = pv[m];
+    const unsigned key = (unsigned)vis_to_im[chan] * (unsigned)ntiles +
+                         (unsigned)((v0 / kTile) * ntx + u0 / kTile);
+    order[offs[key] + r] = (uint32_t)m;
+}
+
+__global__ void k_cf_nitems(int64_t nkeys, const unsigned *__restrict__ offs, unsigned *nit) {
+    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (k >= nkeys) return;
+    nit[k] = (offs[k + 1] - offs[k] + kChunk - 1) / kChunk;
+}
+
+__global__ void k_cf_items(int64_t nkeys, const unsigned *__restrict__ offs,
+                           const unsigned *__restrict__ ioffs, CfItem *__restrict__ items) {
+    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (k >= nkeys) return;
+    const unsigned b = offs[k], e = offs[k + 1];
+    unsigned o = ioffs[k];
+    for (unsigned x = b; x < e; x += kChunk) items[o++] = CfItem{x, min(e, x + kChunk), (uint32_t)k, 0u};
+}
+
+__device__ __forceinline__ double lane_readd(double v, int k) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), k);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// One wave per (item, pol): the item's entries are fetched 64 at a time (one
+// per lane) and broadcast; lane t owns tap t (taps > 64: t, t+64, ...).
+__global__ __launch_bounds__(64) void k_cf_tile(Shape s, int ntx, int ntiles,
+                                                const CfItem *__restrict__ items,
+                                                const uint32_t *__restrict__ order,
+                                                const int32_t *__restrict__ pu,
+                                                const int32_t *__restrict__ pv,
+                                                const int32_t *__restrict__ pwc,
+                                                const int32_t *__restrict__ pdu,
+                                                const int32_t *__restrict__ pdv,
+                                                const double2 *__restrict__ vis,
+                                                const double *__restrict__ wt,
+                                                const double2 *__restrict__ cf, double2 *grid) {
+    extern __shared__ __attribute__((aligned(16))) double2 acc[];
+    const CfItem it = items[blockIdx.x];
+    const int p = blockIdx.y;
+    const int lane = threadIdx.x;
+    const int imchan = (int)(it.key / (unsigned)ntiles);
+    const int tile = (int)(it.key - (unsigned)imchan * (unsigned)ntiles);
+    const int ty = tile / ntx, tx = tile - (tile / ntx) * ntx;
+    const int W2 = kTile + s.gu - 1, H2 = kTile + s.gv - 1;
+    const int taps = s.gv * s.gu;
+    for (int i = lane; i < H2 * W2; i += 64) acc[i] = make_double2(0.0, 0.0);
+    // lane's first tap: offset inside the LDS tile relative to the footprint start
+    const int t0v = lane / s.gu, t0u = lane - (lane / s.gu) * s.gu;
+    const int toff0 = t0v * W2 + t0u;
+    for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
+        const int n = (int)min(64u, it.e - b0);
+        // lane l decodes entry b0 + l
+        int loff = 0;
+        long long cfo = 0;
+        double xr = 0.0, xi = 0.0;
+        if (lane < n) {
+            const uint32_t m = order[b0 + lane];
+            const int chan = (int)(m / (uint32_t)s.nrow);
+            const int64_t row = (int64_t)m - (int64_t)chan * s.nrow;
+            loff = (pv[m] - ty * kTile) * W2 + (pu[m] - tx * kTile);
+            cfo = (long long)cf_index(s, imchan, p, pwc[m], pdv[m], pdu[m]) * taps;
+            const size_t vi = ((size_t)row * s.nchan + chan) * s.npol + p;
+            const double2 x = vis[vi];
+            const double w = wt[vi];
+            xr = x.x * w;
+            xi = x.y * w;
+        }
+        for (int k = 0; k < n; ++k) {
+            const int lo = __builtin_amdgcn_readlane(loff, k);
+            const long long co = ((long long)__builtin_amdgcn_readlane((int)(cfo >> 32), k) << 32) |
+                                 (unsigned)__builtin_amdgcn_readlane((int)(cfo & 0xffffffffll), k);
+            const double kr = lane_readd(xr, k), ki = lane_readd(xi, k);
+            for (int t = lane, to = toff0; t < taps; t += 64) {
+                const double2 c = cf[co + t];
+                double2 a = acc[lo + to];
+                // conj(cf) * x: re = cr xr + ci xi, im = cr xi - ci xr
+                a.x += c.x * kr + c.y * ki;
+                a.y += c.x * ki - c.y * kr;
+                acc[lo + to] = a;
+                if (t + 64 < taps) {
+                    const int nv = (t + 64) / s.gu, nu = (t + 64) - ((t + 64) / s.gu) * s.gu;
+                    to = nv * W2 + nu;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    double *g = reinterpret_cast<double *>(grid + ((size_t)imchan * s.npol + p) * s.ny * s.nx);
+    const double *fa = reinterpret_cast<const double *>(acc);
+    const int v00 = ty * kTile - s.gv / 2, u00 = tx * kTile - s.gu / 2;
+    for (int f = lane; f < 2 * H2 * W2; f += 64) {
+        const double val = fa[f];
+        if (val == 0.0) continue;
+        const int c = f >> 1, lv = c / W2, lu = c - (c / W2) * W2;
+        const int v = v00 + lv, u = u00 + lu;
+        if (v < 0 || v >= s.ny || u < 0 || u >= s.nx) continue;
+        atomicAdd(g + 2 * ((size_t)v * s.nx + u) + (f & 1), val);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_fold_slots(int nsum, const double *__restrict__ wslots,
@@ -213,10 +397,57 @@ int sdp_hip_grid_cf(int64_t nrowvis, int nchan_vis, int npol, const int32_t *pu,
         auto *skslots = scratch<unsigned long long>("cf_skslots", cfgrid::kSlots);
         SDP_HIP_CHECK(hipMemsetAsync(wslots, 0, sizeof(double) * cfgrid::kSlots * nsum, st));
         SDP_HIP_CHECK(hipMemsetAsync(skslots, 0, sizeof(unsigned long long) * cfgrid::kSlots, st));
-        const dim3 blocks((unsigned)((nrowvis + 3) / 4), nchan_vis);
-        cfgrid::k_grid_cf<<<blocks, cfgrid::kThreads, 0, st>>>(
-            s, pu, pv, pwc, pdu, pdv, vis_to_im, static_cast<const double2 *>(vis), wt,
-            static_cast<const double2 *>(cf), static_cast<double2 *>(grid), wslots, skslots);
+        const size_t lds = (size_t)(cfgrid::kTile + gv - 1) * (cfgrid::kTile + gu - 1) *
+                           sizeof(double2);
+        const int64_t nent = nrowvis * (int64_t)nchan_vis;
+        if (lds <= cfgrid::kMaxTileLds && nent < (int64_t)0xffffffffll) {
+            // entries sorted by (image channel, 16x16 tile), LDS-tile accumulation
+            const int ntx = (nx + cfgrid::kTile - 1) / cfgrid::kTile;
+            const int nty = (ny + cfgrid::kTile - 1) / cfgrid::kTile;
+            const int ntiles = ntx * nty;
+            const int64_t nkeys = (int64_t)ntiles * g_nchan;
+            SDP_REQUIRE(nkeys < (int64_t)0x7fffffff, "grid too large for the tile sort");
+            auto *cnt = scratch<unsigned>("cf_cnt", nkeys + 1);
+            auto *offs = scratch<unsigned>("cf_offs", nkeys + 1);
+            auto *nit = scratch<unsigned>("cf_nit", nkeys + 1);
+            auto *ioffs = scratch<unsigned>("cf_ioffs", nkeys + 1);
+            auto *rk = scratch<unsigned>("cf_rank", nent);
+            auto *order = scratch<uint32_t>("cf_order", nent);
+            SDP_HIP_CHECK(hipMemsetAsync(cnt, 0, sizeof(unsigned) * (nkeys + 1), st));
+            SDP_HIP_CHECK(hipMemsetAsync(nit + nkeys, 0, sizeof(unsigned), st));
+            const dim3 eb((unsigned)((nrowvis + cfgrid::kThreads - 1) / cfgrid::kThreads),
+                          nchan_vis);
+            cfgrid::k_cf_count<<<eb, cfgrid::kThreads, 0, st>>>(s, ntx, ntiles, pu, pv, vis_to_im,
+                                                                wt, cnt, rk, wslots, skslots);
+            size_t tb = 0;
+            SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, offs,
+                                                           (int)(nkeys + 1), st));
+            void *tmp = scratch<char>("cf_scan_tmp", tb + 16);
+            size_t tb2 = tb + 16;
+            SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, cnt, offs, (int)(nkeys + 1), st));
+            cfgrid::k_cf_scatter<<<eb, cfgrid::kThreads, 0, st>>>(s, ntx, ntiles, pu, pv, vis_to_im,
+                                                                  offs, rk, order);
+            cfgrid::k_cf_nitems<<<grid1d(nkeys, 256), 256, 0, st>>>(nkeys, offs, nit);
+            tb2 = tb + 16;
+            SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, nit, ioffs, (int)(nkeys + 1), st));
+            unsigned nitems = 0;
+            SDP_HIP_CHECK(hipMemcpyAsync(&nitems, ioffs + nkeys, sizeof(unsigned),
+                                         hipMemcpyDeviceToHost, st));
+            SDP_HIP_CHECK(hipStreamSynchronize(st));
+            if (nitems > 0) {
+                auto *items = scratch<cfgrid::CfItem>("cf_items", nitems);
+                cfgrid::k_cf_items<<<grid1d(nkeys, 256), 256, 0, st>>>(nkeys, offs, ioffs, items);
+                cfgrid::k_cf_tile<<<dim3(nitems, npol), 64, lds, st>>>(
+                    s, ntx, ntiles, items, order, pu, pv, pwc, pdu, pdv,
+                    static_cast<const double2 *>(vis), wt, static_cast<const double2 *>(cf),
+                    static_cast<double2 *>(grid));
+            }
+        } else {
+            const dim3 blocks((unsigned)((nrowvis + 3) / 4), nchan_vis);
+            cfgrid::k_grid_cf<<<blocks, cfgrid::kThreads, 0, st>>>(
+                s, pu, pv, pwc, pdu, pdv, vis_to_im, static_cast<const double2 *>(vis), wt,
+                static_cast<const double2 *>(cf), static_cast<double2 *>(grid), wslots, skslots);
+        }
         cfgrid::k_fold_slots<<<nsum + 1, 256, 0, st>>>(
             nsum, wslots, skslots, sumwt, reinterpret_cast<unsigned long long *>(nskipped));
         SDP_HIP_CHECK(hipGetLastError());
