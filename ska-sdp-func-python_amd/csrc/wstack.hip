@@ -1698,6 +1698,135 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
     }
 }
 
+// MFMA degridder (predict) on one-cell buckets: the adjoint of
+// k_grid_mfma_pad's GEMM.  All records of a cell share their footprint
+// origin, so for 16 records of one cell
+//   D[(q, re/im), r] = sum_(kx,ky) G[q][xo + kx][yo + ky] . tu_r[kx] tv_r[ky]
+// is one 16 x 16 x 64 GEMM (16 K-steps of v_mfma_f32_16x16x4_f32, exact fp32):
+// A = the cell's footprint of the W planes (row (q, re/im), held in 16
+// VGPRs per lane while the cell lasts), B = the records' separable (u, v)
+// taps (column = record).  K-step s covers taps (kx, ky) = (s >> 1,
+// 4 (s & 1) + k), k = lane >> 4.  The w taps then weight the rows:
+// V_r = sum_q tw_r[q] D[(q, .), r], a 4-lane-group reduction.  The 24 taps
+// of a record are evaluated once, 6 by each of its 4 lanes (lane group k:
+// tu 2k, 2k+1; tv k, k+4; tw 2k, 2k+1), the tu taps shared by ds_bpermute.
+// One wave per work item (a chunk of a group of 16 cells, a 2 x 8-cell
+// region whose W planes are staged in LDS once).  The record factor
+// wgt * exp(-2 pi i w s0) is applied and the visibility written in place
+// (vdirect), or the raw sum added to acc[record] for k_finalize.
+template <int W, bool WS, bool FI>
+__global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restrict__ recs,
+                                                    ItemSrc src, const unsigned *__restrict__ offs,
+                                                    const FineItem *__restrict__ fitems,
+                                                    const float2 *__restrict__ grid, int p_lo,
+                                                    int p_hi, float2 *__restrict__ acc,
+                                                    float2 *__restrict__ vdirect) {
+    static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
+    constexpr int NQ = WS ? W : 1;
+    const uint32_t n_items = item_count(src);
+    const uint32_t stride = item_stride(n_items);
+    const int lane = threadIdx.x;
+    const int r16 = lane & 15, kg = lane >> 4;
+    const float ihw = g.inv_half_w, bl = g.beta_l2e;
+    const int aq = r16 >> 1, aim = r16 & 1;  // A row (q, re/im)
+    const float tu0 = (float)(2 * kg) * ihw, tu1 = (float)(2 * kg + 1) * ihw;
+    const float tv0 = (float)kg * ihw, tv1 = (float)(kg + 4) * ihw;
+    const float *const ftile = reinterpret_cast<const float *>(tile);
+    const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        uint32_t fo[kGroupCell];
+        Item it;
+        if (FI) {
+            it = load_fine_item<kGroupCell>(fitems, w_it, n_items, stride, fo);
+            if (it.b >= it.e) continue;
+        } else {
+            it = load_item(src, w_it, n_items, stride);
+            const unsigned *ob = offs + ((size_t)it.p0 * g.ntiles + (size_t)it.tile * kGroupCell);
+#pragma unroll
+            for (int c = 0; c < kGroupCell; ++c) fo[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
+        }
+        const int ntg = FI ? g.wny / 8 : g.nty / 8;  // groups per x pair
+        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
+        const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
+
+        __syncthreads();  // previous item's reads of the region
+        for (int i = lane; i < NQ * PS; i += 64) {
+            const int q = i / PS;
+            const int p = (int)it.p0 + q;
+            const int rem = i - q * PS;
+            const int xl = rem / RY, yl = rem - (rem / RY) * RY;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            tile[i] = (p >= p_lo && p < p_hi)
+                          ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
+                          : make_float2(0.0f, 0.0f);
+        }
+        __syncthreads();
+
+        uint32_t cb = it.b;  // start of cell c's records (clipped to the item)
+        for (int c = 0; c < kGroupCell; ++c) {
+            const uint32_t rb = max(cb, it.b), re = min(fo[c], it.e);
+            cb = fo[c];
+            if (rb >= re) continue;
+            const int xo = c & 1, yo = c >> 1;
+            float a[16];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const int kx = s >> 1, ky = 4 * (s & 1) + kg;
+                a[s] = (aq < NQ && kx < W && ky < W)
+                           ? ftile[((aq * RX + xo + kx) * RY + yo + ky) * 2 + aim]
+                           : 0.0f;
+            }
+            for (uint32_t b0 = rb; b0 < re; b0 += 16) {
+                const uint32_t ri = b0 + (uint32_t)r16;
+                const VisRec rec = recs[min(ri, re - 1)];
+                const float u0 = es_tap<W>(rec.fu, tu0, ihw, bl);
+                const float u1 = es_tap<W>(rec.fu, tu1, ihw, bl);
+                const float v0 = es_tap<W>(rec.fv, tv0, ihw, bl);
+                const float v1 = es_tap<W>(rec.fv, tv1, ihw, bl);
+                const float w0 = WS ? es_tap<W>(rec.fw, tu0, ihw, bl) : (kg == 0 ? 1.0f : 0.0f);
+                const float w1 = WS ? es_tap<W>(rec.fw, tu1, ihw, bl) : 0.0f;
+                float tu[8];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    tu[2 * h] = __shfl(u0, r16 + 16 * h);
+                    tu[2 * h + 1] = __shfl(u1, r16 + 16 * h);
+                }
+                floatx4 d0 = floatx4{0.0f, 0.0f, 0.0f, 0.0f}, d1 = d0;
+#pragma unroll
+                for (int s = 0; s < 16; s += 2) {
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], tu[s >> 1] * v0, d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s + 1], tu[s >> 1] * v1, d1, 0, 0, 0);
+                }
+                // row 4 kg + i of D = (q = 2 kg + (i >> 1), re/im = i & 1)
+                float sr = w0 * (d0[0] + d1[0]) + w1 * (d0[2] + d1[2]);
+                float si = w0 * (d0[1] + d1[1]) + w1 * (d0[3] + d1[3]);
+                sr += __shfl_xor(sr, 16);
+                si += __shfl_xor(si, 16);
+                sr += __shfl_xor(sr, 32);
+                si += __shfl_xor(si, 32);
+                if (kg == 0 && ri < re) {
+                    if (vdirect) {
+                        vdirect[rec.idx] =
+                            make_float2(rec.cre * sr - rec.cim * si, rec.cre * si + rec.cim * sr);
+                    } else {
+                        float2 *dst = acc + ri;
+                        float2 v = *dst;
+                        v.x += sr;
+                        v.y += si;
+                        *dst = v;
+                    }
+                }
+            }
+        }
+    }
+}
+
 // Degridder: one wave per work item (an SX x SY-cell region: a 16x16 tile or
 // a group of kGroupFine 2x2 buckets).  The region's W planes are loaded into
 // LDS; per record, lane (kx, ky) reads its tap's W plane values, and a wave
@@ -2469,7 +2598,9 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     {
         const char *e = std::getenv("SDP_HIP_BUCKET");
         const char *m = std::getenv("SDP_HIP_MFMA");
-        P.cells = grid_mode && !(m && std::atoi(m) == 0);
+        // predict: SDP_HIP_MFMA_DEGRID=0 keeps the register degridder
+        P.cells = !(m && std::atoi(m) == 0) &&
+                  (grid_mode || env_int("SDP_HIP_MFMA_DEGRID", 1) != 0);
         const int64_t cell = (int64_t)g.wnx * g.wny * g.nps;
         const int64_t fine = (int64_t)(g.wnx / kTileFine) * (g.wny / kTileFine) * g.nps;
         if (P.cells) g.sub = cell <= kMaxCellKeys ? kTileCell : kTileCoarse;
@@ -2555,7 +2686,8 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // SDP_HIP_PAD4=0 keeps the unpadded run-walking k_grid_mfma.  The padded
     // record count is read back before the scatter (one host sync), so the
     // host-sync-free pipelined plans stay unpadded.
-    P.pad4 = P.cells && g.sub == kTileCell && !P.aux_bucketing && env_int("SDP_HIP_PAD4", 1) != 0;
+    P.pad4 = grid_mode && P.cells && g.sub == kTileCell && !P.aux_bucketing &&
+             env_int("SDP_HIP_PAD4", 1) != 0;
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
     P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
     return P;
@@ -2918,9 +3050,35 @@ static void launch_degrid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi,
                                                          acc + pt.vbase, P.vdirect);
 }
 
+template <int W, bool WS>
+static void launch_degrid_mfma(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
+                               hipStream_t st) {
+    const size_t lds = (size_t)(WS ? W : 1) * (2 + W - 1) * (8 + W - 1) * sizeof(float2);
+    if (P.subsort) {
+        const auto r = chunk_items(P, pt, p_lo, p_hi);
+        const unsigned n = 16u * (r.second - r.first);
+        if (n == 0) return;
+        k_degrid_mfma<W, WS, true><<<n, 64, lds, st>>>(
+            P.g, P.recs + pt.vbase, ItemSrc{nullptr, n, nullptr}, nullptr,
+            pt.fitems + 16 * (size_t)r.first, P.grid, p_lo, p_hi, acc ? acc + pt.vbase : nullptr,
+            P.vdirect);
+        return;
+    }
+    const void *fn = (const void *)k_degrid_mfma<W, WS, false>;
+    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
+    if (L.blocks == 0) return;
+    k_degrid_mfma<W, WS, false><<<L.blocks, 64, lds, st>>>(
+        P.g, P.recs + pt.vbase, L.src, pt.offs, nullptr, P.grid, p_lo, p_hi,
+        acc ? acc + pt.vbase : nullptr, P.vdirect);
+}
+
 template <int W>
 static void launch_degrid(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
                           hipStream_t st) {
+    if (P.cells && (P.subsort || P.g.sub == kTileCell)) {
+        if (P.g.do_w) return launch_degrid_mfma<W, true>(P, pt, p_lo, p_hi, acc, st);
+        return launch_degrid_mfma<W, false>(P, pt, p_lo, p_hi, acc, st);
+    }
     if (P.subsort) {
         if (P.g.do_w) return launch_degrid_fine_items<W, true>(P, pt, p_lo, p_hi, acc, st);
         return launch_degrid_fine_items<W, false>(P, pt, p_lo, p_hi, acc, st);
@@ -3189,7 +3347,8 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     // once (k_zero_vis above covers the ones with no record)
     const bool trivial_oc = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
     if (P.chunk_planes == g.nplanes && !accumulate && in.vis_dtype != SDP_HIP_C128 && trivial_oc &&
-        in.vcs == 1 && in.vrs == in.nchan && (P.subsort || g.sub == kTileFine) &&
+        in.vcs == 1 && in.vrs == in.nchan &&
+        (P.subsort || g.sub == kTileFine || g.sub == kTileCell) &&
         !std::getenv("SDP_HIP_NO_DIRECT"))
         P.vdirect = static_cast<float2 *>(vis);
     float2 *acc = P.vdirect ? nullptr : scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));

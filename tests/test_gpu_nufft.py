@@ -35,18 +35,21 @@ def _problem(seed, nrow=300, nchan=3, umax=2000.0, frac=0.45):
     return uvw, freq, ms, wgt, frac / umax
 
 
-@pytest.fixture(params=["fine", "fine-reg", "coarse", "coarse-reg", "coarse-lds", "fine-pipelined",
-                        "fine-aux"])
+@pytest.fixture(params=["fine", "fine-reg", "fine-degrid-reg", "coarse", "coarse-reg", "coarse-lds",
+                        "fine-pipelined", "fine-aux"])
 def bucket(request, monkeypatch):
     """Every bucketing: one-cell buckets for the MFMA gridder (invert) and
-    2x2-cell buckets for the register degridder (predict), the default at
-    these sizes; 2x2-cell buckets for the register gridder ("fine-reg",
-    SDP_HIP_MFMA=0); 16x16-cell buckets (very large grids), whose items are
+    the MFMA degridder (predict), the default at these sizes; 2x2-cell
+    buckets for the register gridder and degridder ("fine-reg",
+    SDP_HIP_MFMA=0) or the register degridder only ("fine-degrid-reg",
+    SDP_HIP_MFMA_DEGRID=0); 16x16-cell buckets (very large grids), whose items are
     re-ordered to cells / 2x2 buckets ("coarse", "coarse-reg") or fed to the
     LDS-tile kernels ("coarse-lds", SDP_HIP_SUBSORT=0); and the pipelined plan
     (two row parts bucketed on the auxiliary stream, persistent gridding
     launches)."""
-    if request.param.endswith("-reg"):
+    if request.param == "fine-degrid-reg":
+        monkeypatch.setenv("SDP_HIP_MFMA_DEGRID", "0")
+    elif request.param.endswith("-reg"):
         monkeypatch.setenv("SDP_HIP_MFMA", "0")
     if request.param.startswith("coarse"):
         monkeypatch.setenv("SDP_HIP_BUCKET", "16")
