@@ -59,9 +59,12 @@ def parse():
     ap.add_argument("--no-api", action="store_true",
                     help="skip the invert_ng API (device / host Visibility) timings")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_k_grid.json"))
-    ap.add_argument("--config", choices=("c2", "c4"), default="c2",
-                    help="c2: configs[1], weak scaling (default); c4: configs[3], the SKA-LOW "
-                         "256-channel band on the 8192^2 image, strong scaling")
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2",
+                    help="c2: configs[1], weak scaling (default); c3: configs[2], the sky-"
+                         "component DFT; c4: configs[3], the SKA-LOW 256-channel band on the "
+                         "8192^2 image, strong scaling; c5: configs[4], the StefCal batch")
+    ap.add_argument("--c5-times", type=int, default=1000,
+                    help="c5: time samples of the 512-station x 256-channel solve (1000 = C5)")
     ap.add_argument("--c4-batch", type=int, default=40,
                     help="c4: max channels per streamed batch of a rank's block (a block is "
                          "split into that many near-equal batches; 40 keeps one batch per "
@@ -338,6 +341,227 @@ def run_c4(args, world, rank, local, dev, emulated=False):
         print(json.dumps(line), flush=True)
 
 
+# ---------------------------------------------------------------------------
+# C3: dft_skycomponent_visibility, 1000 point components x 10 Mvis
+# ---------------------------------------------------------------------------
+C3_NCOMP, C3_NTIMES = 1000, 518   # 19,306 SKA-MID baselines x 518 times = 10.0 Mvis
+
+
+def run_c3(args, world, rank, dev):
+    """configs[2]: the point-component DFT (reference imaging/dft.py:135-183,
+    dft_cpu_looped) of 1000 components onto 10.0 Mvis (one channel, stokesI,
+    c64 output).  Rows are split across ranks (strong scaling, no
+    collective: parallel.dft_sharded's partitioning).  `roofline` is the
+    VALU count N_vis N_comp (6 + 8 npol) flops against the
+    fp32 vector peak -- sincos excluded, so the fraction understates the
+    issue rate; `cpu_baseline` is ref_oracle.dft_cpu_looped (the reference's
+    loop restated in numpy) on 100 components x 200k visibilities."""
+    from ska_sdp_func_python_amd import kernels, simulation
+    rng = np.random.default_rng(3)
+    fn_, n_def, lat, dec = simulation.CONFIGS["MID"]
+    ha = np.linspace(-0.5, 0.5, C3_NTIMES) * 8.0 * math.pi / 12.0
+    uvw_h, _ = simulation.observe(fn_(n_def, seed=1), math.radians(lat), math.radians(dec), ha)
+    uvw_h = uvw_h.reshape(-1, 3)
+    nvis_total = uvw_h.shape[0]
+    lo, hi = nvis_total * rank // world, nvis_total * (rank + 1) // world
+    uvw = torch.as_tensor(uvw_h[lo:hi], device=dev)
+    freq_h = np.array([1.4e9])
+    freq = torch.as_tensor(freq_h, device=dev)
+    lm = rng.uniform(-0.05, 0.05, (C3_NCOMP, 2))
+    dc_h = np.concatenate([lm, (np.sqrt(1 - (lm ** 2).sum(1)) - 1)[:, None]], 1)
+    fl_h = rng.uniform(0.1, 10, (C3_NCOMP, 1, 1)).astype(complex)
+    dc, fl = torch.as_tensor(dc_h, device=dev), torch.as_tensor(fl_h, device=dev)
+    out = torch.empty((hi - lo, 1, 1), dtype=torch.complex64, device=dev)
+
+    def step():
+        kernels.dft_point(dc, fl, uvw, freq=freq, out=out)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[dev.index])
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    k_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = elapsed / args.steps * 1e3
+    if rank != 0:
+        return
+    flops = (hi - lo) * C3_NCOMP * (6 + 8 * 1)
+    cpu = None
+    if world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import ref_oracle as ro
+        ns, nc = 200_000, 100
+        uvwl = uvw_h[:ns, None, :] * (freq_h / 299792458.0)[None, :, None]
+        tc0 = time.perf_counter()
+        ro.dft_cpu_looped(dc_h[:nc], uvwl, fl_h[:nc])
+        tc = time.perf_counter() - tc0
+        cpu_rate = ns * nc / tc
+        cpu = {"value": round(cpu_rate / 1e9, 5), "unit": "G comp*vis/s", "cores": 1,
+               "kind": "port",
+               "sample": f"oracle/ref_oracle.dft_cpu_looped (the reference's loop, numpy), {nc} "
+                         f"comps x {ns} vis in {tc:.1f} s; the full C3 extrapolates to "
+                         f"{nvis_total * C3_NCOMP / cpu_rate:.0f} s"}
+    line = {
+        "metric": "G comp*vis/s (dft_skycomponent_visibility, 1000 components x 10 Mvis)",
+        "value": round(nvis_total * C3_NCOMP / (elapsed / args.steps) / 1e9, 2),
+        "unit": "G comp*vis/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32 (fp64 phase)",
+        "data": "synthetic (seeded SKA-MID-like layout, 1000 components |l|,|m| < 0.05, "
+                "fluxes U(0.1, 10))",
+        "config": {"workload": "C3: 1000 point components x 10.0 Mvis (19,306 baselines x 518 "
+                               "times x 1 channel, stokesI), c64 output",
+                   "nvis": nvis_total, "ncomp": C3_NCOMP,
+                   "parallelism": f"rows x{world}, no collective"},
+        "roofline": {"bound": "valu", "achieved": round(flops / (k_ms * 1e-3) / 1e12, 2),
+                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(flops / (k_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+                     "traffic": None, "kernel": "k_dft", "kernel_ms": round(k_ms, 4),
+                     "note": "N_vis N_comp (6 + 8 npol) flops (SURVEY.md 8(d)), sincos excluded; "
+                             "MFMA does not apply (the contraction's N is npol = 1, DESIGN.md 3)"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
+# ---------------------------------------------------------------------------
+# C5: solve_gaintable StefCal, 512 stations x 256 channels x 1000 times
+# ---------------------------------------------------------------------------
+C5_NANTS, C5_NCHAN, C5_BATCH = 512, 256, 16
+
+
+def run_c5(args, world, rank, dev):
+    """configs[4]: 256,000 per-(time, channel) StefCal solves (B jones, the
+    reference's solvers.py:217-300 scalar itsubs path, niter 200, tol 1e-6)
+    of 512 stations.  The inputs of the whole job (33.5 G baseline samples,
+    0.8 TB as c128 + f64) exceed HBM, so the rank's times are solved in
+    batches of 16 gain rows (4096 sub-solves); each batch's x_b and weights
+    are generated on device between timed segments and the step time is the
+    sum of the solve segments (max over ranks).  Times are split across ranks
+    (strong scaling, no collective).  `roofline`: 12 B per baseline per
+    sub-solve iteration over the timed solves against HBM
+    peak; `cpu_baseline`: ref_oracle.stefcal_row (numpy restatement) on 2
+    single-channel sub-solves."""
+    from ska_sdp_func_python_amd import kernels
+    ntime = args.c5_times
+    t_lo, t_hi = ntime * rank // world, ntime * (rank + 1) // world
+    a1, a2 = np.triu_indices(C5_NANTS, 1)
+    nbl = len(a1)
+    perm, _, rs, ant2 = kernels.canonical_baselines(a1, a2, C5_NANTS)
+    a1t = torch.as_tensor(a1[perm], device=dev)
+    a2t = torch.as_tensor(a2[perm], device=dev)
+    gen = torch.Generator(device=dev)
+    stats = {"iters": [], "err": 0.0, "res": 0.0, "sub_iters": 0}
+
+    def batch_inputs(t0, nt):
+        gen.manual_seed(1805550721 + t0)
+        amp = torch.exp(0.1 * torch.randn((nt, C5_NANTS, C5_NCHAN), generator=gen, device=dev,
+                                          dtype=torch.float64))
+        ph = 0.1 * torch.randn((nt, C5_NANTS, C5_NCHAN), generator=gen, device=dev,
+                               dtype=torch.float64)
+        g = torch.polar(amp, ph)
+        xb = (g[:, a1t, :] * torch.conj(g[:, a2t, :]))[..., None].contiguous()
+        wb = torch.ones(xb.shape, dtype=torch.float64, device=dev)
+        gain = torch.ones((nt, C5_NANTS, C5_NCHAN, 1, 1), dtype=torch.complex128, device=dev)
+        gwt = torch.zeros((nt, C5_NANTS, C5_NCHAN, 1, 1), dtype=torch.float64, device=dev)
+        return g, xb, wb, gain, gwt
+
+    def one_pass(record):
+        solve_s = 0.0
+        for t0 in range(t_lo, t_hi, C5_BATCH):
+            nt = min(C5_BATCH, t_hi - t0)
+            g, xb, wb, gain, gwt = batch_inputs(t0, nt)
+            torch.cuda.synchronize(dev)
+            ta = time.perf_counter()
+            res, used = kernels.solve_gains(xb, wb, gain, gwt, rs, ant2, mode=0, niter=200,
+                                            tol=1e-6, phase_only=False)
+            torch.cuda.synchronize(dev)
+            solve_s += time.perf_counter() - ta
+            if record:
+                u = int(used.max())
+                stats["iters"].append(u)
+                stats["sub_iters"] += int(used.sum()) * C5_NCHAN  # used: per gain row
+                est = gain[..., 0, 0]
+                est = est * torch.conj(est[:, :1]) / torch.abs(est[:, :1])
+                tru = g * torch.conj(g[:, :1]) / torch.abs(g[:, :1])
+                stats["err"] = max(stats["err"], float(torch.max(torch.abs(est - tru))))
+                stats["res"] = max(stats["res"], float(res.max()))
+            del g, xb, wb, gain, gwt
+        return solve_s
+
+    for _ in range(args.warmup):
+        one_pass(False)
+    if world > 1:
+        dist.barrier(device_ids=[dev.index])
+    torch.cuda.synchronize(dev)
+    elapsed = sum(one_pass(s == 0) for s in range(args.steps))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        return
+    nsub = ntime * C5_NCHAN
+    nsub_rank = (t_hi - t_lo) * C5_NCHAN
+    gbs = 12 * nbl * stats["sub_iters"] / (elapsed / args.steps) / 1e9
+    cpu = None
+    if world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import ref_oracle as ro
+        rng = np.random.default_rng(1805550721)
+        gh = (rng.lognormal(0, 0.1, (2, C5_NANTS)) * np.exp(1j * rng.normal(0, 0.1, (2, C5_NANTS))))
+        bl = np.stack([a1, a2], 1)
+        tc0 = time.perf_counter()
+        for s in range(2):
+            xbh = (gh[s, a1] * np.conj(gh[s, a2]))[:, None, None]
+            ro.stefcal_row(xbh, np.ones(xbh.shape), bl, C5_NANTS,
+                           np.ones((C5_NANTS, 1, 1, 1), complex), np.zeros((C5_NANTS, 1, 1, 1)),
+                           200, 1e-6, False)
+        tc = (time.perf_counter() - tc0) / 2
+        cpu = {"value": round(1.0 / tc, 3), "unit": "solves/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/ref_oracle.stefcal_row (numpy restatement of solvers.py:217-300), "
+                         f"2 sub-solves of 512 stations, {tc:.2f} s each; C5 extrapolates to "
+                         f"{nsub * tc / 3600:.1f} h"}
+    line = {
+        "metric": "StefCal solves/s (solve_gaintable, 512 stations x 256 chan x 1000 times)",
+        "value": round(nsub / (elapsed / args.steps), 1), "unit": "solves/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64 (c128 gains)",
+        "data": "synthetic: true gains lognormal(0, 0.1) x exp(i N(0, 0.1)) per (time, station, "
+                "chan), x_b = g_a1 conj(g_a2), unit weights, generated on device per batch "
+                "outside the timed segments",
+        "config": {"workload": f"C5: 512 stations x 256 chan x {ntime} times = {nsub} solves "
+                               "(B jones, scalar, niter 200, tol 1e-6)",
+                   "solves": nsub, "solves_rank0": nsub_rank, "batch_rows": C5_BATCH,
+                   "parallelism": f"times x{world}, no collective"},
+        "solve_stats_rank0": {"iterations_max": max(stats["iters"]) if stats["iters"] else 0,
+                              "max_gain_err": stats["err"], "max_residual": stats["res"]},
+        "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "whole solve (k_fill + k_iter + k_residual)",
+                     "note": "12 B per baseline per sub-solve iteration (SURVEY.md 8(d)) over the "
+                             "timed solves, per-sub-solve iteration counts summed"},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -349,6 +573,11 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    if args.config in ("c3", "c5"):
+        (run_c3 if args.config == "c3" else run_c5)(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if args.config == "c4":
         if args.emulate and world == 1:
             er, ew = (int(x) for x in args.emulate.split("/"))

@@ -204,7 +204,7 @@ if "predict" in which:
     emit({"path": "predict_ng / dirty2ms (C2)", "nvis": nvis, "gpu_ms": round(t * 1e3, 3),
           "value": round(nvis / t / 1e6, 1), "unit": "Mvis/s",
           "stages_ms": {k: round(info[k], 3) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
-          "roofline": {"bound": "hbm", "kernel": "k_degrid_reg<8,true>", "achieved": round(gbs, 1),
+          "roofline": {"bound": "hbm", "kernel": "k_degrid_mfma<8,true> (one-cell buckets)" if os.environ.get("SDP_HIP_MFMA_DEGRID", "1") != "0" else "k_degrid_reg<8,true>", "achieved": round(gbs, 1),
                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)},
           "cpu_baseline": predict_cpu(obs, img, cell, nvis)})
     del obs, img, out
