@@ -1351,6 +1351,26 @@ constexpr size_t grid_mfma_pad_lds() {
            (size_t)kTapBatch * kTapRec * sizeof(float);
 }
 
+// One-wave workgroups: the LDS operations of one wavefront execute in
+// program order, so a hand-off between the wave's own lanes through LDS needs
+// only a compiler barrier (wavefront-scope fence), not s_barrier plus the
+// s_waitcnt lgkmcnt(0) that __syncthreads() brings with it -- the wave keeps
+// issuing while its writes drain.  SDP_PAD_WAVESYNC=0 restores __syncthreads.
+#ifndef SDP_PAD_WAVESYNC
+#define SDP_PAD_WAVESYNC 1
+#endif
+#ifndef SDP_PAD_UNROLL
+#define SDP_PAD_UNROLL 1
+#endif
+__device__ __forceinline__ void wave_lds_sync() {
+#if SDP_PAD_WAVESYNC
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#else
+    __syncthreads();
+#endif
+}
+
 template <int W, bool WS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma_pad(
     Geo g, const RecC *__restrict__ recs, ItemSrc src, const unsigned *__restrict__ offs,
@@ -1396,7 +1416,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         for (int c = 0; c < kGroupCell - 1; ++c)
             bnd[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
 
-        __syncthreads();
+        wave_lds_sync();
         for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
 
         floatx4 acc[4];
@@ -1462,27 +1482,61 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             for (int h = 0; h < 64 / kTapBatch; ++h) {
                 const int nbh = min(kTapBatch, nb - kTapBatch * h);
                 if (nbh <= 0) break;
-                __syncthreads();  // previous half's tap block reads
+                wave_lds_sync();  // previous half's tap block reads
                 if (lane / kTapBatch == h) {
                     const int r = lane % kTapBatch;
                     stage[r] = make_float4(fu, fv, fw, 0.0f);
                     *reinterpret_cast<float2 *>(blk + r * kTapRec + 24) =
                         make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
                 }
-                __syncthreads();
+                wave_lds_sync();
+                {
+                    // both staged offsets read before any tap is written: six
+                    // independent ES chains
+                    float4 f[kTapBatch / 8];
 #pragma unroll
-                for (int m = 0; m < kTapBatch / 8; ++m) {
-                    const float4 f = stage[8 * m + (lane >> 3)];
-                    float *d = tap_dst + 8 * m * kTapRec;
-                    d[wu] = es_tap<W>(f.x, tihw, ihw, bl);
-                    d[wv] = es_tap<W>(f.y, tihw, ihw, bl);
-                    d[ww] = WS ? es_tap<W>(f.z, tihw, ihw, bl) : (tt == 0 ? 1.0f : 0.0f);
+                    for (int m = 0; m < kTapBatch / 8; ++m) f[m] = stage[8 * m + (lane >> 3)];
+                    float tv_[kTapBatch / 8][3];
+#pragma unroll
+                    for (int m = 0; m < kTapBatch / 8; ++m) {
+                        tv_[m][0] = es_tap<W>(f[m].x, tihw, ihw, bl);
+                        tv_[m][1] = es_tap<W>(f[m].y, tihw, ihw, bl);
+                        tv_[m][2] = WS ? es_tap<W>(f[m].z, tihw, ihw, bl) : (tt == 0 ? 1.0f : 0.0f);
+                    }
+#pragma unroll
+                    for (int m = 0; m < kTapBatch / 8; ++m) {
+                        float *d = tap_dst + 8 * m * kTapRec;
+                        d[wu] = tv_[m][0];
+                        d[wv] = tv_[m][1];
+                        d[ww] = tv_[m][2];
+                    }
                 }
-                __syncthreads();
-                // segments of K-steps of one cell; inside a segment the operands
-                // of K-step j + 1 are read before the MFMAs of K-step j issue
+                wave_lds_sync();
                 const uint64_t hchg = chg >> (kTapBatch * h);
                 const int nk = nbh >> 2;
+#if SDP_PAD_UNROLL
+                // the block's (up to) 4 K-steps unrolled: every operand read
+                // up front at compile-time offsets, a cell change (bit 4j)
+                // flushes the accumulators between two K-steps
+                {
+                    Ops o[kTapBatch / 4];
+#pragma unroll
+                    for (int jj = 0; jj < kTapBatch / 4; ++jj) o[jj] = kload(jj);
+#pragma unroll
+                    for (int jj = 0; jj < kTapBatch / 4; ++jj) {
+                        if (jj < nk) {
+                            if ((hchg >> (4 * jj)) & 1ull) {
+                                if (cur >= 0) flush_cell();
+                                cur = __builtin_amdgcn_readlane(cj, kTapBatch * h + 4 * jj);
+                            }
+                            kmfma(o[jj]);
+                        }
+                    }
+                }
+                continue;
+#endif
+                // segments of K-steps of one cell; inside a segment the operands
+                // of K-step j + 1 are read before the MFMAs of K-step j issue
                 int j = 0;
                 while (j < nk) {
                     if ((hchg >> (4 * j)) & 1ull) {
@@ -1502,7 +1556,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             }
         }
         if (cur >= 0) flush_cell();
-        __syncthreads();
+        wave_lds_sync();
 
         // flush: float f = i0 + lane of each plane's RX x RY complex cells,
         // buffer atomics off a per-plane descriptor (32-bit offsets), the
@@ -1768,6 +1822,11 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
         }
         __syncthreads();
 
+        // the item's cells are consecutive, so the batch after [b0, b0 + 16)
+        // starts at min(b0 + 16, re) -- in the next cell when this one ends;
+        // its records are loaded one batch ahead (pf = the prefetched start)
+        uint32_t pf = it.b;
+        VisRec nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
         uint32_t cb = it.b;  // start of cell c's records (clipped to the item)
         for (int c = 0; c < kGroupCell; ++c) {
             const uint32_t rb = max(cb, it.b), re = min(fo[c], it.e);
@@ -1784,7 +1843,10 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
             }
             for (uint32_t b0 = rb; b0 < re; b0 += 16) {
                 const uint32_t ri = b0 + (uint32_t)r16;
-                const VisRec rec = recs[min(ri, re - 1)];
+                if (pf != b0) nxt = recs[min(ri, it.e - 1)];  // (wave-uniform; not expected)
+                const VisRec rec = nxt;
+                pf = min(b0 + 16, re);
+                nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
                 const float u0 = es_tap<W>(rec.fu, tu0, ihw, bl);
                 const float u1 = es_tap<W>(rec.fu, tu1, ihw, bl);
                 const float v0 = es_tap<W>(rec.fv, tv0, ihw, bl);
