@@ -1125,6 +1125,42 @@ __device__ __forceinline__ float bperm(int byte_addr, float v) {
                               __builtin_amdgcn_ds_bpermute(byte_addr, __builtin_bit_cast(int, v)));
 }
 
+// One-wave workgroups: the LDS operations of one wavefront execute in
+// program order, so a hand-off between the wave's own lanes through LDS needs
+// only a compiler barrier (wavefront-scope fence), not s_barrier plus the
+// s_waitcnt lgkmcnt(0) that __syncthreads() brings with it -- the wave keeps
+// issuing while its writes drain.  SDP_PAD_WAVESYNC=0 restores __syncthreads
+// in k_grid_mfma_pad (the gridders and degridders below all run one wave per
+// workgroup).
+#ifndef SDP_PAD_WAVESYNC
+#define SDP_PAD_WAVESYNC 1
+#endif
+#ifndef SDP_PAD_UNROLL
+#define SDP_PAD_UNROLL 1
+#endif
+__device__ __forceinline__ void wave_lds_sync() {
+#if SDP_PAD_WAVESYNC
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#else
+    __syncthreads();
+#endif
+}
+
+// the same hand-off in k_grid_mfma / k_degrid_mfma (SDP_MFMA_WAVESYNC=0:
+// __syncthreads)
+#ifndef SDP_MFMA_WAVESYNC
+#define SDP_MFMA_WAVESYNC 1
+#endif
+__device__ __forceinline__ void wave_sync_1w() {
+#if SDP_MFMA_WAVESYNC
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#else
+    __syncthreads();
+#endif
+}
+
 // ES kernel for the MFMA gridder's taps: x = fu*ihw + t*ihw by one fma; for
 // W = 8 every tap of the footprint lies inside the support (|x| <= 1), so
 // no range select (the max() only guards rounding below zero)
@@ -1177,7 +1213,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
-        __syncthreads();
+        wave_sync_1w();
         for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
 
         floatx4 acc[4];
@@ -1250,10 +1286,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             const bool live = lane < nb;
             const int cj = live ? ((int)(my.ij >> 16) - jbase) * 2 + ((int)(my.ij & 0xffffu) - ibase)
                                 : 16;
-            __syncthreads();  // previous batch's stage reads
+            wave_sync_1w();  // previous batch's stage reads
             stage[2 * lane] = make_float4(my.fu, my.fv, my.fw, 0.0f);
             stage[2 * lane + 1] = make_float4(live ? my.cre : 0.0f, live ? my.cim : 0.0f, 0.0f, 0.0f);
-            __syncthreads();
+            wave_sync_1w();
             // run starts: lane 0, and every lane whose cell differs from the previous lane's
             const int prev = __shfl_up(cj, 1);
             uint64_t starts = __ballot(live && (lane == 0 || prev != cj));
@@ -1285,7 +1321,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             }
         }
         if (cur >= 0) flush_cell();
-        __syncthreads();
+        wave_sync_1w();
 
         // flush: float f = i0 + lane of each plane's RX x RY complex cells,
         // buffer atomics off a per-plane descriptor (32-bit offsets), the
@@ -1349,26 +1385,6 @@ template <int W, bool WS>
 constexpr size_t grid_mfma_pad_lds() {
     return (size_t)mfma_tile_f2<W, WS>() * sizeof(float2) + kTapBatch * sizeof(float4) +
            (size_t)kTapBatch * kTapRec * sizeof(float);
-}
-
-// One-wave workgroups: the LDS operations of one wavefront execute in
-// program order, so a hand-off between the wave's own lanes through LDS needs
-// only a compiler barrier (wavefront-scope fence), not s_barrier plus the
-// s_waitcnt lgkmcnt(0) that __syncthreads() brings with it -- the wave keeps
-// issuing while its writes drain.  SDP_PAD_WAVESYNC=0 restores __syncthreads.
-#ifndef SDP_PAD_WAVESYNC
-#define SDP_PAD_WAVESYNC 1
-#endif
-#ifndef SDP_PAD_UNROLL
-#define SDP_PAD_UNROLL 1
-#endif
-__device__ __forceinline__ void wave_lds_sync() {
-#if SDP_PAD_WAVESYNC
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-#else
-    __syncthreads();
-#endif
 }
 
 template <int W, bool WS>
@@ -1806,7 +1822,7 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
-        __syncthreads();  // previous item's reads of the region
+        wave_sync_1w();  // previous item's reads of the region
         for (int i = lane; i < NQ * PS; i += 64) {
             const int q = i / PS;
             const int p = (int)it.p0 + q;
@@ -1820,7 +1836,7 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                           ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
                           : make_float2(0.0f, 0.0f);
         }
-        __syncthreads();
+        wave_sync_1w();
 
         // the item's cells are consecutive, so the batch after [b0, b0 + 16)
         // starts at min(b0 + 16, re) -- in the next cell when this one ends;
@@ -3317,6 +3333,22 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
                     "batched invert: the w planes do not all fit in device memory");
     }
     const double *tab = phi_table(g.W, g.beta, st);
+    // the band zeroing of the first plane chunk (HBM writes) overlaps the
+    // bucketing (bound by memory-side atomics): it runs on the auxiliary
+    // stream after the call's earlier work on `st`; the gridding waits for it
+    hipEvent_t zdone = nullptr;
+    // (single calls only: on C4's streamed batches it measured 1-2 % slower)
+    if (first && !batched && !P.aux_bucketing && env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0) {
+        hipStream_t aux = aux_stream();
+        hipEvent_t ready;
+        SDP_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        SDP_HIP_CHECK(hipEventRecord(ready, st));
+        SDP_HIP_CHECK(hipStreamWaitEvent(aux, ready, 0));
+        SDP_HIP_CHECK(hipEventDestroy(ready));
+        zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
+        SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
+        SDP_HIP_CHECK(hipEventRecord(zdone, aux));
+    }
     std::vector<hipEvent_t> ev;
     if (reuse) {
         // value pass only (weight sums included), then the kept sub-sort
@@ -3334,7 +3366,13 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
-        if (first) zero_band(P, np, st);
+        if (zdone) {
+            SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
+            SDP_HIP_CHECK(hipEventDestroy(zdone));
+            zdone = nullptr;
+        } else if (first) {
+            zero_band(P, np, st);
+        }
         for (size_t i = 0; i < P.parts.size(); ++i) {
             if (!ev.empty()) SDP_HIP_CHECK(hipStreamWaitEvent(st, ev[i], 0));
             StageTimer tg(st);
