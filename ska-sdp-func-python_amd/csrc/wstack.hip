@@ -1381,14 +1381,24 @@ constexpr int mfma_tile_f2() {  // region tile, rounded to 16 B
     return (((WS ? W : 1) * (2 + W - 1) * (8 + W - 1)) + 1) & ~1;
 }
 
+// SDP_PAD_PIPE=1 (experiment, off): two tap blocks; the ES chains of block
+// h + 1 issue between the MFMAs of block h (software pipeline inside each
+// 64-record batch).  Measured 5.08-5.18 -> 5.58-5.70 ms on C2: the second
+// tap block (12.5 KiB per wave, 13 waves per CU) and the 4-wave register cap
+// (accumulators moved to VGPRs) cost more than the overlap gains.
+#ifndef SDP_PAD_PIPE
+#define SDP_PAD_PIPE 0
+#endif
+constexpr int kTapBlocks = SDP_PAD_PIPE ? 2 : 1;
+
 template <int W, bool WS>
 constexpr size_t grid_mfma_pad_lds() {
     return (size_t)mfma_tile_f2<W, WS>() * sizeof(float2) + kTapBatch * sizeof(float4) +
-           (size_t)kTapBatch * kTapRec * sizeof(float);
+           (size_t)kTapBlocks * kTapBatch * kTapRec * sizeof(float);
 }
 
 template <int W, bool WS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma_pad(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE ? 4 : 1, 4))) void k_grid_mfma_pad(
     Geo g, const RecC *__restrict__ recs, ItemSrc src, const unsigned *__restrict__ offs,
     float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
@@ -1494,6 +1504,102 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             const int prev = __shfl_up(cj, 4);
             uint64_t chg = __ballot((lane & 3) == 0 && lane >= 4 && prev != cj);
             if (__builtin_amdgcn_readfirstlane(cj) != cur) chg |= 1ull;
+#if SDP_PAD_PIPE
+            {
+                // blocks of kTapBatch records; block hb's taps live in tap block
+                // hb & 1.  Block 0's taps are evaluated up front; while block hb's
+                // K-steps issue, the offsets of block hb + 1 come from their lanes
+                // (ds_bpermute) and its six ES chains run between the MFMAs.
+                constexpr int BS = kTapBatch * kTapRec;  // floats per tap block
+                const int nblk = (nb + kTapBatch - 1) / kTapBatch;
+                auto put_values = [&](int hb, float *bb) {
+                    if (lane / kTapBatch == hb) {
+                        const int r = lane % kTapBatch;
+                        *reinterpret_cast<float2 *>(bb + r * kTapRec + 24) =
+                            make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
+                    }
+                };
+                float fx[2][3];
+                auto fetch = [&](int hb) {
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) {
+                        const int src = kTapBatch * hb + 8 * m + (lane >> 3);
+                        fx[m][0] = __shfl(fu, src);
+                        fx[m][1] = __shfl(fv, src);
+                        fx[m][2] = __shfl(fw, src);
+                    }
+                };
+                auto es = [&](int m, int k) {
+                    return (WS || k < 2) ? es_tap<W>(fx[m][k], tihw, ihw, bl)
+                                         : (tt == 0 ? 1.0f : 0.0f);
+                };
+                float tv_[2][3];
+                auto put_taps = [&](float *bb) {
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) {
+                        float *d = bb + ((lane >> 3) + 8 * m) * kTapRec;
+                        d[wu] = tv_[m][0];
+                        d[wv] = tv_[m][1];
+                        d[ww] = tv_[m][2];
+                    }
+                };
+                put_values(0, blk);
+                fetch(0);
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) tv_[m][k] = es(m, k);
+                put_taps(blk);
+                wave_lds_sync();
+                for (int hb = 0; hb < nblk; ++hb) {
+                    const int boff = (hb & 1) * BS;
+                    float *const nbuf = blk + (BS - boff);
+                    const int nk = min(kTapBatch, nb - kTapBatch * hb) >> 2;
+                    const uint64_t hchg = chg >> (kTapBatch * hb);
+                    Ops o[kTapBatch / 4];
+#pragma unroll
+                    for (int jj = 0; jj < kTapBatch / 4; ++jj) {
+                        o[jj].a = *reinterpret_cast<const floatx4 *>(kA + boff + 4 * jj * kTapRec);
+                        o[jj].v = kV[boff + 4 * jj * kTapRec];
+                        o[jj].w = kW[boff + 4 * jj * kTapRec];
+                        o[jj].c = kC[boff + 4 * jj * kTapRec];
+                    }
+                    const bool more = hb + 1 < nblk;  // wave-uniform
+                    if (more) {
+                        put_values(hb + 1, nbuf);
+                        fetch(hb + 1);
+                    }
+                    auto kstep = [&](int jj) {
+                        if (jj < nk) {
+                            if ((hchg >> (4 * jj)) & 1ull) {
+                                if (cur >= 0) flush_cell();
+                                cur = __builtin_amdgcn_readlane(cj, kTapBatch * hb + 4 * jj);
+                            }
+                            kmfma(o[jj]);
+                        }
+                    };
+                    kstep(0);
+                    if (more) {
+                        tv_[0][0] = es(0, 0);
+                        tv_[0][1] = es(0, 1);
+                    }
+                    kstep(1);
+                    if (more) {
+                        tv_[0][2] = es(0, 2);
+                        tv_[1][0] = es(1, 0);
+                    }
+                    kstep(2);
+                    if (more) tv_[1][1] = es(1, 1);
+                    kstep(3);
+                    if (more) {
+                        tv_[1][2] = es(1, 2);
+                        put_taps(nbuf);
+                    }
+                    wave_lds_sync();
+                }
+            }
+            continue;
+#endif
             // two halves of kTapBatch records: taps, then their K-steps
             for (int h = 0; h < 64 / kTapBatch; ++h) {
                 const int nbh = min(kTapBatch, nb - kTapBatch * h);
