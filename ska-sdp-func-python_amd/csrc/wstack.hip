@@ -1374,7 +1374,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 //    per K-step 4 LDS reads, 5 multiplies, 4 MFMAs and a cell-change bit
 //    test -- no run bookkeeping, no masking.
 constexpr int kTapRec = 28;    // floats per record row of the tap block (16-B multiple)
-constexpr int kTapBatch = 16;  // records per tap block (half a 64-record load: LDS, occupancy)
+#ifndef SDP_TAP_BATCH
+#define SDP_TAP_BATCH 16
+#endif
+constexpr int kTapBatch = SDP_TAP_BATCH;  // records per tap block (LDS, occupancy)
 
 template <int W, bool WS>
 constexpr int mfma_tile_f2() {  // region tile, rounded to 16 B
