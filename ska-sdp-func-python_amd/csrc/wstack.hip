@@ -1392,6 +1392,14 @@ constexpr int mfma_tile_f2() {  // region tile, rounded to 16 B
 #ifndef SDP_PAD_PIPE
 #define SDP_PAD_PIPE 0
 #endif
+// SDP_PAD_NEXT=1 (experiment, off): grid-stride over the items with the next
+// item's descriptor, bucket ends and first records fetched ahead.  Measured
+// 5.04-5.17 -> 5.49-5.72 ms on C2: one workgroup per item, balanced by the
+// dispatcher, hides the item-start latency better than fewer, longer-lived
+// workgroups.
+#ifndef SDP_PAD_NEXT
+#define SDP_PAD_NEXT 0
+#endif
 constexpr int kTapBlocks = SDP_PAD_PIPE ? 2 : 1;
 
 template <int W, bool WS>
@@ -1433,17 +1441,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
     const int ckx = lane >> 5, cky = 4 * ((lane >> 4) & 1);
     float *const ftile = reinterpret_cast<float *>(tile);
 
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        const Item it = load_item(src, w_it, n_items, stride);
+    // the group's 16 cell buckets end at offs[...][1..16] (record indices)
+    auto load_bnd = [&](const Item &x, uint32_t (&bb)[kGroupCell - 1]) {
+        const unsigned *ob = offs + ((size_t)x.p0 * g.ntiles + (size_t)x.tile * kGroupCell);
+#pragma unroll
+        for (int c = 0; c < kGroupCell - 1; ++c) bb[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
+    };
+    // SDP_PAD_NEXT: a workgroup walks several items (grid stride) and fetches
+    // the next item's descriptor (during this item's setup), its bucket ends
+    // (after this item's first batch) and its first 64 records (with this
+    // item's last batch) ahead of use: item starts no longer wait on three
+    // dependent memory round trips
+    uint32_t w_it = blockIdx.x;
+    Item it{0u, 0u, 0u, 0u};
+    uint32_t bnd[kGroupCell - 1];
+    RecC nx{};
+    if (w_it < n_items) {
+        it = load_item(src, w_it, n_items, stride);
+        load_bnd(it, bnd);
+        nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
+    }
+    for (; w_it < n_items; w_it += gridDim.x) {
+        const uint32_t nw = w_it + gridDim.x;
+        const bool more = SDP_PAD_NEXT && nw < n_items;  // wave-uniform
+        Item raw_next{0u, 0u, 0u, 0u};
+        if (more) raw_next = src.items[(uint32_t)(((uint64_t)nw * stride) % n_items)];
+        Item nit = it;
+        uint32_t nbnd[kGroupCell - 1];
+        bool nit_ready = false;
         const int ntg = g.nty / 8;  // groups per x pair
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
-        // the group's 16 cell buckets end at ob[1..16] (record indices)
-        const unsigned *ob = offs + ((size_t)it.p0 * g.ntiles + (size_t)it.tile * kGroupCell);
-        uint32_t bnd[kGroupCell - 1];
-#pragma unroll
-        for (int c = 0; c < kGroupCell - 1; ++c)
-            bnd[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
 
         wave_lds_sync();
         for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
@@ -1490,10 +1518,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a[t] * o.v, b, acc[t], 0, 0, 0);
         };
 
-        RecC nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
+#if !SDP_PAD_NEXT
+        nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
+#endif
+        // after a batch's K-steps: the next item's descriptor (loaded during
+        // this item's setup) is read, its bucket ends requested, and -- when
+        // this was the item's last batch -- its first records too
+        auto after_batch = [&](bool last) {
+            if (more && !nit_ready) {
+                nit.b = __builtin_amdgcn_readfirstlane(raw_next.b);
+                nit.e = __builtin_amdgcn_readfirstlane(raw_next.e);
+                nit.tile = __builtin_amdgcn_readfirstlane(raw_next.tile);
+                nit.p0 = __builtin_amdgcn_readfirstlane(raw_next.p0);
+                load_bnd(nit, nbnd);
+                nit_ready = true;
+                if (last) nx = recs[min(nit.b + (uint32_t)lane, nit.e - 1)];
+            }
+        };
         for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
             const RecC my = nx;
-            if (b0 + 64 < it.e) nx = recs[min(b0 + 64 + (uint32_t)lane, it.e - 1)];
+            const bool last = b0 + 64 >= it.e;  // wave-uniform
+            if (!last) nx = recs[min(b0 + 64 + (uint32_t)lane, it.e - 1)];
+            else if (nit_ready) nx = recs[min(nit.b + (uint32_t)lane, nit.e - 1)];
             const int nb = (int)min(64u, it.e - b0);  // a multiple of 4
             // cell (x-pair-major index in the group) of the lane's record
             const uint32_t ri = b0 + (uint32_t)lane;
@@ -1601,6 +1647,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                     wave_lds_sync();
                 }
             }
+            after_batch(last);
             continue;
 #endif
             // two halves of kTapBatch records: taps, then their K-steps
@@ -1679,7 +1726,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                     kmfma(o);
                 }
             }
+            after_batch(last);
         }
+        after_batch(true);  // (an item without records)
         if (cur >= 0) flush_cell();
         wave_lds_sync();
 
@@ -1716,6 +1765,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                 ++xl;
             }
         }
+        if (more) {
+            it = nit;
+#pragma unroll
+            for (int c = 0; c < kGroupCell - 1; ++c) bnd[c] = nbnd[c];
+        }
+#if !SDP_PAD_NEXT
+        else if (nw < n_items) {
+            it = load_item(src, nw, n_items, stride);
+            load_bnd(it, bnd);
+        }
+#endif
     }
 }
 
@@ -3178,8 +3238,13 @@ static void launch_grid_mfma_pad(const Plan &P, const Part &pt, int p_lo, int p_
                                  hipStream_t st) {
     constexpr size_t lds = grid_mfma_pad_lds<W, WS>();
     const void *fn = (const void *)k_grid_mfma_pad<W, WS>;
-    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
+    Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
     if (L.blocks == 0) return;
+#if SDP_PAD_NEXT
+    // grid-stride over the items (each workgroup prefetches its next item);
+    // several workgroups per wave slot keep the uneven items balanced
+    if (!P.pipelined) L.blocks = std::min(L.blocks, persistent_blocks(fn, 64, lds));
+#endif
     const int ph = (P.g.dbg & 32) ? p_lo : p_hi;  // SDP_HIP_DBG & 32: no flush (timing)
     k_grid_mfma_pad<W, WS><<<L.blocks, 64, lds, st>>>(
         P.g, reinterpret_cast<const RecC *>(P.recs) + pt.vbase, L.src, pt.offs, (float *)P.grid,
