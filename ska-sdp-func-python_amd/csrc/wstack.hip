@@ -1400,6 +1400,10 @@ constexpr int mfma_tile_f2() {  // region tile, rounded to 16 B
 #ifndef SDP_PAD_NEXT
 #define SDP_PAD_NEXT 0
 #endif
+// SDP_PAD_PRIO=1: s_setprio 1 around each block's K-steps (experiment)
+#ifndef SDP_PAD_PRIO
+#define SDP_PAD_PRIO 0
+#endif
 constexpr int kTapBlocks = SDP_PAD_PIPE ? 2 : 1;
 
 template <int W, bool WS>
@@ -1694,6 +1698,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                     Ops o[kTapBatch / 4];
 #pragma unroll
                     for (int jj = 0; jj < kTapBatch / 4; ++jj) o[jj] = kload(jj);
+#if SDP_PAD_PRIO
+                    __builtin_amdgcn_s_setprio(1);  // MFMA phase first among ready waves
+#endif
 #pragma unroll
                     for (int jj = 0; jj < kTapBatch / 4; ++jj) {
                         if (jj < nk) {
@@ -1704,6 +1711,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                             kmfma(o[jj]);
                         }
                     }
+#if SDP_PAD_PRIO
+                    __builtin_amdgcn_s_setprio(0);
+#endif
                 }
                 continue;
 #endif
@@ -1991,6 +2001,10 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
+        // the item's first 16 records are requested before the region is
+        // staged (both depend only on the item descriptor)
+        uint32_t pf = it.b;
+        VisRec nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
         wave_sync_1w();  // previous item's reads of the region
         for (int i = lane; i < NQ * PS; i += 64) {
             const int q = i / PS;
@@ -2010,8 +2024,6 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
         // the item's cells are consecutive, so the batch after [b0, b0 + 16)
         // starts at min(b0 + 16, re) -- in the next cell when this one ends;
         // its records are loaded one batch ahead (pf = the prefetched start)
-        uint32_t pf = it.b;
-        VisRec nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
         uint32_t cb = it.b;  // start of cell c's records (clipped to the item)
         for (int c = 0; c < kGroupCell; ++c) {
             const uint32_t rb = max(cb, it.b), re = min(fo[c], it.e);
