@@ -648,7 +648,8 @@ __device__ __forceinline__ int sub_class(uint32_t ij) {
 
 template <bool CELLS>
 __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__restrict__ items,
-                                                 VisRec *recs, FineItem *__restrict__ fitems) {
+                                                 VisRec *recs, FineItem *__restrict__ fitems,
+                                                 unsigned *__restrict__ psize = nullptr) {
     constexpr int NC = CELLS ? 256 : 64;  // classes
     constexpr int PG = NC / 16;           // classes per fine group
     __shared__ VisRec stage[kSubChunk];
@@ -664,12 +665,14 @@ __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__re
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned a = 0;
+        unsigned a = 0, pa = 0;
         for (int c = 0; c < NC; ++c) {
             first[c] = a;
             a += cur[c];
+            pa += (cur[c] + 3u) & ~3u;
         }
         first[NC] = a;
+        if (psize) psize[blockIdx.x] = pa;  // the item's size with every cell 4-padded
     }
     __syncthreads();
     for (int c = threadIdx.x; c < NC; c += kSubThreads) cur[c] = first[c];
@@ -692,6 +695,82 @@ __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__re
         const VisRec r = stage[i];
         const unsigned pos = atomicAdd(&cur[sub_class<CELLS>(r.ij)], 1u);
         recs[it.b + pos] = r;
+    }
+}
+
+// Large grids, invert: the sub-sorted coarse item (cells in x-pair-major
+// order, FineItem cell ends) is re-written as 16-byte RecC records with every
+// cell padded to a multiple of 4 (zero-valued pads) at the item's slot of the
+// padded buffer (poffs: exclusive scan of k_subsort's psize), plus FineItems
+// over the padded layout -- so k_grid_mfma_pad<.., FI> runs the large grids.
+__global__ __launch_bounds__(256) void k_subsort_emit(Geo g, const Item *__restrict__ items,
+                                                      const VisRec *__restrict__ recs,
+                                                      const FineItem *__restrict__ fitems,
+                                                      const unsigned *__restrict__ poffs,
+                                                      RecC *__restrict__ out,
+                                                      FineItem *__restrict__ pfitems) {
+    // cell c = 16 gi + j of the item (group gi, cell j): records
+    // [cstart[c], cstart[c + 1]) of `recs`, padded slots from pstart[c] of `out`
+    __shared__ unsigned cstart[257], pstart[256], gtot[16], gbase[16];
+    const Item it = items[blockIdx.x];
+    const FineItem *const fi = fitems + (size_t)blockIdx.x * 16;
+    const int t = threadIdx.x;
+    if (t < 16) {
+        unsigned s0 = fi[t].b, ps = 0;
+        for (int j = 0; j < 16; ++j) {
+            const unsigned e = fi[t].o[j];
+            cstart[t * 16 + j] = s0;
+            pstart[t * 16 + j] = ps;  // group-relative
+            ps += (e - s0 + 3u) & ~3u;
+            s0 = e;
+        }
+        gtot[t] = ps;
+        if (t == 15) cstart[256] = s0;  // = it.e
+    }
+    __syncthreads();
+    if (t == 0) {
+        unsigned b = poffs[blockIdx.x];
+        for (int gi = 0; gi < 16; ++gi) {
+            gbase[gi] = b;
+            b += gtot[gi];
+        }
+    }
+    __syncthreads();
+    pstart[t] += gbase[t >> 4];  // blockDim.x == 256: one cell per thread
+    __syncthreads();
+    const int n = (int)(it.e - it.b);
+    const double fb = 1.0 - 0.5 * g.W;
+    for (int i = t; i < n; i += 256) {
+        const VisRec r = recs[it.b + i];
+        const int c = sub_class<true>(r.ij);
+        const unsigned dst = pstart[c] + (it.b + (unsigned)i - cstart[c]);
+        const uint32_t qu = fix_frac(fb - (double)r.fu, 21), qv = fix_frac(fb - (double)r.fv, 21);
+        const uint32_t qw = g.do_w ? fix_frac(fb - (double)r.fw, 22) : 0u;
+        RecC rc;
+        rc.cre = r.cre;
+        rc.cim = r.cim;
+        rc.lo = qu | (qv << 21);
+        rc.hi = (qv >> 11) | (qw << 10);
+        out[dst] = rc;
+    }
+    {
+        const unsigned cnt = cstart[t + 1] - cstart[t];
+        RecC z;
+        z.cre = z.cim = 0.0f;
+        z.lo = z.hi = 0u;  // offsets 1 - W/2: in range, finite taps
+        for (unsigned k = cnt; k < ((cnt + 3u) & ~3u); ++k) out[pstart[t] + k] = z;
+    }
+    if (t < 16) {
+        FineItem f;
+        f.b = pstart[t * 16];
+        for (int j = 0; j < 16; ++j) {
+            const int c = t * 16 + j;
+            f.o[j] = pstart[c] + ((cstart[c + 1] - cstart[c] + 3u) & ~3u);
+        }
+        f.e = f.o[15];
+        f.tile = fi[t].tile;
+        f.p0 = fi[t].p0;
+        pfitems[(size_t)blockIdx.x * 16 + t] = f;
     }
 }
 
@@ -1392,14 +1471,6 @@ constexpr int mfma_tile_f2() {  // region tile, rounded to 16 B
 #ifndef SDP_PAD_PIPE
 #define SDP_PAD_PIPE 0
 #endif
-// SDP_PAD_NEXT=1 (experiment, off): grid-stride over the items with the next
-// item's descriptor, bucket ends and first records fetched ahead.  Measured
-// 5.04-5.17 -> 5.49-5.72 ms on C2: one workgroup per item, balanced by the
-// dispatcher, hides the item-start latency better than fewer, longer-lived
-// workgroups.
-#ifndef SDP_PAD_NEXT
-#define SDP_PAD_NEXT 0
-#endif
 // SDP_PAD_PRIO=1: s_setprio 1 around each block's K-steps (experiment)
 #ifndef SDP_PAD_PRIO
 #define SDP_PAD_PRIO 0
@@ -1412,10 +1483,12 @@ constexpr size_t grid_mfma_pad_lds() {
            (size_t)kTapBlocks * kTapBatch * kTapRec * sizeof(float);
 }
 
-template <int W, bool WS>
+// FI: the items are FineItems of sub-sorted, 4-padded coarse buckets
+// (k_subsort_emit, large grids): one 2 x 8-cell group each, cell ends in o[]
+template <int W, bool WS, bool FI = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE ? 4 : 1, 4))) void k_grid_mfma_pad(
     Geo g, const RecC *__restrict__ recs, ItemSrc src, const unsigned *__restrict__ offs,
-    float *__restrict__ grid, int p_lo, int p_hi) {
+    const FineItem *__restrict__ fitems, float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
@@ -1445,35 +1518,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
     const int ckx = lane >> 5, cky = 4 * ((lane >> 4) & 1);
     float *const ftile = reinterpret_cast<float *>(tile);
 
-    // the group's 16 cell buckets end at offs[...][1..16] (record indices)
-    auto load_bnd = [&](const Item &x, uint32_t (&bb)[kGroupCell - 1]) {
-        const unsigned *ob = offs + ((size_t)x.p0 * g.ntiles + (size_t)x.tile * kGroupCell);
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        Item it;
+        uint32_t bnd[kGroupCell - 1];  // ends of cells 0..14 of the group (record indices)
+        if (FI) {
+            uint32_t fo[kGroupCell];
+            it = load_fine_item<kGroupCell>(fitems, w_it, n_items, stride, fo);
+            if (it.b >= it.e) continue;
 #pragma unroll
-        for (int c = 0; c < kGroupCell - 1; ++c) bb[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
-    };
-    // SDP_PAD_NEXT: a workgroup walks several items (grid stride) and fetches
-    // the next item's descriptor (during this item's setup), its bucket ends
-    // (after this item's first batch) and its first 64 records (with this
-    // item's last batch) ahead of use: item starts no longer wait on three
-    // dependent memory round trips
-    uint32_t w_it = blockIdx.x;
-    Item it{0u, 0u, 0u, 0u};
-    uint32_t bnd[kGroupCell - 1];
-    RecC nx{};
-    if (w_it < n_items) {
-        it = load_item(src, w_it, n_items, stride);
-        load_bnd(it, bnd);
-        nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
-    }
-    for (; w_it < n_items; w_it += gridDim.x) {
-        const uint32_t nw = w_it + gridDim.x;
-        const bool more = SDP_PAD_NEXT && nw < n_items;  // wave-uniform
-        Item raw_next{0u, 0u, 0u, 0u};
-        if (more) raw_next = src.items[(uint32_t)(((uint64_t)nw * stride) % n_items)];
-        Item nit = it;
-        uint32_t nbnd[kGroupCell - 1];
-        bool nit_ready = false;
-        const int ntg = g.nty / 8;  // groups per x pair
+            for (int c = 0; c < kGroupCell - 1; ++c) bnd[c] = fo[c];
+        } else {
+            it = load_item(src, w_it, n_items, stride);
+            // the group's 16 cell buckets end at ob[1..16]
+            const unsigned *ob = offs + ((size_t)it.p0 * g.ntiles + (size_t)it.tile * kGroupCell);
+#pragma unroll
+            for (int c = 0; c < kGroupCell - 1; ++c)
+                bnd[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
+        }
+        const int ntg = FI ? g.wny / 8 : g.nty / 8;  // groups per x pair
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
@@ -1522,28 +1584,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a[t] * o.v, b, acc[t], 0, 0, 0);
         };
 
-#if !SDP_PAD_NEXT
-        nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
-#endif
-        // after a batch's K-steps: the next item's descriptor (loaded during
-        // this item's setup) is read, its bucket ends requested, and -- when
-        // this was the item's last batch -- its first records too
-        auto after_batch = [&](bool last) {
-            if (more && !nit_ready) {
-                nit.b = __builtin_amdgcn_readfirstlane(raw_next.b);
-                nit.e = __builtin_amdgcn_readfirstlane(raw_next.e);
-                nit.tile = __builtin_amdgcn_readfirstlane(raw_next.tile);
-                nit.p0 = __builtin_amdgcn_readfirstlane(raw_next.p0);
-                load_bnd(nit, nbnd);
-                nit_ready = true;
-                if (last) nx = recs[min(nit.b + (uint32_t)lane, nit.e - 1)];
-            }
-        };
+        RecC nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
         for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
             const RecC my = nx;
-            const bool last = b0 + 64 >= it.e;  // wave-uniform
-            if (!last) nx = recs[min(b0 + 64 + (uint32_t)lane, it.e - 1)];
-            else if (nit_ready) nx = recs[min(nit.b + (uint32_t)lane, nit.e - 1)];
+            if (b0 + 64 < it.e) nx = recs[min(b0 + 64 + (uint32_t)lane, it.e - 1)];
             const int nb = (int)min(64u, it.e - b0);  // a multiple of 4
             // cell (x-pair-major index in the group) of the lane's record
             const uint32_t ri = b0 + (uint32_t)lane;
@@ -1651,7 +1695,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                     wave_lds_sync();
                 }
             }
-            after_batch(last);
             continue;
 #endif
             // two halves of kTapBatch records: taps, then their K-steps
@@ -1736,9 +1779,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                     kmfma(o);
                 }
             }
-            after_batch(last);
         }
-        after_batch(true);  // (an item without records)
         if (cur >= 0) flush_cell();
         wave_lds_sync();
 
@@ -1775,17 +1816,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                 ++xl;
             }
         }
-        if (more) {
-            it = nit;
-#pragma unroll
-            for (int c = 0; c < kGroupCell - 1; ++c) bnd[c] = nbnd[c];
-        }
-#if !SDP_PAD_NEXT
-        else if (nw < n_items) {
-            it = load_item(src, nw, n_items, stride);
-            load_bnd(it, bnd);
-        }
-#endif
     }
 }
 
@@ -2559,6 +2589,8 @@ struct Part {
     unsigned *npad = nullptr;  // pad records of a 4-padded plan (device)
     Item *items = nullptr;
     FineItem *fitems = nullptr;  // 16 per item when sub-sorted (k_subsort)
+    RecC *precs = nullptr;       // sub-sorted, 4-padded 16-B records (subpad plans)
+    FineItem *pfitems = nullptr;  // FineItems over precs
     unsigned *meta = nullptr;  // device: see k_part_meta
     // host copies (filled by read_part_meta; synchronous plans only)
     int64_t nrec = 0, nitems = 0;
@@ -2574,6 +2606,7 @@ struct Plan {
     bool subsort = false;            // 16x16 buckets re-ordered to 2x2 (register kernels)
     bool cells = false;              // invert on k_grid_mfma: one-cell buckets / sub-sort
     bool pad4 = false;               // one-cell buckets padded to 4 records (k_grid_mfma_pad)
+    bool subpad = false;             // sub-sorted coarse items re-written 4-padded (k_grid_mfma_pad FI)
     float2 *vdirect = nullptr;       // dirty2ms: register degridders write c64 vis in place
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
@@ -2622,7 +2655,8 @@ static size_t grid_budget_bytes(size_t need_other) {
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)8 << 30;
     Workspace &ws = Workspace::get();
     const size_t held_planes = ws.held("grid") + ws.held("spec") + ws.held("spec_in");
-    const size_t held_other = ws.held("recs") + ws.held("key_rank") + ws.held("degrid_acc");
+    const size_t held_other = ws.held("recs") + ws.held("key_rank") + ws.held("degrid_acc") +
+                              ws.held("precs#0") + ws.held("pfitems#0");
     const size_t avail = free_b + held_planes + held_other;
     const size_t reserve = (size_t)6 << 30;
     const size_t need = need_other + reserve;
@@ -2904,7 +2938,16 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         (size_t)nvis_all * (sizeof(VisRec) + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2))) +
         (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned) +
         (size_t)P.fft_planes * spec_plane;
-    const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
+    int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
+    // large-grid inverts: the sub-sorted records re-written 4-padded as 16-B
+    // records (~21 B per visibility with the pads) when that costs no plane
+    // residency (SDP_HIP_SUBSORT_PAD=0: never)
+    if (grid_mode && P.cells && g.sub == kTileCoarse && env_int("SDP_HIP_SUBSORT_PAD", 0) != 0 &&
+        !P.aux_bucketing) {
+        const size_t need_pad = need_other + (size_t)nvis_all * 21;
+        const int cpp = (int)std::max<size_t>(1, grid_budget_bytes(need_pad) / grid_plane);
+        if (std::min(cpp, g.nplanes) >= std::min(cp, g.nplanes)) P.subpad = true;
+    }
     P.chunk_planes = std::min(cp, g.nplanes);
     P.fft_planes = std::min(P.fft_planes, P.chunk_planes);
     P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy);
@@ -2940,6 +2983,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         const char *e = std::getenv("SDP_HIP_SUBSORT");
         P.subsort = g.sub == kTileCoarse && !P.aux_bucketing && !(e && std::atoi(e) == 0);
         if (P.subsort) P.chunk = std::min<unsigned>(P.chunk, kSubChunk);
+        P.subpad = P.subpad && P.subsort;
     }
     // one-cell buckets padded to multiples of 4 records (k_grid_mfma_pad);
     // SDP_HIP_PAD4=0 keeps the unpadded run-walking k_grid_mfma.  The padded
@@ -3252,19 +3296,30 @@ static void launch_grid_mfma_pad(const Plan &P, const Part &pt, int p_lo, int p_
     const void *fn = (const void *)k_grid_mfma_pad<W, WS>;
     Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
     if (L.blocks == 0) return;
-#if SDP_PAD_NEXT
-    // grid-stride over the items (each workgroup prefetches its next item);
-    // several workgroups per wave slot keep the uneven items balanced
-    if (!P.pipelined) L.blocks = std::min(L.blocks, persistent_blocks(fn, 64, lds));
-#endif
     const int ph = (P.g.dbg & 32) ? p_lo : p_hi;  // SDP_HIP_DBG & 32: no flush (timing)
     k_grid_mfma_pad<W, WS><<<L.blocks, 64, lds, st>>>(
-        P.g, reinterpret_cast<const RecC *>(P.recs) + pt.vbase, L.src, pt.offs, (float *)P.grid,
-        p_lo, ph);
+        P.g, reinterpret_cast<const RecC *>(P.recs) + pt.vbase, L.src, pt.offs, nullptr,
+        (float *)P.grid, p_lo, ph);
+}
+
+template <int W, bool WS>
+static void launch_grid_mfma_pad_fi(const Plan &P, const Part &pt, int p_lo, int p_hi,
+                                    hipStream_t st) {
+    constexpr size_t lds = grid_mfma_pad_lds<W, WS>();
+    const auto r = chunk_items(P, pt, p_lo, p_hi);
+    const unsigned n = 16u * (r.second - r.first);
+    if (n == 0) return;
+    k_grid_mfma_pad<W, WS, true><<<n, 64, lds, st>>>(
+        P.g, pt.precs, ItemSrc{nullptr, n, nullptr}, nullptr, pt.pfitems + 16 * (size_t)r.first,
+        (float *)P.grid, p_lo, p_hi);
 }
 
 template <int W>
 static void launch_grid(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
+    if (P.subpad) {
+        if (P.g.do_w) return launch_grid_mfma_pad_fi<W, true>(P, pt, p_lo, p_hi, st);
+        return launch_grid_mfma_pad_fi<W, false>(P, pt, p_lo, p_hi, st);
+    }
     if (P.pad4) {
         if (P.g.do_w) return launch_grid_mfma_pad<W, true>(P, pt, p_lo, p_hi, st);
         return launch_grid_mfma_pad<W, false>(P, pt, p_lo, p_hi, st);
@@ -3478,7 +3533,34 @@ static void subsort_parts(Plan &P, hipStream_t st) {
     for (size_t i = 0; i < P.parts.size(); ++i) {
         Part &pt = P.parts[i];
         if (pt.nitems == 0) continue;
-        pt.fitems = scratch<FineItem>("fitems#" + std::to_string(i), (size_t)pt.nitems * 16);
+        const std::string sfx = "#" + std::to_string(i);
+        pt.fitems = scratch<FineItem>("fitems" + sfx, (size_t)pt.nitems * 16);
+        if (P.cells && P.subpad) {
+            // sub-sort, padded sizes, their scan (one host read of the total),
+            // then the 4-padded 16-B re-write with FineItems over it
+            unsigned *psize = scratch<unsigned>("psize" + sfx, (size_t)pt.nitems + 1);
+            unsigned *poffs = scratch<unsigned>("poffs" + sfx, (size_t)pt.nitems + 1);
+            SDP_HIP_CHECK(hipMemsetAsync(psize + pt.nitems, 0, sizeof(unsigned), st));
+            k_subsort<true><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(
+                P.g, pt.items, P.recs + pt.vbase, pt.fitems, psize);
+            SDP_HIP_CHECK(hipGetLastError());
+            size_t tb = 0;
+            SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, psize, poffs,
+                                                           (int)(pt.nitems + 1), st));
+            void *tmp = scratch<char>("pscan_tmp" + sfx, tb + 16);
+            SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, psize, poffs,
+                                                           (int)(pt.nitems + 1), st));
+            unsigned total = 0;
+            SDP_HIP_CHECK(hipMemcpyAsync(&total, poffs + pt.nitems, sizeof(unsigned),
+                                         hipMemcpyDeviceToHost, st));
+            SDP_HIP_CHECK(hipStreamSynchronize(st));
+            pt.precs = scratch<RecC>("precs" + sfx, std::max<size_t>(total, 1));
+            pt.pfitems = scratch<FineItem>("pfitems" + sfx, (size_t)pt.nitems * 16);
+            k_subsort_emit<<<(unsigned)pt.nitems, 256, 0, st>>>(
+                P.g, pt.items, P.recs + pt.vbase, pt.fitems, poffs, pt.precs, pt.pfitems);
+            SDP_HIP_CHECK(hipGetLastError());
+            continue;
+        }
         if (P.cells)
             k_subsort<true><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(
                 P.g, pt.items, P.recs + pt.vbase, pt.fitems);

@@ -257,15 +257,18 @@ def test_fft_batches_match_single_batch(fft_planes, budget, monkeypatch):
     assert rel_rms(vpart.cpu().numpy(), vfull.cpu().numpy()) < 1e-6
 
 
-@pytest.mark.parametrize("subsort", ["1", "0"])
+@pytest.mark.parametrize("subsort", ["1", "0", "pad"])
 def test_large_grid_adjointness(subsort, monkeypatch):
     """C4-size grid (8192^2 image, 16384^2 grid, 2.15 GB planes) on the
-    16x16-bucket path, with (register kernels) and without (LDS-tile
-    kernels) the 2x2 sub-sort: <A x, y> = <x, A^H y> and ms2dirty of the
-    predicted visibilities of a point source peaks at that source."""
+    16x16-bucket path, with (MFMA kernels on sub-sorted cells) and without
+    (LDS-tile kernels) the sub-sort, and with the sub-sorted records
+    re-written 4-padded for k_grid_mfma_pad (SDP_HIP_SUBSORT_PAD=1, opt-in):
+    <A x, y> = <x, A^H y> and ms2dirty of the predicted visibilities of a
+    point source peaks at that source."""
     from ska_sdp_func_python_amd import kernels
     monkeypatch.setenv("SDP_HIP_BUCKET", "16")
-    monkeypatch.setenv("SDP_HIP_SUBSORT", subsort)
+    monkeypatch.setenv("SDP_HIP_SUBSORT", "1" if subsort == "pad" else subsort)
+    monkeypatch.setenv("SDP_HIP_SUBSORT_PAD", "1" if subsort == "pad" else "0")
     npix = 8192
     uvw, freq, ms, _, _ = _problem(11, nrow=20000, nchan=4, umax=3.0e5)
     uvw[:, 2] *= 0.02  # a handful of w planes at this cell size
