@@ -3697,12 +3697,36 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     Plan P = plan_geometry(in, false, st);
     const Geo &g = P.g;
     const double *tab = phi_table(g.W, g.beta, st);
+    const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
+    const int64_t nvis = in.nrow * (int64_t)in.nchan;
+    // the output zeroing and the first plane chunk's band zeroing (HBM
+    // writes) overlap the bucketing (memory-side atomics; it reads uvw and
+    // weights only) on the auxiliary stream, after the call's earlier work
+    hipEvent_t zdone = nullptr;
+    if (!P.aux_bucketing && env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0) {
+        hipStream_t aux = aux_stream();
+        hipEvent_t ready;
+        SDP_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+        SDP_HIP_CHECK(hipEventRecord(ready, st));
+        SDP_HIP_CHECK(hipStreamWaitEvent(aux, ready, 0));
+        SDP_HIP_CHECK(hipEventDestroy(ready));
+        if (!accumulate && nvis > 0) {
+            if (in.vis_dtype == SDP_HIP_C128)
+                k_zero_vis<double2><<<grid1d(nvis, 256), 256, 0, aux>>>(
+                    in.nrow, in.nchan, (double2 *)vis, in.vrs, in.vcs, oc);
+            else
+                k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, aux>>>(
+                    in.nrow, in.nchan, (float2 *)vis, in.vrs, in.vcs, oc);
+            SDP_HIP_CHECK(hipGetLastError());
+        }
+        zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
+        SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
+        SDP_HIP_CHECK(hipEventRecord(zdone, aux));
+    }
     // the bucketing runs on the aux stream under the screen + FFT
     std::vector<hipEvent_t> ev = bucket_parts(P, in, false, st);
     if (P.subsort) subsort_parts(P, st);
-    const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
-    const int64_t nvis = in.nrow * (int64_t)in.nchan;
-    if (!accumulate && nvis > 0) {
+    if (!zdone && !accumulate && nvis > 0) {
         if (in.vis_dtype == SDP_HIP_C128)
             k_zero_vis<double2><<<grid1d(nvis, 256), 256, 0, st>>>(
                 in.nrow, in.nchan, (double2 *)vis, in.vrs, in.vcs, oc);
@@ -3727,7 +3751,13 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
-        zero_band(P, np, st);
+        if (zdone) {
+            SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
+            SDP_HIP_CHECK(hipEventDestroy(zdone));
+            zdone = nullptr;
+        } else {
+            zero_band(P, np, st);
+        }
         for (int sb = 0; sb < np; sb += P.fft_planes) {
             const int nb = std::min(P.fft_planes, np - sb);
             StageTimer t2(st);
@@ -3761,6 +3791,10 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
             tgrid += tg.ms(0, 1);
         }
         waited = true;
+    }
+    if (zdone) {  // (no plane pass ran)
+        SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
+        SDP_HIP_CHECK(hipEventDestroy(zdone));
     }
     for (size_t i = 0; i < P.parts.size() && !P.vdirect; ++i) {
         const Part &pt = P.parts[i];
