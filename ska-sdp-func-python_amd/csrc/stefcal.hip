@@ -70,8 +70,11 @@ __global__ void k_rowmax(Dims d, const double *__restrict__ wb, unsigned long lo
 // x = xb / wb, w = wb / max  (masked where wb <= 0), into [s][chan][comp][dense]:
 // an LDS-tiled transpose of each solve's [bl][chan*pol] block (coalesced
 // reads along chan*pol, coalesced writes along bl)
-constexpr int kTr = 32;
-__global__ __launch_bounds__(256) void k_fill(Dims d, const double2 *__restrict__ xb,
+#ifndef SDP_FILL_TR
+#define SDP_FILL_TR 64
+#endif
+constexpr int kTr = SDP_FILL_TR;  // k_fill tile (kTr x kTr, kTr x 8 threads)
+__global__ __launch_bounds__(kTr * 8) void k_fill(Dims d, const double2 *__restrict__ xb,
                                               const double *__restrict__ wb,
                                               const unsigned long long *__restrict__ rowmax,
                                               const int32_t *__restrict__ dpos, float2 *x,
