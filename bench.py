@@ -15,7 +15,15 @@ scaling weak: every rank grids its own 64 channels; the N-GPU job is the same
         array observed in 64*N channels interleaved over 0.95-1.76 GHz, so
         every shard has the same uv extent and w-plane count.
 
-Rank 0 prints ONE JSON line.  `roofline` uses the dominant kernel (k_grid):
+Rank 0 prints ONE JSON line.  With --gpus 1 (the default) and the default
+config it also carries one object per other configuration, each with its own
+steps, timing, `roofline` and `cpu_baseline` (--no-extra skips them):
+  "c4_n1"  configs[3] at N = 1: the whole 256-channel SKA-LOW band (13.4 Gvis,
+           8192^2 image, 16384^2 grid, 71 w planes) streamed through
+           sdp_hip_ms2dirty_batch -- the metric's own 8k^2 configuration;
+  "c3"     configs[2]: the 1000-component x 10 Mvis sky-component DFT;
+  "c5"     configs[4]: the 256,000-solve StefCal batch.
+`roofline` uses the dominant kernel (k_grid):
 its launch duration is measured live with HIP events recorded by the C ABI
 on the stream the kernel runs on (sdp_hip_set_stage_timing); its algorithmic
 bytes are N_vis * 12.375 B (c64 vis + f32 weight + f64 uvw per row / nchan,
@@ -69,6 +77,13 @@ def parse():
                     help="c4: max channels per streamed batch of a rank's block (a block is "
                          "split into that many near-equal batches; 40 keeps one batch per "
                          "rank at N = 8 and fits the 71 resident planes beside it)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="default config at N=1: skip the c4_n1 / c3 / c5 objects")
+    ap.add_argument("--extra-steps", type=int, default=2,
+                    help="timed steps of the c4_n1 and c5 objects (c3 uses --steps)")
+    ap.add_argument("--c4-cpu-chans", type=int, default=2,
+                    help="c4: channels in the cpu_baseline sample (0 = skip)")
+    ap.add_argument("--c4-traffic", default=os.path.join(ROOT, "profiles", "traffic_c4_k_grid.json"))
     ap.add_argument("--emulate", default=None, metavar="RANK/WORLD",
                     help="c4 on one GPU: run only rank RANK's block of a WORLD-way partition "
                          "(no collective), to measure per-rank times")
@@ -190,7 +205,43 @@ def api_rates(args, obs, cell):
 C4_NCHAN, C4_NTIMES, C4_NPIX, C4_FLO, C4_FHI = 256, 400, 8192, 50e6, 350e6
 
 
-def run_c4(args, world, rank, local, dev, emulated=False):
+def c4_cpu_baseline(uvw_h, freqs, cell, nvis_total, nplanes_full, nchan_sample):
+    """oracle/wgrid_cpu.c (C + OpenMP restatement of the w-stacking invert,
+    matched fp32 precision, W = 8) on the `nchan_sample` lowest channels of
+    the band at the full 8192^2 image: its per-visibility gridding time is
+    extrapolated to all 13.4 Gvis and its per-plane FFT + w-screen time to the
+    band's plane count (the full job grids every visibility once and
+    transforms each of its planes once)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import wgrid_cpu
+    threads = min(16, len(os.sched_getaffinity(0)))
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        threads = min(threads, env)
+    freq = freqs[:nchan_sample]
+    rng = np.random.default_rng(4)
+    ms = (rng.normal(size=(uvw_h.shape[0], nchan_sample))
+          + 1j * rng.normal(size=(uvw_h.shape[0], nchan_sample))).astype(np.complex64)
+    info = {}
+    t0 = time.perf_counter()
+    _, tg, tf = wgrid_cpu.ms2dirty(uvw_h * np.array([-1.0, 1.0, -1.0]), freq, ms, None, C4_NPIX,
+                                   C4_NPIX, cell, cell, EPS_REQUESTED, True, nthreads=threads,
+                                   precision="single", info=info)
+    wall = time.perf_counter() - t0
+    t_vis = (wall - tf) / ms.size
+    t_plane = tf / max(1, info["nplanes"])
+    t_full = t_vis * nvis_total + t_plane * nplanes_full
+    return {"value": round(nvis_total / t_full / 1e6, 4), "unit": "Mvis/s", "cores": threads,
+            "kind": "port",
+            "sample": (f"oracle/wgrid_cpu.c (C+OpenMP w-stacking restatement; ducc0 absent), fp32 "
+                       f"W={info['support']}, {nchan_sample} lowest channels x {uvw_h.shape[0]} rows "
+                       f"({ms.size / 1e6:.1f} Mvis) on the 8192^2 image: {wall:.1f} s wall, "
+                       f"{tf:.1f} s FFT+screen for {info['nplanes']} planes; extrapolated "
+                       f"(gridding per visibility x {nvis_total / 1e9:.2f} Gvis + FFT/screen per "
+                       f"plane x {nplanes_full} planes) = {t_full:.0f} s for the band")}
+
+
+def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
     """Strong scaling of configs[3]: the fixed 256-channel band is split into
     `world` contiguous channel blocks balanced by the measured cost model
     (parallel.balanced_channel_blocks); each rank streams its block through
@@ -201,7 +252,15 @@ def run_c4(args, world, rank, local, dev, emulated=False):
     rank's uvw (52.3 M rows) resident; the batches' visibilities are resident
     when they fit (N >= 4) and the step is timed as one bracket, else each
     batch is generated on device between timed segments (the sum of the
-    segments, then the max over ranks, is the step time)."""
+    segments, then the max over ranks, is the step time).
+
+    `roofline` (dominant kernel: the gridder, summed over the batch launches):
+    algorithmic bytes = every visibility once (8 B c64, unit weights) + the
+    rows' uvw once per batch (24 B) + ONE write of the band's planes
+    (nplanes x 16384^2 x 8 B) per invert -- the planes stay resident across
+    the batches, so they are charged once, not once per batch; `compute` the
+    same launches against the fp32 MFMA peak (4 W^3 flops per visibility).
+    `sub` returns the line as a dict (the default bench's "c4_n1" object)."""
     from ska_sdp_func_python_amd import kernels, parallel, simulation
     freqs = np.linspace(C4_FLO, C4_FHI, C4_NCHAN)
     blocks = parallel.balanced_channel_blocks(freqs, world)
@@ -218,6 +277,8 @@ def run_c4(args, world, rank, local, dev, emulated=False):
     local_freq = freq_all[lo:hi]
     resident = world >= 4
     gen = torch.Generator(device=dev)
+    steps = args.extra_steps if sub else args.steps
+    warmup = min(args.warmup, 1) if sub else args.warmup
 
     def make_vis(a, e):
         gen.manual_seed(7919 * rank + a)
@@ -264,19 +325,19 @@ def run_c4(args, world, rank, local, dev, emulated=False):
         out.div_(sw)
 
     kernels.set_stage_timing(False)
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step(None)
         reduce()
     barrier()
     if resident:
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             step(None)
             reduce()
         barrier()
         elapsed = time.perf_counter() - t0
     else:
-        for _ in range(args.steps):
+        for _ in range(steps):
             step(Seg)
             barrier()
             with Seg():
@@ -293,52 +354,79 @@ def run_c4(args, world, rank, local, dev, emulated=False):
         return r
 
     kernels.ms2dirty_batch = spy
-    step(None)
-    kernels.ms2dirty_batch = orig
-    kernels.set_stage_timing(False)
+    try:
+        step(None)
+    finally:
+        kernels.ms2dirty_batch = orig
+        kernels.set_stage_timing(False)
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ms_step = elapsed / args.steps * 1e3
+    ms_step = elapsed / steps * 1e3
     nvis_total = nrow * C4_NCHAN
     if emulated:
         print(json.dumps({"emulated_rank": rank, "world": world, "block": blocks[rank],
                           "ms_per_step": round(ms_step, 3), "nvis_rank": nvis_rank,
                           "model_ms": round(parallel.c4_block_cost(freqs[lo:hi]), 1),
+                          "stages_ms": {k: round(float(sum(i[k] for i in infos)), 3)
+                                        for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
                           "note": "rank's block only; no all-reduce"}), flush=True)
-        return
-    value = nvis_total / (elapsed / args.steps) / 1e6
+        return None
+    if rank != 0:
+        return None
+    value = nvis_total / (elapsed / steps) / 1e6
     info = infos[-1]
+    W = info["support"]
     ms_grid = float(sum(i["ms_grid"] for i in infos))
-    alg = sum(nrow * (e - a) * (8 + 24.0 / (e - a)) for a, e in batches) + \
-        len(batches) * info["nplanes"] * info["ngrid_x"] * info["ngrid_y"] * 8
+    plane_bytes = info["nplanes"] * info["ngrid_x"] * info["ngrid_y"] * 8
+    alg = nvis_rank * 8 + len(batches) * nrow * 24 + plane_bytes
     achieved = alg / (ms_grid * 1e-3) / 1e9 if ms_grid > 0 else None
+    flops = nvis_rank * 4 * W ** 3
+    traffic = None
+    if os.path.exists(args.c4_traffic):
+        with open(args.c4_traffic) as f:
+            tr = json.load(f)
+        if tr.get("launches") == len(batches):
+            traffic = tr.get("bytes_per_launch")
     model = [round(parallel.c4_block_cost(freqs[a:e]), 1) for a, e in blocks]
-    if rank == 0 and not emulated:
-        line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mvis/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded SKA-LOW-like layout, N(0,1) c64 vis, unit weights, "
-                    "generated on device)",
-            "config": {"workload": "C4: SKA-LOW 512 stations x 400 times x 256 chan (50-350 MHz) "
-                                   "= 13.4 Gvis, 8192^2 image, 16384^2 w-stack grid",
-                       "nvis_total": nvis_total, "npix": C4_NPIX, "cell_rad": cell,
-                       "channel_blocks": blocks, "model_ms_per_rank": model,
-                       "rank0_batches": len(batches), "inputs_resident": resident,
-                       "support": info["support"], "nplanes_rank0": info["nplanes"],
-                       "parallelism": f"channel blocks x{world}, streamed batches, 1 all-reduce"},
-            "stages_ms_rank0": {k: round(float(sum(i[k] for i in infos)), 3)
-                                for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": None, "kernel": f"k_grid_mfma<{info['support']},true,true> (sub-sorted cells)",
-                         "kernel_ms_rank0": round(ms_grid, 3)},
-            "cpu_baseline": None,
-        }
-        print(json.dumps(line), flush=True)
+    cpu = None
+    if world == 1 and args.c4_cpu_chans > 0:
+        cpu = c4_cpu_baseline(uvw.cpu().numpy(), freqs, cell, nvis_total, info["nplanes"],
+                              args.c4_cpu_chans)
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "Mvis/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded SKA-LOW-like layout, N(0,1) c64 vis, unit weights, "
+                "generated on device)",
+        "config": {"workload": "C4: SKA-LOW 512 stations x 400 times x 256 chan (50-350 MHz) "
+                               "= 13.4 Gvis, 8192^2 image, 16384^2 w-stack grid",
+                   "nvis_total": nvis_total, "npix": C4_NPIX, "cell_rad": cell,
+                   "channel_blocks": blocks, "model_ms_per_rank": model,
+                   "rank0_batches": len(batches), "inputs_resident": resident,
+                   "support": W, "nplanes_rank0": info["nplanes"],
+                   "parallelism": f"channel blocks x{world}, streamed batches, 1 all-reduce"},
+        "stages_ms_rank0": {k: round(float(sum(i[k] for i in infos)), 3)
+                            for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": traffic, "kernel": f"k_grid_mfma<{W},true> (sub-sorted cells)",
+                     "kernel_ms_rank0": round(ms_grid, 3), "launches": len(batches),
+                     "alg_bytes": int(alg),
+                     "note": "vis 8 B + uvw 24 B per row per batch + the band's planes written "
+                             "once per invert, over the summed gridding launches",
+                     "compute": {"achieved": round(flops / (ms_grid * 1e-3) / 1e12, 2),
+                                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                 "frac": round(flops / (ms_grid * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                                               4)}},
+        "cpu_baseline": cpu,
+    }
+    if sub:
+        return line
+    print(json.dumps(line), flush=True)
+    return None
 
 
 # ---------------------------------------------------------------------------
@@ -347,7 +435,7 @@ def run_c4(args, world, rank, local, dev, emulated=False):
 C3_NCOMP, C3_NTIMES = 1000, 518   # 19,306 SKA-MID baselines x 518 times = 10.0 Mvis
 
 
-def run_c3(args, world, rank, dev):
+def run_c3(args, world, rank, dev, sub=False):
     """configs[2]: the point-component DFT (reference imaging/dft.py:135-183,
     dft_cpu_looped) of 1000 components onto 10.0 Mvis (one channel, stokesI,
     c64 output).  Rows are split across ranks (strong scaling, no
@@ -381,7 +469,8 @@ def run_c3(args, world, rank, dev):
             dist.barrier(device_ids=[dev.index])
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+    warmup = max(1, args.warmup) if sub else args.warmup
+    for _ in range(warmup):
         step()
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -419,7 +508,7 @@ def run_c3(args, world, rank, dev):
     line = {
         "metric": "G comp*vis/s (dft_skycomponent_visibility, 1000 components x 10 Mvis)",
         "value": round(nvis_total * C3_NCOMP / (elapsed / args.steps) / 1e9, 2),
-        "unit": "G comp*vis/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "unit": "G comp*vis/s", "n_gpus": world, "steps": args.steps, "warmup": warmup,
         "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32 (fp64 phase)",
         "data": "synthetic (seeded SKA-MID-like layout, 1000 components |l|,|m| < 0.05, "
@@ -436,6 +525,8 @@ def run_c3(args, world, rank, dev):
                              "MFMA does not apply (the contraction's N is npol = 1, DESIGN.md 3)"},
         "cpu_baseline": cpu,
     }
+    if sub:
+        return line
     print(json.dumps(line), flush=True)
 
 
@@ -445,7 +536,7 @@ def run_c3(args, world, rank, dev):
 C5_NANTS, C5_NCHAN, C5_BATCH = 512, 256, 16
 
 
-def run_c5(args, world, rank, dev):
+def run_c5(args, world, rank, dev, sub=False):
     """configs[4]: 256,000 per-(time, channel) StefCal solves (B jones, the
     reference's solvers.py:217-300 scalar itsubs path, niter 200, tol 1e-6)
     of 512 stations.  The inputs of the whole job (33.5 G baseline samples,
@@ -504,12 +595,14 @@ def run_c5(args, world, rank, dev):
             del g, xb, wb, gain, gwt
         return solve_s
 
-    for _ in range(args.warmup):
+    steps = args.extra_steps if sub else args.steps
+    warmup = min(args.warmup, 1) if sub else args.warmup
+    for _ in range(warmup):
         one_pass(False)
     if world > 1:
         dist.barrier(device_ids=[dev.index])
     torch.cuda.synchronize(dev)
-    elapsed = sum(one_pass(s == 0) for s in range(args.steps))
+    elapsed = sum(one_pass(s == 0) for s in range(steps))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -518,7 +611,7 @@ def run_c5(args, world, rank, dev):
         return
     nsub = ntime * C5_NCHAN
     nsub_rank = (t_hi - t_lo) * C5_NCHAN
-    gbs = 12 * nbl * stats["sub_iters"] / (elapsed / args.steps) / 1e9
+    gbs = 12 * nbl * stats["sub_iters"] / (elapsed / steps) / 1e9
     cpu = None
     if world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -539,9 +632,9 @@ def run_c5(args, world, rank, dev):
                          f"{nsub * tc / 3600:.1f} h"}
     line = {
         "metric": "StefCal solves/s (solve_gaintable, 512 stations x 256 chan x 1000 times)",
-        "value": round(nsub / (elapsed / args.steps), 1), "unit": "solves/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "value": round(nsub / (elapsed / steps), 1), "unit": "solves/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64 (c128 gains)",
         "data": "synthetic: true gains lognormal(0, 0.1) x exp(i N(0, 0.1)) per (time, station, "
                 "chan), x_b = g_a1 conj(g_a2), unit weights, generated on device per batch "
@@ -559,6 +652,8 @@ def run_c5(args, world, rank, dev):
                              "timed solves, per-sub-solve iteration counts summed"},
         "cpu_baseline": cpu,
     }
+    if sub:
+        return line
     print(json.dumps(line), flush=True)
 
 
@@ -650,8 +745,8 @@ def main():
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": (f"k_grid_mfma_pad<{info['support']},true>" if info["bucket"] == 1
-                       else f"k_grid_reg<{info['support']},true>" if info["bucket"] == 2
-                       else f"k_grid_lds<{info['support']},true,2>"), "kernel_ms": round(ms_grid / launches, 4),
+                       else f"k_grid_mfma<{info['support']},true> (sub-sorted cells)"),
+            "kernel_ms": round(ms_grid / launches, 4),
             "alg_bytes_per_launch": int(alg_bytes / launches),
             # the gridder's work is fp32 MFMA (v_mfma_f32_16x16x4_f32): the
             # same kernel against the fp32 matrix peak (= the fp32 vector peak
@@ -667,6 +762,23 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_chans > 0:
         cpu = cpu_baseline(args, obs["umax"], nchan_total)
+
+    extra = {}
+    if world == 1 and not args.no_extra:
+        # the other configurations, each timed on its own (free the C2 inputs
+        # first: the whole-band C4 needs ~250 GB of HBM)
+        del obs
+        out = None
+        torch.cuda.synchronize(dev)
+        kernels.release_workspace()
+        torch.cuda.empty_cache()
+        extra["c4_n1"] = run_c4(args, 1, 0, local, dev, sub=True)
+        kernels.release_workspace()
+        torch.cuda.empty_cache()
+        extra["c3"] = run_c3(args, 1, 0, dev, sub=True)
+        extra["c5"] = run_c5(args, 1, 0, dev, sub=True)
+        kernels.release_workspace()
+        torch.cuda.empty_cache()
 
     if rank == 0:
         line = {
@@ -687,6 +799,7 @@ def main():
             "cpu_baseline": cpu,
             "api": api,
         }
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

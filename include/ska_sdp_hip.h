@@ -66,10 +66,11 @@ typedef struct sdp_hip_wgrid_info {
     int64_t nitems;       /* gridding work items launched                   */
     int plane_chunk;      /* planes resident per pass                       */
     float ms_prep, ms_grid, ms_fft, ms_screen; /* stage times if timing on  */
-    int bucket;           /* bucket edge in cells: 2 = register gridder,
-                             16 = LDS-tile gridder (large grids)            */
-    int grid_launches;    /* (de)gridding kernel launches (visibility parts
-                             x plane chunks); ms_grid is their summed time  */
+    int bucket;           /* bucket edge in cells: 1 = one-cell buckets,
+                             16 = 16x16-cell buckets sub-sorted by cell
+                             (large grids)                                  */
+    int grid_launches;    /* (de)gridding kernel launches (one per plane
+                             chunk); ms_grid is their summed time           */
 } sdp_hip_wgrid_info;
 
 /* Library/ABI version and a device probe. */
@@ -90,9 +91,12 @@ int sdp_hip_set_stage_timing(int enable);
  *
  * uvw      [nrow, 3] f64 metres, row stride uvw_row_stride (elements)
  * freq     [nchan] f64 Hz
- * vis      [nrow, nchan] c64 (vis_dtype SDP_HIP_C64) with element strides;
- *          NULL means unit visibilities (PSF, ng.py:231-233)
- * wgt      [nrow, nchan] f32 with element strides; NULL means unit weights
+ * vis      [nrow, nchan] c64 or c128 (vis_dtype SDP_HIP_C64 / SDP_HIP_C128)
+ *          with element strides; NULL means unit visibilities (PSF,
+ *          ng.py:231-233)
+ * wgt      [nrow, nchan] f32 or f64 (wgt_dtype SDP_HIP_F32 / SDP_HIP_F64; ducc0
+ *          takes f64) with element strides; NULL means unit weights.  Samples
+ *          of zero weight are skipped (their visibilities are never read)
  * dirty    f64, element (x, y) at dirty[x*dirty_stride_x + y*dirty_stride_y]
  *          (pass strides (1, nx) to receive RASCIL's transposed image)
  * epsilon  requested accuracy; clamped to the fp32 floor 1e-7 (W <= 8)
@@ -100,7 +104,7 @@ int sdp_hip_set_stage_timing(int enable);
 int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride,
                      const double *freq, int nchan, int64_t nrow,
                      const void *vis, int vis_dtype, int64_t vis_row_stride,
-                     int64_t vis_chan_stride, const float *wgt,
+                     int64_t vis_chan_stride, const void *wgt, int wgt_dtype,
                      int64_t wgt_row_stride, int64_t wgt_chan_stride,
                      int npix_x, int npix_y, double pixsize_x,
                      double pixsize_y, double epsilon, int do_wstacking,
@@ -123,13 +127,17 @@ int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride,
  *          (uvw as given, before FLIP_UW) and {min freq, max freq} over all
  *          batches' frequencies (6 doubles)
  * Replaces the reference's per-(pol, chan) ducc0 loop as a streaming form of
- * ms2dirty (ng.py:259-289); the planes must all fit on the device.
+ * ms2dirty (ng.py:259-289); the planes must all fit on the device.  A batch
+ * whose visibilities fall outside `bounds` fails with SDP_HIP_ERR_INVALID_ARG,
+ * and so does a later batch when its sequence's planes are gone (another
+ * NUFFT call or a workspace release after the first batch) or its geometry,
+ * epsilon, flags or bounds differ from the first batch's.
  */
 int sdp_hip_ms2dirty_batch(const double *uvw, int64_t uvw_row_stride,
                            const double *freq, int nchan, int64_t nrow,
                            const void *vis, int vis_dtype,
                            int64_t vis_row_stride, int64_t vis_chan_stride,
-                           const float *wgt, int64_t wgt_row_stride,
+                           const void *wgt, int wgt_dtype, int64_t wgt_row_stride,
                            int64_t wgt_chan_stride, int npix_x, int npix_y,
                            double pixsize_x, double pixsize_y, double epsilon,
                            int do_wstacking, unsigned flags,
@@ -190,8 +198,8 @@ int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride,
                      const double *freq, int nchan, int64_t nrow,
                      const double *dirty, int64_t dirty_stride_x,
                      int64_t dirty_stride_y, int npix_x, int npix_y,
-                     double pixsize_x, double pixsize_y, const float *wgt,
-                     int64_t wgt_row_stride, int64_t wgt_chan_stride,
+                     double pixsize_x, double pixsize_y, const void *wgt,
+                     int wgt_dtype, int64_t wgt_row_stride, int64_t wgt_chan_stride,
                      double epsilon, int do_wstacking, unsigned flags,
                      void *vis, int vis_dtype, int64_t vis_row_stride,
                      int64_t vis_chan_stride, void *stream,

@@ -21,6 +21,8 @@
 #include <cmath>
 #include <vector>
 
+#include <type_traits>
+
 #include "sdp_common.h"
 
 namespace sdp {
@@ -69,11 +71,12 @@ __global__ void k_rowmax(Dims d, const double *__restrict__ wb, unsigned long lo
 
 // x = xb / wb, w = wb / max  (masked where wb <= 0), into [s][chan][comp][dense]:
 // an LDS-tiled transpose of each solve's [bl][chan*pol] block (coalesced
-// reads along chan*pol, coalesced writes along bl)
-#ifndef SDP_FILL_TR
-#define SDP_FILL_TR 64
-#endif
-constexpr int kTr = SDP_FILL_TR;  // k_fill tile (kTr x kTr, kTr x 8 threads)
+// reads along chan*pol, coalesced writes along bl).  Tile kTr x kTr with
+// kTr x 8 threads: 64 when a solve has >= 64 (chan, comp) columns (C5's 256
+// channels: 6.03 -> 4.83 ms per 4096-solve batch against 32,
+// profiles/r02_fill_tile_ab.txt), else 32 so that narrow solves (one channel,
+// 1-4 comps) leave fewer load lanes idle.
+template <int kTr>
 __global__ __launch_bounds__(kTr * 8) void k_fill(Dims d, const double2 *__restrict__ xb,
                                               const double *__restrict__ wb,
                                               const unsigned long long *__restrict__ rowmax,
@@ -565,12 +568,17 @@ static void solve(const Dims &d, const int32_t *row_start, const int32_t *ant2, 
     k_rowmax<<<dim3(std::max<unsigned>(1, std::min<unsigned>(64, (unsigned)((per + 255) / 256))),
                     d.nsolve),
                256, 0, st>>>(d, wb, rowmax);
-    {
+    auto fill = [&](auto tile) {
+        constexpr int kTr = decltype(tile)::value;
         const dim3 grd((unsigned)((d.nbl + kTr - 1) / kTr),
                        (unsigned)((d.nchan * d.ncomp + kTr - 1) / kTr), (unsigned)d.nsolve);
-        k_fill<<<grd, dim3(kTr, 8), 0, st>>>(d, static_cast<const double2 *>(xb), wb, rowmax,
-                                             dpos, x, w);
-    }
+        k_fill<kTr><<<grd, dim3(kTr, 8), 0, st>>>(d, static_cast<const double2 *>(xb), wb,
+                                                  rowmax, dpos, x, w);
+    };
+    if (d.nchan * d.ncomp >= 64)
+        fill(std::integral_constant<int, 64>{});
+    else
+        fill(std::integral_constant<int, 32>{});
     k_load_gains<<<blocks_for(ng), 256, 0, st>>>(d, static_cast<const double2 *>(gain), gwt, g,
                                                   gw);
     SDP_HIP_CHECK(hipGetLastError());

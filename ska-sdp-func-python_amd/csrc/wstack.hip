@@ -44,22 +44,16 @@ namespace sdp {
 namespace wstack {
 
 constexpr double kCLight = 299792458.0;
-constexpr int kTileCoarse = 16;  // bucket edge (cells) of the LDS-tile gridder
-constexpr int kTileFine = 2;     // bucket edge (cells) of the register gridder
-constexpr int kGroupFine = 4;    // fine buckets per work-item group (along y)
-// invert on MFMA (k_grid_mfma): one-cell buckets ordered x-pair major
-// (key tile = ((ic >> 1) * ngy + jc) * 2 + (ic & 1)), so a bucket's records
-// share their footprint origin and 16 consecutive buckets form the same
-// 2 x 8-cell work-item region as kGroupFine 2x2-cell buckets
+constexpr int kTileCoarse = 16;  // bucket edge (cells) of large grids (sub-sorted by cell)
+// one-cell buckets ordered x-pair major (key tile = ((ic >> 1) * ngy + jc) *
+// 2 + (ic & 1)), so a bucket's records share their footprint origin and 16
+// consecutive buckets form one 2 x 8-cell work-item region
 constexpr int kTileCell = 1;
 constexpr int kGroupCell = 16;
 constexpr int64_t kMaxCellKeys = (int64_t)1 << 28;
 constexpr int kGridAlign = 16;   // padded grid edges are multiples of this
-// fine buckets are used while the dense (p0, 2x2-cell) histogram stays small
-constexpr int64_t kMaxFineKeys = (int64_t)1 << 27;
 constexpr int kChunkMin = 1024;   // records per work item: chosen per call in
 constexpr int kChunkMax = 8192;   // [kChunkMin, kChunkMax] (chunk_size())
-constexpr int kPitch = 24;     // LDS row pitch in complex values (b64 conflict-free)
 constexpr int kMaxW = 8;
 constexpr int kPhiTab = 8193;  // Phi(xi) table on xi in [0, 0.5]
 constexpr int kFftBatchMax = 16;                      // planes per FFT batch
@@ -83,7 +77,6 @@ struct Geo {
     // row, so the uv core's hot buckets take several memory-side atomic
     // streams; the sub-buckets are adjacent, so the bucket stays contiguous
     int salt;
-    int dbg;               // experiment knobs (SDP_HIP_DBG)
     double su;  // sign applied to u and w (-1 with SDP_HIP_FLIP_UW)
     int nchan;
     int64_t nrow;
@@ -191,12 +184,21 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
     const int jc = ((int)fb + 1 + g.ngy / 2) % g.ngy;
     c.ic0 = ic < 0 ? ic + g.ngx : ic;
     c.jc0 = jc < 0 ? jc + g.ngy : jc;
+    // the footprint origin must lie in the bucket window and the first plane
+    // in [0, nps): always so when the geometry comes from these
+    // visibilities' own extremes (a margin of >= 2 cells / half a plane), but
+    // a batch of a batched invert is checked against the bounds its caller
+    // gave (out of them it would index outside the histogram or the planes)
+    c.ok = (unsigned)(c.ic0 - g.wx0) < (unsigned)g.wnx &&
+           (unsigned)(c.jc0 - g.wy0) < (unsigned)g.wny;
     if (g.do_w) {
         const double pw = (c.w - g.w0) / g.dw;
-        const double fp = floor(pw - 0.5 * g.W);
+        const double fp = floor(fmin(fmax(pw - 0.5 * g.W, -2.0), 2.0e9));
         c.dw = fp + 1.0 - pw;
         c.fw = (float)c.dw;
-        c.p0 = min(max((int)fp + 1, 0), g.nps - 1);
+        c.p0 = (int)fp + 1;
+        c.ok = c.ok && c.p0 >= 0 && c.p0 < g.nps;
+        c.p0 = min(max(c.p0, 0), g.nps - 1);
     } else {
         c.p0 = 0;
         c.fw = 0.0f;
@@ -372,7 +374,12 @@ __device__ __forceinline__ double eff_weight(const void *wgt, int64_t wrs, int64
         w = x.wgt_f64 ? static_cast<const double *>(wgt)[i]
                       : (double)static_cast<const float *>(wgt)[i];
     }
-    if (x.fbytes) w *= flag_mask(x, row, chan, x.fpol);
+    // select, not multiply: a flagged sample's weight is an exact zero even
+    // when the stored weight is NaN or Inf (ducc0 skips zero-weight samples)
+    if (x.fbytes) {
+        const double m = flag_mask(x, row, chan, x.fpol);
+        w = m == 0.0 ? 0.0 : w * m;
+    }
     return w;
 }
 
@@ -397,21 +404,26 @@ template <class VT>
 __device__ __forceinline__ float2 eff_vis(const VT *vis, int64_t vrs, int64_t vcs,
                                           const VisExtra &x, int64_t row, int chan) {
     const VT *p = vis + row * vrs + chan * vcs;
+    // flagged pols contribute exact zeros (select, not multiply: a NaN in a
+    // flagged visibility must not reach the image)
     if (!x.conv) {
         if (!x.fbytes) return load_vis(p);
-        const double2 v = load_vis_d(p);
         const double m = flag_mask(x, row, chan, x.fpol);
+        if (m == 0.0) return make_float2(0.0f, 0.0f);
+        const double2 v = load_vis_d(p);
         return make_float2((float)(v.x * m), (float)(v.y * m));
     }
     double re = 0.0, im = 0.0;
     for (int k = 0; k < x.npv; ++k) {
         if (x.cre[k] == 0.0 && x.cim[k] == 0.0) continue;
-        double2 v = load_vis_d(p + k * x.vps);
+        double m = 1.0;
         if (x.fbytes) {
-            const double m = flag_mask(x, row, chan, k);
-            v.x *= m;
-            v.y *= m;
+            m = flag_mask(x, row, chan, k);
+            if (m == 0.0) continue;
         }
+        double2 v = load_vis_d(p + k * x.vps);
+        v.x *= m;
+        v.y *= m;
         re += x.cre[k] * v.x - x.cim[k] * v.y;
         im += x.cre[k] * v.y + x.cim[k] * v.x;
     }
@@ -419,15 +431,14 @@ __device__ __forceinline__ float2 eff_vis(const VT *vis, int64_t vrs, int64_t vc
 }
 
 template <class VT, bool kScatter, bool kGrid, bool kCompact = false>
-__global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__restrict__ uvw,
+__global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw,
                          int64_t uvw_rs, const double *__restrict__ freq,
                          const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
                          const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x,
                          double *sw_slots, unsigned *counter, unsigned *__restrict__ rk,
                          VisRec *__restrict__ recs, unsigned long long *nbad) {
-    // v indexes the part's visibilities (rows row0...); vg the call's
     const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t vg = row0 * g.nchan + v;
+    const int64_t vg = v;
     bool valid = v < nvis;
     int64_t row = 0;
     int chan = 0;
@@ -474,7 +485,7 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
             }
         }
         const unsigned key = valid ? coord_key(g, c, row) : 0xffffffffu;
-        const unsigned rank = (g.dbg & 8) ? 0u : run_reserve<true>(key, valid, counter);
+        const unsigned rank = run_reserve<true>(key, valid, counter);
         // only the rank is kept: the scatter pass recomputes the key
         if (v < nvis) rk[v] = valid ? rank : 0xffffffffu;
         if (sw_slots) {
@@ -488,12 +499,15 @@ __global__ void k_bucket(Geo g, int64_t row0, int64_t nvis, const double *__rest
         }
         return;
     }
-    const unsigned pos = (g.dbg & 16) ? (unsigned)v : counter[coord_key(g, c, row)] + mine;
+    const unsigned pos = counter[coord_key(g, c, row)] + mine;
     float cr = wt, ci = 0.0f;
     if (kGrid) {
-        const float2 xv = vis ? eff_vis(vis, vrs, vcs, x, row, chan) : make_float2(1.0f, 0.0f);
-        cr = xv.x * wt;
-        ci = xv.y * wt;
+        // a zero-weight sample (bucketed only by a SDP_HIP_KEEP_BUCKETS plan,
+        // for the other pols) is an exact zero whatever its visibility holds
+        const float2 xv = (vis && wt != 0.0f) ? eff_vis(vis, vrs, vcs, x, row, chan)
+                                              : make_float2(1.0f, 0.0f);
+        cr = wt != 0.0f ? xv.x * wt : 0.0f;
+        ci = wt != 0.0f ? xv.y * wt : 0.0f;
     }
     if (g.do_w || x.shift) {
         double ph = g.do_w ? c.w * g.s0 : 0.0;
@@ -648,8 +662,7 @@ __device__ __forceinline__ int sub_class(uint32_t ij) {
 
 template <bool CELLS>
 __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__restrict__ items,
-                                                 VisRec *recs, FineItem *__restrict__ fitems,
-                                                 unsigned *__restrict__ psize = nullptr) {
+                                                 VisRec *recs, FineItem *__restrict__ fitems) {
     constexpr int NC = CELLS ? 256 : 64;  // classes
     constexpr int PG = NC / 16;           // classes per fine group
     __shared__ VisRec stage[kSubChunk];
@@ -665,14 +678,12 @@ __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__re
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned a = 0, pa = 0;
+        unsigned a = 0;
         for (int c = 0; c < NC; ++c) {
             first[c] = a;
             a += cur[c];
-            pa += (cur[c] + 3u) & ~3u;
         }
         first[NC] = a;
-        if (psize) psize[blockIdx.x] = pa;  // the item's size with every cell 4-padded
     }
     __syncthreads();
     for (int c = threadIdx.x; c < NC; c += kSubThreads) cur[c] = first[c];
@@ -698,111 +709,12 @@ __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__re
     }
 }
 
-// Large grids, invert: the sub-sorted coarse item (cells in x-pair-major
-// order, FineItem cell ends) is re-written as 16-byte RecC records with every
-// cell padded to a multiple of 4 (zero-valued pads) at the item's slot of the
-// padded buffer (poffs: exclusive scan of k_subsort's psize), plus FineItems
-// over the padded layout -- so k_grid_mfma_pad<.., FI> runs the large grids.
-__global__ __launch_bounds__(256) void k_subsort_emit(Geo g, const Item *__restrict__ items,
-                                                      const VisRec *__restrict__ recs,
-                                                      const FineItem *__restrict__ fitems,
-                                                      const unsigned *__restrict__ poffs,
-                                                      RecC *__restrict__ out,
-                                                      FineItem *__restrict__ pfitems) {
-    // cell c = 16 gi + j of the item (group gi, cell j): records
-    // [cstart[c], cstart[c + 1]) of `recs`, padded slots from pstart[c] of `out`
-    __shared__ unsigned cstart[257], pstart[256], gtot[16], gbase[16];
-    const Item it = items[blockIdx.x];
-    const FineItem *const fi = fitems + (size_t)blockIdx.x * 16;
-    const int t = threadIdx.x;
-    if (t < 16) {
-        unsigned s0 = fi[t].b, ps = 0;
-        for (int j = 0; j < 16; ++j) {
-            const unsigned e = fi[t].o[j];
-            cstart[t * 16 + j] = s0;
-            pstart[t * 16 + j] = ps;  // group-relative
-            ps += (e - s0 + 3u) & ~3u;
-            s0 = e;
-        }
-        gtot[t] = ps;
-        if (t == 15) cstart[256] = s0;  // = it.e
-    }
-    __syncthreads();
-    if (t == 0) {
-        unsigned b = poffs[blockIdx.x];
-        for (int gi = 0; gi < 16; ++gi) {
-            gbase[gi] = b;
-            b += gtot[gi];
-        }
-    }
-    __syncthreads();
-    pstart[t] += gbase[t >> 4];  // blockDim.x == 256: one cell per thread
-    __syncthreads();
-    const int n = (int)(it.e - it.b);
-    const double fb = 1.0 - 0.5 * g.W;
-    for (int i = t; i < n; i += 256) {
-        const VisRec r = recs[it.b + i];
-        const int c = sub_class<true>(r.ij);
-        const unsigned dst = pstart[c] + (it.b + (unsigned)i - cstart[c]);
-        const uint32_t qu = fix_frac(fb - (double)r.fu, 21), qv = fix_frac(fb - (double)r.fv, 21);
-        const uint32_t qw = g.do_w ? fix_frac(fb - (double)r.fw, 22) : 0u;
-        RecC rc;
-        rc.cre = r.cre;
-        rc.cim = r.cim;
-        rc.lo = qu | (qv << 21);
-        rc.hi = (qv >> 11) | (qw << 10);
-        out[dst] = rc;
-    }
-    {
-        const unsigned cnt = cstart[t + 1] - cstart[t];
-        RecC z;
-        z.cre = z.cim = 0.0f;
-        z.lo = z.hi = 0u;  // offsets 1 - W/2: in range, finite taps
-        for (unsigned k = cnt; k < ((cnt + 3u) & ~3u); ++k) out[pstart[t] + k] = z;
-    }
-    if (t < 16) {
-        FineItem f;
-        f.b = pstart[t * 16];
-        for (int j = 0; j < 16; ++j) {
-            const int c = t * 16 + j;
-            f.o[j] = pstart[c] + ((cstart[c + 1] - cstart[c] + 3u) & ~3u);
-        }
-        f.e = f.o[15];
-        f.tile = fi[t].tile;
-        f.p0 = fi[t].p0;
-        pfitems[(size_t)blockIdx.x * 16 + t] = f;
-    }
-}
-
 // ------------------------------------------------------------------------
 // kernels: gridding / degridding (the hot loops)
 // ------------------------------------------------------------------------
-// LDS tile of an SX x SY-cell work-item region plus the W-1 footprint halo
-template <int W, int SX, int SY = SX>
-struct TileShape {
-    static constexpr int RX = SX + W - 1, RY = SY + W - 1;
-    static constexpr int R = RX;                                    // (square tiles)
-    static constexpr int PITCH = SX == kTileCoarse ? kPitch : RY;  // LDS row pitch
-    static constexpr int PLANE = RX * PITCH;  // complex values per plane in LDS
-};
-
 // Work items are visited in a strided order (stride coprime with the item
 // count): the heavy chunks of one dense tile are spread over the launch
 // instead of flushing into the same cells at the same time.
-//
-// A launch walks the items either one per workgroup (count known on the
-// host) or persistently (count read from device memory, written by the
-// bucketing of the same call -- no host round trip between the stages).
-struct ItemSrc {
-    const Item *items;
-    uint32_t n;            // item count when ndev == nullptr
-    const unsigned *ndev;  // device-side item count (persistent launches)
-};
-
-__device__ __forceinline__ uint32_t item_count(const ItemSrc &src) {
-    return src.ndev ? (uint32_t)__builtin_amdgcn_readfirstlane((int)*src.ndev) : src.n;
-}
-
 __device__ __forceinline__ uint32_t item_stride(uint32_t n) {
     const uint32_t primes[5] = {7919u, 104729u, 1299709u, 15485863u, 179424673u};
     for (int k = 0; k < 5; ++k)
@@ -810,10 +722,10 @@ __device__ __forceinline__ uint32_t item_stride(uint32_t n) {
     return 1u;
 }
 
-__device__ __forceinline__ Item load_item(const ItemSrc &src, uint32_t w, uint32_t n,
+__device__ __forceinline__ Item load_item(const Item *items, uint32_t w, uint32_t n,
                                           uint32_t stride) {
     const uint32_t i = (uint32_t)(((uint64_t)w * stride) % n);
-    const Item raw = src.items[i];
+    const Item raw = items[i];
     Item it;
     it.b = __builtin_amdgcn_readfirstlane(raw.b);
     it.e = __builtin_amdgcn_readfirstlane(raw.e);
@@ -837,343 +749,6 @@ __device__ __forceinline__ Item load_fine_item(const FineItem *items, uint32_t w
     return it;
 }
 
-__device__ __forceinline__ float lane_readf(float v, int src) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
-}
-
-// Records are fetched 64 at a time, one per lane (coalesced 2 KiB), and
-// broadcast to the wave with v_readlane.
-struct RecRegs {
-    float cre, cim, fu, fv, fw;
-    uint32_t ij;
-};
-
-__device__ __forceinline__ RecRegs rec_at(const VisRec &my, int k) {
-    RecRegs r;
-    r.cre = lane_readf(my.cre, k);
-    r.cim = lane_readf(my.cim, k);
-    r.fu = lane_readf(my.fu, k);
-    r.fv = lane_readf(my.fv, k);
-    r.fw = lane_readf(my.fw, k);
-    r.ij = (uint32_t)__builtin_amdgcn_readlane((int)my.ij, k);
-    return r;
-}
-
-// Kernel taps of a 64-record batch with every lane busy: VGPR u[m] of lane
-// l holds the u tap (l % 8) of record 8m + l/8 (likewise v, w), so 24 ES
-// evaluations per lane cover the 64 records' 3 x 8 taps.  A record's taps
-// are then fetched with one ds_bpermute (u, v: lane-dependent) or
-// v_readlane (w: wave-uniform).  Taps t >= W evaluate to 0 (|x| > 1).
-struct BatchTaps {
-    float u[8], v[8], w[8];
-};
-
-__device__ __forceinline__ BatchTaps batch_taps(const VisRec &my, int lane, float ihw, float bl) {
-    BatchTaps b;
-    const float t = (float)(lane & 7);
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const int src = 8 * m + (lane >> 3);
-        b.u[m] = es_kernel(__shfl(my.fu, src) + t, ihw, bl);
-        b.v[m] = es_kernel(__shfl(my.fv, src) + t, ihw, bl);
-        b.w[m] = es_kernel(__shfl(my.fw, src) + t, ihw, bl);
-    }
-    return b;
-}
-
-// Per-lane roles inside a wave for support W: lane = kx*W + ky is the (u,v)
-// tap it accumulates; lanes [0,W) / [W,2W) / [2W,3W) evaluate the u / v / w
-// 1-D taps of the current record (one ES evaluation per lane).
-template <int W>
-struct LaneRole {
-    int kx, ky;
-    bool act;
-    float m0, m1, m2, toff;
-    __device__ __forceinline__ explicit LaneRole(int lane) {
-        kx = lane / W;
-        ky = lane - kx * W;
-        act = lane < W * W;
-        const int set = lane / W;
-        toff = (float)(lane - set * W);
-        // arithmetic 0/1 selectors: a ternary chain here is lowered to scratch
-        m0 = set == 0 ? 1.0f : 0.0f;
-        m1 = set == 1 ? 1.0f : 0.0f;
-        m2 = set == 2 ? 1.0f : 0.0f;
-    }
-    __device__ __forceinline__ float taps(const RecRegs &rc, float ihw, float bl) const {
-        const float base = fmaf(m0, rc.fu, fmaf(m1, rc.fv, m2 * rc.fw));
-        return es_kernel(base + toff, ihw, bl);
-    }
-};
-
-// One workgroup of NWV waves per work item (= one (p0, tile) bucket chunk).
-// The workgroup owns an LDS tile of W planes and wave wv owns planes
-// [wv*NQW, (wv+1)*NQW): every wave walks all records of the item (coalesced
-// 2 KiB record fetches, hits in L1/L2 after the first wave) and updates only
-// its planes, so accumulation is a plain ds_read_b64/ds_write_b64
-// read-modify-write with no LDS atomics (gfx950 runs ds_add_f32 at ~0.3
-// lanes/clk/CU), exact fp32 sums, and in-order LDS execution
-// inside each wave orders the updates of consecutive records.  Splitting the
-// planes over waves raises occupancy (the 35 KiB tile is shared by NWV waves)
-// to hide the LDS read->write latency of the update chain.
-template <int W, bool WS, int NWV>
-__global__ __launch_bounds__(64 * NWV) void k_grid_lds(Geo g, const VisRec *__restrict__ recs,
-                                                       ItemSrc src, float *__restrict__ grid,
-                                                       int p_lo, int p_hi) {
-    extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int kTile = kTileCoarse;
-    constexpr int R = TileShape<W, kTile>::R;
-    constexpr int PS = TileShape<W, kTile>::PLANE;
-    constexpr int NQ = WS ? W : 1;
-    constexpr int NQW = (NQ + NWV - 1) / NWV;  // planes per wave (the last
-    constexpr int NQP = NQW * NWV;             // wave may own padding planes)
-    const uint32_t n_items = item_count(src);
-    const uint32_t stride = item_stride(n_items);
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        __syncthreads();  // previous item's flush reads of the LDS tile
-        const Item it = load_item(src, w_it, n_items, stride);
-        const int lane = threadIdx.x & 63;
-        const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        for (int i = threadIdx.x; i < NQP * PS; i += 64 * NWV) tile[i] = make_float2(0.0f, 0.0f);
-        __syncthreads();
-
-        const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
-        const LaneRole<W> role(lane);
-        const float ihw = g.inv_half_w, bl = g.beta_l2e;
-        const int lane_off = role.kx * kPitch + role.ky - (g.wx0 + tx * kTile) * kPitch -
-                             (g.wy0 + ty * kTile);
-        const int q0 = wv * NQW;
-        float2 *const wtile = tile + q0 * PS;
-
-        for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
-            const int n = (int)min(64u, it.e - b0);
-            const VisRec my = recs[b0 + min(lane, n - 1)];
-            const BatchTaps bt = batch_taps(my, lane, ihw, bl);
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int rn = min(8, n - 8 * m);  // records of this 8-record group
-                for (int r = 0; r < rn; ++r) {
-                    const int k = 8 * m + r;
-                    const float cre = lane_readf(my.cre, k), cim = lane_readf(my.cim, k);
-                    const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)my.ij, k);
-                    const float ku = __shfl(bt.u[m], 8 * r + role.kx);
-                    const float kv = __shfl(bt.v[m], 8 * r + role.ky);
-                    const float kk = ku * kv;
-                    const float vr = cre * kk, vi = cim * kk;
-                    const int off = lane_off + (int)(ij & 0xffffu) * kPitch + (int)(ij >> 16);
-                    // padding planes (q0 + q >= NQ) get a zero weight: a uniform
-                    // select, so the LDS reads and writes below stay branch-free
-                    float kw[NQW];
-#pragma unroll
-                    for (int q = 0; q < NQW; ++q) {
-                        const float x = WS ? lane_readf(bt.w[m], 8 * r + min(q0 + q, NQ - 1)) : 1.0f;
-                        kw[q] = (NQP == NQ || q0 + q < NQ) ? x : 0.0f;
-                    }
-                    if (role.act) {
-                        float2 a[NQW];
-#pragma unroll
-                        for (int q = 0; q < NQW; ++q) a[q] = wtile[q * PS + off];
-#pragma unroll
-                        for (int q = 0; q < NQW; ++q) {
-                            a[q].x = fmaf(vr, kw[q], a[q].x);
-                            a[q].y = fmaf(vi, kw[q], a[q].y);
-                            wtile[q * PS + off] = a[q];
-                        }
-                    }
-                }
-            }
-        }
-        __syncthreads();
-
-        // flush: float atomics into the resident planes (the halo overlaps the
-        // neighbouring tiles); zero cells are skipped.
-        const int cells = R * R;
-        const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-        for (int c = threadIdx.x; c < NQ * cells; c += 64 * NWV) {
-            const int q = c / cells;
-            const int p = (int)it.p0 + q;
-            if (p < p_lo || p >= p_hi) continue;
-            const int rem = c - q * cells;
-            const int xl = rem / R, yl = rem - (rem / R) * R;
-            const float2 val = tile[q * PS + xl * kPitch + yl];
-            if (val.x != 0.0f || val.y != 0.0f) {
-                int gx = g.wx0 + tx * kTile + xl;
-                if (gx >= g.ngx) gx -= g.ngx;
-                int gy = g.wy0 + ty * kTile + yl;
-                if (gy >= g.ngy) gy -= g.ngy;
-                float *dst =
-                    grid + ((int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy) * 2;
-                atomicAdd(dst, val.x);
-                atomicAdd(dst + 1, val.y);
-            }
-        }
-    }
-}
-
-template <int NQ>
-__device__ __forceinline__ void acc_add(float (&ar)[NQ], float (&ai)[NQ], float vr, float vi,
-                                        const float (&kw)[NQ]) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        ar[q] = fmaf(vr, kw[q], ar[q]);
-        ai[q] = fmaf(vi, kw[q], ai[q]);
-    }
-}
-
-// Register gridder: one wave per work item = a chunk of the records of a
-// group of kGroupFine consecutive 2x2-cell buckets (same first plane p0,
-// same x), i.e. a 2 x 8-cell region.  Lane (kx, ky) is the (u, v) tap it
-// accumulates.  Bucket by bucket, a record whose footprint starts at origin
-// o in {0,1}^2 of its bucket adds vis * ku * kv * kw[q] into the VGPR
-// accumulator acc[o][q] (q = w plane): per-record work is FMAs on registers,
-// with no LDS traffic except two ds_bpermute for the u / v taps.  At the end
-// of each bucket the <= 4 origin sets are added into the group's
-// (2+W-1) x (8+W-1) x W LDS tile; the tile is flushed once per item with
-// global float atomics (zero cells skipped), so neighbouring buckets share
-// one flush of their overlapping halos.  Records of a bucket are consumed in
-// static groups of 8 (zero-valued padding at the end of a bucket).
-template <int W, bool WS, bool FI>
-__global__ __launch_bounds__(64) void k_grid_reg(Geo g, const VisRec *__restrict__ recs,
-                                                 ItemSrc src,
-                                                 const unsigned *__restrict__ offs,
-                                                 const FineItem *__restrict__ fitems,
-                                                 float *__restrict__ grid, int p_lo, int p_hi,
-                                                 int dbg) {
-    constexpr int SUB = kTileFine;
-    constexpr int GRP = kGroupFine;
-    extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    using TS = TileShape<W, SUB, SUB * GRP>;
-    constexpr int RX = TS::RX, RY = TS::RY, PS = TS::PLANE;
-    constexpr int NQ = WS ? W : 1;
-    constexpr int NO = SUB * SUB;
-    static_assert(NO == 4, "origin select below assumes 2x2-cell buckets");
-    const uint32_t n_items = item_count(src);
-    const uint32_t stride = item_stride(n_items);
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        uint32_t fo[4] = {0u, 0u, 0u, 0u};
-        const Item it = FI ? load_fine_item(fitems, w_it, n_items, stride, fo)
-                           : load_item(src, w_it, n_items, stride);
-        if (FI && it.b >= it.e) continue;
-        if (dbg & 4) {
-            if (it.b == 0xfffffffeu) grid[0] = 1.0f;  // keep the item load live
-            continue;
-        }
-        const int lane = threadIdx.x;
-        const LaneRole<W> role(lane);
-        const float ihw = g.inv_half_w, bl = g.beta_l2e;
-        const int ntg = g.nty / GRP;
-        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-        const int ibase = g.wx0 + sx * SUB, jbase = g.wy0 + sg * GRP * SUB;
-        const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
-
-        for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
-
-        const float tap_t = (float)(lane & 7);
-        for (int j = 0; j < GRP; ++j) {
-            const uint32_t rb = FI ? (j == 0 ? it.b : fo[j - 1]) : max(it.b, offs[key0 + j]);
-            const uint32_t re = FI ? fo[j] : min(it.e, offs[key0 + j + 1]);
-            if (rb >= re) continue;
-            const int jb = jbase + j * SUB;  // bucket's first cell along y
-
-            float acc_r[NO][NQ], acc_i[NO][NQ];
-#pragma unroll
-            for (int o = 0; o < NO; ++o)
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) acc_r[o][q] = acc_i[o][q] = 0.0f;
-            uint32_t used = 0;
-
-            for (uint32_t b0 = rb; b0 < ((dbg & 2) ? rb + 1 : re); b0 += 64) {
-                const int n = (int)min(64u, re - b0);
-                const VisRec my = recs[b0 + min(lane, n - 1)];
-                // per-lane decode of the lane's own record; lanes >= n carry
-                // zero-valued padding records
-                const bool live = lane < n;
-                const float cre_l = live ? my.cre : 0.0f, cim_l = live ? my.cim : 0.0f;
-                const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
-#pragma unroll
-                for (int oo = 0; oo < NO; ++oo)
-                    if (__ballot(live && o_l == oo)) used |= 1u << oo;
-#pragma unroll
-                for (int m = 0; m < 8; ++m) {
-                    if (8 * m >= n) break;
-                    // taps of this 8-record group: lane l holds tap (l % 8) of record
-                    // 8m + l/8; the u tap is pre-multiplied by the record's value
-                    const int src = 8 * m + (lane >> 3);
-                    const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
-                    const float tur = tu * __shfl(cre_l, src), tui = tu * __shfl(cim_l, src);
-                    const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
-                    const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const int k = 8 * m + r;
-                        const int o = __builtin_amdgcn_readlane(o_l, k);
-                        const float kv = __shfl(tv, 8 * r + role.ky);
-                        const float vr = __shfl(tur, 8 * r + role.kx) * kv;
-                        const float vi = __shfl(tui, 8 * r + role.kx) * kv;
-                        float kw[NQ];
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
-                        // origin select: uniform branches (one per origin set)
-#pragma unroll
-                        for (int oo = 0; oo < NO; ++oo)
-                            if (o == oo) acc_add<NQ>(acc_r[oo], acc_i[oo], vr, vi, kw);
-                    }
-                }
-            }
-
-            // add the bucket's origin sets into the group tile (plain RMW: one
-            // wave, in-order LDS)
-#pragma unroll
-            for (int oo = 0; oo < NO; ++oo) {
-                if ((used >> oo) & 1u) {
-                    if (role.act) {
-                        const int base = (oo / SUB + role.kx) * RY + j * SUB + (oo % SUB) + role.ky;
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) {
-                            float2 a = tile[q * PS + base];
-                            a.x += acc_r[oo][q];
-                            a.y += acc_i[oo][q];
-                            tile[q * PS + base] = a;
-                        }
-                    }
-                }
-            }
-        }
-
-        // flush: lane f of pass i handles float (64 i + f) of each plane's
-        // RX x RY complex cells (rows of RY contiguous cells, re/im interleaved);
-        // zero floats are skipped.  The address of a float is the same in every
-        // plane, so it is computed once.
-        constexpr int FPP = RX * RY * 2;  // floats per plane
-        const int64_t plane_floats = (int64_t)g.ngx * g.ngy * 2;
-        const float *ftile = reinterpret_cast<const float *>(tile);
-#pragma unroll
-        for (int i0 = 0; i0 < FPP; i0 += 64) {
-            const int f = i0 + lane;
-            if (f >= FPP) break;
-            const int c = f >> 1;
-            const int xl = c / RY, yl = c - (c / RY) * RY;
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            float *dst0 = grid + ((int64_t)gx * g.ngy + gy) * 2 + (f & 1);
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int p = (int)it.p0 + q;
-                const float val = ftile[q * PS * 2 + f];
-                if (p >= p_lo && p < p_hi && val != 0.0f) {
-                    float *dst = dst0 + (int64_t)(p - p_lo) * plane_floats;
-                    if (dbg & 1) {
-                        if (val == 1.2345f) dst[0] = val;  // keep the flush live, no atomics
-                    } else {
-                        atomicAdd(dst, val);
-                    }
-                }
-            }
-        }
-    }
-}
 
 // MFMA gridder (invert): one wave per work item = a chunk of the records of
 // a 2 x 8-cell region (16 one-cell buckets, same first plane p0; records
@@ -1208,36 +783,12 @@ __device__ __forceinline__ float bperm(int byte_addr, float v) {
 // program order, so a hand-off between the wave's own lanes through LDS needs
 // only a compiler barrier (wavefront-scope fence), not s_barrier plus the
 // s_waitcnt lgkmcnt(0) that __syncthreads() brings with it -- the wave keeps
-// issuing while its writes drain.  SDP_PAD_WAVESYNC=0 restores __syncthreads
-// in k_grid_mfma_pad (the gridders and degridders below all run one wave per
-// workgroup).
-#ifndef SDP_PAD_WAVESYNC
-#define SDP_PAD_WAVESYNC 1
-#endif
-#ifndef SDP_PAD_UNROLL
-#define SDP_PAD_UNROLL 1
-#endif
+// issuing while its writes drain (C2 gridding 5.26 -> 5.09 ms,
+// profiles/r02_pad_ab.txt).  Every gridder / degridder below runs one wave
+// per workgroup.
 __device__ __forceinline__ void wave_lds_sync() {
-#if SDP_PAD_WAVESYNC
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
-#else
-    __syncthreads();
-#endif
-}
-
-// the same hand-off in k_grid_mfma / k_degrid_mfma (SDP_MFMA_WAVESYNC=0:
-// __syncthreads)
-#ifndef SDP_MFMA_WAVESYNC
-#define SDP_MFMA_WAVESYNC 1
-#endif
-__device__ __forceinline__ void wave_sync_1w() {
-#if SDP_MFMA_WAVESYNC
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-#else
-    __syncthreads();
-#endif
 }
 
 // ES kernel for the MFMA gridder's taps: x = fu*ihw + t*ihw by one fma; for
@@ -1251,11 +802,10 @@ __device__ __forceinline__ float es_tap(float f, float tihw, float ihw, float bl
     return W == 8 ? e : (y > 0.0f ? e : 0.0f);
 }
 
-template <int W, bool WS, bool FI>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma(Geo g, const VisRec *__restrict__ recs,
-                                                  ItemSrc src, const unsigned *__restrict__ offs,
-                                                  const FineItem *__restrict__ fitems,
-                                                  float *__restrict__ grid, int p_lo, int p_hi) {
+template <int W, bool WS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma(
+    Geo g, const VisRec *__restrict__ recs, uint32_t n_items, const FineItem *__restrict__ fitems,
+    float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
     // LDS: the region tile (W planes x RX x RY complex) + the staged batch
     // (64 records: fu fv fw - | cre cim - - as two float4 rows per record)
@@ -1263,8 +813,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
     constexpr int NQ = WS ? W : 1;
     float4 *const stage = reinterpret_cast<float4 *>(tile + NQ * PS);  // [64][2]
-    (void)offs;
-    const uint32_t n_items = item_count(src);
     const uint32_t stride = item_stride(n_items);
     const int lane = threadIdx.x;
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
@@ -1280,19 +828,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     float *const ftile = reinterpret_cast<float *>(tile);
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        Item it;
-        if (FI) {
-            uint32_t fo[1];
-            it = load_fine_item<1>(fitems, w_it, n_items, stride, fo);
-            if (it.b >= it.e) continue;
-        } else {
-            it = load_item(src, w_it, n_items, stride);
-        }
-        const int ntg = FI ? g.wny / 8 : g.nty / 8;  // groups per x pair
+        uint32_t fo[1];
+        const Item it = load_fine_item<1>(fitems, w_it, n_items, stride, fo);
+        if (it.b >= it.e) continue;
+        const int ntg = g.wny / 8;  // groups per x pair
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
-        wave_sync_1w();
+        wave_lds_sync();
         for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
 
         floatx4 acc[4];
@@ -1365,10 +908,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             const bool live = lane < nb;
             const int cj = live ? ((int)(my.ij >> 16) - jbase) * 2 + ((int)(my.ij & 0xffffu) - ibase)
                                 : 16;
-            wave_sync_1w();  // previous batch's stage reads
+            wave_lds_sync();  // previous batch's stage reads
             stage[2 * lane] = make_float4(my.fu, my.fv, my.fw, 0.0f);
             stage[2 * lane + 1] = make_float4(live ? my.cre : 0.0f, live ? my.cim : 0.0f, 0.0f, 0.0f);
-            wave_sync_1w();
+            wave_lds_sync();
             // run starts: lane 0, and every lane whose cell differs from the previous lane's
             const int prev = __shfl_up(cj, 1);
             uint64_t starts = __ballot(live && (lane == 0 || prev != cj));
@@ -1400,7 +943,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             }
         }
         if (cur >= 0) flush_cell();
-        wave_sync_1w();
+        wave_lds_sync();
 
         // flush: float f = i0 + lane of each plane's RX x RY complex cells,
         // buffer atomics off a per-plane descriptor (32-bit offsets), the
@@ -1453,49 +996,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 //    per K-step 4 LDS reads, 5 multiplies, 4 MFMAs and a cell-change bit
 //    test -- no run bookkeeping, no masking.
 constexpr int kTapRec = 28;    // floats per record row of the tap block (16-B multiple)
-#ifndef SDP_TAP_BATCH
-#define SDP_TAP_BATCH 16
-#endif
-constexpr int kTapBatch = SDP_TAP_BATCH;  // records per tap block (LDS, occupancy)
+constexpr int kTapBatch = 16;  // records per tap block (LDS, occupancy: 14 waves per CU)
 
 template <int W, bool WS>
 constexpr int mfma_tile_f2() {  // region tile, rounded to 16 B
     return (((WS ? W : 1) * (2 + W - 1) * (8 + W - 1)) + 1) & ~1;
 }
 
-// SDP_PAD_PIPE=1 (experiment, off): two tap blocks; the ES chains of block
-// h + 1 issue between the MFMAs of block h (software pipeline inside each
-// 64-record batch).  Measured 5.08-5.18 -> 5.58-5.70 ms on C2: the second
-// tap block (12.5 KiB per wave, 13 waves per CU) and the 4-wave register cap
-// (accumulators moved to VGPRs) cost more than the overlap gains.
-#ifndef SDP_PAD_PIPE
-#define SDP_PAD_PIPE 0
-#endif
-// SDP_PAD_PRIO=1: s_setprio 1 around each block's K-steps (experiment)
-#ifndef SDP_PAD_PRIO
-#define SDP_PAD_PRIO 0
-#endif
-constexpr int kTapBlocks = SDP_PAD_PIPE ? 2 : 1;
-
 template <int W, bool WS>
 constexpr size_t grid_mfma_pad_lds() {
     return (size_t)mfma_tile_f2<W, WS>() * sizeof(float2) + kTapBatch * sizeof(float4) +
-           (size_t)kTapBlocks * kTapBatch * kTapRec * sizeof(float);
+           (size_t)kTapBatch * kTapRec * sizeof(float);
 }
 
-// FI: the items are FineItems of sub-sorted, 4-padded coarse buckets
-// (k_subsort_emit, large grids): one 2 x 8-cell group each, cell ends in o[]
-template <int W, bool WS, bool FI = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE ? 4 : 1, 4))) void k_grid_mfma_pad(
-    Geo g, const RecC *__restrict__ recs, ItemSrc src, const unsigned *__restrict__ offs,
-    const FineItem *__restrict__ fitems, float *__restrict__ grid, int p_lo, int p_hi) {
+template <int W, bool WS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma_pad(
+    Geo g, const RecC *__restrict__ recs, const Item *__restrict__ items, uint32_t n_items,
+    const unsigned *__restrict__ offs, float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
     constexpr int NQ = WS ? W : 1;
     float4 *const stage = reinterpret_cast<float4 *>(tile + mfma_tile_f2<W, WS>());  // fu fv fw -
     float *const blk = reinterpret_cast<float *>(stage + kTapBatch);  // [kTapBatch][kTapRec]
-    const uint32_t n_items = item_count(src);
     const uint32_t stride = item_stride(n_items);
     const int lane = threadIdx.x;
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
@@ -1519,23 +1042,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
     float *const ftile = reinterpret_cast<float *>(tile);
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        Item it;
         uint32_t bnd[kGroupCell - 1];  // ends of cells 0..14 of the group (record indices)
-        if (FI) {
-            uint32_t fo[kGroupCell];
-            it = load_fine_item<kGroupCell>(fitems, w_it, n_items, stride, fo);
-            if (it.b >= it.e) continue;
-#pragma unroll
-            for (int c = 0; c < kGroupCell - 1; ++c) bnd[c] = fo[c];
-        } else {
-            it = load_item(src, w_it, n_items, stride);
+        const Item it = load_item(items, w_it, n_items, stride);
+        {
             // the group's 16 cell buckets end at ob[1..16]
             const unsigned *ob = offs + ((size_t)it.p0 * g.ntiles + (size_t)it.tile * kGroupCell);
 #pragma unroll
             for (int c = 0; c < kGroupCell - 1; ++c)
                 bnd[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
         }
-        const int ntg = FI ? g.wny / 8 : g.nty / 8;  // groups per x pair
+        const int ntg = g.nty / 8;  // groups per x pair
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
@@ -1601,102 +1117,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
             const int prev = __shfl_up(cj, 4);
             uint64_t chg = __ballot((lane & 3) == 0 && lane >= 4 && prev != cj);
             if (__builtin_amdgcn_readfirstlane(cj) != cur) chg |= 1ull;
-#if SDP_PAD_PIPE
-            {
-                // blocks of kTapBatch records; block hb's taps live in tap block
-                // hb & 1.  Block 0's taps are evaluated up front; while block hb's
-                // K-steps issue, the offsets of block hb + 1 come from their lanes
-                // (ds_bpermute) and its six ES chains run between the MFMAs.
-                constexpr int BS = kTapBatch * kTapRec;  // floats per tap block
-                const int nblk = (nb + kTapBatch - 1) / kTapBatch;
-                auto put_values = [&](int hb, float *bb) {
-                    if (lane / kTapBatch == hb) {
-                        const int r = lane % kTapBatch;
-                        *reinterpret_cast<float2 *>(bb + r * kTapRec + 24) =
-                            make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
-                    }
-                };
-                float fx[2][3];
-                auto fetch = [&](int hb) {
-#pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        const int src = kTapBatch * hb + 8 * m + (lane >> 3);
-                        fx[m][0] = __shfl(fu, src);
-                        fx[m][1] = __shfl(fv, src);
-                        fx[m][2] = __shfl(fw, src);
-                    }
-                };
-                auto es = [&](int m, int k) {
-                    return (WS || k < 2) ? es_tap<W>(fx[m][k], tihw, ihw, bl)
-                                         : (tt == 0 ? 1.0f : 0.0f);
-                };
-                float tv_[2][3];
-                auto put_taps = [&](float *bb) {
-#pragma unroll
-                    for (int m = 0; m < 2; ++m) {
-                        float *d = bb + ((lane >> 3) + 8 * m) * kTapRec;
-                        d[wu] = tv_[m][0];
-                        d[wv] = tv_[m][1];
-                        d[ww] = tv_[m][2];
-                    }
-                };
-                put_values(0, blk);
-                fetch(0);
-#pragma unroll
-                for (int m = 0; m < 2; ++m)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) tv_[m][k] = es(m, k);
-                put_taps(blk);
-                wave_lds_sync();
-                for (int hb = 0; hb < nblk; ++hb) {
-                    const int boff = (hb & 1) * BS;
-                    float *const nbuf = blk + (BS - boff);
-                    const int nk = min(kTapBatch, nb - kTapBatch * hb) >> 2;
-                    const uint64_t hchg = chg >> (kTapBatch * hb);
-                    Ops o[kTapBatch / 4];
-#pragma unroll
-                    for (int jj = 0; jj < kTapBatch / 4; ++jj) {
-                        o[jj].a = *reinterpret_cast<const floatx4 *>(kA + boff + 4 * jj * kTapRec);
-                        o[jj].v = kV[boff + 4 * jj * kTapRec];
-                        o[jj].w = kW[boff + 4 * jj * kTapRec];
-                        o[jj].c = kC[boff + 4 * jj * kTapRec];
-                    }
-                    const bool more = hb + 1 < nblk;  // wave-uniform
-                    if (more) {
-                        put_values(hb + 1, nbuf);
-                        fetch(hb + 1);
-                    }
-                    auto kstep = [&](int jj) {
-                        if (jj < nk) {
-                            if ((hchg >> (4 * jj)) & 1ull) {
-                                if (cur >= 0) flush_cell();
-                                cur = __builtin_amdgcn_readlane(cj, kTapBatch * hb + 4 * jj);
-                            }
-                            kmfma(o[jj]);
-                        }
-                    };
-                    kstep(0);
-                    if (more) {
-                        tv_[0][0] = es(0, 0);
-                        tv_[0][1] = es(0, 1);
-                    }
-                    kstep(1);
-                    if (more) {
-                        tv_[0][2] = es(0, 2);
-                        tv_[1][0] = es(1, 0);
-                    }
-                    kstep(2);
-                    if (more) tv_[1][1] = es(1, 1);
-                    kstep(3);
-                    if (more) {
-                        tv_[1][2] = es(1, 2);
-                        put_taps(nbuf);
-                    }
-                    wave_lds_sync();
-                }
-            }
-            continue;
-#endif
             // two halves of kTapBatch records: taps, then their K-steps
             for (int h = 0; h < 64 / kTapBatch; ++h) {
                 const int nbh = min(kTapBatch, nb - kTapBatch * h);
@@ -1733,7 +1153,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                 wave_lds_sync();
                 const uint64_t hchg = chg >> (kTapBatch * h);
                 const int nk = nbh >> 2;
-#if SDP_PAD_UNROLL
                 // the block's (up to) 4 K-steps unrolled: every operand read
                 // up front at compile-time offsets, a cell change (bit 4j)
                 // flushes the accumulators between two K-steps
@@ -1741,9 +1160,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                     Ops o[kTapBatch / 4];
 #pragma unroll
                     for (int jj = 0; jj < kTapBatch / 4; ++jj) o[jj] = kload(jj);
-#if SDP_PAD_PRIO
-                    __builtin_amdgcn_s_setprio(1);  // MFMA phase first among ready waves
-#endif
 #pragma unroll
                     for (int jj = 0; jj < kTapBatch / 4; ++jj) {
                         if (jj < nk) {
@@ -1754,29 +1170,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
                             kmfma(o[jj]);
                         }
                     }
-#if SDP_PAD_PRIO
-                    __builtin_amdgcn_s_setprio(0);
-#endif
-                }
-                continue;
-#endif
-                // segments of K-steps of one cell; inside a segment the operands
-                // of K-step j + 1 are read before the MFMAs of K-step j issue
-                int j = 0;
-                while (j < nk) {
-                    if ((hchg >> (4 * j)) & 1ull) {
-                        if (cur >= 0) flush_cell();
-                        cur = __builtin_amdgcn_readlane(cj, kTapBatch * h + 4 * j);
-                    }
-                    const uint64_t rest = hchg & ~((2ull << (4 * j)) - 1ull);
-                    const int je = rest ? min(nk, (int)(__builtin_ctzll(rest) >> 2)) : nk;
-                    Ops o = kload(j);
-                    for (++j; j < je; ++j) {
-                        const Ops on = kload(j);
-                        kmfma(o);
-                        o = on;
-                    }
-                    kmfma(o);
                 }
             }
         }
@@ -1819,164 +1212,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SDP_PAD_PIPE
     }
 }
 
-// Register degridder (mirror of k_grid_reg): one wave per work item = a
-// chunk of a group of kGroupFine consecutive 2x2-cell buckets.  The group's
-// (2+W-1) x (8+W-1) x W region is staged in LDS once; per bucket, lane
-// (kx, ky) loads the W plane values of its tap cell for each of the 4
-// footprint origins into VGPRs (G[o][q]).  Per record the lane forms
-// kk * sum_q kw[q] G[o][q] with 8 register FMAs; the 64 lanes' partials of
-// 8 records are then summed with one reduce-scatter butterfly (5 lane
-// exchanges per record instead of 12).  Each record belongs to exactly one
-// item, so its raw sum is added to acc[] with a plain read-modify-write; the
-// record factor wgt * exp(-2 pi i w s0) is applied by k_finalize.
-template <int W, bool WS, bool FI>
-__global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restrict__ recs,
-                                                   ItemSrc src,
-                                                   const unsigned *__restrict__ offs,
-                                                   const FineItem *__restrict__ fitems,
-                                                   const float2 *__restrict__ grid, int p_lo,
-                                                   int p_hi, float2 *__restrict__ acc,
-                                                   float2 *__restrict__ vdirect) {
-    constexpr int SUB = kTileFine;
-    constexpr int GRP = kGroupFine;
-    extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    using TS = TileShape<W, SUB, SUB * GRP>;
-    constexpr int RX = TS::RX, RY = TS::RY, PS = TS::PLANE;
-    constexpr int NQ = WS ? W : 1;
-    constexpr int NO = SUB * SUB;
-    static_assert(NO == 4, "origin select below assumes 2x2-cell buckets");
-    const uint32_t n_items = item_count(src);
-    const uint32_t stride = item_stride(n_items);
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        uint32_t fo[4] = {0u, 0u, 0u, 0u};
-        const Item it = FI ? load_fine_item(fitems, w_it, n_items, stride, fo)
-                           : load_item(src, w_it, n_items, stride);
-        if (FI && it.b >= it.e) continue;
-        const int lane = threadIdx.x;
-        const LaneRole<W> role(lane);
-        const float ihw = g.inv_half_w, bl = g.beta_l2e;
-        const int ntg = g.nty / GRP;
-        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-        const int ibase = g.wx0 + sx * SUB, jbase = g.wy0 + sg * GRP * SUB;
-        const int64_t key0 = (int64_t)it.p0 * g.ntiles + (int64_t)sx * g.nty + (int64_t)sg * GRP;
-        const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-
-        // stage the region (planes outside this pass's [p_lo, p_hi) read as 0)
-        for (int i = lane; i < NQ * RX * RY; i += 64) {
-            const int q = i / (RX * RY);
-            const int p = (int)it.p0 + q;
-            const int rem = i - q * RX * RY;
-            const int xl = rem / RY, yl = rem - (rem / RY) * RY;
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            tile[q * PS + xl * RY + yl] =
-                (p >= p_lo && p < p_hi)
-                    ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
-                    : make_float2(0.0f, 0.0f);
-        }
-
-        const float tap_t = (float)(lane & 7);
-        const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
-        for (int j = 0; j < GRP; ++j) {
-            const uint32_t rb = FI ? (j == 0 ? it.b : fo[j - 1]) : max(it.b, offs[key0 + j]);
-            const uint32_t re = FI ? fo[j] : min(it.e, offs[key0 + j + 1]);
-            if (rb >= re) continue;
-            const int jb = jbase + j * SUB;
-
-            float gr[NO][NQ], gi[NO][NQ];
-#pragma unroll
-            for (int o = 0; o < NO; ++o) {
-                const int base = (o / SUB + role.kx) * RY + j * SUB + (o % SUB) + role.ky;
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const float2 v = role.act ? tile[q * PS + base] : make_float2(0.0f, 0.0f);
-                    gr[o][q] = v.x;
-                    gi[o][q] = v.y;
-                }
-            }
-
-            for (uint32_t b0 = rb; b0 < re; b0 += 64) {
-                const int n = (int)min(64u, re - b0);
-                const VisRec my = recs[b0 + min(lane, n - 1)];
-                const int o_l = ((int)(my.ij & 0xffffu) - ibase) * SUB + ((int)(my.ij >> 16) - jb);
-#pragma unroll
-                for (int m = 0; m < 8; ++m) {
-                    if (8 * m >= n) break;
-                    const int src = 8 * m + (lane >> 3);
-                    const float tu = es_kernel(__shfl(my.fu, src) + tap_t, ihw, bl);
-                    const float tv = es_kernel(__shfl(my.fv, src) + tap_t, ihw, bl);
-                    const float tw = WS ? es_kernel(__shfl(my.fw, src) + tap_t, ihw, bl) : 1.0f;
-                    float pr[8], pim[8];
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const int k = 8 * m + r;
-                        const int o = __builtin_amdgcn_readlane(o_l, k);
-                        const float ku = __shfl(tu, 8 * r + role.kx);
-                        const float kv = __shfl(tv, 8 * r + role.ky);
-                        float kw[NQ];
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(tw, 8 * r + q) : 1.0f;
-                        float sr = 0.0f, si = 0.0f;
-#pragma unroll
-                        for (int oo = 0; oo < NO; ++oo) {
-                            if (o == oo) {
-#pragma unroll
-                                for (int q = 0; q < NQ; ++q) {
-                                    sr = fmaf(kw[q], gr[oo][q], sr);
-                                    si = fmaf(kw[q], gi[oo][q], si);
-                                }
-                            }
-                        }
-                        const float kk = ku * kv;
-                        pr[r] = sr * kk;
-                        pim[r] = si * kk;
-                    }
-                    // reduce-scatter: after the xor-32/16/8 halvings lane l holds
-                    // record (l >> 3) & 7 summed over 8 lanes; xor 4/2/1 finish it
-                    float a4r[4], a4i[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const float sr = b5 ? pr[i] : pr[i + 4], si = b5 ? pim[i] : pim[i + 4];
-                        a4r[i] = (b5 ? pr[i + 4] : pr[i]) + __shfl_xor(sr, 32);
-                        a4i[i] = (b5 ? pim[i + 4] : pim[i]) + __shfl_xor(si, 32);
-                    }
-                    float a2r[2], a2i[2];
-#pragma unroll
-                    for (int i = 0; i < 2; ++i) {
-                        const float sr = b4 ? a4r[i] : a4r[i + 2], si = b4 ? a4i[i] : a4i[i + 2];
-                        a2r[i] = (b4 ? a4r[i + 2] : a4r[i]) + __shfl_xor(sr, 16);
-                        a2i[i] = (b4 ? a4i[i + 2] : a4i[i]) + __shfl_xor(si, 16);
-                    }
-                    float tr = (b3 ? a2r[1] : a2r[0]) + __shfl_xor(b3 ? a2r[0] : a2r[1], 8);
-                    float ti = (b3 ? a2i[1] : a2i[0]) + __shfl_xor(b3 ? a2i[0] : a2i[1], 8);
-#pragma unroll
-                    for (int msk = 4; msk > 0; msk >>= 1) {
-                        tr += __shfl_xor(tr, msk);
-                        ti += __shfl_xor(ti, msk);
-                    }
-                    const int rec = 8 * m + ((lane >> 3) & 7);
-                    if (vdirect) {
-                        // single pass: the record factor applied here and the
-                        // visibility written in place (no acc, no k_finalize)
-                        const float cr = __shfl(my.cre, rec), ci = __shfl(my.cim, rec);
-                        const uint32_t ix = (uint32_t)__shfl((int)my.idx, rec);
-                        if ((lane & 7) == 0 && rec < n)
-                            vdirect[ix] = make_float2(cr * tr - ci * ti, cr * ti + ci * tr);
-                    } else if ((lane & 7) == 0 && rec < n) {
-                        float2 *dst = acc + b0 + rec;
-                        float2 a = *dst;
-                        a.x += tr;
-                        a.y += ti;
-                        *dst = a;
-                    }
-                }
-            }
-        }
-    }
-}
-
 // MFMA degridder (predict) on one-cell buckets: the adjoint of
 // k_grid_mfma_pad's GEMM.  All records of a cell share their footprint
 // origin, so for 16 records of one cell
@@ -1995,7 +1230,9 @@ __global__ __launch_bounds__(64) void k_degrid_reg(Geo g, const VisRec *__restri
 // (vdirect), or the raw sum added to acc[record] for k_finalize.
 template <int W, bool WS, bool FI>
 __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restrict__ recs,
-                                                    ItemSrc src, const unsigned *__restrict__ offs,
+                                                    const Item *__restrict__ items,
+                                                    uint32_t n_items,
+                                                    const unsigned *__restrict__ offs,
                                                     const FineItem *__restrict__ fitems,
                                                     const float2 *__restrict__ grid, int p_lo,
                                                     int p_hi, float2 *__restrict__ acc,
@@ -2004,7 +1241,6 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
     constexpr int NQ = WS ? W : 1;
-    const uint32_t n_items = item_count(src);
     const uint32_t stride = item_stride(n_items);
     const int lane = threadIdx.x;
     const int r16 = lane & 15, kg = lane >> 4;
@@ -2022,7 +1258,7 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
             it = load_fine_item<kGroupCell>(fitems, w_it, n_items, stride, fo);
             if (it.b >= it.e) continue;
         } else {
-            it = load_item(src, w_it, n_items, stride);
+            it = load_item(items, w_it, n_items, stride);
             const unsigned *ob = offs + ((size_t)it.p0 * g.ntiles + (size_t)it.tile * kGroupCell);
 #pragma unroll
             for (int c = 0; c < kGroupCell; ++c) fo[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
@@ -2035,7 +1271,7 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
         // staged (both depend only on the item descriptor)
         uint32_t pf = it.b;
         VisRec nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
-        wave_sync_1w();  // previous item's reads of the region
+        wave_lds_sync();  // previous item's reads of the region
         for (int i = lane; i < NQ * PS; i += 64) {
             const int q = i / PS;
             const int p = (int)it.p0 + q;
@@ -2049,7 +1285,7 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                           ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
                           : make_float2(0.0f, 0.0f);
         }
-        wave_sync_1w();
+        wave_lds_sync();
 
         // the item's cells are consecutive, so the batch after [b0, b0 + 16)
         // starts at min(b0 + 16, re) -- in the next cell when this one ends;
@@ -2111,90 +1347,6 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                         *dst = v;
                     }
                 }
-            }
-        }
-    }
-}
-
-// Degridder: one wave per work item (an SX x SY-cell region: a 16x16 tile or
-// a group of kGroupFine 2x2 buckets).  The region's W planes are loaded into
-// LDS; per record, lane (kx, ky) reads its tap's W plane values, and a wave
-// reduction sums the footprint.
-template <int W, bool WS, int SX, int SY>
-__global__ __launch_bounds__(64) void k_degrid(Geo g, const VisRec *__restrict__ recs,
-                                               ItemSrc src,
-                                               const float2 *__restrict__ grid, int p_lo,
-                                               int p_hi, float2 *acc) {
-    extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    using TS = TileShape<W, SX, SY>;
-    constexpr int RX = TS::RX, RY = TS::RY, PS = TS::PLANE, PITCH = TS::PITCH;
-    constexpr int NQ = WS ? W : 1;
-    const uint32_t n_items = item_count(src);
-    const uint32_t stride = item_stride(n_items);
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        const Item it = load_item(src, w_it, n_items, stride);
-        const int ntg = g.nty / g.grp;
-        const int tx = (int)it.tile / ntg, tg = (int)it.tile - tx * ntg;
-        const int ibase = g.wx0 + tx * SX, jbase = g.wy0 + tg * SY;
-        const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
-        const int lane = threadIdx.x;
-        for (int i = lane; i < NQ * RX * RY; i += 64) {
-            const int q = i / (RX * RY);
-            const int p = (int)it.p0 + q;
-            const int rem = i - q * RX * RY;
-            const int xl = rem / RY, yl = rem - (rem / RY) * RY;
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            tile[q * PS + xl * PITCH + yl] =
-                (p >= p_lo && p < p_hi)
-                    ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
-                    : make_float2(0.0f, 0.0f);
-        }
-
-        const LaneRole<W> role(lane);
-        const float ihw = g.inv_half_w, bl = g.beta_l2e;
-        const int lane_off = role.kx * PITCH + role.ky - ibase * PITCH - jbase;
-        for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
-            const int n = (int)min(64u, it.e - b0);
-            const VisRec my = recs[b0 + min(lane, n - 1)];
-            float mine_r = 0.0f, mine_i = 0.0f;
-            for (int k = 0; k < n; ++k) {
-                const RecRegs rc = rec_at(my, k);
-                const float kval = role.taps(rc, ihw, bl);
-                const float ku = __shfl(kval, role.kx);
-                const float kv = __shfl(kval, W + role.ky);
-                const int off = lane_off + (int)(rc.ij & 0xffffu) * PITCH + (int)(rc.ij >> 16);
-                float kw[NQ];
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) kw[q] = WS ? lane_readf(kval, 2 * W + q) : 1.0f;
-                float sr = 0.0f, si = 0.0f;
-                if (role.act) {
-                    float2 a[NQ];
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) a[q] = tile[q * PS + off];
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        sr = fmaf(kw[q], a[q].x, sr);
-                        si = fmaf(kw[q], a[q].y, si);
-                    }
-                }
-                const float kk = role.act ? ku * kv : 0.0f;
-                sr *= kk;
-                si *= kk;
-                for (int o = 32; o > 0; o >>= 1) {
-                    sr += __shfl_xor(sr, o);
-                    si += __shfl_xor(si, o);
-                }
-                if (k == lane) {
-                    mine_r = sr;
-                    mine_i = si;
-                }
-            }
-            if (lane < n) {
-                atomicAdd(&acc[b0 + lane].x, mine_r);
-                atomicAdd(&acc[b0 + lane].y, mine_i);
             }
         }
     }
@@ -2405,13 +1557,11 @@ __global__ void k_zero_vis(int64_t nrow, int nchan, VT *vis, int64_t vrs, int64_
     for (int k = 0; k < oc.npv; ++k) vis[row * vrs + chan * vcs + k * oc.vps] = z;
 }
 
-// record factor and scatter back to visibility order; the record count is
-// read from device memory when `ndev` is given (pipelined plans)
+// record factor and scatter back to visibility order
 template <class VT>
-__global__ void k_finalize(int64_t nrec, const unsigned *__restrict__ ndev, int nchan,
+__global__ void k_finalize(int64_t n, int nchan,
                            const VisRec *__restrict__ recs, const float2 *__restrict__ acc, VT *vis,
                            int64_t vrs, int64_t vcs, int accumulate, OutConv oc) {
-    const int64_t n = ndev ? (int64_t)*ndev : nrec;
     for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
          r += (int64_t)gridDim.x * blockDim.x) {
         const VisRec rc = recs[r];
@@ -2579,20 +1729,17 @@ struct StageTimer {
     }
 };
 
-// One visibility part: a contiguous row range with its own buckets and work
-// items.  Its records occupy recs[vbase, vbase + nvis) of the call's record
-// array (positions are part-local offsets).
+// The visibilities' bucketing: histogram, offsets, work items and the
+// per-call metadata read back by the host.  Records occupy recs[0, nrec).
 struct Part {
-    int64_t r0 = 0, r1 = 0, vbase = 0, nvis = 0;
+    int64_t nvis = 0;
     unsigned *hist = nullptr, *offs = nullptr, *nch = nullptr, *ioffs = nullptr;
     unsigned long long *nbad = nullptr;
     unsigned *npad = nullptr;  // pad records of a 4-padded plan (device)
     Item *items = nullptr;
-    FineItem *fitems = nullptr;  // 16 per item when sub-sorted (k_subsort)
-    RecC *precs = nullptr;       // sub-sorted, 4-padded 16-B records (subpad plans)
-    FineItem *pfitems = nullptr;  // FineItems over precs
-    unsigned *meta = nullptr;  // device: see k_part_meta
-    // host copies (filled by read_part_meta; synchronous plans only)
+    FineItem *fitems = nullptr;  // 16 per coarse item when sub-sorted (k_subsort)
+    unsigned *meta = nullptr;    // device: see k_part_meta
+    // host copies (read_part_meta)
     int64_t nrec = 0, nitems = 0;
     std::vector<unsigned> p0_items;
 };
@@ -2600,19 +1747,14 @@ struct Part {
 struct Plan {
     Geo g;
     VisRec *recs = nullptr;
-    std::vector<Part> parts;
-    bool pipelined = false;          // row parts, persistent launches, no host syncs
-    bool aux_bucketing = false;      // bucketing on the auxiliary stream
-    bool subsort = false;            // 16x16 buckets re-ordered to 2x2 (register kernels)
-    bool cells = false;              // invert on k_grid_mfma: one-cell buckets / sub-sort
+    Part pt;
+    bool subsort = false;            // 16x16-cell buckets re-ordered by cell (k_subsort)
     bool pad4 = false;               // one-cell buckets padded to 4 records (k_grid_mfma_pad)
-    bool subpad = false;             // sub-sorted coarse items re-written 4-padded (k_grid_mfma_pad FI)
-    float2 *vdirect = nullptr;       // dirty2ms: register degridders write c64 vis in place
+    float2 *vdirect = nullptr;       // dirty2ms: the degridder writes c64 vis in place
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
     int row_lo = 0, row_hi = 0;      // grid rows (x) the visibilities reach
     unsigned chunk = kChunkMin;      // max records per work item
-    int64_t nrec = 0, nitems = 0;    // totals
     float2 *grid = nullptr;
     float2 *spec = nullptr;     // T[q][iy][kx]: transposed y-spectra (pruned FFT)
     float2 *spec_in = nullptr;  // band-only input of the backward x-FFT (zeros elsewhere)
@@ -2644,10 +1786,13 @@ struct Inputs {
 // Bytes of w planes kept resident per pass: SDP_HIP_GRID_BUDGET_GB if set,
 // else the device memory this call can still use -- free memory plus what the
 // workspace already holds for the planes and the records, less the records
-// and key/rank arrays still to be allocated (`need_other`) and a reserve of
-// 6 GiB.  A C2 invert keeps its 9 planes resident, and so does a C4 shard
-// (70 planes of 16384^2, 150 GB) on a 288 GB MI355X, gridding every record
-// once instead of once per plane chunk.
+// and key/rank arrays still to be allocated (`need_other`) and a reserve for
+// the caller: max(6 GiB, 1/16 of the device, 18 GB on a 288 GB MI355X), so
+// that the output arrays of the caller's next calls still fit beside the
+// planes the workspace keeps cached (a C4 shard keeps 150 GB of planes).  A
+// C2 invert keeps its 9 planes resident, and so does a C4 shard (70 planes of
+// 16384^2) on a 288 GB MI355X, gridding every record once instead of once
+// per plane chunk.
 static size_t grid_budget_bytes(size_t need_other) {
     const char *e = std::getenv("SDP_HIP_GRID_BUDGET_GB");
     if (e && std::atof(e) > 0) return (size_t)(std::atof(e) * 1073741824.0);
@@ -2655,22 +1800,12 @@ static size_t grid_budget_bytes(size_t need_other) {
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)8 << 30;
     Workspace &ws = Workspace::get();
     const size_t held_planes = ws.held("grid") + ws.held("spec") + ws.held("spec_in");
-    const size_t held_other = ws.held("recs") + ws.held("key_rank") + ws.held("degrid_acc") +
-                              ws.held("precs#0") + ws.held("pfitems#0");
+    const size_t held_other = ws.held("recs") + ws.held("key_rank") + ws.held("degrid_acc");
     const size_t avail = free_b + held_planes + held_other;
-    const size_t reserve = (size_t)6 << 30;
+    const size_t reserve = std::max<size_t>((size_t)6 << 30, total_b / 16);
     const size_t need = need_other + reserve;
     return avail > need ? avail - need : (size_t)1 << 30;
 }
-
-// SDP_HIP_PIPELINE: 0 (default) = bucket on the caller's stream; 1 = dirty2ms
-// buckets on an auxiliary stream under its screen + FFT; 2 = additionally
-// split the rows in two parts bucketed on the auxiliary stream while the
-// previous part (de)grids, with persistent launches reading the device-side
-// item counts.  Both overlaps measured slower on C2: the
-// bucketing is memory/atomic bound and contends with the FFT, and the row
-// halves add 24% work items.
-constexpr int kPipelineParts = 2;
 
 static hipStream_t aux_stream() {
     static std::mutex mu;
@@ -2729,23 +1864,45 @@ struct KeptBuckets {
     Plan P;
 };
 
+// The resident planes of a batched invert between its FIRST and LAST batch:
+// the workspace generation and plane buffer they live in, the geometry and
+// the bounds.  A later batch must match it; any other wstack call (a fresh
+// non-batched plan) or a workspace release invalidates it, so a batch that
+// would accumulate into planes another call has overwritten or freed is
+// refused instead of gridding into them.
+struct BatchSeq {
+    bool valid = false;
+    uint64_t gen = 0;
+    const void *grid = nullptr;
+    int nx = 0, ny = 0, do_w = 0, nplanes = 0;
+    double px = 0, py = 0, eps = 0;
+    unsigned flip = 0;
+    double b[6] = {0, 0, 0, 0, 0, 0};
+};
+
 static std::mutex g_kept_mu;
 static std::map<int, KeptBuckets> g_kept;
+static std::map<int, BatchSeq> g_batch;
 
-static KeptBuckets &kept_buckets() {
+static int cur_device() {
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
-    return g_kept[dev];
+    return dev;
 }
 
 static void drop_kept_buckets() {
     std::lock_guard<std::mutex> lk(g_kept_mu);
-    kept_buckets().valid = false;
+    g_kept[cur_device()].valid = false;
+}
+
+static void drop_batch_seq() {
+    std::lock_guard<std::mutex> lk(g_kept_mu);
+    g_batch[cur_device()].valid = false;
 }
 
 static void keep_buckets(const Plan &P, const Inputs &in) {
     std::lock_guard<std::mutex> lk(g_kept_mu);
-    KeptBuckets &k = kept_buckets();
+    KeptBuckets &k = g_kept[cur_device()];
     k.valid = true;
     k.gen = Workspace::get().generation();
     k.uvw = in.uvw;
@@ -2765,7 +1922,7 @@ static void keep_buckets(const Plan &P, const Inputs &in) {
 
 static Plan reuse_buckets(const Inputs &in) {
     std::lock_guard<std::mutex> lk(g_kept_mu);
-    const KeptBuckets &k = kept_buckets();
+    const KeptBuckets &k = g_kept[cur_device()];
     SDP_REQUIRE(k.valid && k.gen == Workspace::get().generation(),
                 "SDP_HIP_REUSE_BUCKETS: no kept bucketing (another wstack call or a workspace "
                 "release came in between)");
@@ -2778,9 +1935,45 @@ static Plan reuse_buckets(const Inputs &in) {
     return k.P;
 }
 
+static BatchSeq batch_token(const Plan &P, const Inputs &in) {
+    BatchSeq s;
+    s.valid = true;
+    s.gen = Workspace::get().generation();
+    s.grid = P.grid;
+    s.nx = in.nx;
+    s.ny = in.ny;
+    s.do_w = in.do_w;
+    s.nplanes = P.g.nplanes;
+    s.px = in.px;
+    s.py = in.py;
+    s.eps = in.eps;
+    s.flip = in.flags & SDP_HIP_FLIP_UW;
+    for (int k = 0; k < 6; ++k) s.b[k] = in.bounds[k];
+    return s;
+}
+
+static void check_batch_seq(const Plan &P, const Inputs &in, bool first) {
+    std::lock_guard<std::mutex> lk(g_kept_mu);
+    BatchSeq &cur = g_batch[cur_device()];
+    const BatchSeq t = batch_token(P, in);
+    if (first) {
+        cur = t;
+        return;
+    }
+    SDP_REQUIRE(cur.valid && cur.gen == t.gen && cur.grid == t.grid,
+                "batched invert: no resident planes of this sequence (its first batch did not "
+                "run, or another wstack call or a workspace release came in between)");
+    bool same = cur.nx == t.nx && cur.ny == t.ny && cur.do_w == t.do_w &&
+                cur.nplanes == t.nplanes && cur.px == t.px && cur.py == t.py &&
+                cur.eps == t.eps && cur.flip == t.flip;
+    for (int k = 0; k < 6; ++k) same = same && cur.b[k] == t.b[k];
+    SDP_REQUIRE(same, "batched invert: every batch of a sequence needs the geometry, epsilon, "
+                      "flags and bounds of its first batch");
+}
+
 // Geometry shared by both directions: kernel, padded grid, w planes, bucket
-// granularity, row band, plane chunking, part split.  One host sync (uvw and
-// frequency extremes).
+// granularity, row band, plane chunking.  One host sync (uvw and frequency
+// extremes) unless the bounds are given.
 static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     SDP_REQUIRE(in.nx > 0 && in.ny > 0 && in.nx % 2 == 0 && in.ny % 2 == 0,
                 "npix_x and npix_y must be positive and even");
@@ -2789,6 +1982,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     SDP_REQUIRE(in.nrow * (int64_t)in.nchan < (int64_t)0xffffffffll,
                 "more than 2^32 visibilities per call");
     drop_kept_buckets();  // a fresh plan re-uses the bucketing scratch
+    if (!in.bounds) drop_batch_seq();  // and may overwrite a batch sequence's planes
     Plan P;
     Geo &g = P.g;
     g.W = kernel_support(in.eps);
@@ -2805,7 +1999,6 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.su = (in.flags & SDP_HIP_FLIP_UW) ? -1.0 : 1.0;
     g.nchan = in.nchan;
     g.nrow = in.nrow;
-    g.dbg = std::getenv("SDP_HIP_DBG") ? std::atoi(std::getenv("SDP_HIP_DBG")) : 0;
 
     // uvw and frequency extremes (device) -> host, or the batch sequence's
     double *hb = pinned_host<double>(0, 6);
@@ -2860,49 +2053,36 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         g.nplanes = 1;
         g.nps = 1;
     }
-    // bucket window (origins only: the footprints' halo may leave it)
+    // bucket window (origins only: the footprints' halo may leave it).  x
+    // (rows) only: the y stride stays ngy, since a compacted y range packs the
+    // hot histogram counters of the uv core closer together and measured 2x
+    // slower count-pass atomics on C2
     {
-        const double amax = umax * in.px * g.ngx, bmax = vmax * in.py * g.ngy;
-        auto window = [&](double m, int ng, int &w0, int &wn) {
-            const int reach = (int)std::ceil(m + 0.5 * g.W) + 2;
-            int lo = (ng / 2 - reach) & ~(kGridAlign - 1);
-            int hi = ((ng / 2 + reach + kGridAlign - 1) / kGridAlign) * kGridAlign;
-            if (lo <= 0 || hi >= ng || env_int("SDP_HIP_NO_WINDOW", 0)) {
-                lo = 0;
-                hi = ng;
-            }
-            w0 = lo;
-            wn = hi - lo;
-        };
-        // x (rows) only: the y stride stays ngy, since a compacted y range
-        // packs the hot histogram counters of the uv core closer together
-        // and measured 2x slower count-pass atomics on C2
-        (void)bmax;
-        window(amax, g.ngx, g.wx0, g.wnx);
+        const double amax = umax * in.px * g.ngx;
+        const int reach = (int)std::ceil(amax + 0.5 * g.W) + 2;
+        int lo = (g.ngx / 2 - reach) & ~(kGridAlign - 1);
+        int hi = ((g.ngx / 2 + reach + kGridAlign - 1) / kGridAlign) * kGridAlign;
+        if (lo <= 0 || hi >= g.ngx) {
+            lo = 0;
+            hi = g.ngx;
+        }
+        g.wx0 = lo;
+        g.wnx = hi - lo;
         g.wy0 = 0;
         g.wny = g.ngy;
     }
-    // bucket granularity.  Invert: one-cell buckets for the MFMA gridder
-    // while the dense (first plane, cell) histogram stays below kMaxCellKeys
-    // (SDP_HIP_MFMA=0: the register gridder's 2x2-cell buckets).  Predict:
-    // 2x2-cell buckets for the register degridder below kMaxFineKeys.  Else
-    // 16x16-cell buckets (sub-sorted to cells / 2x2 buckets below, or the
-    // LDS-tile kernels).
+    // bucket granularity: one-cell buckets while the dense (first plane, cell)
+    // histogram stays below kMaxCellKeys (C2: 115 M keys), else 16x16-cell
+    // buckets sub-sorted by cell per work item (C4's 16384^2 x 70 planes);
+    // SDP_HIP_BUCKET=16 forces the latter (tests of the large-grid path)
     {
-        const char *e = std::getenv("SDP_HIP_BUCKET");
-        const char *m = std::getenv("SDP_HIP_MFMA");
-        // predict: SDP_HIP_MFMA_DEGRID=0 keeps the register degridder
-        P.cells = !(m && std::atoi(m) == 0) &&
-                  (grid_mode || env_int("SDP_HIP_MFMA_DEGRID", 1) != 0);
         const int64_t cell = (int64_t)g.wnx * g.wny * g.nps;
-        const int64_t fine = (int64_t)(g.wnx / kTileFine) * (g.wny / kTileFine) * g.nps;
-        if (P.cells) g.sub = cell <= kMaxCellKeys ? kTileCell : kTileCoarse;
-        else g.sub = fine <= kMaxFineKeys ? kTileFine : kTileCoarse;
-        if (e && std::atoi(e) == kTileCoarse) g.sub = kTileCoarse;
+        g.sub = cell <= kMaxCellKeys ? kTileCell : kTileCoarse;
+        if (env_int("SDP_HIP_BUCKET", 0) == kTileCoarse) g.sub = kTileCoarse;
     }
     g.nty = g.wny / g.sub;
     g.ntiles = (g.wnx / g.sub) * g.nty;
-    g.grp = g.sub == kTileCell ? kGroupCell : (g.sub == kTileFine ? kGroupFine : 1);
+    g.grp = g.sub == kTileCell ? kGroupCell : 1;
     g.salt = 1;
     if (g.sub == kTileCoarse) {
         const int sv = env_int("SDP_HIP_SALT", 4);
@@ -2933,21 +2113,12 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     if (const char *e = std::getenv("SDP_HIP_FFT_PLANES"))  // tests: force small batches
         if (std::atoi(e) > 0) P.fft_planes = std::atoi(e);
     P.fft_planes = std::min(P.fft_planes, g.nplanes);
-    const int64_t nvis_all = in.nrow * (int64_t)in.nchan;
+    const int64_t nvis = in.nrow * (int64_t)in.nchan;
     const size_t need_other =
-        (size_t)nvis_all * (sizeof(VisRec) + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2))) +
+        (size_t)nvis * (sizeof(VisRec) + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2))) +
         (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned) +
         (size_t)P.fft_planes * spec_plane;
-    int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
-    // large-grid inverts: the sub-sorted records re-written 4-padded as 16-B
-    // records (~21 B per visibility with the pads) when that costs no plane
-    // residency (SDP_HIP_SUBSORT_PAD=0: never)
-    if (grid_mode && P.cells && g.sub == kTileCoarse && env_int("SDP_HIP_SUBSORT_PAD", 0) != 0 &&
-        !P.aux_bucketing) {
-        const size_t need_pad = need_other + (size_t)nvis_all * 21;
-        const int cpp = (int)std::max<size_t>(1, grid_budget_bytes(need_pad) / grid_plane);
-        if (std::min(cpp, g.nplanes) >= std::min(cp, g.nplanes)) P.subpad = true;
-    }
+    const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
     P.chunk_planes = std::min(cp, g.nplanes);
     P.fft_planes = std::min(P.fft_planes, P.chunk_planes);
     P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy);
@@ -2956,69 +2127,43 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
 
     // records per item: large enough to amortise the tile flush over dense
     // tiles, small enough to leave >= ~16k items for the 256 CUs
-    const int64_t nvis = in.nrow * (int64_t)in.nchan;
     P.chunk = (unsigned)std::min<int64_t>(kChunkMax, std::max<int64_t>(kChunkMin, nvis / 16384));
     if (const char *e = std::getenv("SDP_HIP_CHUNK"))
         if (std::atoi(e) >= 64) P.chunk = (unsigned)std::atoi(e);
-
-    // part split
-    const char *pe = std::getenv("SDP_HIP_PIPELINE");
-    const int pmode = pe ? std::atoi(pe) : 0;
-    P.pipelined = pmode == 2 && (g.sub == kTileFine || g.sub == kTileCell) &&
-                  P.chunk_planes == g.nplanes && in.nrow >= 2 &&
-                  !(in.flags & SDP_HIP_KEEP_BUCKETS);
-    P.aux_bucketing = P.pipelined || (pmode == 1 && !grid_mode);
-    const int nparts = P.pipelined ? kPipelineParts : 1;
-    for (int i = 0; i < nparts; ++i) {
-        Part pt;
-        pt.r0 = in.nrow * i / nparts;
-        pt.r1 = in.nrow * (i + 1) / nparts;
-        pt.vbase = pt.r0 * in.nchan;
-        pt.nvis = (pt.r1 - pt.r0) * in.nchan;
-        P.parts.push_back(pt);
-    }
-    // large grids: re-order the 16x16 buckets by 2x2 bucket for the register
-    // kernels (SDP_HIP_SUBSORT=0 keeps the LDS-tile kernels)
-    {
-        const char *e = std::getenv("SDP_HIP_SUBSORT");
-        P.subsort = g.sub == kTileCoarse && !P.aux_bucketing && !(e && std::atoi(e) == 0);
-        if (P.subsort) P.chunk = std::min<unsigned>(P.chunk, kSubChunk);
-        P.subpad = P.subpad && P.subsort;
-    }
-    // one-cell buckets padded to multiples of 4 records (k_grid_mfma_pad);
-    // SDP_HIP_PAD4=0 keeps the unpadded run-walking k_grid_mfma.  The padded
-    // record count is read back before the scatter (one host sync), so the
-    // host-sync-free pipelined plans stay unpadded.
-    P.pad4 = grid_mode && P.cells && g.sub == kTileCell && !P.aux_bucketing &&
-             env_int("SDP_HIP_PAD4", 1) != 0;
+    // large grids: the 16x16-cell items are re-ordered by cell (k_subsort)
+    P.subsort = g.sub == kTileCoarse;
+    if (P.subsort) P.chunk = std::min<unsigned>(P.chunk, kSubChunk);
+    // invert on one-cell buckets: every cell padded to a multiple of 4 records
+    // (k_grid_mfma_pad); the padded record count is read back before the
+    // scatter (one host sync)
+    P.pad4 = grid_mode && g.sub == kTileCell;
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
+    P.pt.nvis = nvis;
     P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
     return P;
 }
 
-// Bucketing of one part on stream `st` (no host sync): histogram with ranks,
-// scan, scatter of the 32-byte records, work items, part metadata.
-static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipStream_t st,
+// Bucketing (no host sync except the 4-padded record total): histogram with
+// ranks, scan, scatter of the records, work items, metadata.
+static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st,
                         bool values_only = false) {
     const Geo &g = P.g;
-    Part &pt = P.parts[ip];
-    const std::string sfx = "#" + std::to_string(ip);
+    Part &pt = P.pt;
     const size_t nkeys = (size_t)g.ntiles * g.nps * g.salt;
     const int kpg = g.grp * g.salt;  // keys per work-item group
     const int64_t ngroups = (int64_t)nkeys / kpg;
     const int gpp = g.ntiles / g.grp;  // groups per first-plane value
-    pt.hist = scratch<unsigned>("hist" + sfx, nkeys + 1);
-    pt.offs = scratch<unsigned>("offs" + sfx, nkeys + 1);
-    pt.nch = scratch<unsigned>("nch" + sfx, ngroups + 1);
-    pt.ioffs = scratch<unsigned>("ioffs" + sfx, ngroups + 1);
-    pt.nbad = scratch<unsigned long long>("nbad" + sfx, 1);
-    pt.meta = scratch<unsigned>("meta" + sfx, g.nps + 5);
+    pt.hist = scratch<unsigned>("hist", nkeys + 1);
+    pt.offs = scratch<unsigned>("offs", nkeys + 1);
+    pt.nch = scratch<unsigned>("nch", ngroups + 1);
+    pt.ioffs = scratch<unsigned>("ioffs", ngroups + 1);
+    pt.nbad = scratch<unsigned long long>("nbad", 1);
+    pt.meta = scratch<unsigned>("meta", g.nps + 5);
     const int64_t icap = std::min<int64_t>(ngroups, pt.nvis) + pt.nvis / P.chunk + 1;
-    pt.items = scratch<Item>("items" + sfx, icap);
-    unsigned *kr = scratch<unsigned>("key_rank", std::max<int64_t>(in.nrow * (int64_t)in.nchan, 1)) +
-                pt.vbase;
-    if (!values_only) SDP_HIP_CHECK(hipMemsetAsync(pt.hist, 0, (nkeys + 1) * sizeof(unsigned), st));
+    pt.items = scratch<Item>("items", icap);
+    unsigned *kr = scratch<unsigned>("key_rank", std::max<int64_t>(pt.nvis, 1));
     if (!values_only) {
+        SDP_HIP_CHECK(hipMemsetAsync(pt.hist, 0, (nkeys + 1) * sizeof(unsigned), st));
         SDP_HIP_CHECK(hipMemsetAsync(pt.nbad, 0, sizeof(unsigned long long), st));
         SDP_HIP_CHECK(hipMemsetAsync(pt.nch + ngroups, 0, sizeof(unsigned), st));
     }
@@ -3028,33 +2173,33 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     // weight sums: in the count pass, or in the value pass of a reused plan
     auto launch_bucket = [&](auto scatter_tag, unsigned *counter) {
         constexpr bool S = decltype(scatter_tag)::value;
-        VisRec *out = S ? P.recs + pt.vbase : nullptr;
+        VisRec *out = S ? P.recs : nullptr;
         double *sl = S == values_only ? slots : nullptr;
         if (in.vis_dtype == SDP_HIP_C128) {
             if (grid_mode && S && P.pad4)  // 16-byte RecC records
                 k_bucket<double2, S, true, true><<<nb, 256, 0, st>>>(
-                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
+                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
                     in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
             else if (grid_mode)
                 k_bucket<double2, S, true><<<nb, 256, 0, st>>>(
-                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
+                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
                     in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
             else
                 k_bucket<double2, S, false><<<nb, 256, 0, st>>>(
-                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
+                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
                     in.wcs, in.x, sl, counter, kr, out, pt.nbad);
         } else {
             if (grid_mode && S && P.pad4)  // 16-byte RecC records
                 k_bucket<float2, S, true, true><<<nb, 256, 0, st>>>(
-                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
+                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
                     in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
             else if (grid_mode)
                 k_bucket<float2, S, true><<<nb, 256, 0, st>>>(
-                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
+                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
                     in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
             else
                 k_bucket<float2, S, false><<<nb, 256, 0, st>>>(
-                    g, pt.r0, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
+                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
                     in.wcs, in.x, sl, counter, kr, out, pt.nbad);
         }
     };
@@ -3067,7 +2212,7 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     size_t tmp_bytes = 0;
     SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, pt.hist, pt.offs,
                                                    (int)(nkeys + 1), st));
-    void *tmp = scratch<char>("scan_tmp" + sfx, tmp_bytes + 16);
+    void *tmp = scratch<char>("scan_tmp", tmp_bytes + 16);
     size_t tb = tmp_bytes + 16;
     if (P.pad4) {
         // scan of the counts rounded up to 4, then the padded total sizes
@@ -3078,7 +2223,7 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
                                                        (int)(nkeys + 1), st));
         if (need > tmp_bytes) {
             tmp_bytes = need;
-            tmp = scratch<char>("scan_tmp" + sfx, tmp_bytes + 16);
+            tmp = scratch<char>("scan_tmp", tmp_bytes + 16);
         }
         tb = tmp_bytes + 16;
         SDP_HIP_CHECK(
@@ -3087,7 +2232,6 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
         SDP_HIP_CHECK(hipMemcpyAsync(htot, pt.offs + nkeys, sizeof(unsigned),
                                      hipMemcpyDeviceToHost, st));
         SDP_HIP_CHECK(hipStreamSynchronize(st));
-        SDP_REQUIRE(P.parts.size() == 1, "4-padded bucketing runs on one part");
         P.recs = scratch<VisRec>("recs", ((int64_t)*htot + 1) / 2 + 1);  // RecC records
     } else {
         SDP_HIP_CHECK(
@@ -3096,7 +2240,7 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
     if (pt.nvis > 0) launch_bucket(std::true_type{}, pt.offs);
     if (P.pad4) {
         unsigned *pslots = scratch<unsigned>("pad_slots", kSumSlots);
-        pt.npad = scratch<unsigned>("npad" + sfx, 1);
+        pt.npad = scratch<unsigned>("npad", 1);
         SDP_HIP_CHECK(hipMemsetAsync(pslots, 0, kSumSlots * sizeof(unsigned), st));
         k_pad_cells<<<grid1d((int64_t)nkeys, 256), 256, 0, st>>>(
             (unsigned)nkeys, pt.hist, pt.offs, reinterpret_cast<RecC *>(P.recs), pslots);
@@ -3110,305 +2254,93 @@ static void bucket_part(Plan &P, int ip, const Inputs &in, bool grid_mode, hipSt
         hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.nch, pt.ioffs, (int)(ngroups + 1), st));
     k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, kpg, gpp, pt.offs, pt.ioffs,
                                                        P.chunk, pt.items);
-    k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys, pt.npad, pt.ioffs, gpp,
+    k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys,
+                                                      P.pad4 ? pt.npad : nullptr, pt.ioffs, gpp,
                                                       g.nps, pt.meta);
     SDP_HIP_CHECK(hipGetLastError());
 }
 
-// Host copy of every part's metadata (one sync): counts, the first-plane item
+// Host copy of the metadata (one sync): counts, the first-plane item
 // offsets (plane-chunked launches need them) and the out-of-grid check.
 static void read_part_meta(Plan &P, hipStream_t st) {
     const int nps = P.g.nps;
     const size_t per = (size_t)nps + 5;
-    unsigned *hm = pinned_host<unsigned>(64, per * P.parts.size());
-    for (size_t i = 0; i < P.parts.size(); ++i)
-        SDP_HIP_CHECK(hipMemcpyAsync(hm + i * per, P.parts[i].meta, per * sizeof(unsigned),
-                                     hipMemcpyDeviceToHost, st));
+    unsigned *m = pinned_host<unsigned>(64, per);
+    SDP_HIP_CHECK(hipMemcpyAsync(m, P.pt.meta, per * sizeof(unsigned), hipMemcpyDeviceToHost, st));
     SDP_HIP_CHECK(hipStreamSynchronize(st));
-    P.nrec = P.nitems = 0;
-    for (size_t i = 0; i < P.parts.size(); ++i) {
-        const unsigned *m = hm + i * per;
-        const unsigned long long nbad = (unsigned long long)m[0] | ((unsigned long long)m[1] << 32);
-        SDP_REQUIRE(nbad == 0, "visibilities outside the padded grid");
-        Part &pt = P.parts[i];
-        pt.nrec = m[2];
-        pt.nitems = m[3];
-        pt.p0_items.assign(m + 4, m + 4 + nps + 1);
-        P.nrec += pt.nrec;
-        P.nitems += pt.nitems;
-    }
+    const unsigned long long nbad = (unsigned long long)m[0] | ((unsigned long long)m[1] << 32);
+    SDP_REQUIRE(nbad == 0,
+                "visibilities outside the padded grid (or, in a batched invert, outside the "
+                "sequence's bounds)");
+    Part &pt = P.pt;
+    pt.nrec = m[2];
+    pt.nitems = m[3];
+    pt.p0_items.assign(m + 4, m + 4 + nps + 1);
 }
 
-// Item range of a part whose W-plane windows intersect planes [p_lo, p_hi).
-static std::pair<unsigned, unsigned> chunk_items(const Plan &P, const Part &pt, int p_lo,
-                                                 int p_hi) {
+// Item range whose W-plane windows intersect planes [p_lo, p_hi).
+static std::pair<unsigned, unsigned> chunk_items(const Plan &P, int p_lo, int p_hi) {
     const int a = std::max(0, p_lo - (P.g.do_w ? P.g.W : 1) + 1);
     const int b = std::min(P.g.nps - 1, p_hi - 1);
     if (a > b) return {0u, 0u};
-    return {pt.p0_items[a], pt.p0_items[b + 1]};
-}
-
-// Launch shape of one gridding pass over a part: one workgroup per item when
-// the host knows the range, else a persistent grid reading the count.
-struct Launch {
-    ItemSrc src;
-    unsigned blocks;
-};
-
-static unsigned persistent_blocks(const void *fn, int threads, size_t lds) {
-    static std::mutex mu;
-    static std::map<std::pair<const void *, size_t>, unsigned> cache;
-    std::lock_guard<std::mutex> lk(mu);
-    auto key = std::make_pair(fn, lds);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    int dev = 0, ncu = 0, per = 0;
-    SDP_HIP_CHECK(hipGetDevice(&dev));
-    SDP_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    SDP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds));
-    unsigned nb = (unsigned)std::max(1, ncu * std::max(1, per));
-    if (const char *e = std::getenv("SDP_HIP_PBLOCKS")) nb = (unsigned)std::max(1, std::atoi(e));
-    else nb *= 8;  // several workgroups per slot: the hardware balances the uneven items
-    cache[key] = nb;
-    return nb;
-}
-
-static Launch part_launch(const Plan &P, const Part &pt, int p_lo, int p_hi, const void *fn,
-                          int threads, size_t lds) {
-    Launch L;
-    if (P.pipelined) {
-        L.src = ItemSrc{pt.items, 0u, pt.meta + 3};
-        L.blocks = persistent_blocks(fn, threads, lds);
-    } else {
-        const auto r = chunk_items(P, pt, p_lo, p_hi);
-        L.src = ItemSrc{pt.items + r.first, r.second - r.first, nullptr};
-        L.blocks = r.second - r.first;
-    }
-    return L;
-}
-
-static void allow_lds(const void *fn, size_t bytes) {
-    if (bytes > 65536)
-        SDP_HIP_CHECK(
-            hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-}
-
-// waves per gridding workgroup (planes split across them); SDP_HIP_GRID_WAVES
-// overrides the default for experiments
-static int grid_waves(int W, bool do_w) {
-    if (!do_w) return 1;
-    const char *e = std::getenv("SDP_HIP_GRID_WAVES");
-    const int v = e ? std::atoi(e) : 2;
-    return (v == 1 || v == 2 || v == 4) && v <= W ? v : 2;
-}
-
-template <int W, bool WS, int NWV>
-static void launch_grid_n(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
-    constexpr int NQ = WS ? W : 1;
-    const size_t lds = (size_t)((NQ + NWV - 1) / NWV * NWV) *
-                       TileShape<W, kTileCoarse>::PLANE * sizeof(float2);
-    const void *fn = (const void *)k_grid_lds<W, WS, NWV>;
-    allow_lds(fn, lds);
-    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64 * NWV, lds);
-    if (L.blocks == 0) return;
-    k_grid_lds<W, WS, NWV><<<L.blocks, 64 * NWV, lds, st>>>(P.g, P.recs + pt.vbase, L.src,
-                                                          (float *)P.grid, p_lo, p_hi);
+    return {P.pt.p0_items[a], P.pt.p0_items[b + 1]};
 }
 
 template <int W, bool WS>
-static void launch_grid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) *
-                       TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
-    const void *fn = (const void *)k_grid_reg<W, WS, false>;
-    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
-    if (L.blocks == 0) return;
-    k_grid_reg<W, WS, false><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
-                                                       nullptr, (float *)P.grid, p_lo, p_hi,
-                                                       P.g.dbg);
-}
-
-// The register kernels' view of a sub-sorted coarse plan: 2x2-cell buckets
-// in groups of kGroupFine (the work items carry their bucket offsets).
-static Geo fine_view(const Geo &g) {
-    Geo f = g;
-    f.sub = kTileFine;
-    f.nty = g.wny / kTileFine;
-    f.ntiles = (g.wnx / kTileFine) * f.nty;
-    f.grp = kGroupFine;
-    return f;
-}
-
-template <int W, bool WS>
-static void launch_grid_fine_items(const Plan &P, const Part &pt, int p_lo, int p_hi,
-                                   hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) *
-                       TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
-    const auto r = chunk_items(P, pt, p_lo, p_hi);
-    const unsigned n = 16u * (r.second - r.first);
-    if (n == 0) return;
-    k_grid_reg<W, WS, true><<<n, 64, lds, st>>>(fine_view(P.g), P.recs + pt.vbase,
-                                                ItemSrc{nullptr, n, nullptr}, nullptr,
-                                                pt.fitems + 16 * (size_t)r.first, (float *)P.grid,
-                                                p_lo, p_hi, P.g.dbg);
-}
-
-template <int W, bool WS>
-static void launch_degrid_fine_items(const Plan &P, const Part &pt, int p_lo, int p_hi,
-                                     float2 *acc, hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) *
-                       TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
-    const auto r = chunk_items(P, pt, p_lo, p_hi);
-    const unsigned n = 16u * (r.second - r.first);
-    if (n == 0) return;
-    k_degrid_reg<W, WS, true><<<n, 64, lds, st>>>(fine_view(P.g), P.recs + pt.vbase,
-                                                  ItemSrc{nullptr, n, nullptr}, nullptr,
-                                                  pt.fitems + 16 * (size_t)r.first, P.grid, p_lo,
-                                                  p_hi, acc + pt.vbase, P.vdirect);
-}
-
-template <int W, bool WS>
-static void launch_grid_mfma(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
+static void launch_grid_mfma_fi(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) * (2 + W - 1) * (8 + W - 1) * sizeof(float2) +
                        128 * sizeof(float4);
-    if (P.subsort) {
-        const auto r = chunk_items(P, pt, p_lo, p_hi);
-        const unsigned n = 16u * (r.second - r.first);
-        if (n == 0) return;
-        k_grid_mfma<W, WS, true><<<n, 64, lds, st>>>(P.g, P.recs + pt.vbase,
-                                                     ItemSrc{nullptr, n, nullptr}, nullptr,
-                                                     pt.fitems + 16 * (size_t)r.first,
-                                                     (float *)P.grid, p_lo, p_hi);
-        return;
-    }
-    const void *fn = (const void *)k_grid_mfma<W, WS, false>;
-    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
-    if (L.blocks == 0) return;
-    // SDP_HIP_DBG & 32 (timing experiment): an empty plane range skips the flush
-    const int ph = (P.g.dbg & 32) ? p_lo : p_hi;
-    k_grid_mfma<W, WS, false><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
-                                                        nullptr, (float *)P.grid, p_lo, ph);
-}
-
-template <int W, bool WS>
-static void launch_grid_mfma_pad(const Plan &P, const Part &pt, int p_lo, int p_hi,
-                                 hipStream_t st) {
-    constexpr size_t lds = grid_mfma_pad_lds<W, WS>();
-    const void *fn = (const void *)k_grid_mfma_pad<W, WS>;
-    Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
-    if (L.blocks == 0) return;
-    const int ph = (P.g.dbg & 32) ? p_lo : p_hi;  // SDP_HIP_DBG & 32: no flush (timing)
-    k_grid_mfma_pad<W, WS><<<L.blocks, 64, lds, st>>>(
-        P.g, reinterpret_cast<const RecC *>(P.recs) + pt.vbase, L.src, pt.offs, nullptr,
-        (float *)P.grid, p_lo, ph);
-}
-
-template <int W, bool WS>
-static void launch_grid_mfma_pad_fi(const Plan &P, const Part &pt, int p_lo, int p_hi,
-                                    hipStream_t st) {
-    constexpr size_t lds = grid_mfma_pad_lds<W, WS>();
-    const auto r = chunk_items(P, pt, p_lo, p_hi);
+    const auto r = chunk_items(P, p_lo, p_hi);
     const unsigned n = 16u * (r.second - r.first);
     if (n == 0) return;
-    k_grid_mfma_pad<W, WS, true><<<n, 64, lds, st>>>(
-        P.g, pt.precs, ItemSrc{nullptr, n, nullptr}, nullptr, pt.pfitems + 16 * (size_t)r.first,
-        (float *)P.grid, p_lo, p_hi);
+    k_grid_mfma<W, WS><<<n, 64, lds, st>>>(P.g, P.recs, n, P.pt.fitems + 16 * (size_t)r.first,
+                                           (float *)P.grid, p_lo, p_hi);
+}
+
+template <int W, bool WS>
+static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
+    constexpr size_t lds = grid_mfma_pad_lds<W, WS>();
+    const auto r = chunk_items(P, p_lo, p_hi);
+    const unsigned n = r.second - r.first;
+    if (n == 0) return;
+    k_grid_mfma_pad<W, WS><<<n, 64, lds, st>>>(P.g, reinterpret_cast<const RecC *>(P.recs),
+                                               P.pt.items + r.first, n, P.pt.offs,
+                                               (float *)P.grid, p_lo, p_hi);
 }
 
 template <int W>
-static void launch_grid(const Plan &P, const Part &pt, int p_lo, int p_hi, hipStream_t st) {
-    if (P.subpad) {
-        if (P.g.do_w) return launch_grid_mfma_pad_fi<W, true>(P, pt, p_lo, p_hi, st);
-        return launch_grid_mfma_pad_fi<W, false>(P, pt, p_lo, p_hi, st);
-    }
+static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
     if (P.pad4) {
-        if (P.g.do_w) return launch_grid_mfma_pad<W, true>(P, pt, p_lo, p_hi, st);
-        return launch_grid_mfma_pad<W, false>(P, pt, p_lo, p_hi, st);
+        if (P.g.do_w) return launch_grid_mfma_pad<W, true>(P, p_lo, p_hi, st);
+        return launch_grid_mfma_pad<W, false>(P, p_lo, p_hi, st);
     }
-    if (P.cells && (P.subsort || P.g.sub == kTileCell)) {
-        if (P.g.do_w) return launch_grid_mfma<W, true>(P, pt, p_lo, p_hi, st);
-        return launch_grid_mfma<W, false>(P, pt, p_lo, p_hi, st);
-    }
-    if (P.subsort) {
-        if (P.g.do_w) return launch_grid_fine_items<W, true>(P, pt, p_lo, p_hi, st);
-        return launch_grid_fine_items<W, false>(P, pt, p_lo, p_hi, st);
-    }
-    if (P.g.sub == kTileFine) {
-        if (P.g.do_w) return launch_grid_reg<W, true>(P, pt, p_lo, p_hi, st);
-        return launch_grid_reg<W, false>(P, pt, p_lo, p_hi, st);
-    }
-    if (!P.g.do_w) return launch_grid_n<W, false, 1>(P, pt, p_lo, p_hi, st);
-    switch (grid_waves(W, true)) {
-        case 1: return launch_grid_n<W, true, 1>(P, pt, p_lo, p_hi, st);
-        case 4: return launch_grid_n<W, true, (W >= 4 ? 4 : 2)>(P, pt, p_lo, p_hi, st);
-        default: return launch_grid_n<W, true, 2>(P, pt, p_lo, p_hi, st);
-    }
-}
-
-template <int W, bool WS, int SX, int SY>
-static void launch_degrid_n(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
-                            hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) * TileShape<W, SX, SY>::PLANE * sizeof(float2);
-    const void *fn = (const void *)k_degrid<W, WS, SX, SY>;
-    allow_lds(fn, lds);
-    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
-    if (L.blocks == 0) return;
-    k_degrid<W, WS, SX, SY><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, P.grid,
-                                                      p_lo, p_hi, acc + pt.vbase);
+    if (P.g.do_w) return launch_grid_mfma_fi<W, true>(P, p_lo, p_hi, st);
+    return launch_grid_mfma_fi<W, false>(P, p_lo, p_hi, st);
 }
 
 template <int W, bool WS>
-static void launch_degrid_reg(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
-                              hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) *
-                       TileShape<W, kTileFine, kTileFine * kGroupFine>::PLANE * sizeof(float2);
-    const void *fn = (const void *)k_degrid_reg<W, WS, false>;
-    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
-    if (L.blocks == 0) return;
-    k_degrid_reg<W, WS, false><<<L.blocks, 64, lds, st>>>(P.g, P.recs + pt.vbase, L.src, pt.offs,
-                                                         nullptr, P.grid, p_lo, p_hi,
-                                                         acc + pt.vbase, P.vdirect);
-}
-
-template <int W, bool WS>
-static void launch_degrid_mfma(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
-                               hipStream_t st) {
+static void launch_degrid_mfma(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) * (2 + W - 1) * (8 + W - 1) * sizeof(float2);
+    const auto r = chunk_items(P, p_lo, p_hi);
     if (P.subsort) {
-        const auto r = chunk_items(P, pt, p_lo, p_hi);
         const unsigned n = 16u * (r.second - r.first);
         if (n == 0) return;
         k_degrid_mfma<W, WS, true><<<n, 64, lds, st>>>(
-            P.g, P.recs + pt.vbase, ItemSrc{nullptr, n, nullptr}, nullptr,
-            pt.fitems + 16 * (size_t)r.first, P.grid, p_lo, p_hi, acc ? acc + pt.vbase : nullptr,
-            P.vdirect);
+            P.g, P.recs, nullptr, n, nullptr, P.pt.fitems + 16 * (size_t)r.first, P.grid, p_lo,
+            p_hi, acc, P.vdirect);
         return;
     }
-    const void *fn = (const void *)k_degrid_mfma<W, WS, false>;
-    const Launch L = part_launch(P, pt, p_lo, p_hi, fn, 64, lds);
-    if (L.blocks == 0) return;
-    k_degrid_mfma<W, WS, false><<<L.blocks, 64, lds, st>>>(
-        P.g, P.recs + pt.vbase, L.src, pt.offs, nullptr, P.grid, p_lo, p_hi,
-        acc ? acc + pt.vbase : nullptr, P.vdirect);
+    const unsigned n = r.second - r.first;
+    if (n == 0) return;
+    k_degrid_mfma<W, WS, false><<<n, 64, lds, st>>>(P.g, P.recs, P.pt.items + r.first, n,
+                                                    P.pt.offs, nullptr, P.grid, p_lo, p_hi, acc,
+                                                    P.vdirect);
 }
 
 template <int W>
-static void launch_degrid(const Plan &P, const Part &pt, int p_lo, int p_hi, float2 *acc,
-                          hipStream_t st) {
-    if (P.cells && (P.subsort || P.g.sub == kTileCell)) {
-        if (P.g.do_w) return launch_degrid_mfma<W, true>(P, pt, p_lo, p_hi, acc, st);
-        return launch_degrid_mfma<W, false>(P, pt, p_lo, p_hi, acc, st);
-    }
-    if (P.subsort) {
-        if (P.g.do_w) return launch_degrid_fine_items<W, true>(P, pt, p_lo, p_hi, acc, st);
-        return launch_degrid_fine_items<W, false>(P, pt, p_lo, p_hi, acc, st);
-    }
-    if (P.g.sub == kTileFine) {
-        if (P.g.do_w) return launch_degrid_reg<W, true>(P, pt, p_lo, p_hi, acc, st);
-        return launch_degrid_reg<W, false>(P, pt, p_lo, p_hi, acc, st);
-    }
-    if (P.g.do_w)
-        return launch_degrid_n<W, true, kTileCoarse, kTileCoarse>(P, pt, p_lo, p_hi, acc, st);
-    return launch_degrid_n<W, false, kTileCoarse, kTileCoarse>(P, pt, p_lo, p_hi, acc, st);
+static void launch_degrid(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
+    if (P.g.do_w) return launch_degrid_mfma<W, true>(P, p_lo, p_hi, acc, st);
+    return launch_degrid_mfma<W, false>(P, p_lo, p_hi, acc, st);
 }
 
 #define SDP_W_DISPATCH(W, CALL) \
@@ -3431,12 +2363,11 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
     info->nplanes = P.g.nplanes;
     info->w0 = P.g.w0;
     info->dw = P.g.dw;
-    info->nvis_used = P.nrec;
-    info->nitems = P.nitems;
+    info->nvis_used = P.pt.nrec;
+    info->nitems = P.pt.nitems;
     info->plane_chunk = P.chunk_planes;
     info->bucket = P.g.sub;
-    info->grid_launches = (int)P.parts.size() *
-                          ((P.g.nplanes + P.chunk_planes - 1) / P.chunk_planes);
+    info->grid_launches = (P.g.nplanes + P.chunk_planes - 1) / P.chunk_planes;
 }
 
 // Pruned 2-D FFT of each resident plane.  The uv grid is non-zero only in
@@ -3489,91 +2420,38 @@ static dim3 tr_grid(const Geo &g, int xrows, int np) {
                 (unsigned)np);
 }
 
-// Bucket every part.  Synchronous plans bucket on `st` and read the
-// metadata back (plane-chunked launches need the item offsets).  Pipelined
-// plans bucket on the auxiliary stream after an event on `st` (inputs ready)
-// and record one event per part for the consumer launches to wait on.
-static std::vector<hipEvent_t> bucket_parts(Plan &P, const Inputs &in, bool grid_mode,
-                                            hipStream_t st) {
-    std::vector<hipEvent_t> ev;
-    // weight sum of the fused prologue: slots zeroed before the parts' count
-    // passes, folded into *sumwt after the first part (all parts share slots)
+// Bucketing with the fused weight sum (slots zeroed before the count pass,
+// folded into *sumwt after it), then the metadata read back by the host.
+static void bucket_all(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st) {
     double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
-    auto sum_end = [&](hipStream_t s) {
-        if (slots) k_sum_slots<<<1, 64, 0, s>>>(slots, in.x.sumwt);
-    };
-    if (!P.aux_bucketing) {
-        if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
-        for (size_t i = 0; i < P.parts.size(); ++i) bucket_part(P, (int)i, in, grid_mode, st);
-        sum_end(st);
-        read_part_meta(P, st);
-        return ev;
-    }
-    hipStream_t aux = aux_stream();
-    hipEvent_t ready;
-    SDP_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-    SDP_HIP_CHECK(hipEventRecord(ready, st));
-    SDP_HIP_CHECK(hipStreamWaitEvent(aux, ready, 0));
-    SDP_HIP_CHECK(hipEventDestroy(ready));
-    if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), aux));
-    for (size_t i = 0; i < P.parts.size(); ++i) {
-        bucket_part(P, (int)i, in, grid_mode, aux);
-        if (i + 1 == P.parts.size()) sum_end(aux);
-        hipEvent_t e;
-        SDP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        SDP_HIP_CHECK(hipEventRecord(e, aux));
-        ev.push_back(e);
-    }
-    return ev;
+    if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
+    bucket_part(P, in, grid_mode, st);
+    if (slots) k_sum_slots<<<1, 64, 0, st>>>(slots, in.x.sumwt);
+    read_part_meta(P, st);
 }
 
-// Sub-sort of every part's coarse items (synchronous plans: the item counts
-// are on the host)
-static void subsort_parts(Plan &P, hipStream_t st) {
-    for (size_t i = 0; i < P.parts.size(); ++i) {
-        Part &pt = P.parts[i];
-        if (pt.nitems == 0) continue;
-        const std::string sfx = "#" + std::to_string(i);
-        pt.fitems = scratch<FineItem>("fitems" + sfx, (size_t)pt.nitems * 16);
-        if (P.cells && P.subpad) {
-            // sub-sort, padded sizes, their scan (one host read of the total),
-            // then the 4-padded 16-B re-write with FineItems over it
-            unsigned *psize = scratch<unsigned>("psize" + sfx, (size_t)pt.nitems + 1);
-            unsigned *poffs = scratch<unsigned>("poffs" + sfx, (size_t)pt.nitems + 1);
-            SDP_HIP_CHECK(hipMemsetAsync(psize + pt.nitems, 0, sizeof(unsigned), st));
-            k_subsort<true><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(
-                P.g, pt.items, P.recs + pt.vbase, pt.fitems, psize);
-            SDP_HIP_CHECK(hipGetLastError());
-            size_t tb = 0;
-            SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, psize, poffs,
-                                                           (int)(pt.nitems + 1), st));
-            void *tmp = scratch<char>("pscan_tmp" + sfx, tb + 16);
-            SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, psize, poffs,
-                                                           (int)(pt.nitems + 1), st));
-            unsigned total = 0;
-            SDP_HIP_CHECK(hipMemcpyAsync(&total, poffs + pt.nitems, sizeof(unsigned),
-                                         hipMemcpyDeviceToHost, st));
-            SDP_HIP_CHECK(hipStreamSynchronize(st));
-            pt.precs = scratch<RecC>("precs" + sfx, std::max<size_t>(total, 1));
-            pt.pfitems = scratch<FineItem>("pfitems" + sfx, (size_t)pt.nitems * 16);
-            k_subsort_emit<<<(unsigned)pt.nitems, 256, 0, st>>>(
-                P.g, pt.items, P.recs + pt.vbase, pt.fitems, poffs, pt.precs, pt.pfitems);
-            SDP_HIP_CHECK(hipGetLastError());
-            continue;
-        }
-        if (P.cells)
-            k_subsort<true><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(
-                P.g, pt.items, P.recs + pt.vbase, pt.fitems);
-        else
-            k_subsort<false><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(
-                P.g, pt.items, P.recs + pt.vbase, pt.fitems);
-        SDP_HIP_CHECK(hipGetLastError());
-    }
+// Sub-sort of the coarse items by cell (large grids)
+static void subsort_items(Plan &P, hipStream_t st) {
+    Part &pt = P.pt;
+    if (pt.nitems == 0) return;
+    pt.fitems = scratch<FineItem>("fitems", (size_t)pt.nitems * 16);
+    k_subsort<true><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(P.g, pt.items, P.recs,
+                                                                 pt.fitems);
+    SDP_HIP_CHECK(hipGetLastError());
 }
 
-static void release_events(std::vector<hipEvent_t> &ev) {
-    for (auto e : ev) (void)hipEventDestroy(e);
-    ev.clear();
+// Record `e` on `from` and make `to` wait for it.
+static void stream_after(hipStream_t to, hipStream_t from) {
+    hipEvent_t e;
+    SDP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    SDP_HIP_CHECK(hipEventRecord(e, from));
+    SDP_HIP_CHECK(hipStreamWaitEvent(to, e, 0));
+    SDP_HIP_CHECK(hipEventDestroy(e));
+}
+
+static int weight_is_f64(int wgt_dtype) {
+    SDP_REQUIRE(wgt_dtype == SDP_HIP_F32 || wgt_dtype == SDP_HIP_F64, "weights must be f32 or f64");
+    return wgt_dtype == SDP_HIP_F64 ? 1 : 0;
 }
 
 static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
@@ -3599,38 +2477,34 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     if (batched) {
         SDP_REQUIRE(P.chunk_planes == g.nplanes,
                     "batched invert: the w planes do not all fit in device memory");
+        check_batch_seq(P, in, first);
     }
     const double *tab = phi_table(g.W, g.beta, st);
     // the band zeroing of the first plane chunk (HBM writes) overlaps the
     // bucketing (bound by memory-side atomics): it runs on the auxiliary
     // stream after the call's earlier work on `st`; the gridding waits for it
-    hipEvent_t zdone = nullptr;
     // (single calls only: on C4's streamed batches it measured 1-2 % slower)
-    if (first && !batched && !P.aux_bucketing && env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0) {
+    hipEvent_t zdone = nullptr;
+    if (first && !batched && env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0) {
         hipStream_t aux = aux_stream();
-        hipEvent_t ready;
-        SDP_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-        SDP_HIP_CHECK(hipEventRecord(ready, st));
-        SDP_HIP_CHECK(hipStreamWaitEvent(aux, ready, 0));
-        SDP_HIP_CHECK(hipEventDestroy(ready));
+        stream_after(aux, st);
         zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
         SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
         SDP_HIP_CHECK(hipEventRecord(zdone, aux));
     }
-    std::vector<hipEvent_t> ev;
     if (reuse) {
-        // value pass only (weight sums included), then the kept sub-sort
+        // value pass only (weight sums included)
         double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
         if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
-        for (size_t i = 0; i < P.parts.size(); ++i) bucket_part(P, (int)i, inx, true, st, true);
+        bucket_part(P, inx, true, st, true);
         if (slots) k_sum_slots<<<1, 64, 0, st>>>(slots, in.x.sumwt);
     } else {
-        ev = bucket_parts(P, inx, true, st);
+        bucket_all(P, inx, true, st);
     }
-    if (P.subsort) subsort_parts(P, st);
+    if (P.subsort) subsort_items(P, st);
     if (keep) keep_buckets(P, in);
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
-    float tprep = 0, tgrid = 0, tfft = 0, tscr = 0;
+    float tgrid = 0, tfft = 0, tscr = 0;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
@@ -3641,11 +2515,10 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
         } else if (first) {
             zero_band(P, np, st);
         }
-        for (size_t i = 0; i < P.parts.size(); ++i) {
-            if (!ev.empty()) SDP_HIP_CHECK(hipStreamWaitEvent(st, ev[i], 0));
+        {
             StageTimer tg(st);
             tg.mark();
-#define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, P.parts[i], p_lo, p_hi, st)
+#define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, p_lo, p_hi, st)
             SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
 #undef SDP_LAUNCH_GRID
             SDP_HIP_CHECK(hipGetLastError());
@@ -3673,15 +2546,17 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
             tscr += t2.ms(1, 2);
         }
     }
+    if (zdone) {  // (no plane pass ran)
+        SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
+        SDP_HIP_CHECK(hipEventDestroy(zdone));
+    }
+    if (batched && last) drop_batch_seq();
     tm.mark();
-    if (P.pipelined) read_part_meta(P, st);
-    release_events(ev);
     fill_info(P, info);
     if (info) {
         // everything on the call's stream that is not gridding, FFT or screen:
-        // geometry, bucketing not hidden behind gridding, band zeroing
-        tprep = tm.ms(0, 1) - tgrid - tfft - tscr;
-        info->ms_prep = tm.on ? tprep : 0.0f;
+        // geometry, bucketing, band zeroing not hidden behind the bucketing
+        info->ms_prep = tm.on ? tm.ms(0, 1) - tgrid - tfft - tscr : 0.0f;
         info->ms_grid = tgrid;
         info->ms_fft = tfft;
         info->ms_screen = tscr;
@@ -3703,51 +2578,40 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     // writes) overlap the bucketing (memory-side atomics; it reads uvw and
     // weights only) on the auxiliary stream, after the call's earlier work
     hipEvent_t zdone = nullptr;
-    if (!P.aux_bucketing && env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0) {
+    auto zero_vis = [&](hipStream_t s) {
+        if (accumulate || nvis <= 0) return;
+        if (in.vis_dtype == SDP_HIP_C128)
+            k_zero_vis<double2><<<grid1d(nvis, 256), 256, 0, s>>>(in.nrow, in.nchan,
+                                                                   (double2 *)vis, in.vrs,
+                                                                   in.vcs, oc);
+        else
+            k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, s>>>(in.nrow, in.nchan, (float2 *)vis,
+                                                                  in.vrs, in.vcs, oc);
+        SDP_HIP_CHECK(hipGetLastError());
+    };
+    if (env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0) {
         hipStream_t aux = aux_stream();
-        hipEvent_t ready;
-        SDP_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-        SDP_HIP_CHECK(hipEventRecord(ready, st));
-        SDP_HIP_CHECK(hipStreamWaitEvent(aux, ready, 0));
-        SDP_HIP_CHECK(hipEventDestroy(ready));
-        if (!accumulate && nvis > 0) {
-            if (in.vis_dtype == SDP_HIP_C128)
-                k_zero_vis<double2><<<grid1d(nvis, 256), 256, 0, aux>>>(
-                    in.nrow, in.nchan, (double2 *)vis, in.vrs, in.vcs, oc);
-            else
-                k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, aux>>>(
-                    in.nrow, in.nchan, (float2 *)vis, in.vrs, in.vcs, oc);
-            SDP_HIP_CHECK(hipGetLastError());
-        }
+        stream_after(aux, st);
+        zero_vis(aux);
         zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
         SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
         SDP_HIP_CHECK(hipEventRecord(zdone, aux));
+    } else {
+        zero_vis(st);
     }
-    // the bucketing runs on the aux stream under the screen + FFT
-    std::vector<hipEvent_t> ev = bucket_parts(P, in, false, st);
-    if (P.subsort) subsort_parts(P, st);
-    if (!zdone && !accumulate && nvis > 0) {
-        if (in.vis_dtype == SDP_HIP_C128)
-            k_zero_vis<double2><<<grid1d(nvis, 256), 256, 0, st>>>(
-                in.nrow, in.nchan, (double2 *)vis, in.vrs, in.vcs, oc);
-        else
-            k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, st>>>(
-                in.nrow, in.nchan, (float2 *)vis, in.vrs, in.vcs, oc);
-    }
+    bucket_all(P, in, false, st);
+    if (P.subsort) subsort_items(P, st);
     // all planes in one pass into plain contiguous c64 visibilities: the
-    // register degridders apply the record factor and write each visibility
-    // once (k_zero_vis above covers the ones with no record)
+    // degridder applies the record factor and writes each visibility once
+    // (the zeroing above covers the ones with no record)
     const bool trivial_oc = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
     if (P.chunk_planes == g.nplanes && !accumulate && in.vis_dtype != SDP_HIP_C128 && trivial_oc &&
-        in.vcs == 1 && in.vrs == in.nchan &&
-        (P.subsort || g.sub == kTileFine || g.sub == kTileCell) &&
-        !std::getenv("SDP_HIP_NO_DIRECT"))
+        in.vcs == 1 && in.vrs == in.nchan)
         P.vdirect = static_cast<float2 *>(vis);
     float2 *acc = P.vdirect ? nullptr : scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));
     if (acc)
         SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(nvis, 1) * sizeof(float2), st));
     float tgrid = 0, tfft = 0, tscr = 0;
-    bool waited = false;
     for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
@@ -3777,43 +2641,30 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
             tscr += t2.ms(0, 1);
             tfft += t2.ms(1, 2);
         }
-        if (P.aux_bucketing && !P.pipelined && !waited)
-            read_part_meta(P, aux_stream());  // host waits for the bucketing only
-        for (size_t i = 0; i < P.parts.size(); ++i) {
-            if (!ev.empty() && !waited) SDP_HIP_CHECK(hipStreamWaitEvent(st, ev[i], 0));
-            StageTimer tg(st);
-            tg.mark();
-#define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, P.parts[i], p_lo, p_hi, acc, st)
-            SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
+        StageTimer tg(st);
+        tg.mark();
+#define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, acc, st)
+        SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
 #undef SDP_LAUNCH_DEGRID
-            SDP_HIP_CHECK(hipGetLastError());
-            tg.mark();
-            tgrid += tg.ms(0, 1);
-        }
-        waited = true;
+        SDP_HIP_CHECK(hipGetLastError());
+        tg.mark();
+        tgrid += tg.ms(0, 1);
     }
     if (zdone) {  // (no plane pass ran)
         SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
         SDP_HIP_CHECK(hipEventDestroy(zdone));
     }
-    for (size_t i = 0; i < P.parts.size() && !P.vdirect; ++i) {
-        const Part &pt = P.parts[i];
-        if (pt.nvis == 0) continue;
-        const unsigned *ndev = P.pipelined ? pt.meta + 2 : nullptr;
-        const unsigned nb = std::min<unsigned>(grid1d(pt.nvis, 256), 16384);
+    if (!P.vdirect && P.pt.nvis > 0) {
+        const unsigned nb = std::min<unsigned>(grid1d(P.pt.nvis, 256), 16384);
         if (in.vis_dtype == SDP_HIP_C128)
-            k_finalize<double2><<<nb, 256, 0, st>>>(pt.nrec, ndev, in.nchan, P.recs + pt.vbase,
-                                                    acc + pt.vbase, (double2 *)vis, in.vrs,
-                                                    in.vcs, accumulate, oc);
+            k_finalize<double2><<<nb, 256, 0, st>>>(P.pt.nrec, in.nchan, P.recs, acc,
+                                                    (double2 *)vis, in.vrs, in.vcs, accumulate, oc);
         else
-            k_finalize<float2><<<nb, 256, 0, st>>>(pt.nrec, ndev, in.nchan, P.recs + pt.vbase,
-                                                   acc + pt.vbase, (float2 *)vis, in.vrs, in.vcs,
-                                                   accumulate, oc);
+            k_finalize<float2><<<nb, 256, 0, st>>>(P.pt.nrec, in.nchan, P.recs, acc, (float2 *)vis,
+                                                   in.vrs, in.vcs, accumulate, oc);
         SDP_HIP_CHECK(hipGetLastError());
     }
     tm.mark();
-    if (P.pipelined) read_part_meta(P, st);
-    release_events(ev);
     fill_info(P, info);
     if (info) {
         info->ms_prep = tm.on ? tm.ms(0, 1) - tgrid - tfft - tscr : 0.0f;
@@ -3854,27 +2705,30 @@ int sdp_hip_release_workspace(char *errbuf, size_t errbuf_len) {
 
 int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride, const double *freq, int nchan,
                      int64_t nrow, const void *vis, int vis_dtype, int64_t vis_row_stride,
-                     int64_t vis_chan_stride, const float *wgt, int64_t wgt_row_stride,
-                     int64_t wgt_chan_stride, int npix_x, int npix_y, double pixsize_x,
+                     int64_t vis_chan_stride, const void *wgt, int wgt_dtype,
+                     int64_t wgt_row_stride, int64_t wgt_chan_stride, int npix_x, int npix_y,
+                     double pixsize_x,
                      double pixsize_y, double epsilon, int do_wstacking, unsigned flags,
                      double *dirty, int64_t dirty_stride_x, int64_t dirty_stride_y, void *stream,
                      sdp_hip_wgrid_info *info, char *errbuf, size_t errbuf_len) {
     return guarded(errbuf, errbuf_len, [&] {
         SDP_REQUIRE(dirty != nullptr && freq != nullptr && (uvw != nullptr || nrow == 0),
                     "null pointer argument");
-        const wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
-                                nrow,        vis,             vis_dtype,      vis_row_stride,
-                                vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
-                                npix_x,      npix_y,          pixsize_x,      pixsize_y,
-                                epsilon,     do_wstacking,    flags};
+        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                          nrow,        vis,             vis_dtype,      vis_row_stride,
+                          vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
+                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                          epsilon,     do_wstacking,    flags};
+        in.x.wgt_f64 = wstack::weight_is_f64(wgt_dtype);
         wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
     });
 }
 
 int sdp_hip_ms2dirty_batch(const double *uvw, int64_t uvw_row_stride, const double *freq,
                            int nchan, int64_t nrow, const void *vis, int vis_dtype,
-                           int64_t vis_row_stride, int64_t vis_chan_stride, const float *wgt,
-                           int64_t wgt_row_stride, int64_t wgt_chan_stride, int npix_x,
+                           int64_t vis_row_stride, int64_t vis_chan_stride, const void *wgt,
+                           int wgt_dtype, int64_t wgt_row_stride, int64_t wgt_chan_stride,
+                           int npix_x,
                            int npix_y, double pixsize_x, double pixsize_y, double epsilon,
                            int do_wstacking, unsigned flags, const double *bounds,
                            double *dirty, int64_t dirty_stride_x, int64_t dirty_stride_y,
@@ -3890,6 +2744,7 @@ int sdp_hip_ms2dirty_batch(const double *uvw, int64_t uvw_row_stride, const doub
                           vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
                           npix_x,      npix_y,          pixsize_x,      pixsize_y,
                           epsilon,     do_wstacking,    flags};
+        in.x.wgt_f64 = wstack::weight_is_f64(wgt_dtype);
         in.bounds = bounds;
         wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
     });
@@ -3956,7 +2811,7 @@ int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride, const double
 int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride, const double *freq, int nchan,
                      int64_t nrow, const double *dirty, int64_t dirty_stride_x,
                      int64_t dirty_stride_y, int npix_x, int npix_y, double pixsize_x,
-                     double pixsize_y, const float *wgt, int64_t wgt_row_stride,
+                     double pixsize_y, const void *wgt, int wgt_dtype, int64_t wgt_row_stride,
                      int64_t wgt_chan_stride, double epsilon, int do_wstacking, unsigned flags,
                      void *vis, int vis_dtype, int64_t vis_row_stride, int64_t vis_chan_stride,
                      void *stream, sdp_hip_wgrid_info *info, char *errbuf, size_t errbuf_len) {
@@ -3964,11 +2819,12 @@ int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride, const double *fr
         SDP_REQUIRE(dirty != nullptr && freq != nullptr && vis != nullptr &&
                         (uvw != nullptr || nrow == 0),
                     "null pointer argument");
-        const wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
-                                nrow,        nullptr,         vis_dtype,      vis_row_stride,
-                                vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
-                                npix_x,      npix_y,          pixsize_x,      pixsize_y,
-                                epsilon,     do_wstacking,    flags};
+        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                          nrow,        nullptr,         vis_dtype,      vis_row_stride,
+                          vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
+                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                          epsilon,     do_wstacking,    flags};
+        in.x.wgt_f64 = wstack::weight_is_f64(wgt_dtype);
         wstack::dirty2ms(in, dirty, dirty_stride_x, dirty_stride_y, vis, info,
                          as_stream(stream));
     });

@@ -75,14 +75,14 @@ SIGNATURES = {
     "sdp_hip_ms2dirty": [
         c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
         c_vp, c_int, c_i64, c_i64,                # vis, dtype, strides
-        c_vp, c_i64, c_i64,                       # wgt, strides
+        c_vp, c_int, c_i64, c_i64,                # wgt, dtype (f32 / f64), strides
         c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,
         c_vp, c_i64, c_i64,                       # dirty, strides
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_ms2dirty_batch": [
         c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
         c_vp, c_int, c_i64, c_i64,                # vis, dtype, strides
-        c_vp, c_i64, c_i64,                       # wgt, strides
+        c_vp, c_int, c_i64, c_i64,                # wgt, dtype (f32 / f64), strides
         c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,
         c_vp,                                     # bounds (host, 6 doubles)
         c_vp, c_i64, c_i64,                       # dirty, strides
@@ -100,7 +100,7 @@ SIGNATURES = {
     "sdp_hip_dirty2ms": [
         c_vp, c_i64, c_vp, c_int, c_i64,
         c_vp, c_i64, c_i64, c_int, c_int, c_dbl, c_dbl,
-        c_vp, c_i64, c_i64,
+        c_vp, c_int, c_i64, c_i64,                # wgt, dtype (f32 / f64), strides
         c_dbl, c_int, c_u32,
         c_vp, c_int, c_i64, c_i64,
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,

@@ -56,6 +56,34 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+def _alloc(shape, dtype, dev):
+    """torch.empty on the device; when the caching allocator cannot serve it
+    because the library's workspace holds the memory (cached w planes and
+    records of an earlier large call), the workspace is released and the
+    allocation retried once (the w planes are re-made on the next call)."""
+    try:
+        return torch.empty(shape, dtype=dtype, device=dev)
+    except torch.OutOfMemoryError:
+        release_workspace()
+        torch.cuda.empty_cache()
+        return torch.empty(shape, dtype=dtype, device=dev)
+
+
+def _check_wgt(wgt, nrow, nchan):
+    """ducc0 takes f64 weights; f32 (the bench's) and f64 are both read in place."""
+    if wgt is None:
+        return
+    _on_gpu(wgt, "wgt")
+    if wgt.dtype not in (torch.float32, torch.float64) or tuple(wgt.shape) != (nrow, nchan):
+        raise ValueError("wgt must be float32 or float64 [nrow, nchan]")
+
+
+def _wgt_args(wgt):
+    if wgt is None:
+        return (_ptr(None), _lib.SDP_HIP_F32, 0, 0)
+    return (_ptr(wgt), _DT_CODE[wgt.dtype], wgt.stride(0), wgt.stride(1))
+
+
 def _check_uvw(uvw):
     _on_gpu(uvw, "uvw")
     if uvw.dtype != torch.float64 or uvw.dim() != 2 or uvw.shape[1] != 3 or uvw.stride(1) != 1:
@@ -81,12 +109,9 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
         _on_gpu(vis, "vis")
         if vis.dtype not in (torch.complex64, torch.complex128) or tuple(vis.shape) != (nrow, nchan):
             raise ValueError("vis must be complex [nrow, nchan]")
-    if wgt is not None:
-        _on_gpu(wgt, "wgt")
-        if wgt.dtype != torch.float32 or tuple(wgt.shape) != (nrow, nchan):
-            raise ValueError("wgt must be float32 [nrow, nchan]")
+    _check_wgt(wgt, nrow, nchan)
     if out is None:
-        out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=dev)
+        out = _alloc((npix_x, npix_y), torch.float64, dev)
         out_strides = (npix_y, 1)
     elif out_strides is None:
         out_strides = out.stride()
@@ -100,7 +125,7 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
         _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
         _ptr(vis), _DT_CODE[vis.dtype] if vis is not None else _lib.SDP_HIP_C64,
         vis.stride(0) if vis is not None else 0, vis.stride(1) if vis is not None else 0,
-        _ptr(wgt), wgt.stride(0) if wgt is not None else 0, wgt.stride(1) if wgt is not None else 0,
+        *_wgt_args(wgt),
         int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
         int(bool(do_wstacking)), flags,
         _ptr(out), int(out_strides[0]), int(out_strides[1]),
@@ -140,13 +165,10 @@ def ms2dirty_batch(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y, bo
         _on_gpu(vis, "vis")
         if vis.dtype not in (torch.complex64, torch.complex128) or tuple(vis.shape) != (nrow, nchan):
             raise ValueError("vis must be complex [nrow, nchan]")
-    if wgt is not None:
-        _on_gpu(wgt, "wgt")
-        if wgt.dtype != torch.float32 or tuple(wgt.shape) != (nrow, nchan):
-            raise ValueError("wgt must be float32 [nrow, nchan]")
+    _check_wgt(wgt, nrow, nchan)
     if last:
         if out is None:
-            out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=dev)
+            out = _alloc((npix_x, npix_y), torch.float64, dev)
             out_strides = (npix_y, 1)
         elif out_strides is None:
             out_strides = out.stride()
@@ -164,7 +186,7 @@ def ms2dirty_batch(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y, bo
         _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
         _ptr(vis), _DT_CODE[vis.dtype] if vis is not None else _lib.SDP_HIP_C64,
         vis.stride(0) if vis is not None else 0, vis.stride(1) if vis is not None else 0,
-        _ptr(wgt), wgt.stride(0) if wgt is not None else 0, wgt.stride(1) if wgt is not None else 0,
+        *_wgt_args(wgt),
         int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
         int(bool(do_wstacking)), flags, ctypes.cast(bbuf, ctypes.c_void_p),
         _ptr(out if last else None), int(out_strides[0]) if last else 0,
@@ -228,7 +250,7 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
             raise ValueError("coef must have one entry per visibility pol")
         cbuf = (ctypes.c_double * (2 * npv))(*[v for z in c for v in (z.real, z.imag)])
     if out is None:
-        out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=dev)
+        out = _alloc((npix_x, npix_y), torch.float64, dev)
         out_strides = (npix_y, 1)
     elif out_strides is None:
         out_strides = out.stride()
@@ -315,12 +337,9 @@ def dirty2ms(uvw, freq, dirty, wgt, pixsize_x, pixsize_y, epsilon=1e-7,
         npix_x, npix_y = npix
     if dirty_strides is None:
         dirty_strides = dirty.stride()[-2:]
-    if wgt is not None:
-        _on_gpu(wgt, "wgt")
-        if wgt.dtype != torch.float32 or tuple(wgt.shape) != (nrow, nchan):
-            raise ValueError("wgt must be float32 [nrow, nchan]")
+    _check_wgt(wgt, nrow, nchan)
     if out is None:
-        out = torch.empty((nrow, nchan), dtype=vis_dtype, device=dev)
+        out = _alloc((nrow, nchan), vis_dtype, dev)
     _on_gpu(out, "vis out")
     if out.dtype not in (torch.complex64, torch.complex128) or tuple(out.shape) != (nrow, nchan):
         raise ValueError("vis out must be complex [nrow, nchan]")
@@ -331,7 +350,7 @@ def dirty2ms(uvw, freq, dirty, wgt, pixsize_x, pixsize_y, epsilon=1e-7,
         _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
         _ptr(dirty), int(dirty_strides[0]), int(dirty_strides[1]), int(npix_x), int(npix_y),
         float(pixsize_x), float(pixsize_y),
-        _ptr(wgt), wgt.stride(0) if wgt is not None else 0, wgt.stride(1) if wgt is not None else 0,
+        *_wgt_args(wgt),
         float(epsilon), int(bool(do_wstacking)), flags,
         _ptr(out), _DT_CODE[out.dtype], out.stride(0), out.stride(1),
         _stream(dev), ctypes.byref(info))
@@ -366,7 +385,7 @@ def dft_point(direction_cosines, fluxes, uvw, freq=None, out=None, vis_dtype=tor
     else:
         nrow, nchan = uvw.shape[0], uvw.shape[1]
     if out is None:
-        out = torch.empty((nrow, nchan, npol), dtype=vis_dtype, device=uvw.device)
+        out = _alloc((nrow, nchan, npol), vis_dtype, uvw.device)
     if not out.is_contiguous() or tuple(out.shape) != (nrow, nchan, npol):
         raise ValueError("vis out must be contiguous [nrow, nchan, npol]")
     if freq is not None:
@@ -457,7 +476,14 @@ def _check_cf_operands(maps, vis_to_im, cf, grid, nrow, nchan, npol):
     if bool((v2i >= lim).any()) or bool((v2i < -lim).any()):
         raise IndexError(f"vis_to_im {v2i.tolist()} out of range for {gn} grid / {cfn} cf "
                          "channels")
-    v2i = torch.where(v2i < 0, v2i + lim, v2i)
+    if bool((v2i < 0).any()):
+        # numpy wraps gd[imchan] by the grid's channel count and cf[imchan] by
+        # the CF's: one kernel index serves both only when the counts agree
+        if gn != cfn:
+            raise IndexError(f"negative vis_to_im {v2i.tolist()} with {gn} grid and {cfn} cf "
+                             "channels: the reference would pick different grid and cf "
+                             "channels; pass non-negative channel indices")
+        v2i = torch.where(v2i < 0, v2i + gn, v2i)
     return v2i.to(device=grid.device, dtype=torch.int32)
 
 

@@ -35,30 +35,15 @@ def _problem(seed, nrow=300, nchan=3, umax=2000.0, frac=0.45):
     return uvw, freq, ms, wgt, frac / umax
 
 
-@pytest.fixture(params=["fine", "fine-reg", "fine-degrid-reg", "coarse", "coarse-reg", "coarse-lds",
-                        "fine-pipelined", "fine-aux"])
+@pytest.fixture(params=["fine", "coarse"])
 def bucket(request, monkeypatch):
-    """Every bucketing: one-cell buckets for the MFMA gridder (invert) and
-    the MFMA degridder (predict), the default at these sizes; 2x2-cell
-    buckets for the register gridder and degridder ("fine-reg",
-    SDP_HIP_MFMA=0) or the register degridder only ("fine-degrid-reg",
-    SDP_HIP_MFMA_DEGRID=0); 16x16-cell buckets (very large grids), whose items are
-    re-ordered to cells / 2x2 buckets ("coarse", "coarse-reg") or fed to the
-    LDS-tile kernels ("coarse-lds", SDP_HIP_SUBSORT=0); and the pipelined plan
-    (two row parts bucketed on the auxiliary stream, persistent gridding
-    launches)."""
-    if request.param == "fine-degrid-reg":
-        monkeypatch.setenv("SDP_HIP_MFMA_DEGRID", "0")
-    elif request.param.endswith("-reg"):
-        monkeypatch.setenv("SDP_HIP_MFMA", "0")
-    if request.param.startswith("coarse"):
+    """Both bucketings: one-cell buckets (4-padded for the invert's MFMA
+    gridder, plain for the MFMA degridder), the default at these sizes, and
+    16x16-cell buckets sub-sorted by cell per work item (the path of very
+    large grids such as C4's 16384^2 x 70 planes, forced here by
+    SDP_HIP_BUCKET=16)."""
+    if request.param == "coarse":
         monkeypatch.setenv("SDP_HIP_BUCKET", "16")
-    if request.param == "coarse-lds":
-        monkeypatch.setenv("SDP_HIP_SUBSORT", "0")
-    if request.param == "fine-pipelined":
-        monkeypatch.setenv("SDP_HIP_PIPELINE", "2")
-    if request.param == "fine-aux":  # bucketing on the auxiliary stream
-        monkeypatch.setenv("SDP_HIP_PIPELINE", "1")
     return request.param
 
 
@@ -74,9 +59,8 @@ def test_ms2dirty_matches_exact(dow, vdt, flip, bucket):
     out, info = kernels.ms2dirty(T(uvw), T(freq), T(ms, vdt), T(wgt), npix, 48 + 16 * dow, cell,
                                  cell * 0.9, 1e-7, dow, flip_uw=flip)
     assert info["support"] == 8
-    assert info["bucket"] == (16 if bucket.startswith("coarse") else
-                              (2 if bucket == "fine-reg" else 1))
-    assert info["grid_launches"] == (2 if bucket == "fine-pipelined" else 1)
+    assert info["bucket"] == (16 if bucket == "coarse" else 1)
+    assert info["grid_launches"] == 1
     assert rel_rms(out.cpu().numpy(), ex) < TOL
 
 
@@ -257,18 +241,13 @@ def test_fft_batches_match_single_batch(fft_planes, budget, monkeypatch):
     assert rel_rms(vpart.cpu().numpy(), vfull.cpu().numpy()) < 1e-6
 
 
-@pytest.mark.parametrize("subsort", ["1", "0", "pad"])
-def test_large_grid_adjointness(subsort, monkeypatch):
+def test_large_grid_adjointness(monkeypatch):
     """C4-size grid (8192^2 image, 16384^2 grid, 2.15 GB planes) on the
-    16x16-bucket path, with (MFMA kernels on sub-sorted cells) and without
-    (LDS-tile kernels) the sub-sort, and with the sub-sorted records
-    re-written 4-padded for k_grid_mfma_pad (SDP_HIP_SUBSORT_PAD=1, opt-in):
+    16x16-bucket path (MFMA kernels on cell-sub-sorted items):
     <A x, y> = <x, A^H y> and ms2dirty of the predicted visibilities of a
     point source peaks at that source."""
     from ska_sdp_func_python_amd import kernels
     monkeypatch.setenv("SDP_HIP_BUCKET", "16")
-    monkeypatch.setenv("SDP_HIP_SUBSORT", "1" if subsort == "pad" else subsort)
-    monkeypatch.setenv("SDP_HIP_SUBSORT_PAD", "1" if subsort == "pad" else "0")
     npix = 8192
     uvw, freq, ms, _, _ = _problem(11, nrow=20000, nchan=4, umax=3.0e5)
     uvw[:, 2] *= 0.02  # a handful of w planes at this cell size
@@ -599,3 +578,126 @@ def test_batched_invert_equals_single_call(flip, monkeypatch):
     with pytest.raises(ValueError, match="do not all fit"):
         kernels.ms2dirty_batch(U, F[:2], M[:, :2].contiguous(), None, 256, 192, cell, cell, b,
                                first=True, last=False, epsilon=1e-7)
+
+
+def test_batch_bounds_too_tight_are_refused():
+    """A batch of a batched invert whose visibilities fall outside the
+    sequence's bounds (u beyond max|u|, or w beyond the w range) is refused
+    with ValueError instead of indexing outside the histogram / planes."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(22, nrow=2000, nchan=3, umax=6000.0)
+    U, F, M = T(uvw), T(freq), T(ms)
+    b = kernels.uvw_bounds(U, F)
+    for tight in ([b[0], b[1], 0.5 * b[2], b[3], b[4], b[5]],           # u range too small
+                  [b[0], 0.5 * (b[0] + b[1]), b[2], b[3], b[4], b[5]],   # w range too small
+                  [b[0], b[1], b[2], b[3], b[4], 0.7 * b[5]]):           # fmax too low
+        with pytest.raises(ValueError, match="outside"):
+            kernels.ms2dirty_batch(U, F, M, None, 256, 256, cell, cell, tight, first=True,
+                                   last=True, epsilon=1e-7)
+    out, _ = kernels.ms2dirty_batch(U, F, M, None, 256, 256, cell, cell, b, first=True,
+                                    last=True, epsilon=1e-7)
+    ref, _ = kernels.ms2dirty(U, F, M, None, 256, 256, cell, cell, 1e-7, True)
+    assert rel_rms(out.cpu().numpy(), ref.cpu().numpy()) < 1e-6
+
+
+def test_batch_sequence_guard():
+    """The resident planes of a batch sequence belong to it until its last
+    batch: another NUFFT call or a workspace release in between, or a batch
+    with other bounds / geometry, makes the next batch fail with ValueError
+    rather than accumulate into overwritten or freed planes."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, _, cell = _problem(23, nrow=2000, nchan=4, umax=5000.0)
+    U, F, M = T(uvw), T(freq), T(ms)
+    b = kernels.merge_bounds(kernels.uvw_bounds(U, F[:2]), kernels.uvw_bounds(U, F[2:]))
+    args = (256, 256, cell, cell)
+
+    def batch(i, bb=b, first=False, last=False, npix=256):
+        return kernels.ms2dirty_batch(U, F[2 * i:2 * i + 2], M[:, 2 * i:2 * i + 2].contiguous(),
+                                      None, npix, npix, cell, cell, bb, first=first, last=last,
+                                      epsilon=1e-7)
+
+    batch(0, first=True)
+    kernels.ms2dirty(U, F, M, None, *args, 1e-7, True)  # another call overwrites the planes
+    with pytest.raises(ValueError, match="no resident planes"):
+        batch(1, last=True)
+    batch(0, first=True)
+    kernels.release_workspace()
+    with pytest.raises(ValueError, match="no resident planes"):
+        batch(1, last=True)
+    batch(0, first=True)
+    wider = list(b)
+    wider[2] *= 1.01
+    with pytest.raises(ValueError, match="first batch|no resident planes"):
+        batch(1, bb=wider, last=True)
+    # an uninterrupted sequence still equals the single call
+    batch(0, first=True)
+    out, _ = batch(1, last=True)
+    ref, _ = kernels.ms2dirty(U, F, M, None, *args, 1e-7, True)
+    assert rel_rms(out.cpu().numpy(), ref.cpu().numpy()) < 1e-6
+    with pytest.raises(ValueError, match="no resident planes"):  # the sequence has ended
+        batch(1, last=True)
+
+
+def test_f64_weights_in_the_bare_entries():
+    """ducc0's ms2dirty / dirty2ms take f64 weights: the bare C ABI entries
+    accept f64 (and f32) weights, with identical results for weights exact in
+    both precisions, and match the exact sums."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(24)
+    w64 = np.round(wgt.astype(np.float64) * 64) / 64
+    ex = orc.ms2dirty_exact(uvw, freq, ms, w64, 64, 64, cell, cell, True)
+    a, _ = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(w64), 64, 64, cell, cell, 1e-7, True)
+    b, _ = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(w64, torch.float32), 64, 64, cell, cell,
+                            1e-7, True)
+    # (the flush atomics make the fp32 sum order vary from run to run)
+    assert rel_rms(a.cpu().numpy(), b.cpu().numpy()) < 1e-6
+    assert rel_rms(a.cpu().numpy(), ex) < TOL
+    img = np.random.default_rng(3).normal(size=(64, 64))
+    vx = orc.dirty2ms_exact(uvw, freq, img, w64, cell, cell, True)
+    v, _ = kernels.dirty2ms(T(uvw), T(freq), T(img), T(w64), cell, cell, 1e-7, True)
+    assert rel_rms(v.cpu().numpy(), vx) < TOL
+
+
+@pytest.mark.parametrize("pf,ipf", [("linear", "stokesIQUV"), ("stokesI", "stokesI")])
+def test_nan_in_flagged_samples_does_not_reach_the_image(pf, ipf):
+    """NaN / Inf visibilities and weights on flagged samples, and NaN / Inf
+    visibilities on samples whose weights are zero in every pol, contribute
+    nothing, as ducc0 skips zero-weight samples: invert_ng (multi-pol: shared
+    bucketing across the image pols, which buckets zero-weight samples too)
+    equals the same call with those values replaced by zeros.  (An unflagged
+    non-finite visibility of a pol with zero weight still enters the other
+    image pols through the pol conversion, as it does in the reference's
+    numpy convert_pol_frame -- not exercised here.)"""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import invert_ng
+    rng = np.random.default_rng(31)
+    nt, nb, nchan = 4, 40, 3
+    npol = dm.PolarisationFrame(pf).npol
+    freq = np.linspace(1.0e9, 1.1e9, nchan)
+    umax = 1500.0
+    uvw = rng.uniform(-1, 1, (nt, nb, 3)) * umax * orc.C_LIGHT / freq.max()
+    shape = (nt, nb, nchan, npol)
+    v = rng.normal(size=shape) + 1j * rng.normal(size=shape)
+    w = rng.uniform(0.5, 2.0, shape)
+    fl = (rng.uniform(size=shape) < 0.2).astype(int)
+    zw = np.broadcast_to(rng.uniform(size=shape[:3] + (1,)) < 0.1, shape)
+    w[zw] = 0.0
+    bad_v, bad_w = v.copy(), w.copy()
+    bad_v[fl == 1] = np.nan
+    bad_v[zw] = complex(np.inf, np.nan)
+    bad_w[fl == 1] = np.nan
+    im = dm.create_image(96, 0.4 / umax, dm.SkyCoord(0.0, -0.6),
+                         polarisation_frame=dm.PolarisationFrame(ipf), frequency=float(freq.mean()),
+                         channel_bandwidth=1e9)
+    clean_v = np.where(fl == 1, 0.0, v)
+    clean_v[zw] = 0.0
+    res = []
+    for vv, ww in ((bad_v, bad_w), (clean_v, np.where(fl == 1, 0.0, w))):
+        vis = vis_from_arrays(uvw, freq, vv, flags=fl, pf=pf, phasecentre=dm.SkyCoord(0.0, -0.6))
+        vis["imaging_weight"] = ww
+        res.append(invert_ng(vis, im, normalise=False))
+    (d_bad, sw_bad), (d_ok, sw_ok) = res
+    assert np.all(np.isfinite(d_bad["pixels"].data)) and np.all(np.isfinite(sw_bad))
+    np.testing.assert_allclose(sw_bad, sw_ok, rtol=1e-12)
+    for p in range(npol):
+        assert rel_rms(d_bad["pixels"].data[0, p], d_ok["pixels"].data[0, p]) < 1e-6, p
