@@ -100,8 +100,19 @@ class Workspace {
                                 std::to_string(bytes) + " bytes");
             }
             b.bytes = want;
+            b.epoch = ++epoch_;
         }
         return b.ptr;
+    }
+    // identity of the allocation currently held under `name` (0: none): it
+    // changes whenever that buffer is (re)allocated or released, so data a
+    // caller left in it is known to be intact while the epoch is unchanged
+    uint64_t epoch(const std::string &name) {
+        int dev = 0;
+        SDP_HIP_CHECK(hipGetDevice(&dev));
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = bufs_.find({dev, name});
+        return it == bufs_.end() ? 0 : it->second.epoch;
     }
     // bytes currently held under `name` on the current device (0 if none)
     size_t held(const std::string &name) {
@@ -130,9 +141,11 @@ class Workspace {
     struct Buf {
         void *ptr = nullptr;
         size_t bytes = 0;
+        uint64_t epoch = 0;
     };
     std::mutex mu_;
     uint64_t gen_ = 0;
+    uint64_t epoch_ = 0;
     std::map<std::pair<int, std::string>, Buf> bufs_;
 };
 

@@ -981,32 +981,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     }
 }
 
-// MFMA gridder on 4-padded cells (invert, one-cell buckets): the bucketing
+// MFMA gridder on 4-padded cells (invert, one-cell buckets).  The bucketing
 // rounds every cell's record count up to a multiple of 4 with zero-valued
-// pad records (k_pad_cells), so every K-step of 4 consecutive records
-// belongs to one cell and no K-step straddles a batch or an item.  Same GEMM
-// and region tile as k_grid_mfma; what changes is the work per K-step:
-//  * per batch of 64 records, the 64 x 3 x 8 one-dimensional taps are
-//    evaluated once with every lane busy (lane l: tap l & 7 of records
-//    8m + (l >> 3), 24 ES evaluations) into an LDS tap block of one
-//    kTapRec-float row per record: tu in h-major order (tu[2t + h] at
-//    4h + t, so a lane's four A taps are one ds_read_b128), tv, tw, value;
-//  * the 16 K-steps of a batch are unrolled with compile-time LDS offsets,
-//    the operands of K-step j + 1 read before the MFMAs of K-step j issue:
-//    per K-step 4 LDS reads, 5 multiplies, 4 MFMAs and a cell-change bit
-//    test -- no run bookkeeping, no masking.
-constexpr int kTapRec = 28;    // floats per record row of the tap block (16-B multiple)
-constexpr int kTapBatch = 16;  // records per tap block (LDS, occupancy: 14 waves per CU)
+// pad records (k_pad_cells), so every K-step of 4 consecutive records belongs
+// to one cell.  A cell's contribution to its W x W x W footprint is one GEMM
+//     C[(q, re/im), (kx, ky)] += sum_r  tw_r[q] c_r  *  tu_r[kx] tv_r[ky]
+// on v_mfma_f32_16x16x4_f32 (exact fp32 multiply-adds): A = the w taps x
+// value (16 rows: 8 planes x re/im), B = the separable (u, v) taps (4 N-tiles
+// of 16 columns), K = 4 records per K-step.
+//
+// Region-resident accumulation.  With (q, re/im) on the rows, lane l holds
+// element i of N-tile t at plane q = 2 (l >> 4) + (i >> 1), component i & 1,
+// tap (kx, ky) = (2t + ((l & 15) >> 3), l & 7): its 4 values are 4
+// consecutive floats of the footprint cell (xo + kx, yo + ky) when the LDS
+// region tile stores each cell's 8 planes x re/im as 16 consecutive floats
+// ([x][y][q][re/im], 64 B per cell).  So a cell's accumulators are LOADED
+// from the region tile when the cell starts (4 ds_read_b128), the MFMAs add
+// on top, and they are STORED back when it ends (4 ds_write_b128): no
+// zeroing, no read-add-write per element (the previous layout spent ~80
+// VALU + LDS instructions per cell change on that).  A cell's footprint
+// overlaps its neighbours', and one wave's LDS operations execute in
+// program order, so the store of a cell always precedes the load of the next.
+//
+// Taps: per block of 16 records the 16 x 3 x 8 one-dimensional taps are
+// evaluated once with every lane busy (lane l: tap l & 7 of records
+// 8m + (l >> 3)) into an LDS tap block of one 24-float row per record (tu in
+// h-major order so a lane's four B taps are one ds_read_b128, tv, tw) and a
+// 2-float value row; the 24-float pitch (24 mod 32 banks) makes the tap
+// writes and the operand reads bank-conflict-free (the 28-float pitch cost
+// 88 % of the LDS cycles in conflicts, profiles/r02_k_grid_mfma_pad_pmc.json).
+// The block's (up to) 4 K-steps are unrolled with compile-time LDS offsets.
+// The region tile is flushed once per item with buffer float atomics.
+constexpr int kTapRec = 24;    // floats per record row of the tap block
+constexpr int kTapBatch = 16;  // records per tap block
+constexpr int kRegX = 9, kRegY = 15;  // region tile: (2 + 8 - 1) x (8 + 8 - 1) cells
+constexpr int kRegCell = 16;          // floats per region cell: 8 planes x re/im
 
-template <int W, bool WS>
-constexpr int mfma_tile_f2() {  // region tile, rounded to 16 B
-    return (((WS ? W : 1) * (2 + W - 1) * (8 + W - 1)) + 1) & ~1;
-}
-
-template <int W, bool WS>
 constexpr size_t grid_mfma_pad_lds() {
-    return (size_t)mfma_tile_f2<W, WS>() * sizeof(float2) + kTapBatch * sizeof(float4) +
-           (size_t)kTapBatch * kTapRec * sizeof(float);
+    return (size_t)kRegX * kRegY * kRegCell * sizeof(float) + kTapBatch * sizeof(float4) +
+           (size_t)kTapBatch * kTapRec * sizeof(float) + kTapBatch * sizeof(float2);
 }
 
 template <int W, bool WS>
@@ -1015,10 +1028,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     const unsigned *__restrict__ offs, float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
     constexpr int NQ = WS ? W : 1;
-    float4 *const stage = reinterpret_cast<float4 *>(tile + mfma_tile_f2<W, WS>());  // fu fv fw -
+    constexpr int RX = 2 + W - 1, RY = 8 + W - 1;  // cells a footprint of the group reaches
+    float *const reg = reinterpret_cast<float *>(tile);  // [kRegX][kRegY][16]
+    float4 *const stage = reinterpret_cast<float4 *>(reg + kRegX * kRegY * kRegCell);
     float *const blk = reinterpret_cast<float *>(stage + kTapBatch);  // [kTapBatch][kTapRec]
+    float2 *const cval = reinterpret_cast<float2 *>(blk + kTapBatch * kTapRec);
     const uint32_t stride = item_stride(n_items);
     const int lane = threadIdx.x;
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
@@ -1028,18 +1043,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     const float tihw = (float)tt * ihw;
     float *const tap_dst = blk + (lane >> 3) * kTapRec;
     const int wu = (tt & 1) * 4 + (tt >> 1), wv = 8 + tt, ww = 16 + tt;
-    // K-step j: record 4j + (lane >> 4); A row lane & 15 = (tu h, tv tap),
-    // B column lane & 15 = (tw tap, re / im)
-    const float *const kA = blk + (lane >> 4) * kTapRec + ((lane >> 3) & 1) * 4;
+    // K-step j: record 4j + (lane >> 4).  B column lane & 15 = (tu h, tv
+    // tap); A row lane & 15 = (tw tap, re / im)
+    const float *const kB = blk + (lane >> 4) * kTapRec + ((lane >> 3) & 1) * 4;
     const float *const kV = blk + (lane >> 4) * kTapRec + 8 + (lane & 7);
     const float *const kW = blk + (lane >> 4) * kTapRec + 16 + ((lane & 15) >> 1);
-    const float *const kC = blk + (lane >> 4) * kTapRec + 24 + (lane & 1);
-    const bool col_im = lane & 1;
-    // accumulator element i of M-tile t: tap (2t + (lane >> 5), 4 ((lane >> 4) & 1) + i),
-    // column (q, re/im) = ((lane & 15) >> 1, lane & 1)
-    const int cq = (lane & 15) >> 1;
-    const int ckx = lane >> 5, cky = 4 * ((lane >> 4) & 1);
-    float *const ftile = reinterpret_cast<float *>(tile);
+    const float *const kC = reinterpret_cast<const float *>(cval) + (lane >> 4) * 2 + (lane & 1);
+    // this lane's accumulator slot in a footprint cell (xo, yo) + (kx, ky):
+    // float offset ((xo + 2t + h) * kRegY + yo + (l & 7)) * 16 + 4 (l >> 4)
+    const int acc_lane = ((((lane & 15) >> 3) * kRegY) + (lane & 7)) * kRegCell + 4 * (lane >> 4);
+    constexpr int acc_t = 2 * kRegY * kRegCell;  // + t N-tiles (two x rows each)
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
         uint32_t bnd[kGroupCell - 1];  // ends of cells 0..14 of the group (record indices)
@@ -1055,49 +1068,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
-        wave_lds_sync();
-        for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
+        wave_lds_sync();  // the previous item's flush reads of the region
+        {
+            float4 *r4 = reinterpret_cast<float4 *>(reg);
+            for (int i = lane; i < kRegX * kRegY * kRegCell / 4; i += 64)
+                r4[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
 
         floatx4 acc[4];
+        int cur = -1;    // cell of the accumulators (wave-uniform)
+        int cbase = 0;   // its accumulator base offset (floats) in the region
+        auto store_cell = [&]() {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-        int cur = -1;  // cell of the accumulators (wave-uniform)
-        auto flush_cell = [&]() {
-            const int xo = cur & 1, yo = cur >> 1;
-            if (cq < NQ) {
+            for (int t = 0; t < 4; ++t)
+                *reinterpret_cast<floatx4 *>(reg + cbase + t * acc_t) = acc[t];
+        };
+        auto load_cell = [&](int cell) {
+            const int xo = cell & 1, yo = cell >> 1;
+            cbase = (xo * kRegY + yo) * kRegCell + acc_lane;
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int kx = 2 * t + ckx;
-                    if (kx >= W) continue;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int ky = cky + i;
-                        if (ky >= W) continue;
-                        float *d = ftile + ((cq * RX + xo + kx) * RY + yo + ky) * 2 + (col_im ? 1 : 0);
-                        *d += acc[t][i];
-                    }
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int t = 0; t < 4; ++t)
+                acc[t] = *reinterpret_cast<const floatx4 *>(reg + cbase + t * acc_t);
         };
         struct Ops {
-            floatx4 a;
+            floatx4 b;
             float v, w, c;
         };
         auto kload = [&](int j) {
             Ops o;
-            o.a = *reinterpret_cast<const floatx4 *>(kA + 4 * j * kTapRec);
+            o.b = *reinterpret_cast<const floatx4 *>(kB + 4 * j * kTapRec);
             o.v = kV[4 * j * kTapRec];
             o.w = kW[4 * j * kTapRec];
-            o.c = kC[4 * j * kTapRec];
+            o.c = kC[8 * j];
             return o;
         };
         auto kmfma = [&](const Ops &o) {
-            const float b = o.w * o.c;
+            const float a = o.w * o.c;
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.a[t] * o.v, b, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, o.b[t] * o.v, acc[t], 0, 0, 0);
         };
 
         RecC nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
@@ -1117,16 +1126,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             const int prev = __shfl_up(cj, 4);
             uint64_t chg = __ballot((lane & 3) == 0 && lane >= 4 && prev != cj);
             if (__builtin_amdgcn_readfirstlane(cj) != cur) chg |= 1ull;
-            // two halves of kTapBatch records: taps, then their K-steps
+            // blocks of kTapBatch records: taps, then their K-steps
             for (int h = 0; h < 64 / kTapBatch; ++h) {
                 const int nbh = min(kTapBatch, nb - kTapBatch * h);
                 if (nbh <= 0) break;
-                wave_lds_sync();  // previous half's tap block reads
+                wave_lds_sync();  // the previous block's tap reads
                 if (lane / kTapBatch == h) {
                     const int r = lane % kTapBatch;
                     stage[r] = make_float4(fu, fv, fw, 0.0f);
-                    *reinterpret_cast<float2 *>(blk + r * kTapRec + 24) =
-                        make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
+                    cval[r] = make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
                 }
                 wave_lds_sync();
                 {
@@ -1154,59 +1162,54 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                 const uint64_t hchg = chg >> (kTapBatch * h);
                 const int nk = nbh >> 2;
                 // the block's (up to) 4 K-steps unrolled: every operand read
-                // up front at compile-time offsets, a cell change (bit 4j)
-                // flushes the accumulators between two K-steps
-                {
-                    Ops o[kTapBatch / 4];
+                // up front at compile-time offsets; a cell change (bit 4j)
+                // stores the accumulators and loads the next cell's
+                Ops o[kTapBatch / 4];
 #pragma unroll
-                    for (int jj = 0; jj < kTapBatch / 4; ++jj) o[jj] = kload(jj);
+                for (int jj = 0; jj < kTapBatch / 4; ++jj) o[jj] = kload(jj);
 #pragma unroll
-                    for (int jj = 0; jj < kTapBatch / 4; ++jj) {
-                        if (jj < nk) {
-                            if ((hchg >> (4 * jj)) & 1ull) {
-                                if (cur >= 0) flush_cell();
-                                cur = __builtin_amdgcn_readlane(cj, kTapBatch * h + 4 * jj);
-                            }
-                            kmfma(o[jj]);
+                for (int jj = 0; jj < kTapBatch / 4; ++jj) {
+                    if (jj < nk) {
+                        if ((hchg >> (4 * jj)) & 1ull) {
+                            if (cur >= 0) store_cell();
+                            cur = __builtin_amdgcn_readlane(cj, kTapBatch * h + 4 * jj);
+                            load_cell(cur);
                         }
+                        kmfma(o[jj]);
                     }
                 }
             }
         }
-        if (cur >= 0) flush_cell();
+        if (cur >= 0) store_cell();
         wave_lds_sync();
 
-        // flush: float f = i0 + lane of each plane's RX x RY complex cells,
-        // buffer atomics off a per-plane descriptor (32-bit offsets), the
-        // cell index advanced incrementally; zero floats are skipped
+        // flush: lane l takes float f = i0 + l of a plane's RX x RY cells in
+        // the grid's order (x rows of RY cells, re/im interleaved), i.e.
+        // region float (x * kRegY + y) * 16 + 2 q + (f & 1); buffer atomics off
+        // a per-plane descriptor (32-bit offsets); zero floats are skipped
         constexpr int FPP = RX * RY * 2;
         const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
-        int xl = (lane >> 1) / RY, yl = (lane >> 1) - xl * RY;
 #pragma unroll
         for (int i0 = 0; i0 < FPP; i0 += 64) {
             const int f = i0 + lane;
             if (f >= FPP) break;
+            const int c = f >> 1, xl = c / RY, yl = c - xl * RY;
             int gx = ibase + xl;
             if (gx >= g.ngx) gx -= g.ngx;
             int gy = jbase + yl;
             if (gy >= g.ngy) gy -= g.ngy;
             const int voff = ((gx * g.ngy + gy) * 2 + (f & 1)) * (int)sizeof(float);
+            const float *src = reg + (xl * kRegY + yl) * kRegCell + (f & 1);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int p = (int)it.p0 + q;
-                const float val = ftile[q * PS * 2 + f];
+                const float val = src[2 * q];
                 if (p >= p_lo && p < p_hi && val != 0.0f) {
                     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                         grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)), 0,
                         (int)plane_bytes, 0x00020000);
                     __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, rs, voff, 0, 0);
                 }
-            }
-            yl += 32 % RY;
-            xl += 32 / RY;
-            if (yl >= RY) {
-                yl -= RY;
-                ++xl;
             }
         }
     }
@@ -1865,14 +1868,14 @@ struct KeptBuckets {
 };
 
 // The resident planes of a batched invert between its FIRST and LAST batch:
-// the workspace generation and plane buffer they live in, the geometry and
-// the bounds.  A later batch must match it; any other wstack call (a fresh
+// the plane buffer they live in (its workspace epoch: any reallocation or
+// release changes it), the geometry and the bounds.  A later batch must match it; any other wstack call (a fresh
 // non-batched plan) or a workspace release invalidates it, so a batch that
 // would accumulate into planes another call has overwritten or freed is
 // refused instead of gridding into them.
 struct BatchSeq {
     bool valid = false;
-    uint64_t gen = 0;
+    uint64_t epoch = 0;
     const void *grid = nullptr;
     int nx = 0, ny = 0, do_w = 0, nplanes = 0;
     double px = 0, py = 0, eps = 0;
@@ -1938,7 +1941,7 @@ static Plan reuse_buckets(const Inputs &in) {
 static BatchSeq batch_token(const Plan &P, const Inputs &in) {
     BatchSeq s;
     s.valid = true;
-    s.gen = Workspace::get().generation();
+    s.epoch = Workspace::get().epoch("grid");
     s.grid = P.grid;
     s.nx = in.nx;
     s.ny = in.ny;
@@ -1960,7 +1963,7 @@ static void check_batch_seq(const Plan &P, const Inputs &in, bool first) {
         cur = t;
         return;
     }
-    SDP_REQUIRE(cur.valid && cur.gen == t.gen && cur.grid == t.grid,
+    SDP_REQUIRE(cur.valid && cur.epoch == t.epoch && cur.grid == t.grid,
                 "batched invert: no resident planes of this sequence (its first batch did not "
                 "run, or another wstack call or a workspace release came in between)");
     bool same = cur.nx == t.nx && cur.ny == t.ny && cur.do_w == t.do_w &&
@@ -2299,7 +2302,7 @@ static void launch_grid_mfma_fi(const Plan &P, int p_lo, int p_hi, hipStream_t s
 
 template <int W, bool WS>
 static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
-    constexpr size_t lds = grid_mfma_pad_lds<W, WS>();
+    constexpr size_t lds = grid_mfma_pad_lds();
     const auto r = chunk_items(P, p_lo, p_hi);
     const unsigned n = r.second - r.first;
     if (n == 0) return;

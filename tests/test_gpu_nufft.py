@@ -586,11 +586,12 @@ def test_batch_bounds_too_tight_are_refused():
     with ValueError instead of indexing outside the histogram / planes."""
     from ska_sdp_func_python_amd import kernels
     uvw, freq, ms, wgt, cell = _problem(22, nrow=2000, nchan=3, umax=6000.0)
+    uvw[:, 2] *= 200.0  # w spans many planes at this field of view
     U, F, M = T(uvw), T(freq), T(ms)
     b = kernels.uvw_bounds(U, F)
     for tight in ([b[0], b[1], 0.5 * b[2], b[3], b[4], b[5]],           # u range too small
                   [b[0], 0.5 * (b[0] + b[1]), b[2], b[3], b[4], b[5]],   # w range too small
-                  [b[0], b[1], b[2], b[3], b[4], 0.7 * b[5]]):           # fmax too low
+                  [b[0], b[1], b[2], b[3], 0.7 * b[4], 0.7 * b[5]]):     # frequencies too low
         with pytest.raises(ValueError, match="outside"):
             kernels.ms2dirty_batch(U, F, M, None, 256, 256, cell, cell, tight, first=True,
                                    last=True, epsilon=1e-7)
