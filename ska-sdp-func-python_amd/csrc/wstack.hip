@@ -465,7 +465,7 @@ __global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw,
                           wd);
         }
         if (!valid) return;
-        mine = rk[v];
+        mine = rk[vg];
         if (mine == 0xffffffffu) return;
         c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
     } else {
@@ -581,6 +581,29 @@ __global__ void k_items_fill(int64_t ngroups, int grp, int groups_per_plane,
         x.e = min(e, s + chunk);
         x.tile = tile;
         x.p0 = p0;
+        items[o++] = x;
+    }
+}
+
+// work items of one-cell buckets: FineItem descriptors that carry the
+// group's 16 cell ends, so a (de)gridding wave has them from one 80-byte
+// scalar load instead of a second dependent round trip to the offsets
+__global__ void k_items_fill_cells(int64_t ngroups, int groups_per_plane,
+                                   const unsigned *__restrict__ offs,
+                                   const unsigned *__restrict__ ioffs, unsigned chunk,
+                                   FineItem *items) {
+    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (k >= ngroups) return;
+    FineItem x;
+    const unsigned b = offs[k * kGroupCell], e = offs[(k + 1) * kGroupCell];
+#pragma unroll
+    for (int j = 0; j < kGroupCell; ++j) x.o[j] = offs[k * kGroupCell + j + 1];
+    x.p0 = (uint32_t)(k / groups_per_plane);
+    x.tile = (uint32_t)(k - (int64_t)x.p0 * groups_per_plane);
+    unsigned o = ioffs[k];
+    for (unsigned s = b; s < e; s += chunk) {
+        x.b = s;
+        x.e = min(e, s + chunk);
         items[o++] = x;
     }
 }
@@ -712,20 +735,24 @@ __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__re
 // ------------------------------------------------------------------------
 // kernels: gridding / degridding (the hot loops)
 // ------------------------------------------------------------------------
-// Work items are visited in a strided order (stride coprime with the item
-// count): the heavy chunks of one dense tile are spread over the launch
-// instead of flushing into the same cells at the same time.
-__device__ __forceinline__ uint32_t item_stride(uint32_t n) {
-    const uint32_t primes[5] = {7919u, 104729u, 1299709u, 15485863u, 179424673u};
-    for (int k = 0; k < 5; ++k)
-        if (n <= 1 || n % primes[k] != 0) return primes[k];
-    return 1u;
+// Work items are visited transposed: workgroup w = q m + r (m = n / K)
+// takes item r K + q, so the consecutive items of one dense tile (the chunks
+// of a heavy cell group) go to workgroups m apart -- spread over the launch
+// instead of flushing into the same grid cells at the same time (visiting
+// them a few workgroups apart made C2 gridding 5x slower on atomic
+// contention), and consecutive workgroups take items K apart.  32-bit
+// scalar arithmetic (the previous 64-bit "w * prime % n" cost ~100 SALU per
+// item).
+constexpr uint32_t kItemSpread = 64;
+__device__ __forceinline__ uint32_t item_index(uint32_t w, uint32_t n) {
+    const uint32_t m = n / kItemSpread;
+    if (w >= kItemSpread * m) return w;
+    const uint32_t q = w / m, r = w - q * m;
+    return r * kItemSpread + q;
 }
 
-__device__ __forceinline__ Item load_item(const Item *items, uint32_t w, uint32_t n,
-                                          uint32_t stride) {
-    const uint32_t i = (uint32_t)(((uint64_t)w * stride) % n);
-    const Item raw = items[i];
+__device__ __forceinline__ Item load_item(const Item *items, uint32_t w, uint32_t n) {
+    const Item raw = items[item_index(w, n)];
     Item it;
     it.b = __builtin_amdgcn_readfirstlane(raw.b);
     it.e = __builtin_amdgcn_readfirstlane(raw.e);
@@ -736,9 +763,8 @@ __device__ __forceinline__ Item load_item(const Item *items, uint32_t w, uint32_
 
 template <int NO>
 __device__ __forceinline__ Item load_fine_item(const FineItem *items, uint32_t w, uint32_t n,
-                                               uint32_t stride, uint32_t (&fo)[NO]) {
-    const uint32_t i = (uint32_t)(((uint64_t)w * stride) % n);
-    const FineItem raw = items[i];
+                                               uint32_t (&fo)[NO]) {
+    const FineItem raw = items[item_index(w, n)];
     Item it;
     it.b = __builtin_amdgcn_readfirstlane(raw.b);
     it.e = __builtin_amdgcn_readfirstlane(raw.e);
@@ -791,14 +817,17 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// ES kernel for the MFMA gridder's taps: x = fu*ihw + t*ihw by one fma; for
-// W = 8 every tap of the footprint lies inside the support (|x| <= 1), so
-// no range select (the max() only guards rounding below zero)
+// ES kernel for the MFMA gridder's taps: x = fu*ihw + t*ihw by one fma.  For
+// W = 8 every tap of the footprint lies inside the support: the first tap's
+// offset f is in [-4, -3] and ihw = 1/4 scales exactly, so x = (f + t) / 4 in
+// [-1, 1] and y = 1 - x^2 >= 0 with no range select and no clamp (for other
+// W, 2/W rounds, so y is clamped and taps outside the support are zeroed)
 template <int W>
 __device__ __forceinline__ float es_tap(float f, float tihw, float ihw, float bl) {
     const float x = fmaf(f, ihw, tihw);
     const float y = fmaf(-x, x, 1.0f);
-    const float e = __builtin_amdgcn_exp2f(fmaf(bl, __builtin_amdgcn_sqrtf(fmaxf(y, 0.0f)), -bl));
+    const float e = __builtin_amdgcn_exp2f(
+        fmaf(bl, __builtin_amdgcn_sqrtf(W == 8 ? y : fmaxf(y, 0.0f)), -bl));
     return W == 8 ? e : (y > 0.0f ? e : 0.0f);
 }
 
@@ -813,7 +842,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
     constexpr int NQ = WS ? W : 1;
     float4 *const stage = reinterpret_cast<float4 *>(tile + NQ * PS);  // [64][2]
-    const uint32_t stride = item_stride(n_items);
     const int lane = threadIdx.x;
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
     const float tihw = (float)(lane & 7) * ihw;
@@ -829,7 +857,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
         uint32_t fo[1];
-        const Item it = load_fine_item<1>(fitems, w_it, n_items, stride, fo);
+        const Item it = load_fine_item<1>(fitems, w_it, n_items, fo);
         if (it.b >= it.e) continue;
         const int ntg = g.wny / 8;  // groups per x pair
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
@@ -1024,8 +1052,8 @@ constexpr size_t grid_mfma_pad_lds() {
 
 template <int W, bool WS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma_pad(
-    Geo g, const RecC *__restrict__ recs, const Item *__restrict__ items, uint32_t n_items,
-    const unsigned *__restrict__ offs, float *__restrict__ grid, int p_lo, int p_hi) {
+    Geo g, const RecC *__restrict__ recs, const FineItem *__restrict__ items, uint32_t n_items,
+    float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int NQ = WS ? W : 1;
@@ -1034,7 +1062,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     float4 *const stage = reinterpret_cast<float4 *>(reg + kRegX * kRegY * kRegCell);
     float *const blk = reinterpret_cast<float *>(stage + kTapBatch);  // [kTapBatch][kTapRec]
     float2 *const cval = reinterpret_cast<float2 *>(blk + kTapBatch * kTapRec);
-    const uint32_t stride = item_stride(n_items);
     const int lane = threadIdx.x;
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
     const float fbase = 1.0f - 0.5f * (float)W;  // RecC offset origin
@@ -1055,15 +1082,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     constexpr int acc_t = 2 * kRegY * kRegCell;  // + t N-tiles (two x rows each)
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        uint32_t bnd[kGroupCell - 1];  // ends of cells 0..14 of the group (record indices)
-        const Item it = load_item(items, w_it, n_items, stride);
-        {
-            // the group's 16 cell buckets end at ob[1..16]
-            const unsigned *ob = offs + ((size_t)it.p0 * g.ntiles + (size_t)it.tile * kGroupCell);
-#pragma unroll
-            for (int c = 0; c < kGroupCell - 1; ++c)
-                bnd[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
-        }
+        // the item and the ends of its group's cells 0..14 (record indices):
+        // one 80-byte descriptor, scalar loads
+        uint32_t bnd[kGroupCell];
+        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
         const int ntg = g.nty / 8;  // groups per x pair
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
@@ -1231,11 +1253,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 // region whose W planes are staged in LDS once).  The record factor
 // wgt * exp(-2 pi i w s0) is applied and the visibility written in place
 // (vdirect), or the raw sum added to acc[record] for k_finalize.
-template <int W, bool WS, bool FI>
+template <int W, bool WS>
 __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restrict__ recs,
-                                                    const Item *__restrict__ items,
                                                     uint32_t n_items,
-                                                    const unsigned *__restrict__ offs,
                                                     const FineItem *__restrict__ fitems,
                                                     const float2 *__restrict__ grid, int p_lo,
                                                     int p_hi, float2 *__restrict__ acc,
@@ -1244,7 +1264,6 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
     constexpr int NQ = WS ? W : 1;
-    const uint32_t stride = item_stride(n_items);
     const int lane = threadIdx.x;
     const int r16 = lane & 15, kg = lane >> 4;
     const float ihw = g.inv_half_w, bl = g.beta_l2e;
@@ -1257,16 +1276,9 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
         uint32_t fo[kGroupCell];
         Item it;
-        if (FI) {
-            it = load_fine_item<kGroupCell>(fitems, w_it, n_items, stride, fo);
-            if (it.b >= it.e) continue;
-        } else {
-            it = load_item(items, w_it, n_items, stride);
-            const unsigned *ob = offs + ((size_t)it.p0 * g.ntiles + (size_t)it.tile * kGroupCell);
-#pragma unroll
-            for (int c = 0; c < kGroupCell; ++c) fo[c] = __builtin_amdgcn_readfirstlane(ob[c + 1]);
-        }
-        const int ntg = FI ? g.wny / 8 : g.nty / 8;  // groups per x pair
+        it = load_fine_item<kGroupCell>(fitems, w_it, n_items, fo);
+        if (it.b >= it.e) continue;
+        const int ntg = g.wny / 8;  // groups per x pair
         const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
         const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
 
@@ -1739,8 +1751,9 @@ struct Part {
     unsigned *hist = nullptr, *offs = nullptr, *nch = nullptr, *ioffs = nullptr;
     unsigned long long *nbad = nullptr;
     unsigned *npad = nullptr;  // pad records of a 4-padded plan (device)
-    Item *items = nullptr;
-    FineItem *fitems = nullptr;  // 16 per coarse item when sub-sorted (k_subsort)
+    Item *items = nullptr;       // coarse (16x16-cell) plans
+    FineItem *fitems = nullptr;  // one-cell plans: one per item; coarse plans: 16 per
+                                 // item after the sub-sort (k_subsort)
     unsigned *meta = nullptr;    // device: see k_part_meta
     // host copies (read_part_meta)
     int64_t nrec = 0, nitems = 0;
@@ -2163,7 +2176,9 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
     pt.nbad = scratch<unsigned long long>("nbad", 1);
     pt.meta = scratch<unsigned>("meta", g.nps + 5);
     const int64_t icap = std::min<int64_t>(ngroups, pt.nvis) + pt.nvis / P.chunk + 1;
-    pt.items = scratch<Item>("items", icap);
+    const bool cells = g.sub == kTileCell;
+    if (cells) pt.fitems = scratch<FineItem>("fitems", icap);
+    else pt.items = scratch<Item>("items", icap);
     unsigned *kr = scratch<unsigned>("key_rank", std::max<int64_t>(pt.nvis, 1));
     if (!values_only) {
         SDP_HIP_CHECK(hipMemsetAsync(pt.hist, 0, (nkeys + 1) * sizeof(unsigned), st));
@@ -2255,8 +2270,12 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
     tb = tmp_bytes + 16;
     SDP_HIP_CHECK(
         hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.nch, pt.ioffs, (int)(ngroups + 1), st));
-    k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, kpg, gpp, pt.offs, pt.ioffs,
-                                                       P.chunk, pt.items);
+    if (cells)
+        k_items_fill_cells<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, gpp, pt.offs, pt.ioffs,
+                                                                 P.chunk, pt.fitems);
+    else
+        k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, kpg, gpp, pt.offs, pt.ioffs,
+                                                           P.chunk, pt.items);
     k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys,
                                                       P.pad4 ? pt.npad : nullptr, pt.ioffs, gpp,
                                                       g.nps, pt.meta);
@@ -2307,8 +2326,8 @@ static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t 
     const unsigned n = r.second - r.first;
     if (n == 0) return;
     k_grid_mfma_pad<W, WS><<<n, 64, lds, st>>>(P.g, reinterpret_cast<const RecC *>(P.recs),
-                                               P.pt.items + r.first, n, P.pt.offs,
-                                               (float *)P.grid, p_lo, p_hi);
+                                               P.pt.fitems + r.first, n, (float *)P.grid, p_lo,
+                                               p_hi);
 }
 
 template <int W>
@@ -2324,20 +2343,13 @@ static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
 template <int W, bool WS>
 static void launch_degrid_mfma(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) * (2 + W - 1) * (8 + W - 1) * sizeof(float2);
+    // one-cell plans: one FineItem per item; sub-sorted coarse plans: 16
     const auto r = chunk_items(P, p_lo, p_hi);
-    if (P.subsort) {
-        const unsigned n = 16u * (r.second - r.first);
-        if (n == 0) return;
-        k_degrid_mfma<W, WS, true><<<n, 64, lds, st>>>(
-            P.g, P.recs, nullptr, n, nullptr, P.pt.fitems + 16 * (size_t)r.first, P.grid, p_lo,
-            p_hi, acc, P.vdirect);
-        return;
-    }
-    const unsigned n = r.second - r.first;
+    const unsigned per = P.subsort ? 16u : 1u;
+    const unsigned n = per * (r.second - r.first);
     if (n == 0) return;
-    k_degrid_mfma<W, WS, false><<<n, 64, lds, st>>>(P.g, P.recs, P.pt.items + r.first, n,
-                                                    P.pt.offs, nullptr, P.grid, p_lo, p_hi, acc,
-                                                    P.vdirect);
+    k_degrid_mfma<W, WS><<<n, 64, lds, st>>>(P.g, P.recs, n, P.pt.fitems + per * (size_t)r.first,
+                                             P.grid, p_lo, p_hi, acc, P.vdirect);
 }
 
 template <int W>

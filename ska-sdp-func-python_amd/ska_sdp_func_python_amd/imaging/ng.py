@@ -20,6 +20,17 @@ Mirrors reference ``src/ska_sdp_func_python/imaging/ng.py``:
   (ng.py:238) is not a separate pass here.
 
 The image transpose (:102, :257) is folded into the C ABI's output strides.
+
+Multi-GPU: when torch.distributed is initialised with more
+than one rank and every rank calls with the same Visibility and model (the
+drop-in use: the reference call, unchanged, on each rank), the visibility
+channels are split into contiguous blocks balanced by the measured cost
+model (parallel.balanced_channel_blocks).  invert_ng grids only its block
+and combines the partial images and weight sums with one all-reduce each
+(the reference's only exchange point, before normalise_sumwt); predict_ng
+predicts its block and all-gathers the channel blocks.  Every rank returns
+the reference's full result.  ``shard=False`` (or SDP_HIP_SHARD=0) computes
+everything on each rank.
 Kwargs ``epsilon`` (default 1e-12, clamped to the fp32 floor 1e-7),
 ``do_wstacking`` (True), ``threads`` and ``verbosity`` are accepted as in
 the reference; ``threads`` is ignored (one GPU per process).
@@ -30,7 +41,7 @@ import logging
 import numpy as np
 import torch
 
-from .. import _device, kernels
+from .. import _device, kernels, parallel
 from ..datamodels import Image, pol_conversion_matrix
 from .base import normalise_sumwt, shift_lmn
 
@@ -61,7 +72,13 @@ def predict_ng(bvis, model, **kwargs):
     nrows, nbaselines, vnchan, vnpol = bvis.vis.shape
     uvw = _device.to_dev(bvis.uvw.data, torch.float64, dev).reshape(nrows * nbaselines, 3)
     uvw = torch.nan_to_num(uvw).contiguous()
-    freq_t = _device.to_dev(freq, torch.float64, dev)
+    shard = parallel.shard_info(kwargs)
+    blocks = [(0, vnchan)]
+    lo, hi = 0, vnchan
+    if shard:
+        blocks = parallel.balanced_channel_blocks(freq, shard[1])
+        lo, hi = blocks[shard[0]]
+    freq_t = _device.to_dev(freq[lo:hi], torch.float64, dev)
 
     pixels = _device.to_dev(model["pixels"].data, torch.float64, dev)
     m_nchan, m_npol, ny, nx = pixels.shape
@@ -76,7 +93,7 @@ def predict_ng(bvis, model, **kwargs):
     src = bvis["vis"].data
     lmn = shift_lmn(bvis, model)  # shift_vis_to_image(inverse=True) (ng.py:143), in-kernel
     vdt = src.dtype if _device.is_device(src) and src.is_complex() else torch.complex128
-    vist = torch.empty((nrows * nbaselines, vnchan, vnpol), dtype=vdt, device=dev)
+    vist = torch.empty((nrows * nbaselines, hi - lo, vnpol), dtype=vdt, device=dev)
 
     def coef(p):
         if conv is None:
@@ -86,22 +103,26 @@ def predict_ng(bvis, model, **kwargs):
         return conv[:, p]
 
     info = None
-    for vpol in range(vnpol):
+    for vpol in range(vnpol if hi > lo else 0):
         if m_nchan == 1:
             _, info = kernels.dirty2ms_vis(uvw, freq_t, pixels[0, vpol], vist, coef(vpol), pixsize,
                                            pixsize, epsilon, do_wstacking, flip_uw=True,
                                            dirty_strides=(1, nx), npix=(nx, ny),
                                            accumulate=vpol > 0, shift_lmn=lmn)
         else:
-            for vchan in range(vnchan):
+            for vchan in range(lo, hi):
                 img = pixels[int(vis_to_im[vchan]), vpol]
-                _, info = kernels.dirty2ms_vis(uvw, freq_t[vchan:vchan + 1], img,
-                                               vist[:, vchan:vchan + 1, :], coef(vpol), pixsize,
+                c = vchan - lo
+                _, info = kernels.dirty2ms_vis(uvw, freq_t[c:c + 1], img,
+                                               vist[:, c:c + 1, :], coef(vpol), pixsize,
                                                pixsize, epsilon, do_wstacking, flip_uw=True,
                                                dirty_strides=(1, nx), npix=(nx, ny),
                                                accumulate=vpol > 0, shift_lmn=lmn)
     if verbosity and info is not None:
         log.info("predict_ng: %s", info)
+    if shard:
+        # every rank's channel block, assembled on every rank
+        vist = parallel.gather_blocks(vist, blocks, shard[0], dim=1, group=shard[2])
 
     vis = vist.reshape(nrows, nbaselines, vnchan, vnpol)
     # the reference's bvis.copy(deep=True, zero=True) (ng.py:77), with the
@@ -129,6 +150,7 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     dev = _device.device()
     nchan, npol, ny, nx = model["pixels"].data.shape
     image = torch.zeros((nchan, npol, ny, nx), dtype=torch.float64, device=dev)
+    shard = parallel.shard_info(kwargs)
     # the reference's deep copy + zero fill (ng.py:173, :218) without
     # copying the model's pixels
     im = model.copy(deep=True, data=image)
@@ -138,29 +160,34 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     freq = np.asarray(sbvis.frequency.data, dtype=float)
     nrows, nbaselines, vnchan, vnpol = sbvis.vis.shape
     nrow = nrows * nbaselines
+    # this rank's visibility channels [lo, hi) (all of them unsharded)
+    lo, hi = 0, vnchan
+    if shard:
+        lo, hi = parallel.balanced_channel_blocks(freq, shard[1])[shard[0]]
+    nloc = hi - lo
 
     # The Visibility's own arrays, read in place by the fused prologue of
     # sdp_hip_ms2dirty_vis: flag masking (ng.py:191, :202), the pol-frame
     # conversion (ng.py:193-198) as one matrix row per image pol, f64 weights
     # and the weight sums (ng.py:258, :289) -- no O(Nvis) passes here.
-    flags = _device.to_dev(sbvis.flags.data, None, dev)
+    flags = _device.to_dev(sbvis.flags.data[:, :, lo:hi], None, dev)
     if flags.dtype not in kernels._FLAG_DT:
         flags = flags.to(torch.int64)
-    flags = flags.reshape(nrow, vnchan, vnpol)
-    wgt = _device.to_dev(sbvis.imaging_weight.data, None, dev)
+    flags = flags.reshape(nrow, nloc, vnpol)
+    wgt = _device.to_dev(sbvis.imaging_weight.data[:, :, lo:hi], None, dev)
     if wgt.dtype not in (torch.float32, torch.float64):
         wgt = wgt.to(torch.float64)
-    wgt = wgt.reshape(nrow, vnchan, vnpol)
+    wgt = wgt.reshape(nrow, nloc, vnpol)
     ms = None
     if not dopsf:
-        ms = _device.to_dev(sbvis.vis.data, None, dev)
+        ms = _device.to_dev(sbvis.vis.data[:, :, lo:hi], None, dev)
         if ms.dtype not in (torch.complex64, torch.complex128):
             ms = ms.to(torch.complex128)
-        ms = ms.reshape(nrow, vnchan, vnpol)
+        ms = ms.reshape(nrow, nloc, vnpol)
     conv = pol_conversion_matrix(bvis.visibility_acc.polarisation_frame,
                                  im.image_acc.polarisation_frame)
     uvw = _device.to_dev(sbvis.uvw.data, torch.float64, dev).reshape(nrow, 3).contiguous()
-    freq_t = _device.to_dev(freq, torch.float64, dev)
+    freq_t = _device.to_dev(freq[lo:hi], torch.float64, dev)
 
     npixdirty = nx
     pixsize = _pixsize(im)
@@ -191,14 +218,19 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
             log.info("invert_ng: %s", info)
 
     if mfs:
-        for pol in range(npol):
-            grid_pol(pol, slice(0, vnchan), 0)
+        for pol in range(npol if nloc > 0 else 0):
+            grid_pol(pol, slice(0, nloc), 0)
     else:
         # channel-major (the reference loops pol-major, ng.py:259-289; each
         # (pol, chan) image is independent, so the order does not matter)
-        for vchan in range(vnchan):
+        for vchan in range(lo, hi):
             for pol in range(npol):
-                grid_pol(pol, slice(vchan, vchan + 1), int(vis_to_im[vchan]))
+                grid_pol(pol, slice(vchan - lo, vchan - lo + 1), int(vis_to_im[vchan]))
+    if shard:
+        # the one exchange: partial images and weight sums of the ranks'
+        # channel blocks (before normalise_sumwt, ng.py:292)
+        parallel.all_reduce_sum(image, shard[2])
+        parallel.all_reduce_sum(sumwt_d, shard[2])
     sumwt = sumwt_d.cpu().numpy()
 
     im["pixels"].data = image

@@ -15,6 +15,54 @@ import torch
 import torch.distributed as dist
 
 
+def shard_info(kwargs=None):
+    """(rank, world, group) when the reference-shaped API (invert_ng,
+    predict_ng, solve_gaintable) should shard its work across the ranks of
+    the default process group: torch.distributed initialised with more than
+    one rank, every rank calling with the same (replicated) inputs.  Each rank
+    then computes its share and one collective combines the shares, so every
+    rank returns the reference's full result.  Disabled by the kwarg
+    ``shard=False`` or SDP_HIP_SHARD=0 (each rank then computes everything)."""
+    import os
+    if kwargs is not None and kwargs.get("shard", True) is False:
+        return None
+    if os.environ.get("SDP_HIP_SHARD", "1") == "0":
+        return None
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    world = dist.get_world_size()
+    if world <= 1:
+        return None
+    return dist.get_rank(), world, None
+
+
+def all_reduce_sum(t, group=None):
+    """In-place SUM all-reduce of a real or complex tensor (complex as its
+    real view, which every backend accepts)."""
+    dist.all_reduce(torch.view_as_real(t) if t.is_complex() else t, op=dist.ReduceOp.SUM,
+                    group=group)
+    return t
+
+
+def gather_blocks(local, blocks, rank, dim, group=None):
+    """Every rank's contiguous block [lo, hi) of axis ``dim`` (blocks =
+    [(lo, hi)] per rank, ``local`` = this rank's block) assembled into the
+    full tensor on every rank: one all_gather of the blocks padded to the
+    largest (complex tensors as their real view)."""
+    width = max(hi - lo for lo, hi in blocks)
+    x = local.movedim(dim, 0)
+    pad = torch.zeros((width,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    pad[:x.shape[0]] = x
+    if pad.is_complex():
+        pad = torch.view_as_real(pad)
+    parts = [torch.empty_like(pad) for _ in blocks]
+    dist.all_gather(parts, pad.contiguous(), group=group)
+    if local.is_complex():
+        parts = [torch.view_as_complex(q) for q in parts]
+    full = torch.cat([q[:hi - lo] for q, (lo, hi) in zip(parts, blocks)], dim=0)
+    return full.movedim(0, dim).contiguous()
+
+
 def shard_range(n, rank, world):
     """Contiguous [lo, hi) block of n items for ``rank`` of ``world``."""
     base, extra = divmod(n, world)
