@@ -17,6 +17,14 @@ Mirrors reference ``src/ska_sdp_func_python/calibration/solvers.py``:
 The point-source sums (:99-107) are formed on the device; the reference's
 dense [nants, nants] matrix (:108-114) is replaced by a canonical packed
 baseline order (kernels.canonical_baselines).
+
+Multi-GPU: with torch.distributed initialised (more than
+one rank, every rank calling with the same inputs) each rank forms the sums
+and solves a contiguous block of the gain rows, with no collective in the
+solve; one all-gather assembles the table on every rank, and the
+mean/median normalisation (:135-143) then runs over the whole table as in
+the reference.  ``shard=False`` (a keyword beyond the reference's) or
+SDP_HIP_SHARD=0 solves every row on every rank.
 """
 
 import logging
@@ -24,7 +32,7 @@ import logging
 import numpy as np
 import torch
 
-from .. import _device, kernels
+from .. import _device, kernels, parallel
 from ..datamodels import create_gaintable_from_visibility
 
 log = logging.getLogger("func-python-logger")
@@ -45,7 +53,8 @@ def _windows(vis_time, gain_table):
 
 
 def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=200, tol=1e-6,
-                    crosspol=False, normalise_gains="mean", jones_type="T", timeslice=None):
+                    crosspol=False, normalise_gains="mean", jones_type="T", timeslice=None,
+                    shard=True):
     if modelvis is not None:
         mv = modelvis.vis.data
         mx = float(mv.abs().max()) if isinstance(mv, torch.Tensor) else float(np.max(np.abs(mv)))
@@ -81,6 +90,17 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
     ptr, tidx, present = _windows(np.asarray(vis.time.data, dtype=float), gain_table)
     for row in np.nonzero(~present)[0]:
         log.warning("Gaintable %s, vis time mismatch %s", gain_table.time.data, vis.time.data)
+    # this rank's gain rows [r0, r1) (all of them unsharded)
+    nrow_g = len(present)
+    sh = parallel.shard_info({"shard": shard})
+    rblocks = [(0, nrow_g)]
+    r0, r1 = 0, nrow_g
+    if sh:
+        rblocks = [parallel.shard_range(nrow_g, r, sh[1]) for r in range(sh[1])]
+        r0, r1 = rblocks[sh[0]]
+    tidx = tidx[ptr[r0]:ptr[r1]]
+    ptr = (ptr[r0:r1 + 1] - ptr[r0]).astype(np.int32)
+    present = present[r0:r1]
     bl = np.asarray(vis.baselines.data)
     perm, conj, row_start, ant2 = kernels.canonical_baselines(bl[:, 0], bl[:, 1], nants)
     # autocorrelations go after the canonical baselines: the solver never
@@ -92,11 +112,15 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
     mfl = None
     if modelvis is not None and modelvis["flags"].data is not vis["flags"].data:
         mfl = _device.to_dev(modelvis["flags"].data, None, dev)
-    xb_all, xwt = kernels.point_sums(
-        v, m, w, fl.contiguous(), torch.as_tensor(ptr, device=dev),
-        torch.as_tensor(tidx if len(tidx) else np.zeros(1, np.int32), device=dev), nchan,
-        perm=torch.as_tensor(full_perm, device=dev),
-        conj=torch.as_tensor(full_conj.astype(np.uint8), device=dev), model_flags=mfl)
+    if r1 > r0:
+        xb_all, xwt = kernels.point_sums(
+            v, m, w, fl.contiguous(), torch.as_tensor(ptr, device=dev),
+            torch.as_tensor(tidx if len(tidx) else np.zeros(1, np.int32), device=dev), nchan,
+            perm=torch.as_tensor(full_perm, device=dev),
+            conj=torch.as_tensor(full_conj.astype(np.uint8), device=dev), model_flags=mfl)
+    else:  # more ranks than gain rows: this rank has none
+        xb_all = torch.zeros((0, len(full_perm), nchan, npol), dtype=torch.complex128, device=dev)
+        xwt = torch.zeros((0, len(full_perm), nchan, npol), dtype=torch.float64, device=dev)
     if len(autos):
         xb_c, xwt_c = xb_all[:, :nc].contiguous(), xwt[:, :nc].contiguous()
     else:
@@ -109,11 +133,17 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
     else:
         mode = 0
 
-    gain_h = gain_table["gain"].data
+    gain_h = gain_table["gain"].data[r0:r1]
+    wt_h = gain_table["weight"].data[r0:r1]
+    res_h = gain_table["residual"].data[r0:r1]
     gain = _device.to_dev(gain_h, torch.complex128, dev).contiguous().clone()
-    gwt = _device.to_dev(gain_table["weight"].data, torch.float64, dev).contiguous().clone()
-    residual, used = kernels.solve_gains(xb_c, xwt_c, gain, gwt, row_start, ant2, mode,
-                                         niter=niter, tol=tol, phase_only=phase_only)
+    gwt = _device.to_dev(wt_h, torch.float64, dev).contiguous().clone()
+    if r1 > r0:
+        residual, used = kernels.solve_gains(xb_c, xwt_c, gain, gwt, row_start, ant2, mode,
+                                             niter=niter, tol=tol, phase_only=phase_only)
+    else:
+        residual = torch.zeros(res_h.shape, dtype=torch.float64, device=dev)
+        used = torch.zeros(0, dtype=torch.int32, device=dev)
     used_h = used.cpu().numpy()
     for row in np.nonzero(used_h > niter)[0]:
         if present[row]:
@@ -131,10 +161,15 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
         gain = torch.where(keep[:, None, None, None, None],
                            _device.to_dev(gain_h, torch.complex128, dev), gain)
         gwt = torch.where(keep[:, None, None, None, None],
-                          _device.to_dev(gain_table["weight"].data, torch.float64, dev), gwt)
+                          _device.to_dev(wt_h, torch.float64, dev), gwt)
         residual = torch.where(keep[:, None, None, None],
-                               _device.to_dev(gain_table["residual"].data, torch.float64, dev),
-                               residual)
+                               _device.to_dev(res_h, torch.float64, dev), residual)
+    if sh:
+        # the ranks' row blocks assembled on every rank (the solve itself
+        # needed no exchange); the normalisation below sees the whole table
+        gain = parallel.gather_blocks(gain, rblocks, sh[0], dim=0, group=sh[2])
+        gwt = parallel.gather_blocks(gwt, rblocks, sh[0], dim=0, group=sh[2])
+        residual = parallel.gather_blocks(residual, rblocks, sh[0], dim=0, group=sh[2])
 
     if normalise_gains in ["median", "mean"] and not phase_only:
         ga = gain.abs().flatten()

@@ -36,11 +36,21 @@ def shard_info(kwargs=None):
     return dist.get_rank(), world, None
 
 
+def _host_staged(group, t):
+    """gloo (the CPU backend) is given host copies of device tensors."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def all_reduce_sum(t, group=None):
     """In-place SUM all-reduce of a real or complex tensor (complex as its
     real view, which every backend accepts)."""
-    dist.all_reduce(torch.view_as_real(t) if t.is_complex() else t, op=dist.ReduceOp.SUM,
-                    group=group)
+    x = torch.view_as_real(t) if t.is_complex() else t
+    if _host_staged(group, x):
+        h = x.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        x.copy_(h)
+    else:
+        dist.all_reduce(x, op=dist.ReduceOp.SUM, group=group)
     return t
 
 
@@ -55,8 +65,12 @@ def gather_blocks(local, blocks, rank, dim, group=None):
     pad[:x.shape[0]] = x
     if pad.is_complex():
         pad = torch.view_as_real(pad)
+    dev = pad.device
+    if _host_staged(group, pad):
+        pad = pad.cpu()
     parts = [torch.empty_like(pad) for _ in blocks]
     dist.all_gather(parts, pad.contiguous(), group=group)
+    parts = [q.to(dev) for q in parts]
     if local.is_complex():
         parts = [torch.view_as_complex(q) for q in parts]
     full = torch.cat([q[:hi - lo] for q, (lo, hi) in zip(parts, blocks)], dim=0)

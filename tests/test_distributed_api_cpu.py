@@ -1,0 +1,141 @@
+"""CPU, world_size 2 over gloo: the reference-shaped API itself -- invert_ng
+and predict_ng -- sharding a replicated Visibility across ranks when
+torch.distributed is initialised (imaging/ng.py: channel blocks from
+parallel.balanced_channel_blocks, one all-reduce of image + sumwt for
+invert, an all-gather of the channel blocks for predict).  Every rank must
+return the unsharded result.
+
+There is no GPU here, so inside the test processes the two HIP entry points
+invert_ng / predict_ng call (kernels.ms2dirty_vis, kernels.dirty2ms_vis) are
+replaced by the exact-sum oracle and the device by the CPU (test injection:
+what is checked is the API's partitioning and collectives, which run
+unchanged).  The GPU counterpart, through the real kernels, is
+tests/test_gpu_parallel.py::test_api_sharding_two_ranks_one_gpu."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import nufft_oracle as orc
+
+FLIP = np.array([-1.0, 1.0, -1.0])
+SEEN = set()  # visibility channels (frequencies) this process computed
+
+
+def _oracle_ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, px, py,
+                         epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
+                         out_strides=None, accumulate=False, sumwt=None, shift_lmn=None,
+                         keep_buckets=False, reuse_buckets=False):
+    assert shift_lmn is None
+    SEEN.update(freq.numpy().tolist())
+    m = 1.0 - flags.numpy().astype(float)
+    w = wgt.numpy() * m[..., pol]
+    if vis is None:
+        v = np.ones(w.shape, complex)
+    elif coef is None:
+        v = vis.numpy()[..., pol] * m[..., pol]
+    else:
+        v = sum(complex(c) * vis.numpy()[..., k] * m[..., k] for k, c in enumerate(coef))
+    d = orc.ms2dirty_exact(uvw.numpy() * (FLIP if flip_uw else 1.0), freq.numpy(), v, w, npix_x,
+                           npix_y, px, py, do_wstacking)
+    assert tuple(out_strides) == (1, npix_x)  # RASCIL's [y, x] image
+    out += torch.as_tensor(d.T)
+    if sumwt is not None:
+        sumwt += float(w.sum())
+    return out, {}
+
+
+def _oracle_dirty2ms_vis(uvw, freq, dirty, out, coef, px, py, epsilon=1e-7, do_wstacking=True,
+                         flip_uw=False, dirty_strides=None, npix=None, accumulate=False,
+                         shift_lmn=None):
+    assert shift_lmn is None and tuple(dirty_strides) == (1, npix[0])
+    SEEN.update(freq.numpy().tolist())
+    v = orc.dirty2ms_exact(uvw.numpy() * (FLIP if flip_uw else 1.0), freq.numpy(),
+                           dirty.numpy().T, None, px, py, do_wstacking)
+    coef = [1.0] + [0.0] * (out.shape[2] - 1) if coef is None else coef
+    for k, c in enumerate(coef):
+        val = torch.as_tensor(complex(c) * v).to(out.dtype)
+        if accumulate:
+            out[..., k] += val
+        else:
+            out[..., k] = val
+    return out, {}
+
+
+def _patch():
+    from ska_sdp_func_python_amd import _device, kernels
+    _device.device = lambda: torch.device("cpu")
+    kernels.ms2dirty_vis = _oracle_ms2dirty_vis
+    kernels.dirty2ms_vis = _oracle_dirty2ms_vis
+
+
+def _case(kind):
+    from ska_sdp_func_python_amd import datamodels as dm
+    from gpu_helpers import vis_from_arrays
+    rng = np.random.default_rng(51)
+    nt, nb, nchan = 3, 12, 5
+    freq = np.linspace(1.0e9, 1.2e9, nchan)
+    umax = 1200.0
+    uvw = rng.uniform(-1, 1, (nt, nb, 3)) * umax * orc.C_LIGHT / freq.max()
+    shape = (nt, nb, nchan, 1)
+    v = rng.normal(size=shape) + 1j * rng.normal(size=shape)
+    fl = (rng.uniform(size=shape) < 0.1).astype(int)
+    vis = vis_from_arrays(uvw, freq, v, flags=fl, phasecentre=dm.SkyCoord(0.0, -0.6))
+    vis["imaging_weight"] = rng.uniform(0.5, 2.0, shape)
+    cube = kind == "invert_cube"
+    fc, bw = (float(freq[0]), float(freq[1] - freq[0])) if cube else (float(freq.mean()), 1e9)
+    im = dm.create_image(32, 0.4 / umax, dm.SkyCoord(0.0, -0.6), frequency=fc,
+                         channel_bandwidth=bw, nchan=nchan if cube else 1)
+    if kind == "predict":
+        im["pixels"].data[...] = rng.normal(size=im["pixels"].data.shape)
+    return vis, im
+
+
+def _run(kind):
+    from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng
+    vis, im = _case(kind)
+    if kind == "predict":
+        return (np.asarray(predict_ng(vis, im).vis.data),)
+    d, sw = invert_ng(vis, im, normalise=True)
+    return np.asarray(d["pixels"].data), np.asarray(sw)
+
+
+def _worker(rank, world, port, kind, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _patch()
+    try:
+        out = _run(kind)
+        q.put((rank, out, sorted(SEEN)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["invert_mfs", "invert_cube", "predict"])
+def test_reference_api_shards_across_ranks(kind, monkeypatch):
+    from ska_sdp_func_python_amd import _device, kernels
+    monkeypatch.setattr(_device, "device", lambda: torch.device("cpu"))
+    monkeypatch.setattr(kernels, "ms2dirty_vis", _oracle_ms2dirty_vis)
+    monkeypatch.setattr(kernels, "dirty2ms_vis", _oracle_dirty2ms_vis)
+    ref = _run(kind)  # this process: no process group, so unsharded
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + int(np.random.default_rng().integers(0, 300))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert len(res) == 2
+    # the ranks computed disjoint channel blocks that cover the band
+    seen = [set(s) for _, _, s in res]
+    assert seen[0] and seen[1] and not (seen[0] & seen[1]) and len(seen[0] | seen[1]) == 5
+    for _, out, _ in res:
+        for a, b in zip(out, ref):
+            np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
