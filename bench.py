@@ -412,7 +412,10 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic, "kernel": f"k_grid_mfma<{W},true> (sub-sorted cells)",
+                     "traffic": traffic,
+                     "kernel": (f"k_grid_mfma_pad<{W},true> (sub-sorted, 4-padded cells)"
+                                if info.get("padded") else
+                                f"k_grid_mfma<{W},true> (sub-sorted cells)"),
                      "kernel_ms_rank0": round(ms_grid, 3), "launches": len(batches),
                      "alg_bytes": int(alg),
                      "note": "vis 8 B + uvw 24 B per row per batch + the band's planes written "
@@ -744,7 +747,7 @@ def main():
             traffic = json.load(f).get("bytes_per_launch")
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": (f"k_grid_mfma_pad<{info['support']},true>" if info["bucket"] == 1
+            "kernel": (f"k_grid_mfma_pad<{info['support']},true>" if info.get("padded")
                        else f"k_grid_mfma<{info['support']},true> (sub-sorted cells)"),
             "kernel_ms": round(ms_grid / launches, 4),
             "alg_bytes_per_launch": int(alg_bytes / launches),

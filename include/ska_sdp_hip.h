@@ -71,6 +71,8 @@ typedef struct sdp_hip_wgrid_info {
                              (large grids)                                  */
     int grid_launches;    /* (de)gridding kernel launches (one per plane
                              chunk); ms_grid is their summed time           */
+    int padded;           /* invert: gridded on cells padded to 4 records
+                             (k_grid_mfma_pad; 0: k_grid_mfma)              */
 } sdp_hip_wgrid_info;
 
 /* Library/ABI version and a device probe. */

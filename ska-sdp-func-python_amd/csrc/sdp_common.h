@@ -128,6 +128,19 @@ class Workspace {
         std::lock_guard<std::mutex> lk(mu_);
         return gen_;
     }
+    // free the buffer held under `name` on the current device (if any), so
+    // that memory a plan does not use is not counted as reusable
+    void drop(const std::string &name) {
+        int dev = 0;
+        SDP_HIP_CHECK(hipGetDevice(&dev));
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = bufs_.find({dev, name});
+        if (it == bufs_.end() || !it->second.ptr) return;
+        ++gen_;
+        SDP_HIP_CHECK(hipDeviceSynchronize());
+        SDP_HIP_CHECK(hipFree(it->second.ptr));
+        bufs_.erase(it);
+    }
     void release() {
         std::lock_guard<std::mutex> lk(mu_);
         ++gen_;

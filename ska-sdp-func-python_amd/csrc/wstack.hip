@@ -34,6 +34,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
+#include <memory>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -80,6 +82,9 @@ struct Geo {
     double su;  // sign applied to u and w (-1 with SDP_HIP_FLIP_UW)
     int nchan;
     int64_t nrow;
+    // one-cell keys: blocks of bx x 8 cells (bx = 2, 4 or 8; bxs = log2 bx),
+    // each bx / 2 groups of 2 x 8 cells, consecutive in the key order
+    int bx, bxs;
 };
 
 struct __attribute__((aligned(32))) VisRec {
@@ -208,10 +213,15 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
 }
 
 // p0-major bucket keys: the items of a range of first planes are contiguous.
+// One-cell keys inside a plane: block (x-major), x pair in the block, y, x
+// parity -- 16 consecutive keys are a group of 2 x 8 cells.
 __device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c, int64_t row) {
     const int ic = c.ic0 - g.wx0, jc = c.jc0 - g.wy0;
-    const int tile = g.sub == kTileCell ? ((ic >> 1) * g.nty + jc) * 2 + (ic & 1)
-                                        : (ic / g.sub) * g.nty + (jc / g.sub);
+    const int tile =
+        g.sub == kTileCell
+            ? ((((ic >> g.bxs) * (g.wny >> 3) + (jc >> 3)) << (g.bxs - 1)) + ((ic & (g.bx - 1)) >> 1)) *
+                      16 + (jc & 7) * 2 + (ic & 1)
+            : (ic / g.sub) * g.nty + (jc / g.sub);
     return ((unsigned)c.p0 * (unsigned)g.ntiles + (unsigned)tile) * (unsigned)g.salt +
            ((unsigned)row & (unsigned)(g.salt - 1));
 }
@@ -430,18 +440,26 @@ __device__ __forceinline__ float2 eff_vis(const VT *vis, int64_t vrs, int64_t vc
     return make_float2((float)re, (float)im);
 }
 
-template <class VT, bool kScatter, bool kGrid, bool kCompact = false>
-__global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw,
-                         int64_t uvw_rs, const double *__restrict__ freq,
-                         const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
-                         const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x,
-                         double *sw_slots, unsigned *counter, unsigned *__restrict__ rk,
-                         VisRec *__restrict__ recs, unsigned long long *nbad) {
-    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t vg = v;
+template <class T>
+struct TypeTag {
+    using type = T;
+};
+
+// One visibility of k_bucket.
+template <class VT, bool kScatter, bool kGrid, bool kCompact>
+__device__ __forceinline__ void bucket_one(const Geo &g, int64_t v, int64_t nvis,
+                                           const double *__restrict__ uvw, int64_t uvw_rs,
+                                           const double *__restrict__ freq,
+                                           const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
+                                           const void *__restrict__ wgt, int64_t wrs,
+                                           int64_t wcs, const VisExtra &x, double *sw_slots,
+                                           unsigned *counter, unsigned *__restrict__ rk,
+                                           VisRec *__restrict__ recs, unsigned long long *nbad,
+                                           uint8_t *__restrict__ cls) {
     bool valid = v < nvis;
     int64_t row = 0;
     int chan = 0;
+    int64_t vg = v;  // row * nchan + chan
     float wt = 1.0f;
     Coord c;
     c.ok = false;
@@ -465,7 +483,7 @@ __global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw,
                           wd);
         }
         if (!valid) return;
-        mine = rk[vg];
+        mine = rk[v];
         if (mine == 0xffffffffu) return;
         c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
     } else {
@@ -534,6 +552,9 @@ __global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw,
         rc.lo = qu | (qv << 21);
         rc.hi = (qv >> 11) | (qw << 10);
         reinterpret_cast<RecC *>(recs)[pos] = rc;
+        // large grids (16x16-cell buckets): the record's cell in its bucket,
+        // for the padded sub-sort (k_subsort_pad)
+        if (cls) cls[pos] = (uint8_t)(((c.ic0 & 15) >> 1) * 32 + (c.jc0 & 15) * 2 + (c.ic0 & 1));
         return;
     }
     VisRec rec;
@@ -546,6 +567,19 @@ __global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw,
     rec.p0 = (uint32_t)c.p0;
     rec.idx = (uint32_t)vg;
     recs[pos] = rec;
+}
+
+template <class VT, bool kScatter, bool kGrid, bool kCompact = false>
+__global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw,
+                         int64_t uvw_rs, const double *__restrict__ freq,
+                         const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
+                         const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x,
+                         double *sw_slots, unsigned *counter, unsigned *__restrict__ rk,
+                         VisRec *__restrict__ recs, unsigned long long *nbad,
+                         uint8_t *__restrict__ cls = nullptr) {
+    bucket_one<VT, kScatter, kGrid, kCompact>(g, blockIdx.x * (int64_t)blockDim.x + threadIdx.x,
+                                              nvis, uvw, uvw_rs, freq, vis, vrs, vcs, wgt, wrs,
+                                              wcs, x, sw_slots, counter, rk, recs, nbad, cls);
 }
 
 __global__ __launch_bounds__(64) void k_sum_slots(const double *__restrict__ slots, double *out) {
@@ -585,53 +619,39 @@ __global__ void k_items_fill(int64_t ngroups, int grp, int groups_per_plane,
     }
 }
 
-// work items of one-cell buckets: FineItem descriptors that carry the
-// group's 16 cell ends, so a (de)gridding wave has them from one 80-byte
-// scalar load instead of a second dependent round trip to the offsets
-__global__ void k_items_fill_cells(int64_t ngroups, int groups_per_plane,
-                                   const unsigned *__restrict__ offs,
-                                   const unsigned *__restrict__ ioffs, unsigned chunk,
-                                   FineItem *items) {
-    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (k >= ngroups) return;
-    FineItem x;
-    const unsigned b = offs[k * kGroupCell], e = offs[(k + 1) * kGroupCell];
-#pragma unroll
-    for (int j = 0; j < kGroupCell; ++j) x.o[j] = offs[k * kGroupCell + j + 1];
-    x.p0 = (uint32_t)(k / groups_per_plane);
-    x.tile = (uint32_t)(k - (int64_t)x.p0 * groups_per_plane);
-    unsigned o = ioffs[k];
-    for (unsigned s = b; s < e; s += chunk) {
-        x.b = s;
-        x.e = min(e, s + chunk);
-        items[o++] = x;
-    }
-}
-
-// 4-padding of the one-cell buckets for k_grid_mfma_pad: key k's records
-// fill [offs[k], offs[k] + hist[k]) of a slot range rounded up to a multiple
-// of 4 (the scan ran over the rounded counts); the remaining slots get
-// zero-valued RecC records.  Per block the pad count is added into one of
-// kSumSlots slots (k_sum_pads folds them).
-__global__ __launch_bounds__(256) void k_pad_cells(unsigned nkeys,
-                                                   const unsigned *__restrict__ hist,
-                                                   const unsigned *__restrict__ offs,
-                                                   RecC *__restrict__ recs,
-                                                   unsigned *__restrict__ pad_slots) {
+// One-cell plans: the offsets, pads and work items come from two passes over
+// units of `ucells` consecutive cells (the groups of kGroupCell cells whose
+// FineItem work items carry the 16 cell ends) instead of a scan over every
+// cell.  k_group_sums: per unit its record total (each cell rounded up to a
+// multiple of 4 when PAD) and work-item count, packed as (records << 32) |
+// items so one 64-bit exclusive scan over the units yields both bases (the
+// totals stay below 2^32, so the low half never carries); the pad count is
+// added per block into one of kSumSlots slots.
+template <bool PAD>
+__global__ __launch_bounds__(256) void k_group_sums(int64_t nunits, int ucells,
+                                                    const unsigned *__restrict__ hist,
+                                                    unsigned chunk,
+                                                    unsigned long long *__restrict__ gsum,
+                                                    unsigned *__restrict__ pad_slots) {
     __shared__ unsigned red[4];
-    const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     unsigned npad = 0;
-    if (k < nkeys) {
-        const unsigned n = hist[k];
-        if (n & 3u) {
-            npad = 4u - (n & 3u);
-            const unsigned base = offs[k] + n;
-            RecC r;
-            r.cre = r.cim = 0.0f;
-            r.lo = r.hi = 0u;  // offsets 1 - W/2: in range, finite taps
-            for (unsigned i = 0; i < npad; ++i) recs[base + i] = r;
+    if (k < nunits) {
+        const uint4 *h = reinterpret_cast<const uint4 *>(hist + k * ucells);
+        unsigned tot = 0;
+        for (int q = 0; q < ucells / 4; ++q) {
+            const uint4 v = h[q];
+            const unsigned n[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const unsigned r = PAD ? (n[j] + 3u) & ~3u : n[j];
+                tot += r;
+                npad += r - n[j];
+            }
         }
+        gsum[k] = ((unsigned long long)tot << 32) | (unsigned long long)((tot + chunk - 1) / chunk);
     }
+    if (!PAD) return;
     unsigned s = npad;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -643,6 +663,64 @@ __global__ __launch_bounds__(256) void k_pad_cells(unsigned nkeys,
     }
 }
 
+// k_group_fill: from the scanned unit bases, the cells' record offsets
+// (offs[key], what the scatter adds the ranks to; offs[nkeys] = total), the
+// zero-valued pad records of the 4-padded cells (RecC, offsets 1 - W/2: in
+// range, finite taps; they sit behind each cell's records, where the
+// scatter never writes), the units' item bases (ioffs) and their FineItem
+// work items.
+template <bool PAD>
+__global__ __launch_bounds__(256) void k_group_fill(int64_t nunits, int units_per_plane,
+                                                    int ucells,
+                                                    const unsigned *__restrict__ hist,
+                                                    const unsigned long long *__restrict__ gofs,
+                                                    unsigned chunk, unsigned *__restrict__ offs,
+                                                    unsigned *__restrict__ ioffs,
+                                                    RecC *__restrict__ recs, void *items) {
+    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (k > nunits) return;
+    const unsigned long long go = gofs[k];
+    const unsigned base = (unsigned)(go >> 32), ib = (unsigned)go;
+    ioffs[k] = ib;
+    if (k == nunits) {
+        offs[k * ucells] = base;
+        return;
+    }
+    const uint4 *h = reinterpret_cast<const uint4 *>(hist + k * ucells);
+    uint4 *of = reinterpret_cast<uint4 *>(offs + k * ucells);
+    FineItem x;
+    unsigned run = base;
+    for (int q = 0; q < ucells / 4; ++q) {
+        const uint4 v = h[q];
+        const unsigned n[4] = {v.x, v.y, v.z, v.w};
+        unsigned st[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            st[j] = run;
+            const unsigned r = PAD ? (n[j] + 3u) & ~3u : n[j];
+            if (PAD && r != n[j]) {
+                RecC z;
+                z.cre = z.cim = 0.0f;
+                z.lo = z.hi = 0u;
+                for (unsigned i = run + n[j]; i < run + r; ++i) recs[i] = z;
+            }
+            run += r;
+            x.o[(q * 4 + j) & (kGroupCell - 1)] = run;
+        }
+        of[q] = make_uint4(st[0], st[1], st[2], st[3]);
+    }
+    x.p0 = (uint32_t)(k / units_per_plane);
+    x.tile = (uint32_t)(k - (int64_t)x.p0 * units_per_plane);
+    unsigned o = ib;
+    FineItem *fi = static_cast<FineItem *>(items);
+    for (unsigned s = base; s < run; s += chunk) {
+        x.b = s;
+        x.e = min(run, s + chunk);
+        fi[o++] = x;
+    }
+}
+
+// the pad count of a 4-padded plan (k_group_sums' per-block slots)
 __global__ __launch_bounds__(256) void k_sum_pads(const unsigned *__restrict__ slots,
                                                   unsigned *out) {
     __shared__ unsigned red[4];
@@ -654,12 +732,6 @@ __global__ __launch_bounds__(256) void k_sum_pads(const unsigned *__restrict__ s
     __syncthreads();
     if (threadIdx.x == 0) *out = red[0] + red[1] + red[2] + red[3];
 }
-
-struct Round4 {
-    __host__ __device__ __forceinline__ unsigned operator()(unsigned n) const {
-        return (n + 3u) & ~3u;
-    }
-};
 
 // Large grids: the dense 2x2-cell histogram would be too large (C4: 70
 // planes of 8192^2 buckets), so visibilities are bucketed by 16x16 cells and
@@ -732,9 +804,121 @@ __global__ __launch_bounds__(kSubThreads) void k_subsort(Geo g, const Item *__re
     }
 }
 
+// Large-grid gridding (invert) on 4-padded cells: the value pass wrote
+// 16-byte RecC records in 16x16-cell bucket order plus each record's cell
+// class (sub_class<true>, one byte).  k_sub_count: per coarse item its
+// record count with every cell rounded up to a multiple of 4 (the scan of
+// these places the items' padded records);  k_subsort_pad: the item's
+// records staged in LDS, ordered by cell into the padded layout (zero pad
+// records, offsets 1 - W/2), and its 16 FineItems (2 x 8-cell groups; empty
+// groups have b == e) for k_grid_mfma_pad.
+__global__ __launch_bounds__(256) void k_sub_count(const Item *__restrict__ items,
+                                                   const uint8_t *__restrict__ cls,
+                                                   unsigned *__restrict__ pcnt) {
+    __shared__ unsigned h[256];
+    __shared__ unsigned red[4];
+    const Item it = items[blockIdx.x];
+    h[threadIdx.x] = 0u;
+    __syncthreads();
+    for (uint32_t i = it.b + threadIdx.x; i < it.e; i += 256) atomicAdd(&h[cls[i]], 1u);
+    __syncthreads();
+    unsigned r = (h[threadIdx.x] + 3u) & ~3u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) pcnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(kSubThreads) void k_subsort_pad(Geo g, const Item *__restrict__ items,
+                                                             const RecC *__restrict__ in,
+                                                             const uint8_t *__restrict__ cls,
+                                                             const unsigned *__restrict__ pbase,
+                                                             RecC *__restrict__ out,
+                                                             FineItem *__restrict__ fitems) {
+    constexpr int NC = 256, PG = 16;
+    __shared__ RecC stage[kSubChunk];
+    __shared__ uint8_t scls[kSubChunk];
+    __shared__ unsigned cnt[NC], first[NC + 1], cur[NC];
+    const Item it = items[blockIdx.x];
+    const int n = (int)(it.e - it.b);
+    const unsigned pb = pbase[blockIdx.x];
+    for (int c = threadIdx.x; c < NC; c += kSubThreads) cnt[c] = 0u;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += kSubThreads) {
+        stage[i] = in[it.b + i];
+        const uint8_t k = cls[it.b + i];
+        scls[i] = k;
+        atomicAdd(&cnt[k], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        // padded exclusive prefix over the 256 cells: 4 per lane, then a
+        // wave scan of the lane sums
+        const int l = threadIdx.x;
+        unsigned r[4], t = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            r[j] = (cnt[4 * l + j] + 3u) & ~3u;
+            t += r[j];
+        }
+        unsigned incl = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(incl, o, 64);
+            if (l >= o) incl += y;
+        }
+        unsigned a = incl - t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            first[4 * l + j] = a;
+            cur[4 * l + j] = a;
+            a += r[j];
+        }
+        if (l == 63) first[NC] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        // fine group gi = 2 * (x pair) + (y half): a 2 x 8-cell region
+        const int gi = threadIdx.x, xp = gi >> 1, hf = gi & 1;
+        const int c0 = gi * PG;
+        FineItem f;
+        f.b = pb + first[c0];
+        f.e = pb + first[c0 + PG];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) f.o[j] = pb + first[c0 + j + 1];
+        const int tx = (int)it.tile / g.nty, ty = (int)it.tile - tx * g.nty;
+        f.tile = (uint32_t)((tx * 8 + xp) * (g.wny / 8) + ty * 2 + hf);
+        f.p0 = it.p0;
+        fitems[(size_t)blockIdx.x * 16 + threadIdx.x] = f;
+    }
+    // zero pad records behind each cell's records
+    for (int c = threadIdx.x; c < NC; c += kSubThreads) {
+        const unsigned e = first[c] + cnt[c], pe = first[c + 1];
+        RecC z;
+        z.cre = z.cim = 0.0f;
+        z.lo = z.hi = 0u;
+        for (unsigned i = e; i < pe; ++i) out[pb + i] = z;
+    }
+    for (int i = threadIdx.x; i < n; i += kSubThreads) {
+        const unsigned pos = atomicAdd(&cur[scls[i]], 1u);
+        out[pb + pos] = stage[i];
+    }
+}
+
 // ------------------------------------------------------------------------
 // kernels: gridding / degridding (the hot loops)
 // ------------------------------------------------------------------------
+// first cell (centred grid) of 16-key group `gi` (index inside its first
+// plane) of a one-cell plan: block gi / (bx / 2), x pair gi % (bx / 2)
+__device__ __forceinline__ void group_origin(const Geo &g, int gi, int &ib, int &jb) {
+    const int ppb = g.bx >> 1;
+    const int blk = gi / ppb, xp = gi - blk * ppb;
+    const int nby = g.wny >> 3;
+    const int bxi = blk / nby, byi = blk - bxi * nby;
+    ib = g.wx0 + bxi * g.bx + 2 * xp;
+    jb = g.wy0 + byi * 8;
+}
 // Work items are visited transposed: workgroup w = q m + r (m = n / K)
 // takes item r K + q, so the consecutive items of one dense tile (the chunks
 // of a heavy cell group) go to workgroups m apart -- spread over the launch
@@ -1011,7 +1195,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 
 // MFMA gridder on 4-padded cells (invert, one-cell buckets).  The bucketing
 // rounds every cell's record count up to a multiple of 4 with zero-valued
-// pad records (k_pad_cells), so every K-step of 4 consecutive records belongs
+// pad records (k_group_fill), so every K-step of 4 consecutive records belongs
 // to one cell.  A cell's contribution to its W x W x W footprint is one GEMM
 //     C[(q, re/im), (kx, ky)] += sum_r  tw_r[q] c_r  *  tu_r[kx] tv_r[ky]
 // on v_mfma_f32_16x16x4_f32 (exact fp32 multiply-adds): A = the w taps x
@@ -1042,11 +1226,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 // The region tile is flushed once per item with buffer float atomics.
 constexpr int kTapRec = 24;    // floats per record row of the tap block
 constexpr int kTapBatch = 16;  // records per tap block
-constexpr int kRegX = 9, kRegY = 15;  // region tile: (2 + 8 - 1) x (8 + 8 - 1) cells
-constexpr int kRegCell = 16;          // floats per region cell: 8 planes x re/im
+constexpr int kRegY = 15;     // region tile rows: 8 + 8 - 1 cells
+constexpr int kRegCell = 16;  // floats per region cell: 8 planes x re/im
 
-constexpr size_t grid_mfma_pad_lds() {
-    return (size_t)kRegX * kRegY * kRegCell * sizeof(float) + kTapBatch * sizeof(float4) +
+// region tile of a block BXC cells wide: (BXC + 8 - 1) x kRegY cells
+constexpr size_t grid_mfma_pad_lds(int bxc) {
+    return (size_t)(bxc + 7) * kRegY * kRegCell * sizeof(float) + kTapBatch * sizeof(float4) +
            (size_t)kTapBatch * kTapRec * sizeof(float) + kTapBatch * sizeof(float2);
 }
 
@@ -1055,9 +1240,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     Geo g, const RecC *__restrict__ recs, const FineItem *__restrict__ items, uint32_t n_items,
     float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
+    constexpr int BXC = 2;  // cells per group in x
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int NQ = WS ? W : 1;
-    constexpr int RX = 2 + W - 1, RY = 8 + W - 1;  // cells a footprint of the group reaches
+    constexpr int RX = BXC + W - 1, RY = 8 + W - 1;  // cells a footprint of the block reaches
+    constexpr int kRegX = BXC + 7;
     float *const reg = reinterpret_cast<float *>(tile);  // [kRegX][kRegY][16]
     float4 *const stage = reinterpret_cast<float4 *>(reg + kRegX * kRegY * kRegCell);
     float *const blk = reinterpret_cast<float *>(stage + kTapBatch);  // [kTapBatch][kTapRec]
@@ -1082,13 +1269,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     constexpr int acc_t = 2 * kRegY * kRegCell;  // + t N-tiles (two x rows each)
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        // the item and the ends of its group's cells 0..14 (record indices):
-        // one 80-byte descriptor, scalar loads
+        // the item and the ends of its group's 16 cells (record indices): one
+        // 80-byte descriptor, scalar loads
         uint32_t bnd[kGroupCell];
         const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
-        const int ntg = g.nty / 8;  // groups per x pair
-        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-        const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
+        if (it.b >= it.e) continue;  // (empty groups of a sub-sorted coarse item)
+        int ibase, jbase;
+        group_origin(g, (int)it.tile, ibase, jbase);
 
         wave_lds_sync();  // the previous item's flush reads of the region
         {
@@ -1098,19 +1285,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         }
 
         floatx4 acc[4];
-        int cur = -1;    // cell of the accumulators (wave-uniform)
-        int cbase = 0;   // its accumulator base offset (floats) in the region
+        int cbase = 0;  // the accumulators' base offset (floats) in the region
         auto store_cell = [&]() {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 *reinterpret_cast<floatx4 *>(reg + cbase + t * acc_t) = acc[t];
-        };
-        auto load_cell = [&](int cell) {
-            const int xo = cell & 1, yo = cell >> 1;
-            cbase = (xo * kRegY + yo) * kRegCell + acc_lane;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                acc[t] = *reinterpret_cast<const floatx4 *>(reg + cbase + t * acc_t);
         };
         struct Ops {
             floatx4 b;
@@ -1131,78 +1310,93 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, o.b[t] * o.v, acc[t], 0, 0, 0);
         };
 
-        RecC nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
-        for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
-            const RecC my = nx;
-            if (b0 + 64 < it.e) nx = recs[min(b0 + 64 + (uint32_t)lane, it.e - 1)];
-            const int nb = (int)min(64u, it.e - b0);  // a multiple of 4
-            // cell (x-pair-major index in the group) of the lane's record
-            const uint32_t ri = b0 + (uint32_t)lane;
-            int cj = 0;
+        {
+            const uint32_t rb = it.b, re = it.e;
+            int cur = -1;  // cell of the accumulators (wave-uniform)
+            auto load_cell = [&](int cell) {
+                const int xo = cell & 1, yo = cell >> 1;
+                cbase = (xo * kRegY + yo) * kRegCell + acc_lane;
 #pragma unroll
-            for (int c = 0; c < kGroupCell - 1; ++c) cj += ri >= bnd[c] ? 1 : 0;
-            const float fu = fbase - (float)(my.lo & 0x1fffffu) * 0x1p-21f;
-            const float fv = fbase - (float)((my.lo >> 21) | ((my.hi & 0x3ffu) << 11)) * 0x1p-21f;
-            const float fw = fbase - (float)(my.hi >> 10) * 0x1p-22f;
-            // K-steps whose cell differs from the previous K-step's (bit 4j)
-            const int prev = __shfl_up(cj, 4);
-            uint64_t chg = __ballot((lane & 3) == 0 && lane >= 4 && prev != cj);
-            if (__builtin_amdgcn_readfirstlane(cj) != cur) chg |= 1ull;
-            // blocks of kTapBatch records: taps, then their K-steps
-            for (int h = 0; h < 64 / kTapBatch; ++h) {
-                const int nbh = min(kTapBatch, nb - kTapBatch * h);
-                if (nbh <= 0) break;
-                wave_lds_sync();  // the previous block's tap reads
-                if (lane / kTapBatch == h) {
-                    const int r = lane % kTapBatch;
-                    stage[r] = make_float4(fu, fv, fw, 0.0f);
-                    cval[r] = make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
-                }
-                wave_lds_sync();
-                {
-                    // both staged offsets read before any tap is written: six
-                    // independent ES chains
-                    float4 f[kTapBatch / 8];
+                for (int t = 0; t < 4; ++t)
+                    acc[t] = *reinterpret_cast<const floatx4 *>(reg + cbase + t * acc_t);
+            };
+
+            RecC nx = recs[min(rb + (uint32_t)lane, re - 1)];
+            for (uint32_t b0 = rb; b0 < re; b0 += 64) {
+                const RecC my = nx;
+                if (b0 + 64 < re) nx = recs[min(b0 + 64 + (uint32_t)lane, re - 1)];
+                const int nb = (int)min(64u, re - b0);  // a multiple of 4
+                // cell (x-pair-major index in the group) of the lane's record
+                const uint32_t ri = b0 + (uint32_t)lane;
+                int cj = 0;
 #pragma unroll
-                    for (int m = 0; m < kTapBatch / 8; ++m) f[m] = stage[8 * m + (lane >> 3)];
-                    float tv_[kTapBatch / 8][3];
-#pragma unroll
-                    for (int m = 0; m < kTapBatch / 8; ++m) {
-                        tv_[m][0] = es_tap<W>(f[m].x, tihw, ihw, bl);
-                        tv_[m][1] = es_tap<W>(f[m].y, tihw, ihw, bl);
-                        tv_[m][2] = WS ? es_tap<W>(f[m].z, tihw, ihw, bl) : (tt == 0 ? 1.0f : 0.0f);
+                for (int c = 0; c < kGroupCell - 1; ++c) cj += ri >= bnd[c] ? 1 : 0;
+                const float fu = fbase - (float)(my.lo & 0x1fffffu) * 0x1p-21f;
+                const float fv =
+                    fbase - (float)((my.lo >> 21) | ((my.hi & 0x3ffu) << 11)) * 0x1p-21f;
+                const float fw = fbase - (float)(my.hi >> 10) * 0x1p-22f;
+                // K-steps whose cell differs from the previous K-step's (bit 4j)
+                const int prev = __shfl_up(cj, 4);
+                uint64_t chg = __ballot((lane & 3) == 0 && lane >= 4 && prev != cj);
+                if (__builtin_amdgcn_readfirstlane(cj) != cur) chg |= 1ull;
+                // blocks of kTapBatch records: taps, then their K-steps
+                for (int h = 0; h < 64 / kTapBatch; ++h) {
+                    const int nbh = min(kTapBatch, nb - kTapBatch * h);
+                    if (nbh <= 0) break;
+                    wave_lds_sync();  // the previous block's tap reads
+                    if (lane / kTapBatch == h) {
+                        const int r = lane % kTapBatch;
+                        stage[r] = make_float4(fu, fv, fw, 0.0f);
+                        cval[r] =
+                            make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
                     }
+                    wave_lds_sync();
+                    {
+                        // both staged offsets read before any tap is written: six
+                        // independent ES chains
+                        float4 f[kTapBatch / 8];
 #pragma unroll
-                    for (int m = 0; m < kTapBatch / 8; ++m) {
-                        float *d = tap_dst + 8 * m * kTapRec;
-                        d[wu] = tv_[m][0];
-                        d[wv] = tv_[m][1];
-                        d[ww] = tv_[m][2];
-                    }
-                }
-                wave_lds_sync();
-                const uint64_t hchg = chg >> (kTapBatch * h);
-                const int nk = nbh >> 2;
-                // the block's (up to) 4 K-steps unrolled: every operand read
-                // up front at compile-time offsets; a cell change (bit 4j)
-                // stores the accumulators and loads the next cell's
-                Ops o[kTapBatch / 4];
+                        for (int m = 0; m < kTapBatch / 8; ++m) f[m] = stage[8 * m + (lane >> 3)];
+                        float tv_[kTapBatch / 8][3];
 #pragma unroll
-                for (int jj = 0; jj < kTapBatch / 4; ++jj) o[jj] = kload(jj);
-#pragma unroll
-                for (int jj = 0; jj < kTapBatch / 4; ++jj) {
-                    if (jj < nk) {
-                        if ((hchg >> (4 * jj)) & 1ull) {
-                            if (cur >= 0) store_cell();
-                            cur = __builtin_amdgcn_readlane(cj, kTapBatch * h + 4 * jj);
-                            load_cell(cur);
+                        for (int m = 0; m < kTapBatch / 8; ++m) {
+                            tv_[m][0] = es_tap<W>(f[m].x, tihw, ihw, bl);
+                            tv_[m][1] = es_tap<W>(f[m].y, tihw, ihw, bl);
+                            tv_[m][2] =
+                                WS ? es_tap<W>(f[m].z, tihw, ihw, bl) : (tt == 0 ? 1.0f : 0.0f);
                         }
-                        kmfma(o[jj]);
+#pragma unroll
+                        for (int m = 0; m < kTapBatch / 8; ++m) {
+                            float *d = tap_dst + 8 * m * kTapRec;
+                            d[wu] = tv_[m][0];
+                            d[wv] = tv_[m][1];
+                            d[ww] = tv_[m][2];
+                        }
+                    }
+                    wave_lds_sync();
+                    const uint64_t hchg = chg >> (kTapBatch * h);
+                    const int nk = nbh >> 2;
+                    // the block's (up to) 4 K-steps unrolled: every operand read
+                    // up front at compile-time offsets; a cell change (bit 4j)
+                    // stores the accumulators and loads the next cell's
+                    Ops o[kTapBatch / 4];
+#pragma unroll
+                    for (int jj = 0; jj < kTapBatch / 4; ++jj) o[jj] = kload(jj);
+#pragma unroll
+                    for (int jj = 0; jj < kTapBatch / 4; ++jj) {
+                        if (jj < nk) {
+                            if ((hchg >> (4 * jj)) & 1ull) {
+                                if (cur >= 0) store_cell();
+                                cur = __builtin_amdgcn_readlane(cj, kTapBatch * h + 4 * jj);
+                                load_cell(cur);
+                            }
+                            kmfma(o[jj]);
+                        }
                     }
                 }
             }
+            if (cur >= 0) store_cell();
         }
-        if (cur >= 0) store_cell();
         wave_lds_sync();
 
         // flush: lane l takes float f = i0 + l of a plane's RX x RY cells in
@@ -1278,9 +1472,8 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
         Item it;
         it = load_fine_item<kGroupCell>(fitems, w_it, n_items, fo);
         if (it.b >= it.e) continue;
-        const int ntg = g.wny / 8;  // groups per x pair
-        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-        const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
+        int ibase, jbase;
+        group_origin(g, (int)it.tile, ibase, jbase);
 
         // the item's first 16 records are requested before the region is
         // staged (both depend only on the item descriptor)
@@ -1765,6 +1958,9 @@ struct Plan {
     VisRec *recs = nullptr;
     Part pt;
     bool subsort = false;            // 16x16-cell buckets re-ordered by cell (k_subsort)
+    bool subpad = false;             // ... into 4-padded RecC cells (invert: k_subsort_pad)
+    uint8_t *cls = nullptr;          // subpad: each RecC record's cell in its bucket
+    RecC *recs_pad = nullptr;        // subpad: the 4-padded, cell-ordered records
     bool pad4 = false;               // one-cell buckets padded to 4 records (k_grid_mfma_pad)
     float2 *vdirect = nullptr;       // dirty2ms: the degridder writes c64 vis in place
     int chunk_planes = 1;            // planes resident per pass
@@ -1816,7 +2012,8 @@ static size_t grid_budget_bytes(size_t need_other) {
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)8 << 30;
     Workspace &ws = Workspace::get();
     const size_t held_planes = ws.held("grid") + ws.held("spec") + ws.held("spec_in");
-    const size_t held_other = ws.held("recs") + ws.held("key_rank") + ws.held("degrid_acc");
+    const size_t held_other = ws.held("recs") + ws.held("key_rank") + ws.held("degrid_acc") +
+                              ws.held("recs_pad") + ws.held("rec_cls");
     const size_t avail = free_b + held_planes + held_other;
     const size_t reserve = std::max<size_t>((size_t)6 << 30, total_b / 16);
     const size_t need = need_other + reserve;
@@ -2097,6 +2294,13 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         if (env_int("SDP_HIP_BUCKET", 0) == kTileCoarse) g.sub = kTileCoarse;
     }
     g.nty = g.wny / g.sub;
+    // gridding on one-cell keys: blocks of bx x 8 cells per work item (the
+    // region flushed with atomics is (bx + W - 1) x (8 + W - 1) cells)
+    // (blocks of 4 x 8 and 8 x 8 cells halve the flushed atomics but measured
+    // slower on C2, 4.9 and 5.5 vs 4.6 ms: the larger LDS region lowers the
+    // waves per CU this latency-bound kernel runs with)
+    g.bx = 2;
+    g.bxs = 1;
     g.ntiles = (g.wnx / g.sub) * g.nty;
     g.grp = g.sub == kTileCell ? kGroupCell : 1;
     g.salt = 1;
@@ -2130,8 +2334,20 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         if (std::atoi(e) > 0) P.fft_planes = std::atoi(e);
     P.fft_planes = std::min(P.fft_planes, g.nplanes);
     const int64_t nvis = in.nrow * (int64_t)in.nchan;
+    // large-grid invert: RecC records + cell bytes, then the 4-padded copy
+    // (k_subsort_pad; budgeted at 1.35x -- C4's top channels pad to <= 1.5x
+    // one channel at a time, less over a batch of channels)
+    P.subpad = grid_mode && g.sub == kTileCoarse && env_int("SDP_HIP_SUBSORT_PAD", 1) != 0;
+    const double rec_bytes = P.subpad ? sizeof(RecC) + 1 + 1.35 * sizeof(RecC) : sizeof(VisRec);
+    // buffers of the other kind of plan are freed, not left cached: the plane
+    // budget below counts the held record buffers as reusable
+    if (!P.subpad) {
+        Workspace::get().drop("recs_pad");
+        Workspace::get().drop("rec_cls");
+    }
+    if (grid_mode) Workspace::get().drop("degrid_acc");
     const size_t need_other =
-        (size_t)nvis * (sizeof(VisRec) + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2))) +
+        (size_t)((double)nvis * (rec_bytes + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2)))) +
         (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned) +
         (size_t)P.fft_planes * spec_plane;
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
@@ -2155,14 +2371,17 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     P.pad4 = grid_mode && g.sub == kTileCell;
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
     P.pt.nvis = nvis;
-    P.recs = scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
+    P.recs = P.subpad ? scratch<VisRec>("recs", (std::max<int64_t>(nvis, 1) + 1) / 2 + 1)  // RecC
+                      : scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
+    if (P.subpad) P.cls = scratch<uint8_t>("rec_cls", std::max<int64_t>(nvis, 1));
     return P;
 }
 
 // Bucketing (no host sync except the 4-padded record total): histogram with
 // ranks, scan, scatter of the records, work items, metadata.
 static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st,
-                        bool values_only = false) {
+                        bool values_only = false,
+                        const std::function<void()> &after_clear = nullptr) {
     const Geo &g = P.g;
     Part &pt = P.pt;
     const size_t nkeys = (size_t)g.ntiles * g.nps * g.salt;
@@ -2175,8 +2394,15 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
     pt.ioffs = scratch<unsigned>("ioffs", ngroups + 1);
     pt.nbad = scratch<unsigned long long>("nbad", 1);
     pt.meta = scratch<unsigned>("meta", g.nps + 5);
-    const int64_t icap = std::min<int64_t>(ngroups, pt.nvis) + pt.nvis / P.chunk + 1;
+    // items: <= one per non-empty group plus one per chunk of (padded) records
     const bool cells = g.sub == kTileCell;
+    // one-cell plans: units of ucells keys (gridding: blocks of bx x 8 cells;
+    // degridding: groups of 16)
+    const int ucells = kGroupCell;
+    const int64_t nunits = cells ? (int64_t)nkeys / ucells : ngroups;
+    const int upp = cells ? g.ntiles / ucells : gpp;
+    const int64_t icap =
+        std::min<int64_t>(nunits, pt.nvis) + (P.pad4 ? 4 : 1) * pt.nvis / P.chunk + 1;
     if (cells) pt.fitems = scratch<FineItem>("fitems", icap);
     else pt.items = scratch<Item>("items", icap);
     unsigned *kr = scratch<unsigned>("key_rank", std::max<int64_t>(pt.nvis, 1));
@@ -2193,92 +2419,100 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
         constexpr bool S = decltype(scatter_tag)::value;
         VisRec *out = S ? P.recs : nullptr;
         double *sl = S == values_only ? slots : nullptr;
-        if (in.vis_dtype == SDP_HIP_C128) {
-            if (grid_mode && S && P.pad4)  // 16-byte RecC records
-                k_bucket<double2, S, true, true><<<nb, 256, 0, st>>>(
-                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
-                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
+        auto go = [&](auto vt_tag, auto grid_tag, auto compact_tag, const void *visp) {
+            using VT = typename decltype(vt_tag)::type;
+            constexpr bool G = decltype(grid_tag)::value, C = decltype(compact_tag)::value;
+            const VT *vp = static_cast<const VT *>(visp);
+            k_bucket<VT, S, G, C><<<nb, 256, 0, st>>>(g, pt.nvis, in.uvw, in.uvw_rs, in.freq, vp,
+                                                      in.vrs, in.vcs, in.wgt, in.wrs, in.wcs,
+                                                      in.x, sl, counter, kr, out, pt.nbad,
+                                                      S && P.subpad ? P.cls : nullptr);
+        };
+        auto by_mode = [&](auto vt_tag) {
+            if (grid_mode && S && (P.pad4 || P.subpad))  // 16-byte RecC records
+                go(vt_tag, std::true_type{}, std::true_type{}, in.vis);
             else if (grid_mode)
-                k_bucket<double2, S, true><<<nb, 256, 0, st>>>(
-                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const double2 *)in.vis,
-                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
+                go(vt_tag, std::true_type{}, std::false_type{}, in.vis);
             else
-                k_bucket<double2, S, false><<<nb, 256, 0, st>>>(
-                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
-                    in.wcs, in.x, sl, counter, kr, out, pt.nbad);
-        } else {
-            if (grid_mode && S && P.pad4)  // 16-byte RecC records
-                k_bucket<float2, S, true, true><<<nb, 256, 0, st>>>(
-                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
-                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
-            else if (grid_mode)
-                k_bucket<float2, S, true><<<nb, 256, 0, st>>>(
-                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, (const float2 *)in.vis,
-                    in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, out, pt.nbad);
-            else
-                k_bucket<float2, S, false><<<nb, 256, 0, st>>>(
-                    g, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
-                    in.wcs, in.x, sl, counter, kr, out, pt.nbad);
-        }
+                go(vt_tag, std::false_type{}, std::false_type{}, nullptr);
+        };
+        if (in.vis_dtype == SDP_HIP_C128) by_mode(TypeTag<double2>{});
+        else by_mode(TypeTag<float2>{});
     };
     if (values_only) {  // SDP_HIP_REUSE_BUCKETS: keys, ranks, offsets, items kept
         if (pt.nvis > 0) launch_bucket(std::true_type{}, pt.offs);
         SDP_HIP_CHECK(hipGetLastError());
         return;
     }
+    if (after_clear) after_clear();
     if (pt.nvis > 0) launch_bucket(std::false_type{}, pt.hist);
+    if (cells) {
+        // offsets, pads and items from the units (k_group_sums, one 64-bit
+        // scan over the units, k_group_fill)
+        auto *gsum = scratch<unsigned long long>("gsum", nunits + 1);
+        auto *gofs = scratch<unsigned long long>("gofs", nunits + 1);
+        pt.ioffs = scratch<unsigned>("ioffs", nunits + 1);
+        unsigned *pslots = nullptr;
+        if (P.pad4) {
+            pslots = scratch<unsigned>("pad_slots", kSumSlots);
+            pt.npad = scratch<unsigned>("npad", 1);
+            SDP_HIP_CHECK(hipMemsetAsync(pslots, 0, kSumSlots * sizeof(unsigned), st));
+        }
+        SDP_HIP_CHECK(hipMemsetAsync(gsum + nunits, 0, sizeof(unsigned long long), st));
+        const unsigned gb = grid1d(nunits, 256);
+        if (P.pad4)
+            k_group_sums<true><<<gb, 256, 0, st>>>(nunits, ucells, pt.hist, P.chunk, gsum, pslots);
+        else
+            k_group_sums<false><<<gb, 256, 0, st>>>(nunits, ucells, pt.hist, P.chunk, gsum,
+                                                    nullptr);
+        size_t gtmp = 0;
+        SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, gtmp, gsum, gofs,
+                                                       (int)(nunits + 1), st));
+        void *tmp = scratch<char>("scan_tmp", gtmp + 16);
+        SDP_HIP_CHECK(
+            hipcub::DeviceScan::ExclusiveSum(tmp, gtmp, gsum, gofs, (int)(nunits + 1), st));
+        if (P.pad4) {
+            // the padded record total sizes the record array (one host sync)
+            unsigned long long *htot = pinned_host<unsigned long long>(48, 1);
+            SDP_HIP_CHECK(hipMemcpyAsync(htot, gofs + nunits, sizeof(unsigned long long),
+                                         hipMemcpyDeviceToHost, st));
+            SDP_HIP_CHECK(hipStreamSynchronize(st));
+            P.recs = scratch<VisRec>("recs", ((int64_t)(*htot >> 32) + 1) / 2 + 1);  // RecC
+            k_sum_pads<<<1, 256, 0, st>>>(pslots, pt.npad);
+        }
+        const unsigned fb = grid1d(nunits + 1, 256);
+        if (P.pad4)
+            k_group_fill<true><<<fb, 256, 0, st>>>(nunits, upp, ucells, pt.hist, gofs, P.chunk,
+                                                   pt.offs, pt.ioffs,
+                                                   reinterpret_cast<RecC *>(P.recs), pt.fitems);
+        else
+            k_group_fill<false><<<fb, 256, 0, st>>>(nunits, upp, ucells, pt.hist, gofs, P.chunk,
+                                                    pt.offs, pt.ioffs, nullptr, pt.fitems);
+        if (pt.nvis > 0) launch_bucket(std::true_type{}, pt.offs);
+        k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys,
+                                                          P.pad4 ? pt.npad : nullptr, pt.ioffs,
+                                                          upp, g.nps, pt.meta);
+        SDP_HIP_CHECK(hipGetLastError());
+        return;
+    }
     size_t tmp_bytes = 0;
     SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, pt.hist, pt.offs,
                                                    (int)(nkeys + 1), st));
     void *tmp = scratch<char>("scan_tmp", tmp_bytes + 16);
     size_t tb = tmp_bytes + 16;
-    if (P.pad4) {
-        // scan of the counts rounded up to 4, then the padded total sizes
-        // the record array (one host sync)
-        hipcub::TransformInputIterator<unsigned, Round4, const unsigned *> r4(pt.hist, Round4{});
-        size_t need = 0;
-        SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, r4, pt.offs,
-                                                       (int)(nkeys + 1), st));
-        if (need > tmp_bytes) {
-            tmp_bytes = need;
-            tmp = scratch<char>("scan_tmp", tmp_bytes + 16);
-        }
-        tb = tmp_bytes + 16;
-        SDP_HIP_CHECK(
-            hipcub::DeviceScan::ExclusiveSum(tmp, tb, r4, pt.offs, (int)(nkeys + 1), st));
-        unsigned *htot = pinned_host<unsigned>(48, 1);
-        SDP_HIP_CHECK(hipMemcpyAsync(htot, pt.offs + nkeys, sizeof(unsigned),
-                                     hipMemcpyDeviceToHost, st));
-        SDP_HIP_CHECK(hipStreamSynchronize(st));
-        P.recs = scratch<VisRec>("recs", ((int64_t)*htot + 1) / 2 + 1);  // RecC records
-    } else {
-        SDP_HIP_CHECK(
-            hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.hist, pt.offs, (int)(nkeys + 1), st));
-    }
+    SDP_HIP_CHECK(
+        hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.hist, pt.offs, (int)(nkeys + 1), st));
     if (pt.nvis > 0) launch_bucket(std::true_type{}, pt.offs);
-    if (P.pad4) {
-        unsigned *pslots = scratch<unsigned>("pad_slots", kSumSlots);
-        pt.npad = scratch<unsigned>("npad", 1);
-        SDP_HIP_CHECK(hipMemsetAsync(pslots, 0, kSumSlots * sizeof(unsigned), st));
-        k_pad_cells<<<grid1d((int64_t)nkeys, 256), 256, 0, st>>>(
-            (unsigned)nkeys, pt.hist, pt.offs, reinterpret_cast<RecC *>(P.recs), pslots);
-        k_sum_pads<<<1, 256, 0, st>>>(pslots, pt.npad);
-    }
 
     // work items (p0-major, so a first-plane range is a contiguous item range)
     k_items_count<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, kpg, pt.offs, P.chunk, pt.nch);
     tb = tmp_bytes + 16;
     SDP_HIP_CHECK(
         hipcub::DeviceScan::ExclusiveSum(tmp, tb, pt.nch, pt.ioffs, (int)(ngroups + 1), st));
-    if (cells)
-        k_items_fill_cells<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, gpp, pt.offs, pt.ioffs,
-                                                                 P.chunk, pt.fitems);
-    else
-        k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, kpg, gpp, pt.offs, pt.ioffs,
-                                                           P.chunk, pt.items);
-    k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys,
-                                                      P.pad4 ? pt.npad : nullptr, pt.ioffs, gpp,
-                                                      g.nps, pt.meta);
+    k_items_fill<<<grid1d(ngroups, 256), 256, 0, st>>>(ngroups, kpg, gpp, pt.offs, pt.ioffs,
+                                                       P.chunk, pt.items);
+    k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys, nullptr, pt.ioffs,
+                                                      gpp, g.nps, pt.meta);
     SDP_HIP_CHECK(hipGetLastError());
 }
 
@@ -2321,18 +2555,20 @@ static void launch_grid_mfma_fi(const Plan &P, int p_lo, int p_hi, hipStream_t s
 
 template <int W, bool WS>
 static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
-    constexpr size_t lds = grid_mfma_pad_lds();
+    constexpr size_t lds = grid_mfma_pad_lds(2);
+    // one-cell plans: one FineItem per item; padded sub-sorted coarse plans: 16
     const auto r = chunk_items(P, p_lo, p_hi);
-    const unsigned n = r.second - r.first;
+    const unsigned per = P.subpad ? 16u : 1u;
+    const unsigned n = per * (r.second - r.first);
     if (n == 0) return;
-    k_grid_mfma_pad<W, WS><<<n, 64, lds, st>>>(P.g, reinterpret_cast<const RecC *>(P.recs),
-                                               P.pt.fitems + r.first, n, (float *)P.grid, p_lo,
-                                               p_hi);
+    const RecC *recs = P.subpad ? P.recs_pad : reinterpret_cast<const RecC *>(P.recs);
+    k_grid_mfma_pad<W, WS><<<n, 64, lds, st>>>(P.g, recs, P.pt.fitems + per * (size_t)r.first, n,
+                                               (float *)P.grid, p_lo, p_hi);
 }
 
 template <int W>
 static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
-    if (P.pad4) {
+    if (P.pad4 || P.subpad) {
         if (P.g.do_w) return launch_grid_mfma_pad<W, true>(P, p_lo, p_hi, st);
         return launch_grid_mfma_pad<W, false>(P, p_lo, p_hi, st);
     }
@@ -2382,6 +2618,7 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
     info->nitems = P.pt.nitems;
     info->plane_chunk = P.chunk_planes;
     info->bucket = P.g.sub;
+    info->padded = (P.pad4 || P.subpad) ? 1 : 0;
     info->grid_launches = (P.g.nplanes + P.chunk_planes - 1) / P.chunk_planes;
 }
 
@@ -2437,10 +2674,13 @@ static dim3 tr_grid(const Geo &g, int xrows, int np) {
 
 // Bucketing with the fused weight sum (slots zeroed before the count pass,
 // folded into *sumwt after it), then the metadata read back by the host.
-static void bucket_all(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st) {
+// `after_clear` runs once the histogram clearing is queued (work put on
+// another stream there does not compete with that memset).
+static void bucket_all(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st,
+                       const std::function<void()> &after_clear = nullptr) {
     double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
     if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
-    bucket_part(P, in, grid_mode, st);
+    bucket_part(P, in, grid_mode, st, false, after_clear);
     if (slots) k_sum_slots<<<1, 64, 0, st>>>(slots, in.x.sumwt);
     read_part_meta(P, st);
 }
@@ -2450,8 +2690,28 @@ static void subsort_items(Plan &P, hipStream_t st) {
     Part &pt = P.pt;
     if (pt.nitems == 0) return;
     pt.fitems = scratch<FineItem>("fitems", (size_t)pt.nitems * 16);
-    k_subsort<true><<<(unsigned)pt.nitems, kSubThreads, 0, st>>>(P.g, pt.items, P.recs,
-                                                                 pt.fitems);
+    const unsigned ni = (unsigned)pt.nitems;
+    if (!P.subpad) {
+        k_subsort<true><<<ni, kSubThreads, 0, st>>>(P.g, pt.items, P.recs, pt.fitems);
+        SDP_HIP_CHECK(hipGetLastError());
+        return;
+    }
+    // padded item sizes -> item bases (scan) -> total (one host sync) -> the
+    // padded, cell-ordered copy of the records
+    unsigned *pcnt = scratch<unsigned>("sub_pcnt", (size_t)ni + 1);
+    unsigned *pbase = scratch<unsigned>("sub_pbase", (size_t)ni + 1);
+    SDP_HIP_CHECK(hipMemsetAsync(pcnt + ni, 0, sizeof(unsigned), st));
+    k_sub_count<<<ni, 256, 0, st>>>(pt.items, P.cls, pcnt);
+    size_t tb = 0;
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, pcnt, pbase, (int)ni + 1, st));
+    void *tmp = scratch<char>("scan_tmp", tb + 16);
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, pcnt, pbase, (int)ni + 1, st));
+    unsigned *htot = pinned_host<unsigned>(56, 1);
+    SDP_HIP_CHECK(hipMemcpyAsync(htot, pbase + ni, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    SDP_HIP_CHECK(hipStreamSynchronize(st));
+    P.recs_pad = scratch<RecC>("recs_pad", (size_t)*htot + 1);
+    k_subsort_pad<<<ni, kSubThreads, 0, st>>>(P.g, pt.items, reinterpret_cast<const RecC *>(P.recs),
+                                              P.cls, pbase, P.recs_pad, pt.fitems);
     SDP_HIP_CHECK(hipGetLastError());
 }
 
@@ -2500,21 +2760,23 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     // stream after the call's earlier work on `st`; the gridding waits for it
     // (single calls only: on C4's streamed batches it measured 1-2 % slower)
     hipEvent_t zdone = nullptr;
-    if (first && !batched && env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0) {
+    auto start_zero = [&] {
+        if (!(first && !batched && env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0)) return;
         hipStream_t aux = aux_stream();
         stream_after(aux, st);
         zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
         SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
         SDP_HIP_CHECK(hipEventRecord(zdone, aux));
-    }
+    };
     if (reuse) {
+        start_zero();
         // value pass only (weight sums included)
         double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
         if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
         bucket_part(P, inx, true, st, true);
         if (slots) k_sum_slots<<<1, 64, 0, st>>>(slots, in.x.sumwt);
     } else {
-        bucket_all(P, inx, true, st);
+        bucket_all(P, inx, true, st, start_zero);
     }
     if (P.subsort) subsort_items(P, st);
     if (keep) keep_buckets(P, in);
@@ -2589,10 +2851,6 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     const double *tab = phi_table(g.W, g.beta, st);
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
     const int64_t nvis = in.nrow * (int64_t)in.nchan;
-    // the output zeroing and the first plane chunk's band zeroing (HBM
-    // writes) overlap the bucketing (memory-side atomics; it reads uvw and
-    // weights only) on the auxiliary stream, after the call's earlier work
-    hipEvent_t zdone = nullptr;
     auto zero_vis = [&](hipStream_t s) {
         if (accumulate || nvis <= 0) return;
         if (in.vis_dtype == SDP_HIP_C128)
@@ -2604,17 +2862,46 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
                                                                   in.vrs, in.vcs, oc);
         SDP_HIP_CHECK(hipGetLastError());
     };
-    if (env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0) {
+    // screens + FFTs of planes [p_lo, p_lo + np) into the grid
+    std::vector<std::unique_ptr<StageTimer>> stage_t;
+    auto plane_stage = [&](int p_lo, int np, hipStream_t s) {
+        for (int sb = 0; sb < np; sb += P.fft_planes) {
+            const int nb = std::min(P.fft_planes, np - sb);
+            stage_t.emplace_back(new StageTimer(s));
+            StageTimer &t2 = *stage_t.back();
+            t2.mark();
+            const dim3 grd(grid1d(g.ngx, 256), g.ny);
+            k_screen_adj_t<<<grd, 256, 0, s>>>(g, dirty, sx, sy, p_lo + sb, nb, P.spec, tab);
+            SDP_HIP_CHECK(hipGetLastError());
+            t2.mark();
+            fft_rows_x(P, nb, HIPFFT_FORWARD, s);
+            if (P.row_hi > P.row_lo)
+                k_tr_t_to_grid<<<tr_grid(g, P.row_hi - P.row_lo, nb), dim3(kTr, kTrRows), 0,
+                                 s>>>(g, P.spec, P.grid + (size_t)sb * g.ngx * g.ngy, P.row_lo,
+                                      P.row_hi);
+            SDP_HIP_CHECK(hipGetLastError());
+            fft_rows_y(P, sb, nb, HIPFFT_FORWARD, s);
+            t2.mark();
+        }
+    };
+    // the output zeroing and the first plane chunk's band zeroing (HBM
+    // writes) overlap the bucketing on the auxiliary stream, once the
+    // histogram clearing is queued.  (Running the whole plane stage there
+    // too measured slower on C2: 15.6 vs 15.4 ms -- the FFTs' HBM streaming
+    // and the bucketing's memory-side atomics slow each other down.)
+    const bool overlap = env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0;
+    hipEvent_t zdone = nullptr;
+    auto start_aux = [&] {
+        if (!overlap) return;
         hipStream_t aux = aux_stream();
         stream_after(aux, st);
         zero_vis(aux);
         zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
         SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
         SDP_HIP_CHECK(hipEventRecord(zdone, aux));
-    } else {
-        zero_vis(st);
-    }
-    bucket_all(P, in, false, st);
+    };
+    if (!overlap) zero_vis(st);
+    bucket_all(P, in, false, st, start_aux);
     if (P.subsort) subsort_items(P, st);
     // all planes in one pass into plain contiguous c64 visibilities: the
     // degridder applies the record factor and writes each visibility once
@@ -2637,25 +2924,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         } else {
             zero_band(P, np, st);
         }
-        for (int sb = 0; sb < np; sb += P.fft_planes) {
-            const int nb = std::min(P.fft_planes, np - sb);
-            StageTimer t2(st);
-            t2.mark();
-            const dim3 grd(grid1d(g.ngx, 256), g.ny);
-            k_screen_adj_t<<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_lo + sb, nb, P.spec, tab);
-            SDP_HIP_CHECK(hipGetLastError());
-            t2.mark();
-            fft_rows_x(P, nb, HIPFFT_FORWARD, st);
-            if (P.row_hi > P.row_lo)
-                k_tr_t_to_grid<<<tr_grid(g, P.row_hi - P.row_lo, nb), dim3(kTr, kTrRows), 0,
-                                 st>>>(g, P.spec, P.grid + (size_t)sb * g.ngx * g.ngy, P.row_lo,
-                                       P.row_hi);
-            SDP_HIP_CHECK(hipGetLastError());
-            fft_rows_y(P, sb, nb, HIPFFT_FORWARD, st);
-            t2.mark();
-            tscr += t2.ms(0, 1);
-            tfft += t2.ms(1, 2);
-        }
+        plane_stage(p_lo, np, st);
         StageTimer tg(st);
         tg.mark();
 #define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, acc, st)
@@ -2668,6 +2937,10 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     if (zdone) {  // (no plane pass ran)
         SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
         SDP_HIP_CHECK(hipEventDestroy(zdone));
+    }
+    for (auto &t : stage_t) {
+        tscr += t->ms(0, 1);
+        tfft += t->ms(1, 2);
     }
     if (!P.vdirect && P.pt.nvis > 0) {
         const unsigned nb = std::min<unsigned>(grid1d(P.pt.nvis, 256), 16384);

@@ -59,6 +59,7 @@ class WGridInfo(ctypes.Structure):
         ("ms_screen", ctypes.c_float),
         ("bucket", c_int),
         ("grid_launches", c_int),
+        ("padded", c_int),
     ]
 
     def as_dict(self):

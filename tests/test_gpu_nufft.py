@@ -60,6 +60,7 @@ def test_ms2dirty_matches_exact(dow, vdt, flip, bucket):
                                  cell * 0.9, 1e-7, dow, flip_uw=flip)
     assert info["support"] == 8
     assert info["bucket"] == (16 if bucket == "coarse" else 1)
+    assert info["padded"] == 1  # invert: k_grid_mfma_pad on 4-padded cells
     assert info["grid_launches"] == 1
     assert rel_rms(out.cpu().numpy(), ex) < TOL
 
