@@ -54,6 +54,12 @@ extern "C" {
  * in between drops the kept bucketing: the call then fails with
  * SDP_HIP_ERR_INVALID_ARG. */
 #define SDP_HIP_REUSE_BUCKETS 32u
+/* epsilon below 1e-7 (the reference's default 1e-12 included) runs the fp64
+ * NUFFT: W = ceil(-log10(epsilon/10)) in [9, 16], fp64 taps, records, c128
+ * planes, Z2Z FFTs, one-cell buckets (grids whose (first plane, cell)
+ * histogram exceeds 2^28 keys are refused).  SDP_HIP_FP32 keeps the fp32
+ * NUFFT at its floor instead (W = 8, ~1e-6 relative RMS), as before. */
+#define SDP_HIP_FP32 64u
 
 /* Diagnostics filled by the NUFFT entry points (may be NULL). */
 typedef struct sdp_hip_wgrid_info {
@@ -73,6 +79,7 @@ typedef struct sdp_hip_wgrid_info {
                              chunk); ms_grid is their summed time           */
     int padded;           /* invert: gridded on cells padded to 4 records
                              (k_grid_mfma_pad; 0: k_grid_mfma)              */
+    int fp64;             /* the fp64 NUFFT ran (epsilon < 1e-7)            */
 } sdp_hip_wgrid_info;
 
 /* Library/ABI version and a device probe. */

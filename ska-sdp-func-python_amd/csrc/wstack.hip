@@ -1226,25 +1226,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 // The region tile is flushed once per item with buffer float atomics.
 constexpr int kTapRec = 24;    // floats per record row of the tap block
 constexpr int kTapBatch = 16;  // records per tap block
-constexpr int kRegY = 15;     // region tile rows: 8 + 8 - 1 cells
 constexpr int kRegCell = 16;  // floats per region cell: 8 planes x re/im
 
-// region tile of a block BXC cells wide: (BXC + 8 - 1) x kRegY cells
-constexpr size_t grid_mfma_pad_lds(int bxc) {
-    return (size_t)(bxc + 7) * kRegY * kRegCell * sizeof(float) + kTapBatch * sizeof(float4) +
-           (size_t)kTapBatch * kTapRec * sizeof(float) + kTapBatch * sizeof(float2);
+// Work unit of NG groups: 1 (one-cell plans: a chunk of one 2 x 8-cell
+// group) or 16 (large grids: the 16 groups of a sub-sorted 16 x 16-cell
+// coarse item, gridded into one 23 x 23-cell region -- a quarter of the
+// flushed atomics of 16 separate 9 x 15-cell regions; C4's sparse groups,
+// ~120 records each, were bound by those atomics: 121 GB per 1.67 Gvis).
+template <int NG>
+struct PadUnit {
+    static constexpr int TX = NG == 1 ? 2 : 16, TY = NG == 1 ? 8 : 16;  // cells
+    static constexpr int RGX = TX + 7, RGY = TY + 7;                     // region cells
+};
+
+template <int NG>
+constexpr size_t grid_mfma_pad_lds() {
+    return (size_t)PadUnit<NG>::RGX * PadUnit<NG>::RGY * kRegCell * sizeof(float) +
+           kTapBatch * sizeof(float4) + (size_t)kTapBatch * kTapRec * sizeof(float) +
+           kTapBatch * sizeof(float2);
 }
 
-template <int W, bool WS>
+template <int W, bool WS, int NG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma_pad(
     Geo g, const RecC *__restrict__ recs, const FineItem *__restrict__ items, uint32_t n_items,
     float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
-    constexpr int BXC = 2;  // cells per group in x
+    static_assert(NG == 1 || NG == 16, "units of one group or of a 16x16-cell item");
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int NQ = WS ? W : 1;
-    constexpr int RX = BXC + W - 1, RY = 8 + W - 1;  // cells a footprint of the block reaches
-    constexpr int kRegX = BXC + 7;
+    constexpr int kRegX = PadUnit<NG>::RGX, kRegY = PadUnit<NG>::RGY;
+    // cells a footprint of the unit reaches
+    constexpr int RX = PadUnit<NG>::TX + W - 1, RY = PadUnit<NG>::TY + W - 1;
     float *const reg = reinterpret_cast<float *>(tile);  // [kRegX][kRegY][16]
     float4 *const stage = reinterpret_cast<float4 *>(reg + kRegX * kRegY * kRegCell);
     float *const blk = reinterpret_cast<float *>(stage + kTapBatch);  // [kTapBatch][kTapRec]
@@ -1269,13 +1281,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     constexpr int acc_t = 2 * kRegY * kRegCell;  // + t N-tiles (two x rows each)
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        // the item and the ends of its group's 16 cells (record indices): one
-        // 80-byte descriptor, scalar loads
+        // the unit's first group: its origin is the unit's; for NG = 1 the
+        // item and the ends of its group's 16 cells (one 80-byte
+        // descriptor, scalar loads)
+        const uint32_t u = NG == 1 ? w_it : item_index(w_it, n_items);
         uint32_t bnd[kGroupCell];
-        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
-        if (it.b >= it.e) continue;  // (empty groups of a sub-sorted coarse item)
+        Item it = NG == 1 ? load_fine_item<kGroupCell>(items, w_it, n_items, bnd)
+                          : load_fine_item<kGroupCell>(items + (size_t)u * NG, 0, 1, bnd);
+        if (NG == 1 && it.b >= it.e) continue;
         int ibase, jbase;
         group_origin(g, (int)it.tile, ibase, jbase);
+        const uint32_t p0 = it.p0;
 
         wave_lds_sync();  // the previous item's flush reads of the region
         {
@@ -1310,11 +1326,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, o.b[t] * o.v, acc[t], 0, 0, 0);
         };
 
-        {
+        for (int gi = 0; gi < NG; ++gi) {
+            if (NG > 1 && gi > 0) it = load_fine_item<kGroupCell>(items + (size_t)u * NG + gi, 0, 1, bnd);
             const uint32_t rb = it.b, re = it.e;
+            if (rb >= re) continue;  // (empty groups of a sub-sorted coarse item)
+            // the group's first cell in the unit: x pair gi >> 1, y half gi & 1
+            const int gxo = NG == 1 ? 0 : 2 * (gi >> 1), gyo = NG == 1 ? 0 : 8 * (gi & 1);
             int cur = -1;  // cell of the accumulators (wave-uniform)
             auto load_cell = [&](int cell) {
-                const int xo = cell & 1, yo = cell >> 1;
+                const int xo = gxo + (cell & 1), yo = gyo + (cell >> 1);
                 cbase = (xo * kRegY + yo) * kRegCell + acc_lane;
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
@@ -1418,7 +1438,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             const float *src = reg + (xl * kRegY + yl) * kRegCell + (f & 1);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                const int p = (int)it.p0 + q;
+                const int p = (int)p0 + q;
                 const float val = src[2 * q];
                 if (p >= p_lo && p < p_hi && val != 0.0f) {
                     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1589,6 +1609,26 @@ __device__ __forceinline__ PixelGeom pixel_geom(const Geo &g, int ix, int iy,
     return p;
 }
 
+// complex element of the planes: float2 (fp32 path) or double2 (fp64 path)
+template <class T>
+__device__ __forceinline__ T cplx(double re, double im) {
+    T v;
+    v.x = re;
+    v.y = im;
+    return v;
+}
+template <class T>
+__device__ __forceinline__ void sincospi_t(double x, double *sn, double *cs) {
+    if constexpr (std::is_same<T, double2>::value) {
+        sincospi(x, sn, cs);
+    } else {
+        float s_, c_;
+        sincospif((float)x, &s_, &c_);
+        *sn = s_;
+        *cs = c_;
+    }
+}
+
 // ---- transposed y-spectrum layout for the pruned 2-D FFT -------------
 // T[q][iy][kx] (iy = image row index 0..ny-1, i.e. ky = (iy - ny/2) mod ngy;
 // kx = 0..ngx-1) holds, per plane, the needed y-frequency columns of the grid
@@ -1598,15 +1638,15 @@ constexpr int kTrRows = 4;   // threads along the tile's second axis (64 x 4 = 2
 
 // grid[q][x][ky(iy)] -> T[q][iy][x] for the rows x in [row_lo, row_hi); the
 // rest of each T row is kept zero by the caller (persistent zeros)
-__global__ __launch_bounds__(256) void k_tr_grid_to_t(Geo g, const float2 *__restrict__ grid,
-                                                      float2 *__restrict__ t, int row_lo,
-                                                      int row_hi) {
-    __shared__ float2 sm[kTr][kTr + 1];
+template <class T>
+__global__ __launch_bounds__(256) void k_tr_grid_to_t(Geo g, const T *__restrict__ grid,
+                                                      T *__restrict__ t, int row_lo, int row_hi) {
+    __shared__ T sm[kTr][kTr + 1];
     const int x0 = row_lo + blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
     const int64_t plane = (int64_t)g.ngx * g.ngy, tplane = (int64_t)g.ny * g.ngx;
     for (int r = threadIdx.y; r < kTr; r += kTrRows) {
         const int x = x0 + r, iy = i0 + threadIdx.x;
-        float2 v = make_float2(0.0f, 0.0f);
+        T v = cplx<T>(0.0, 0.0);
         if (x < row_hi && iy < g.ny) {
             const int Y = iy - g.ny / 2;
             const int ky = Y < 0 ? Y + g.ngy : Y;
@@ -1622,16 +1662,16 @@ __global__ __launch_bounds__(256) void k_tr_grid_to_t(Geo g, const float2 *__res
 }
 
 // T[q][iy][x] -> grid[q][x][ky(iy)] for the rows x in [row_lo, row_hi)
-__global__ __launch_bounds__(256) void k_tr_t_to_grid(Geo g, const float2 *__restrict__ t,
-                                                      float2 *__restrict__ grid, int row_lo,
-                                                      int row_hi) {
-    __shared__ float2 sm[kTr][kTr + 1];
+template <class T>
+__global__ __launch_bounds__(256) void k_tr_t_to_grid(Geo g, const T *__restrict__ t,
+                                                      T *__restrict__ grid, int row_lo, int row_hi) {
+    __shared__ T sm[kTr][kTr + 1];
     const int x0 = row_lo + blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
     const int64_t plane = (int64_t)g.ngx * g.ngy, tplane = (int64_t)g.ny * g.ngx;
     for (int r = threadIdx.y; r < kTr; r += kTrRows) {
         const int iy = i0 + r, x = x0 + threadIdx.x;
         sm[r][threadIdx.x] = (iy < g.ny && x < row_hi) ? t[q * tplane + (int64_t)iy * g.ngx + x]
-                                                       : make_float2(0.0f, 0.0f);
+                                                       : cplx<T>(0.0, 0.0);
     }
     __syncthreads();
     for (int r = threadIdx.y; r < kTr; r += kTrRows) {
@@ -1646,7 +1686,8 @@ __global__ __launch_bounds__(256) void k_tr_t_to_grid(Geo g, const float2 *__res
 
 // w screens + grid correction reading the transposed spectrum (ix fastest:
 // coalesced T reads; RASCIL's transposed output (sx = 1) is coalesced too)
-__global__ void k_screen_fwd_t(Geo g, const float2 *__restrict__ t, int p_begin, int np,
+template <class T>
+__global__ void k_screen_fwd_t(Geo g, const T *__restrict__ t, int p_begin, int np,
                                double *dirty, int64_t sx, int64_t sy, int accumulate,
                                const double *__restrict__ tab) {
     const int ix = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1656,15 +1697,15 @@ __global__ void k_screen_fwd_t(Geo g, const float2 *__restrict__ t, int p_begin,
     double res = 0.0;
     if (p.inside) {
         const int64_t tplane = (int64_t)g.ny * g.ngx;
-        const float2 *src = t + (int64_t)iy * g.ngx + p.gx;
+        const T *src = t + (int64_t)iy * g.ngx + p.gx;
         if (g.do_w) {
             double acc = 0.0;
             for (int q = 0; q < np; ++q) {
-                const float2 h = src[q * tplane];
+                const T h = src[q * tplane];
                 double ph = (g.w0 + (p_begin + q) * g.dw) * p.s;
                 ph -= rint(ph);
-                float sn, cs;
-                sincospif((float)(2.0 * ph), &sn, &cs);
+                double sn, cs;
+                sincospi_t<T>(2.0 * ph, &sn, &cs);
                 acc += (double)h.x * cs - (double)h.y * sn;
             }
             res = acc * p.corr;
@@ -1678,8 +1719,9 @@ __global__ void k_screen_fwd_t(Geo g, const float2 *__restrict__ t, int p_begin,
 
 // adjoint: T[q][iy][kx] = screen(q) * corr * dirty for kx in the image's
 // x-frequencies, 0 for the other kx (full rows are written)
+template <class T>
 __global__ void k_screen_adj_t(Geo g, const double *__restrict__ dirty, int64_t sx, int64_t sy,
-                               int p_begin, int np, float2 *__restrict__ t,
+                               int p_begin, int np, T *__restrict__ t,
                                const double *__restrict__ tab) {
     const int kx = blockIdx.x * blockDim.x + threadIdx.x;
     const int iy = blockIdx.y;
@@ -1687,9 +1729,9 @@ __global__ void k_screen_adj_t(Geo g, const double *__restrict__ dirty, int64_t 
     const int X = kx < g.ngx / 2 ? kx : kx - g.ngx;
     const int ix = X + g.nx / 2;
     const int64_t tplane = (int64_t)g.ny * g.ngx;
-    float2 *dst = t + (int64_t)iy * g.ngx + kx;
+    T *dst = t + (int64_t)iy * g.ngx + kx;
     if (ix < 0 || ix >= g.nx) {
-        for (int q = 0; q < np; ++q) dst[q * tplane] = make_float2(0.0f, 0.0f);
+        for (int q = 0; q < np; ++q) dst[q * tplane] = cplx<T>(0.0, 0.0);
         return;
     }
     const PixelGeom p = pixel_geom(g, ix, iy, tab);
@@ -1698,12 +1740,12 @@ __global__ void k_screen_adj_t(Geo g, const double *__restrict__ dirty, int64_t 
         for (int q = 0; q < np; ++q) {
             double ph = (g.w0 + (p_begin + q) * g.dw) * p.s;
             ph -= rint(ph);
-            float sn, cs;
-            sincospif((float)(2.0 * ph), &sn, &cs);
-            dst[q * tplane] = make_float2((float)(val * cs), (float)(-val * sn));
+            double sn, cs;
+            sincospi_t<T>(2.0 * ph, &sn, &cs);
+            dst[q * tplane] = cplx<T>(val * cs, -val * sn);
         }
     } else {
-        dst[0] = make_float2((float)val, 0.0f);
+        dst[0] = cplx<T>(val, 0.0);
     }
 }
 
@@ -1792,6 +1834,378 @@ __global__ void k_finalize(int64_t n, int nchan,
 }
 
 // ------------------------------------------------------------------------
+// kernels: the fp64 NUFFT (epsilon < 1e-7, the reference's default 1e-12)
+// ------------------------------------------------------------------------
+// ducc0 computes in fp64 (ng.py:251-254, double_precision_accumulation), so
+// a request below the fp32 floor runs this path: W = ceil(-log10(eps/10)) in
+// [9, 16], fp64 coordinates, taps, records, grid planes (c128), FFT (Z2Z)
+// and screens.  One-cell buckets (no padding) and FineItem work items as in
+// fp32; the gridder/degridder are VALU (fp64 FMA; the fp64 matrix rate of
+// gfx950 equals its vector rate, and W = 13 does not tile the 16x16x4 shape).
+constexpr int kMinW64 = 9, kMaxW64 = 16;
+constexpr int kTap64 = 16;  // records per tap block
+
+struct __attribute__((aligned(16))) VisRec64 {
+    double cre, cim;    // gridding: vis*wgt*exp(2 pi i w s0); degridding: wgt*exp(-2 pi i w s0)
+    double du, dv, dw;  // offset of the first tap from the exact position (cells / planes)
+    uint32_t ij, p0, idx, pad;
+};
+static_assert(sizeof(VisRec64) == 64, "record layout");
+
+// tap t of offset f: exp(beta (sqrt(1 - x^2) - 1)), x = (f + t) 2 / W
+__device__ __forceinline__ double es_tap64(double f, int t, double ihw, double beta) {
+    const double x = (f + (double)t) * ihw;
+    const double y = 1.0 - x * x;
+    return y > 0.0 ? exp(beta * (sqrt(y) - 1.0)) : 0.0;
+}
+
+template <class VT>
+__device__ __forceinline__ double2 eff_vis_d(const VT *vis, int64_t vrs, int64_t vcs,
+                                             const VisExtra &x, int64_t row, int chan) {
+    const VT *p = vis + row * vrs + chan * vcs;
+    if (!x.conv) {
+        if (!x.fbytes) return load_vis_d(p);
+        const double m = flag_mask(x, row, chan, x.fpol);
+        if (m == 0.0) return make_double2(0.0, 0.0);
+        const double2 v = load_vis_d(p);
+        return make_double2(v.x * m, v.y * m);
+    }
+    double re = 0.0, im = 0.0;
+    for (int k = 0; k < x.npv; ++k) {
+        if (x.cre[k] == 0.0 && x.cim[k] == 0.0) continue;
+        double m = 1.0;
+        if (x.fbytes) {
+            m = flag_mask(x, row, chan, k);
+            if (m == 0.0) continue;
+        }
+        double2 v = load_vis_d(p + k * x.vps);
+        v.x *= m;
+        v.y *= m;
+        re += x.cre[k] * v.x - x.cim[k] * v.y;
+        im += x.cre[k] * v.y + x.cim[k] * v.x;
+    }
+    return make_double2(re, im);
+}
+
+// value pass of the fp64 path (the count pass is k_bucket's): VisRec64 at
+// offs[key] + rank, value and phase factor in fp64
+template <class VT, bool kGrid>
+__global__ void k_bucket_f64(Geo g, int64_t nvis, const double *__restrict__ uvw, int64_t uvw_rs,
+                             const double *__restrict__ freq, const VT *__restrict__ vis,
+                             int64_t vrs, int64_t vcs, const void *__restrict__ wgt, int64_t wrs,
+                             int64_t wcs, VisExtra x, double *sw_slots,
+                             const unsigned *__restrict__ counter,
+                             const unsigned *__restrict__ rk, VisRec64 *__restrict__ recs) {
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const bool valid = v < nvis;
+    int64_t row = 0;
+    int chan = 0;
+    double wd = 0.0;
+    if (valid) {
+        row = v / g.nchan;
+        chan = (int)(v - row * g.nchan);
+        wd = eff_weight(wgt, wrs, wcs, x, row, chan);
+    }
+    if (sw_slots) {  // (a reused bucketing: the count pass did not sum the weights)
+        double ws = wd;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ws += __shfl_xor(ws, o, 64);
+        if ((threadIdx.x & 63) == 0 && ws != 0.0)
+            atomicAdd(&sw_slots[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) &
+                                (kSumSlots - 1)],
+                      ws);
+    }
+    if (!valid) return;
+    const unsigned mine = rk[v];
+    if (mine == 0xffffffffu) return;
+    const Coord c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
+    const unsigned pos = counter[coord_key(g, c, row)] + mine;
+    double cr = wd, ci = 0.0;
+    if (kGrid) {
+        const double2 xv = (vis && wd != 0.0) ? eff_vis_d(vis, vrs, vcs, x, row, chan)
+                                              : make_double2(1.0, 0.0);
+        cr = wd != 0.0 ? xv.x * wd : 0.0;
+        ci = wd != 0.0 ? xv.y * wd : 0.0;
+    }
+    if (g.do_w || x.shift) {
+        double ph = g.do_w ? c.w * g.s0 : 0.0;
+        if (x.shift) {
+            const double *u = uvw + row * uvw_rs;
+            ph += (u[0] * x.sl + u[1] * x.sm + u[2] * x.sn) * (freq[chan] / kCLight);
+        }
+        ph -= rint(ph);
+        double sn, cs;
+        sincospi(2.0 * ph, &sn, &cs);
+        if (!kGrid) sn = -sn;
+        const double r_ = cr * cs - ci * sn, i_ = cr * sn + ci * cs;
+        cr = r_;
+        ci = i_;
+    }
+    VisRec64 rec;
+    rec.cre = cr;
+    rec.cim = ci;
+    rec.du = c.du;
+    rec.dv = c.dv;
+    rec.dw = c.dw;
+    rec.ij = (uint32_t)c.ic0 | ((uint32_t)c.jc0 << 16);
+    rec.p0 = (uint32_t)c.p0;
+    rec.idx = (uint32_t)v;
+    rec.pad = 0u;
+    recs[pos] = rec;
+}
+
+template <int W, bool WS>
+constexpr size_t grid_f64_lds() {
+    return (size_t)(WS ? W : 1) * (W + 1) * (W + 7) * sizeof(double2) +
+           (size_t)kTap64 * (3 * W * sizeof(double) + sizeof(double2));
+}
+
+// The taps of up to kTap64 records into LDS ([record][u | v | w][W]) and
+// their values (cv), every lane busy; returns the record count.
+template <int W, bool WS>
+__device__ __forceinline__ int stage_taps64(const VisRec64 *__restrict__ recs, uint32_t b0,
+                                            uint32_t e, double *tap, double2 *cv, double ihw,
+                                            double beta) {
+    constexpr int TR = 3 * W;
+    const int nb = (int)min((uint32_t)kTap64, e - b0);
+    for (int t = threadIdx.x; t < nb * TR; t += 64) {
+        const int r = t / TR, k = t - r * TR, ax = k / W, j = k - ax * W;
+        const VisRec64 *R = recs + b0 + r;
+        double tv;
+        if (ax == 2 && !WS) tv = j == 0 ? 1.0 : 0.0;
+        else tv = es_tap64(ax == 0 ? R->du : (ax == 1 ? R->dv : R->dw), j, ihw, beta);
+        tap[t] = tv;
+    }
+    if ((int)threadIdx.x < nb)
+        cv[threadIdx.x] = make_double2(recs[b0 + threadIdx.x].cre, recs[b0 + threadIdx.x].cim);
+    return nb;
+}
+
+// fp64 gridder: one wave per FineItem (a chunk of a 2 x 8-cell group's
+// records, ordered by cell).  Lane l owns the footprint taps (kx, ky) =
+// divmod(l + 64 i, W) and accumulates, per cell, c tw[q] tu[kx] tv[ky] for
+// every plane q in registers; a cell change adds them into the region's
+// (2 + W - 1) x (8 + W - 1) x W c128 LDS tile, flushed once per item with
+// fp64 global atomics (zeros skipped).
+template <int W, bool WS>
+__global__ __launch_bounds__(64) void k_grid_f64(Geo g, const VisRec64 *__restrict__ recs,
+                                                 const FineItem *__restrict__ items,
+                                                 uint32_t n_items, double *__restrict__ grid,
+                                                 int p_lo, int p_hi) {
+    constexpr int NQ = WS ? W : 1;
+    constexpr int RX = W + 1, RY = W + 7, NP = (W * W + 63) / 64, TR = 3 * W;
+    extern __shared__ __attribute__((aligned(16))) double2 sm64[];
+    double2 *const reg = sm64;  // [NQ][RX][RY]
+    double *const tap = reinterpret_cast<double *>(reg + NQ * RX * RY);
+    double2 *const cv = reinterpret_cast<double2 *>(tap + kTap64 * TR);
+    const int lane = threadIdx.x;
+    const double ihw = 2.0 / W, beta = (double)g.beta;
+    int px[NP], py[NP];
+    bool pv[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int pp = lane + 64 * i;
+        pv[i] = pp < W * W;
+        px[i] = pv[i] ? pp / W : 0;
+        py[i] = pv[i] ? pp % W : 0;
+    }
+    const size_t plane_elems = (size_t)g.ngx * g.ngy;
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        uint32_t bnd[kGroupCell];
+        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
+        if (it.b >= it.e) continue;
+        int ibase, jbase;
+        group_origin(g, (int)it.tile, ibase, jbase);
+        wave_lds_sync();  // the previous item's flush reads of the region
+        for (int i = lane; i < NQ * RX * RY; i += 64) reg[i] = make_double2(0.0, 0.0);
+        double2 acc[NP][NQ];
+#pragma unroll
+        for (int i = 0; i < NP; ++i)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) acc[i][q] = make_double2(0.0, 0.0);
+        int cur = -1;
+        auto flush_acc = [&]() {
+            const int xo = cur & 1, yo = cur >> 1;
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                if (!pv[i]) continue;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    double2 *d = reg + (q * RX + xo + px[i]) * RY + yo + py[i];
+                    double2 o = *d;
+                    o.x += acc[i][q].x;
+                    o.y += acc[i][q].y;
+                    *d = o;
+                    acc[i][q] = make_double2(0.0, 0.0);
+                }
+            }
+        };
+        for (uint32_t b0 = it.b; b0 < it.e; b0 += kTap64) {
+            wave_lds_sync();  // the previous block's tap reads
+            const int nb = stage_taps64<W, WS>(recs, b0, it.e, tap, cv, ihw, beta);
+            wave_lds_sync();
+            for (int r = 0; r < nb; ++r) {
+                const uint32_t ri = b0 + (uint32_t)r;
+                int cell = 0;
+#pragma unroll
+                for (int c = 0; c < kGroupCell - 1; ++c) cell += ri >= bnd[c] ? 1 : 0;
+                if (cell != cur) {
+                    if (cur >= 0) flush_acc();
+                    cur = cell;
+                }
+                const double *T = tap + r * TR;
+                const double2 c = cv[r];
+                double2 ctw[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const double tw = T[2 * W + q];
+                    ctw[q] = make_double2(c.x * tw, c.y * tw);
+                }
+#pragma unroll
+                for (int i = 0; i < NP; ++i) {
+                    const double t = T[px[i]] * T[W + py[i]];
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        acc[i][q].x = fma(t, ctw[q].x, acc[i][q].x);
+                        acc[i][q].y = fma(t, ctw[q].y, acc[i][q].y);
+                    }
+                }
+            }
+        }
+        if (cur >= 0) flush_acc();
+        wave_lds_sync();
+        for (int i = lane; i < NQ * RX * RY; i += 64) {
+            const int q = i / (RX * RY), rem = i - q * (RX * RY);
+            const int p = (int)it.p0 + q;
+            if (p < p_lo || p >= p_hi) continue;
+            const double2 v = reg[i];
+            if (v.x == 0.0 && v.y == 0.0) continue;
+            const int xl = rem / RY, yl = rem - xl * RY;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            double *dst = grid + 2 * ((size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy);
+            if (v.x != 0.0) atomicAdd(dst, v.x);
+            if (v.y != 0.0) atomicAdd(dst + 1, v.y);
+        }
+    }
+}
+
+// fp64 degridder (predict), the adjoint: the item's region of the W planes
+// staged in LDS; per cell each lane holds its footprint taps' values of every
+// plane in registers; per record V = sum over the lane's taps of
+// tu tv sum_q G[q] tw[q], reduced over the wave, times the record factor,
+// written to the visibility (through the pol conversion of OutConv).
+template <int W, bool WS, class VT>
+__global__ __launch_bounds__(64) void k_degrid_f64(Geo g, const VisRec64 *__restrict__ recs,
+                                                   const FineItem *__restrict__ items,
+                                                   uint32_t n_items,
+                                                   const double2 *__restrict__ grid, int p_lo,
+                                                   int p_hi, VT *vis, int64_t vrs, int64_t vcs,
+                                                   int accumulate, OutConv oc) {
+    constexpr int NQ = WS ? W : 1;
+    constexpr int RX = W + 1, RY = W + 7, NP = (W * W + 63) / 64, TR = 3 * W;
+    extern __shared__ __attribute__((aligned(16))) double2 sm64[];
+    double2 *const reg = sm64;  // [NQ][RX][RY]
+    double *const tap = reinterpret_cast<double *>(reg + NQ * RX * RY);
+    double2 *const cv = reinterpret_cast<double2 *>(tap + kTap64 * TR);
+    const int lane = threadIdx.x;
+    const double ihw = 2.0 / W, beta = (double)g.beta;
+    int px[NP], py[NP];
+    bool pv[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        const int pp = lane + 64 * i;
+        pv[i] = pp < W * W;
+        px[i] = pv[i] ? pp / W : 0;
+        py[i] = pv[i] ? pp % W : 0;
+    }
+    const size_t plane_elems = (size_t)g.ngx * g.ngy;
+    const bool plain = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        uint32_t bnd[kGroupCell];
+        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
+        if (it.b >= it.e) continue;
+        int ibase, jbase;
+        group_origin(g, (int)it.tile, ibase, jbase);
+        wave_lds_sync();  // the previous item's reads of the region
+        for (int i = lane; i < NQ * RX * RY; i += 64) {
+            const int q = i / (RX * RY), rem = i - q * (RX * RY);
+            const int p = (int)it.p0 + q;
+            const int xl = rem / RY, yl = rem - xl * RY;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            reg[i] = (p >= p_lo && p < p_hi)
+                         ? grid[(size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy]
+                         : make_double2(0.0, 0.0);
+        }
+        double2 gq[NP][NQ];
+        int cur = -1;
+        for (uint32_t b0 = it.b; b0 < it.e; b0 += kTap64) {
+            wave_lds_sync();  // the region staging / previous block's tap reads
+            const int nb = stage_taps64<W, WS>(recs, b0, it.e, tap, cv, ihw, beta);
+            wave_lds_sync();
+            for (int r = 0; r < nb; ++r) {
+                const uint32_t ri = b0 + (uint32_t)r;
+                int cell = 0;
+#pragma unroll
+                for (int c = 0; c < kGroupCell - 1; ++c) cell += ri >= bnd[c] ? 1 : 0;
+                if (cell != cur) {
+                    cur = cell;
+                    const int xo = cur & 1, yo = cur >> 1;
+#pragma unroll
+                    for (int i = 0; i < NP; ++i)
+#pragma unroll
+                        for (int q = 0; q < NQ; ++q)
+                            gq[i][q] = pv[i] ? reg[(q * RX + xo + px[i]) * RY + yo + py[i]]
+                                             : make_double2(0.0, 0.0);
+                }
+                const double *T = tap + r * TR;
+                double sr = 0.0, si = 0.0;
+#pragma unroll
+                for (int i = 0; i < NP; ++i) {
+                    double ar = 0.0, ai = 0.0;
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const double tw = T[2 * W + q];
+                        ar = fma(gq[i][q].x, tw, ar);
+                        ai = fma(gq[i][q].y, tw, ai);
+                    }
+                    const double t = T[px[i]] * T[W + py[i]];
+                    sr = fma(t, ar, sr);
+                    si = fma(t, ai, si);
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    sr += __shfl_xor(sr, o, 64);
+                    si += __shfl_xor(si, o, 64);
+                }
+                if (lane == 0) {
+                    const double2 c = cv[r];
+                    const double xr = c.x * sr - c.y * si, xi = c.x * si + c.y * sr;
+                    const uint32_t idx = recs[ri].idx;
+                    const int64_t row = idx / (uint32_t)g.nchan;
+                    const int chan = (int)(idx - row * g.nchan);
+                    VT *pv_ = vis + row * vrs + chan * vcs;
+                    if (plain) {
+                        store_vis_d(pv_, xr, xi, accumulate);
+                    } else {
+                        for (int k = 0; k < oc.npv; ++k) {
+                            if (oc.cre[k] == 0.0 && oc.cim[k] == 0.0) continue;
+                            store_vis_d(pv_ + k * oc.vps, oc.cre[k] * xr - oc.cim[k] * xi,
+                                        oc.cre[k] * xi + oc.cim[k] * xr, accumulate);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------
 static double es_kernel_host(double t, int W, double beta) {
@@ -1856,19 +2270,20 @@ static const double *phi_table(int W, double beta, hipStream_t stream) {
 
 // Cached hipFFT plans: 1-D c2c of length n over `batch` transforms whose
 // elements are `stride` apart and whose starts are `dist` apart.
-static hipfftHandle fft_plan_1d(int n, int stride, int dist, int batch, hipStream_t stream) {
+static hipfftHandle fft_plan_1d(int n, int stride, int dist, int batch, hipStream_t stream,
+                               bool f64 = false) {
     static std::mutex mu;
-    static std::map<std::tuple<int, int, int, int, int>, hipfftHandle> plans;
+    static std::map<std::tuple<int, int, int, int, int, int>, hipfftHandle> plans;
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_tuple(dev, n, stride, dist, batch);
+    const auto key = std::make_tuple(dev, n, stride, dist, batch, f64 ? 1 : 0);
     auto itp = plans.find(key);
     hipfftHandle h;
     if (itp == plans.end()) {
         int nn[1] = {n};
-        if (hipfftPlanMany(&h, 1, nn, nn, stride, dist, nn, stride, dist, HIPFFT_C2C, batch) !=
-            HIPFFT_SUCCESS)
+        if (hipfftPlanMany(&h, 1, nn, nn, stride, dist, nn, stride, dist,
+                           f64 ? HIPFFT_Z2Z : HIPFFT_C2C, batch) != HIPFFT_SUCCESS)
             throw Error(SDP_HIP_ERR_RUNTIME, "hipfftPlanMany failed");
         plans[key] = h;
     } else {
@@ -1892,6 +2307,13 @@ static int kernel_support(double epsilon) {
     const int W = (int)std::ceil(-std::log10(eps / 10.0) - 1e-9);
     return std::min(std::max(W, 2), kMaxW);
 }
+
+// fp64 path: epsilon below the fp32 floor, W in [kMinW64, kMaxW64]
+static int kernel_support64(double epsilon) {
+    const int W = (int)std::ceil(-std::log10(std::max(epsilon, 1e-15) / 10.0) - 1e-9);
+    return std::min(std::max(W, kMinW64), kMaxW64);
+}
+
 
 // Pinned host staging for the plan's small device->host reads (pageable
 // destinations go through a slow staging copy).  Byte offset `off` into a
@@ -1957,6 +2379,7 @@ struct Plan {
     Geo g;
     VisRec *recs = nullptr;
     Part pt;
+    bool f64 = false;                // fp64 NUFFT (epsilon < 1e-7): VisRec64, c128 planes
     bool subsort = false;            // 16x16-cell buckets re-ordered by cell (k_subsort)
     bool subpad = false;             // ... into 4-padded RecC cells (invert: k_subsort_pad)
     uint8_t *cls = nullptr;          // subpad: each RecC record's cell in its bucket
@@ -1971,6 +2394,9 @@ struct Plan {
     float2 *spec = nullptr;     // T[q][iy][kx]: transposed y-spectra (pruned FFT)
     float2 *spec_in = nullptr;  // band-only input of the backward x-FFT (zeros elsewhere)
 };
+
+// the element size of the planes and spectra: c64, or c128 on the fp64 path
+static size_t cbytes(const Plan &P) { return P.f64 ? sizeof(double2) : sizeof(float2); }
 
 struct Inputs {
     const double *uvw;
@@ -2048,7 +2474,7 @@ static float2 *band_input(const Plan &P, hipStream_t st) {
     static std::mutex mu;
     static std::map<int, BandState> states;
     const Geo &g = P.g;
-    const size_t elems = (size_t)P.fft_planes * g.ny * g.ngx;
+    const size_t elems = (size_t)P.fft_planes * g.ny * g.ngx * (cbytes(P) / sizeof(float2));
     float2 *buf = scratch<float2>("spec_in", elems);
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
@@ -2198,7 +2624,8 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     if (!in.bounds) drop_batch_seq();  // and may overwrite a batch sequence's planes
     Plan P;
     Geo &g = P.g;
-    g.W = kernel_support(in.eps);
+    P.f64 = in.eps < 1.0e-7 && !(in.flags & SDP_HIP_FP32);
+    g.W = P.f64 ? kernel_support64(in.eps) : kernel_support(in.eps);
     g.beta = (float)(2.30 * g.W);
     g.inv_half_w = 2.0f / (float)g.W;
     g.beta_l2e = (float)(2.30 * g.W * 1.4426950408889634);
@@ -2294,6 +2721,9 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         if (env_int("SDP_HIP_BUCKET", 0) == kTileCoarse) g.sub = kTileCoarse;
     }
     g.nty = g.wny / g.sub;
+    SDP_REQUIRE(!P.f64 || g.sub == kTileCell,
+                "epsilon < 1e-7 runs the fp64 NUFFT, which needs the one-cell bucket histogram "
+                "(first planes x window cells <= 2^28): use a larger epsilon or SDP_HIP_FP32");
     // gridding on one-cell keys: blocks of bx x 8 cells per work item (the
     // region flushed with atomics is (bx + W - 1) x (8 + W - 1) cells)
     // (blocks of 4 x 8 and 8 x 8 cells halve the flushed atomics but measured
@@ -2326,8 +2756,8 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // plane chunking against the grid memory budget.  The y-spectra buffers
     // (spec, spec_in: ny x ngx per plane) serve batches of fft_planes planes,
     // so the resident planes cost one grid each (C4: 70 planes of 16384^2)
-    const size_t grid_plane = (size_t)g.ngx * g.ngy * sizeof(float2);
-    const size_t spec_plane = 2 * (size_t)g.ny * g.ngx * sizeof(float2);
+    const size_t grid_plane = (size_t)g.ngx * g.ngy * cbytes(P);
+    const size_t spec_plane = 2 * (size_t)g.ny * g.ngx * cbytes(P);
     P.fft_planes = (int)std::max<size_t>(
         1, std::min<size_t>(kFftBatchMax, kFftBatchBytes / spec_plane));
     if (const char *e = std::getenv("SDP_HIP_FFT_PLANES"))  // tests: force small batches
@@ -2338,7 +2768,9 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // (k_subsort_pad; budgeted at 1.35x -- C4's top channels pad to <= 1.5x
     // one channel at a time, less over a batch of channels)
     P.subpad = grid_mode && g.sub == kTileCoarse && env_int("SDP_HIP_SUBSORT_PAD", 1) != 0;
-    const double rec_bytes = P.subpad ? sizeof(RecC) + 1 + 1.35 * sizeof(RecC) : sizeof(VisRec);
+    const double rec_bytes = P.f64      ? sizeof(VisRec64)
+                             : P.subpad ? sizeof(RecC) + 1 + 1.35 * sizeof(RecC)
+                                        : sizeof(VisRec);
     // buffers of the other kind of plan are freed, not left cached: the plane
     // budget below counts the held record buffers as reusable
     if (!P.subpad) {
@@ -2346,6 +2778,15 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         Workspace::get().drop("rec_cls");
     }
     if (grid_mode) Workspace::get().drop("degrid_acc");
+    {
+        // a record buffer held much larger than this plan needs (a predict's
+        // 32-B records before a large-grid invert's 16-B ones) is freed too:
+        // kept, its surplus would be counted as free but stay allocated
+        const size_t want = (size_t)std::max<int64_t>(nvis, 1) *
+                            (P.f64 ? sizeof(VisRec64) : P.subpad ? sizeof(RecC) : sizeof(VisRec));
+        if (Workspace::get().held("recs") > want + want / 4 + ((size_t)256 << 20))
+            Workspace::get().drop("recs");
+    }
     const size_t need_other =
         (size_t)((double)nvis * (rec_bytes + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2)))) +
         (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned) +
@@ -2353,8 +2794,9 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
     P.chunk_planes = std::min(cp, g.nplanes);
     P.fft_planes = std::min(P.fft_planes, P.chunk_planes);
-    P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy);
-    P.spec = scratch<float2>("spec", (size_t)P.fft_planes * g.ny * g.ngx);
+    const size_t cf = cbytes(P) / sizeof(float2);  // float2 slots per element
+    P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy * cf);
+    P.spec = scratch<float2>("spec", (size_t)P.fft_planes * g.ny * g.ngx * cf);
     if (grid_mode) P.spec_in = band_input(P, st);
 
     // records per item: large enough to amortise the tile flush over dense
@@ -2368,11 +2810,12 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // invert on one-cell buckets: every cell padded to a multiple of 4 records
     // (k_grid_mfma_pad); the padded record count is read back before the
     // scatter (one host sync)
-    P.pad4 = grid_mode && g.sub == kTileCell;
+    P.pad4 = grid_mode && g.sub == kTileCell && !P.f64;
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
     P.pt.nvis = nvis;
-    P.recs = P.subpad ? scratch<VisRec>("recs", (std::max<int64_t>(nvis, 1) + 1) / 2 + 1)  // RecC
-                      : scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
+    P.recs = P.f64      ? scratch<VisRec>("recs", 2 * std::max<int64_t>(nvis, 1))  // VisRec64
+             : P.subpad ? scratch<VisRec>("recs", (std::max<int64_t>(nvis, 1) + 1) / 2 + 1)  // RecC
+                        : scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
     if (P.subpad) P.cls = scratch<uint8_t>("rec_cls", std::max<int64_t>(nvis, 1));
     return P;
 }
@@ -2429,6 +2872,19 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
                                                       S && P.subpad ? P.cls : nullptr);
         };
         auto by_mode = [&](auto vt_tag) {
+            using VT = typename decltype(vt_tag)::type;
+            if (S && P.f64) {  // 64-byte VisRec64 records
+                VisRec64 *o64 = reinterpret_cast<VisRec64 *>(P.recs);
+                if (grid_mode)
+                    k_bucket_f64<VT, true><<<nb, 256, 0, st>>>(
+                        g, pt.nvis, in.uvw, in.uvw_rs, in.freq, static_cast<const VT *>(in.vis),
+                        in.vrs, in.vcs, in.wgt, in.wrs, in.wcs, in.x, sl, counter, kr, o64);
+                else
+                    k_bucket_f64<VT, false><<<nb, 256, 0, st>>>(
+                        g, pt.nvis, in.uvw, in.uvw_rs, in.freq, nullptr, 0, 0, in.wgt, in.wrs,
+                        in.wcs, in.x, sl, counter, kr, o64);
+                return;
+            }
             if (grid_mode && S && (P.pad4 || P.subpad))  // 16-byte RecC records
                 go(vt_tag, std::true_type{}, std::true_type{}, in.vis);
             else if (grid_mode)
@@ -2555,15 +3011,83 @@ static void launch_grid_mfma_fi(const Plan &P, int p_lo, int p_hi, hipStream_t s
 
 template <int W, bool WS>
 static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
-    constexpr size_t lds = grid_mfma_pad_lds(2);
-    // one-cell plans: one FineItem per item; padded sub-sorted coarse plans: 16
+    // one-cell plans: one FineItem per work unit; padded sub-sorted coarse
+    // plans: a coarse item's 16 FineItems per unit
     const auto r = chunk_items(P, p_lo, p_hi);
-    const unsigned per = P.subpad ? 16u : 1u;
-    const unsigned n = per * (r.second - r.first);
+    const unsigned n = r.second - r.first;
     if (n == 0) return;
-    const RecC *recs = P.subpad ? P.recs_pad : reinterpret_cast<const RecC *>(P.recs);
-    k_grid_mfma_pad<W, WS><<<n, 64, lds, st>>>(P.g, recs, P.pt.fitems + per * (size_t)r.first, n,
-                                               (float *)P.grid, p_lo, p_hi);
+    if (P.subpad)
+        k_grid_mfma_pad<W, WS, 16><<<n, 64, grid_mfma_pad_lds<16>(), st>>>(
+            P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, n, (float *)P.grid, p_lo, p_hi);
+    else
+        k_grid_mfma_pad<W, WS, 1><<<n, 64, grid_mfma_pad_lds<1>(), st>>>(
+            P.g, reinterpret_cast<const RecC *>(P.recs), P.pt.fitems + r.first, n, (float *)P.grid,
+            p_lo, p_hi);
+}
+
+template <int W, bool WS>
+static void launch_grid_f64(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
+    const auto r = chunk_items(P, p_lo, p_hi);
+    const unsigned n = r.second - r.first;
+    if (n == 0) return;
+    static const bool attr = [] {  // dynamic LDS above 64 KiB (W = 16: 106 KiB)
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_grid_f64<W, WS>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)grid_f64_lds<W, WS>()));
+        return true;
+    }();
+    (void)attr;
+    k_grid_f64<W, WS><<<n, 64, grid_f64_lds<W, WS>(), st>>>(
+        P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
+        reinterpret_cast<double *>(P.grid), p_lo, p_hi);
+}
+
+template <int W, bool WS, class VT>
+static void launch_degrid_f64(const Plan &P, int p_lo, int p_hi, VT *vis, int64_t vrs,
+                              int64_t vcs, int accumulate, const OutConv &oc, hipStream_t st) {
+    const auto r = chunk_items(P, p_lo, p_hi);
+    const unsigned n = r.second - r.first;
+    if (n == 0) return;
+    static const bool attr = [] {
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_degrid_f64<W, WS, VT>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)grid_f64_lds<W, WS>()));
+        return true;
+    }();
+    (void)attr;
+    k_degrid_f64<W, WS, VT><<<n, 64, grid_f64_lds<W, WS>(), st>>>(
+        P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
+        reinterpret_cast<const double2 *>(P.grid), p_lo, p_hi, vis, vrs, vcs, accumulate, oc);
+}
+
+#define SDP_W64_DISPATCH(W, CALL) \
+    switch (W) {                  \
+        case 9: CALL(9); break;   \
+        case 10: CALL(10); break; \
+        case 11: CALL(11); break; \
+        case 12: CALL(12); break; \
+        case 13: CALL(13); break; \
+        case 14: CALL(14); break; \
+        case 15: CALL(15); break; \
+        default: CALL(16); break; \
+    }
+
+static void grid_f64(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
+#define SDP_G64(WW)                                                          \
+    (P.g.do_w ? launch_grid_f64<WW, true>(P, p_lo, p_hi, st)                 \
+              : launch_grid_f64<WW, false>(P, p_lo, p_hi, st))
+    SDP_W64_DISPATCH(P.g.W, SDP_G64);
+#undef SDP_G64
+}
+
+template <class VT>
+static void degrid_f64(const Plan &P, int p_lo, int p_hi, VT *vis, int64_t vrs, int64_t vcs,
+                       int accumulate, const OutConv &oc, hipStream_t st) {
+#define SDP_D64(WW)                                                                        \
+    (P.g.do_w ? launch_degrid_f64<WW, true, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, st) \
+              : launch_degrid_f64<WW, false, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, st))
+    SDP_W64_DISPATCH(P.g.W, SDP_D64);
+#undef SDP_D64
 }
 
 template <int W>
@@ -2619,6 +3143,7 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
     info->plane_chunk = P.chunk_planes;
     info->bucket = P.g.sub;
     info->padded = (P.pad4 || P.subpad) ? 1 : 0;
+    info->fp64 = P.f64 ? 1 : 0;
     info->grid_launches = (P.g.nplanes + P.chunk_planes - 1) / P.chunk_planes;
 }
 
@@ -2632,44 +3157,104 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
 //             needed columns into T -> x-FFT of T rows (one batched call)
 //   forward:  x-FFT of T rows -> transpose back into the band rows of the
 //             (zeroed) grid -> y-FFT of the band rows
-static void exec_fft(hipfftHandle h, float2 *p, int direction) {
-    if (hipfftExecC2C(h, (hipfftComplex *)p, (hipfftComplex *)p, direction) != HIPFFT_SUCCESS)
-        throw Error(SDP_HIP_ERR_RUNTIME, "hipfftExecC2C failed");
+static void exec_fft(hipfftHandle h, bool f64, void *in, void *out, int direction) {
+    const hipfftResult r =
+        f64 ? hipfftExecZ2Z(h, (hipfftDoubleComplex *)in, (hipfftDoubleComplex *)out, direction)
+            : hipfftExecC2C(h, (hipfftComplex *)in, (hipfftComplex *)out, direction);
+    if (r != HIPFFT_SUCCESS) throw Error(SDP_HIP_ERR_RUNTIME, "hipfftExec failed");
+}
+
+// element e of plane q of the resident planes (c64 or c128)
+static void *plane_ptr(const Plan &P, int q, size_t e) {
+    return reinterpret_cast<char *>(P.grid) +
+           ((size_t)q * P.g.ngx * P.g.ngy + e) * cbytes(P);
 }
 
 static void fft_rows_y(const Plan &P, int q0, int np, int direction, hipStream_t st) {
     const Geo &g = P.g;
     const int nrow = P.row_hi - P.row_lo;
     if (nrow <= 0) return;
-    hipfftHandle hr = fft_plan_1d(g.ngy, 1, g.ngy, nrow, st);
-    for (int q = q0; q < q0 + np; ++q)
-        exec_fft(hr, P.grid + (size_t)q * g.ngx * g.ngy + (size_t)P.row_lo * g.ngy, direction);
+    hipfftHandle hr = fft_plan_1d(g.ngy, 1, g.ngy, nrow, st, P.f64);
+    for (int q = q0; q < q0 + np; ++q) {
+        void *p = plane_ptr(P, q, (size_t)P.row_lo * g.ngy);
+        exec_fft(hr, P.f64, p, p, direction);
+    }
 }
 
 // x transforms of the T rows into P.spec, in place or from `in`
 static void fft_rows_x(const Plan &P, int np, int direction, hipStream_t st,
-                       float2 *in = nullptr) {
+                       void *in = nullptr) {
     const Geo &g = P.g;
-    hipfftHandle hc = fft_plan_1d(g.ngx, 1, g.ngx, np * g.ny, st);
-    if (!in) return exec_fft(hc, P.spec, direction);
-    if (hipfftExecC2C(hc, (hipfftComplex *)in, (hipfftComplex *)P.spec, direction) !=
-        HIPFFT_SUCCESS)
-        throw Error(SDP_HIP_ERR_RUNTIME, "hipfftExecC2C failed");
+    hipfftHandle hc = fft_plan_1d(g.ngx, 1, g.ngx, np * g.ny, st, P.f64);
+    exec_fft(hc, P.f64, in ? in : (void *)P.spec, P.spec, direction);
 }
 
 // Only the row band [row_lo, row_hi) of a plane is ever written or read.
 static void zero_band(const Plan &P, int np, hipStream_t st) {
     const Geo &g = P.g;
     if (P.row_hi <= P.row_lo || np <= 0) return;
-    const size_t width = (size_t)(P.row_hi - P.row_lo) * g.ngy * sizeof(float2);
+    const size_t width = (size_t)(P.row_hi - P.row_lo) * g.ngy * cbytes(P);
     for (int q = 0; q < np; ++q)
-        SDP_HIP_CHECK(hipMemsetAsync(
-            P.grid + (size_t)q * g.ngx * g.ngy + (size_t)P.row_lo * g.ngy, 0, width, st));
+        SDP_HIP_CHECK(hipMemsetAsync(plane_ptr(P, q, (size_t)P.row_lo * g.ngy), 0, width, st));
 }
 
 static dim3 tr_grid(const Geo &g, int xrows, int np) {
     return dim3((unsigned)((xrows + kTr - 1) / kTr), (unsigned)((g.ny + kTr - 1) / kTr),
                 (unsigned)np);
+}
+
+// plane-stage kernels at the plan's precision (planes q0 .. q0 + nb - 1)
+static void tr_grid_to_t(const Plan &P, int q0, int nb, hipStream_t st) {
+    const Geo &g = P.g;
+    if (P.row_hi <= P.row_lo) return;
+    const dim3 grd = tr_grid(g, P.row_hi - P.row_lo, nb), blk(kTr, kTrRows);
+    if (P.f64)
+        k_tr_grid_to_t<double2><<<grd, blk, 0, st>>>(
+            g, static_cast<const double2 *>(plane_ptr(P, q0, 0)),
+            reinterpret_cast<double2 *>(P.spec_in), P.row_lo, P.row_hi);
+    else
+        k_tr_grid_to_t<float2><<<grd, blk, 0, st>>>(
+            g, static_cast<const float2 *>(plane_ptr(P, q0, 0)), P.spec_in, P.row_lo, P.row_hi);
+    SDP_HIP_CHECK(hipGetLastError());
+}
+
+static void tr_t_to_grid(const Plan &P, int q0, int nb, hipStream_t st) {
+    const Geo &g = P.g;
+    if (P.row_hi <= P.row_lo) return;
+    const dim3 grd = tr_grid(g, P.row_hi - P.row_lo, nb), blk(kTr, kTrRows);
+    if (P.f64)
+        k_tr_t_to_grid<double2><<<grd, blk, 0, st>>>(
+            g, reinterpret_cast<const double2 *>(P.spec),
+            static_cast<double2 *>(plane_ptr(P, q0, 0)), P.row_lo, P.row_hi);
+    else
+        k_tr_t_to_grid<float2><<<grd, blk, 0, st>>>(
+            g, P.spec, static_cast<float2 *>(plane_ptr(P, q0, 0)), P.row_lo, P.row_hi);
+    SDP_HIP_CHECK(hipGetLastError());
+}
+
+static void screen_fwd(const Plan &P, int p_begin, int nb, double *dirty, int64_t sx, int64_t sy,
+                       int accumulate, const double *tab, hipStream_t st) {
+    const Geo &g = P.g;
+    const dim3 grd(grid1d(g.nx, 256), g.ny);
+    if (P.f64)
+        k_screen_fwd_t<double2><<<grd, 256, 0, st>>>(g, reinterpret_cast<const double2 *>(P.spec),
+                                                     p_begin, nb, dirty, sx, sy, accumulate, tab);
+    else
+        k_screen_fwd_t<float2><<<grd, 256, 0, st>>>(g, P.spec, p_begin, nb, dirty, sx, sy,
+                                                    accumulate, tab);
+    SDP_HIP_CHECK(hipGetLastError());
+}
+
+static void screen_adj(const Plan &P, const double *dirty, int64_t sx, int64_t sy, int p_begin,
+                       int nb, const double *tab, hipStream_t st) {
+    const Geo &g = P.g;
+    const dim3 grd(grid1d(g.ngx, 256), g.ny);
+    if (P.f64)
+        k_screen_adj_t<double2><<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_begin, nb,
+                                                     reinterpret_cast<double2 *>(P.spec), tab);
+    else
+        k_screen_adj_t<float2><<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_begin, nb, P.spec, tab);
+    SDP_HIP_CHECK(hipGetLastError());
 }
 
 // Bucketing with the fused weight sum (slots zeroed before the count pass,
@@ -2796,7 +3381,8 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
             StageTimer tg(st);
             tg.mark();
 #define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, p_lo, p_hi, st)
-            SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
+            if (P.f64) grid_f64(P, p_lo, p_hi, st);
+            else SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
 #undef SDP_LAUNCH_GRID
             SDP_HIP_CHECK(hipGetLastError());
             tg.mark();
@@ -2807,17 +3393,11 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
             StageTimer t2(st);
             t2.mark();
             fft_rows_y(P, sb, nb, HIPFFT_BACKWARD, st);
-            if (P.row_hi > P.row_lo)
-                k_tr_grid_to_t<<<tr_grid(g, P.row_hi - P.row_lo, nb), dim3(kTr, kTrRows), 0,
-                                 st>>>(g, P.grid + (size_t)sb * g.ngx * g.ngy, P.spec_in,
-                                       P.row_lo, P.row_hi);
-            SDP_HIP_CHECK(hipGetLastError());
+            tr_grid_to_t(P, sb, nb, st);
             fft_rows_x(P, nb, HIPFFT_BACKWARD, st, P.spec_in);
             t2.mark();
-            const dim3 grd(grid1d(g.nx, 256), g.ny);
-            k_screen_fwd_t<<<grd, 256, 0, st>>>(g, P.spec, p_lo + sb, nb, dirty, sx, sy,
-                                                (accumulate || p_lo + sb > 0) ? 1 : 0, tab);
-            SDP_HIP_CHECK(hipGetLastError());
+            screen_fwd(P, p_lo + sb, nb, dirty, sx, sy, (accumulate || p_lo + sb > 0) ? 1 : 0, tab,
+                       st);
             t2.mark();
             tfft += t2.ms(0, 1);
             tscr += t2.ms(1, 2);
@@ -2870,16 +3450,10 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
             stage_t.emplace_back(new StageTimer(s));
             StageTimer &t2 = *stage_t.back();
             t2.mark();
-            const dim3 grd(grid1d(g.ngx, 256), g.ny);
-            k_screen_adj_t<<<grd, 256, 0, s>>>(g, dirty, sx, sy, p_lo + sb, nb, P.spec, tab);
-            SDP_HIP_CHECK(hipGetLastError());
+            screen_adj(P, dirty, sx, sy, p_lo + sb, nb, tab, s);
             t2.mark();
             fft_rows_x(P, nb, HIPFFT_FORWARD, s);
-            if (P.row_hi > P.row_lo)
-                k_tr_t_to_grid<<<tr_grid(g, P.row_hi - P.row_lo, nb), dim3(kTr, kTrRows), 0,
-                                 s>>>(g, P.spec, P.grid + (size_t)sb * g.ngx * g.ngy, P.row_lo,
-                                      P.row_hi);
-            SDP_HIP_CHECK(hipGetLastError());
+            tr_t_to_grid(P, sb, nb, s);
             fft_rows_y(P, sb, nb, HIPFFT_FORWARD, s);
             t2.mark();
         }
@@ -2908,9 +3482,13 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     // (the zeroing above covers the ones with no record)
     const bool trivial_oc = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
     if (P.chunk_planes == g.nplanes && !accumulate && in.vis_dtype != SDP_HIP_C128 && trivial_oc &&
-        in.vcs == 1 && in.vrs == in.nchan)
+        in.vcs == 1 && in.vrs == in.nchan && !P.f64)
         P.vdirect = static_cast<float2 *>(vis);
-    float2 *acc = P.vdirect ? nullptr : scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));
+    // (the fp64 degridder writes each visibility itself, through the pol
+    // conversion, adding into the zeroed output)
+    float2 *acc = (P.vdirect || P.f64)
+                      ? nullptr
+                      : scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));
     if (acc)
         SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(nvis, 1) * sizeof(float2), st));
     float tgrid = 0, tfft = 0, tscr = 0;
@@ -2928,7 +3506,14 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         StageTimer tg(st);
         tg.mark();
 #define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, acc, st)
-        SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
+        if (P.f64 && in.vis_dtype == SDP_HIP_C128)
+            degrid_f64<double2>(P, p_lo, p_hi, static_cast<double2 *>(vis), in.vrs, in.vcs, 1, oc,
+                                st);
+        else if (P.f64)
+            degrid_f64<float2>(P, p_lo, p_hi, static_cast<float2 *>(vis), in.vrs, in.vcs, 1, oc,
+                               st);
+        else
+            SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
 #undef SDP_LAUNCH_DEGRID
         SDP_HIP_CHECK(hipGetLastError());
         tg.mark();
@@ -2942,7 +3527,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         tscr += t->ms(0, 1);
         tfft += t->ms(1, 2);
     }
-    if (!P.vdirect && P.pt.nvis > 0) {
+    if (!P.vdirect && !P.f64 && P.pt.nvis > 0) {
         const unsigned nb = std::min<unsigned>(grid1d(P.pt.nvis, 256), 16384);
         if (in.vis_dtype == SDP_HIP_C128)
             k_finalize<double2><<<nb, 256, 0, st>>>(P.pt.nrec, in.nchan, P.recs, acc,

@@ -31,6 +31,7 @@ SDP_HIP_BATCH_FIRST = 4
 SDP_HIP_BATCH_LAST = 8
 SDP_HIP_KEEP_BUCKETS = 16
 SDP_HIP_REUSE_BUCKETS = 32
+SDP_HIP_FP32 = 64
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
@@ -60,6 +61,7 @@ class WGridInfo(ctypes.Structure):
         ("bucket", c_int),
         ("grid_launches", c_int),
         ("padded", c_int),
+        ("fp64", c_int),
     ]
 
     def as_dict(self):

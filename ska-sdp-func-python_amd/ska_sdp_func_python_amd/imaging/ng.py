@@ -31,9 +31,11 @@ and combines the partial images and weight sums with one all-reduce each
 predicts its block and all-gathers the channel blocks.  Every rank returns
 the reference's full result.  ``shard=False`` (or SDP_HIP_SHARD=0) computes
 everything on each rank.
-Kwargs ``epsilon`` (default 1e-12, clamped to the fp32 floor 1e-7),
-``do_wstacking`` (True), ``threads`` and ``verbosity`` are accepted as in
-the reference; ``threads`` is ignored (one GPU per process).
+Kwargs ``epsilon`` (default 1e-12), ``do_wstacking`` (True), ``threads``
+and ``verbosity`` are accepted as in the reference; ``threads`` is ignored
+(one GPU per process).  epsilon < 1e-7 runs the fp64 NUFFT (as ducc0 with
+double_precision_accumulation); ``precision="fp32"`` (beyond the reference)
+serves such requests with the fp32 NUFFT at its floor (W = 8, ~1e-6).
 """
 
 import logging
@@ -66,6 +68,7 @@ def predict_ng(bvis, model, **kwargs):
     epsilon = kwargs.get("epsilon", 1e-12)
     do_wstacking = kwargs.get("do_wstacking", True)
     verbosity = kwargs.get("verbosity", 0)
+    precision = kwargs.get("precision")
 
     dev = _device.device()
     freq = np.asarray(bvis.frequency.data, dtype=float)
@@ -108,7 +111,8 @@ def predict_ng(bvis, model, **kwargs):
             _, info = kernels.dirty2ms_vis(uvw, freq_t, pixels[0, vpol], vist, coef(vpol), pixsize,
                                            pixsize, epsilon, do_wstacking, flip_uw=True,
                                            dirty_strides=(1, nx), npix=(nx, ny),
-                                           accumulate=vpol > 0, shift_lmn=lmn)
+                                           accumulate=vpol > 0, shift_lmn=lmn,
+                                           precision=precision)
         else:
             for vchan in range(lo, hi):
                 img = pixels[int(vis_to_im[vchan]), vpol]
@@ -117,7 +121,8 @@ def predict_ng(bvis, model, **kwargs):
                                                vist[:, c:c + 1, :], coef(vpol), pixsize,
                                                pixsize, epsilon, do_wstacking, flip_uw=True,
                                                dirty_strides=(1, nx), npix=(nx, ny),
-                                               accumulate=vpol > 0, shift_lmn=lmn)
+                                               accumulate=vpol > 0, shift_lmn=lmn,
+                                           precision=precision)
     if verbosity and info is not None:
         log.info("predict_ng: %s", info)
     if shard:
@@ -146,6 +151,7 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     epsilon = kwargs.get("epsilon", 1e-12)
     do_wstacking = kwargs.get("do_wstacking", True)
     verbosity = kwargs.get("verbosity", 0)
+    precision = kwargs.get("precision")
 
     dev = _device.device()
     nchan, npol, ny, nx = model["pixels"].data.shape
@@ -213,7 +219,7 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
             flags[:, chans, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
             do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
             accumulate=True, sumwt=sw, shift_lmn=lmn, keep_buckets=share and pol == 0,
-            reuse_buckets=share and pol > 0)
+            reuse_buckets=share and pol > 0, precision=precision)
         if verbosity:
             log.info("invert_ng: %s", info)
 

@@ -15,24 +15,46 @@ from . import _lib
 
 log = logging.getLogger("func-python-logger")
 
-# The w-stacking NUFFT computes in fp32 (taps, uv planes) with fp64
-# coordinates, phases and image accumulation: its accuracy floor is epsilon
-# 1e-7 (support W = 8).  The reference asks ducc0 for 1e-12 with
-# double_precision_accumulation (imaging/ng.py:178, :240-256); such requests
-# are served at the floor and said so once per process.  Measured on the full
-# C2 workload against the fp64 W = 13 oracle: 9.1e-7 (invert) / 8.1e-7
-# (predict) relative RMS (tests/test_gpu_fullsize.py).
+# The w-stacking NUFFT has two precisions.  epsilon >= 1e-7: fp32 taps and
+# uv planes with fp64 coordinates, phases and image accumulation (W <= 8;
+# measured on the full C2 workload against the fp64 W = 13 oracle: 9.1e-7
+# invert / 8.1e-7 predict relative RMS, tests/test_gpu_fullsize.py).
+# epsilon < 1e-7 -- the reference's default 1e-12, which it asks of ducc0
+# with double_precision_accumulation (imaging/ng.py:178, :240-256) -- runs
+# the fp64 NUFFT (W = ceil(-log10(epsilon/10)) in [9, 16], c128 planes, Z2Z
+# FFTs).  precision="fp32" (per call, or set_precision("fp32") for the
+# process) keeps such requests on the fp32 path at its floor instead, said so
+# once per process.
 EPS_FLOOR = 1e-7
+_PRECISION = "auto"
 _eps_warned = False
 
 
-def _eps_note(epsilon):
+def set_precision(mode):
+    """Process default for the NUFFT precision: "auto" (fp64 below epsilon
+    1e-7) or "fp32" (the fp32 NUFFT at its floor for every epsilon)."""
+    global _PRECISION
+    if mode not in ("auto", "fp32"):
+        raise ValueError("precision must be 'auto' or 'fp32'")
+    _PRECISION = mode
+
+
+def _prec_bits(epsilon, precision=None):
+    """Flag bits of a NUFFT call for `epsilon` under `precision`."""
     global _eps_warned
-    if float(epsilon) < EPS_FLOOR and not _eps_warned:
+    mode = precision or _PRECISION
+    if mode not in ("auto", "fp32"):
+        raise ValueError("precision must be 'auto' or 'fp32'")
+    if float(epsilon) >= EPS_FLOOR or mode == "auto":
+        return 0
+    if not _eps_warned:
         _eps_warned = True
-        log.warning("epsilon %.1e requested: the HIP w-stacking NUFFT computes in fp32 and runs "
-                    "at its floor epsilon %.0e (support W = 8); measured dirty-image error vs an "
-                    "fp64 epsilon=1e-12 reference ~1e-6 relative RMS", float(epsilon), EPS_FLOOR)
+        log.warning("epsilon %.1e requested with precision='fp32': the HIP w-stacking NUFFT "
+                    "runs in fp32 at its floor epsilon %.0e (support W = 8); measured "
+                    "dirty-image error vs an fp64 epsilon=1e-12 reference ~1e-6 relative RMS",
+                    float(epsilon), EPS_FLOOR)
+    return _lib.SDP_HIP_FP32
+
 
 _DT_CODE = {
     torch.complex64: _lib.SDP_HIP_C64,
@@ -92,7 +114,7 @@ def _check_uvw(uvw):
 
 def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
              epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
-             out_strides=None, accumulate=False):
+             out_strides=None, accumulate=False, precision=None):
     """ducc0.wgridder.ms2dirty semantics on device.
 
     uvw [nrow,3] f64, freq [nchan] f64, vis [nrow,nchan] c64/c128 (or None
@@ -100,7 +122,7 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
     f64 dirty image [npix_x, npix_y] (or writes ``out`` with
     ``out_strides`` = (stride_x, stride_y) in elements) and an info dict.
     """
-    _eps_note(epsilon)
+    pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
     dev = uvw.device
     freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
@@ -118,7 +140,8 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
     _on_gpu(out, "out")
     if out.dtype != torch.float64:
         raise ValueError("dirty output must be float64")
-    flags = (_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+    flags = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+             | pbits)
     info = _lib.WGridInfo()
     _lib.call(
         "sdp_hip_ms2dirty",
@@ -150,13 +173,13 @@ def merge_bounds(*bs):
 
 def ms2dirty_batch(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y, bounds,
                    first, last, epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
-                   out_strides=None, accumulate=False):
+                   out_strides=None, accumulate=False, precision=None):
     """One batch of a batched invert (sdp_hip_ms2dirty_batch): the batch is
     gridded into the resident w planes shared by the whole sequence; the
     ``first`` batch zeroes them, the ``last`` runs the FFT and w-screens into
     ``out`` (allocated if None; earlier batches return None).  ``bounds``:
     merge_bounds over every batch of the sequence."""
-    _eps_note(epsilon)
+    pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
     dev = uvw.device
     freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
@@ -207,7 +230,7 @@ _FLAG_DT = {torch.int64: 8, torch.int32: 4, torch.int8: 1, torch.uint8: 1, torch
 def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_x, pixsize_y,
                  epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None, out_strides=None,
                  accumulate=False, sumwt=None, shift_lmn=None, keep_buckets=False,
-                 reuse_buckets=False):
+                 reuse_buckets=False, precision=None):
     """ms2dirty with invert_ng's visibility prologue fused in
     (sdp_hip_ms2dirty_vis): ``vis`` [nrow, nchan, npol_vis] complex (any
     strides, read in place; None = unit visibilities), ``flags`` the same
@@ -220,7 +243,7 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
     on the device; a following call with ``reuse_buckets`` and the same uvw,
     freq and geometry (another image pol) runs only the value pass, gridding
     and FFT (SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS)."""
-    _eps_note(epsilon)
+    pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
     dev = uvw.device
     freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
@@ -259,7 +282,8 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
         raise ValueError("dirty output must be float64")
     if sumwt is not None and (sumwt.dtype != torch.float64 or not sumwt.is_cuda):
         raise ValueError("sumwt must be a float64 device tensor")
-    bits = (_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+    bits = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+            | pbits)
     bits |= (_lib.SDP_HIP_KEEP_BUCKETS if keep_buckets else 0) | \
         (_lib.SDP_HIP_REUSE_BUCKETS if reuse_buckets else 0)
     info = _lib.WGridInfo()
@@ -282,11 +306,11 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
 
 def dirty2ms_vis(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7,
                  do_wstacking=True, flip_uw=False, dirty_strides=None, npix=None,
-                 accumulate=False, shift_lmn=None):
+                 accumulate=False, shift_lmn=None, precision=None):
     """One image pol of predict_ng with the pol conversion fused into the
     write-back (sdp_hip_dirty2ms_vis): ``out`` [nrow, nchan, npol_vis] complex
     (any strides) gets coef[k] * predicted vis in pol k (coef None: pol 0)."""
-    _eps_note(epsilon)
+    pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
     dev = uvw.device
     freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
@@ -308,7 +332,8 @@ def dirty2ms_vis(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7
         if len(c) != npv:
             raise ValueError("coef must have one entry per visibility pol")
         cbuf = (ctypes.c_double * (2 * npv))(*[v for z in c for v in (z.real, z.imag)])
-    bits = (_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+    bits = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+            | pbits)
     info = _lib.WGridInfo()
     _lib.call("sdp_hip_dirty2ms_vis", _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
               _ptr(dirty), int(dirty_strides[0]), int(dirty_strides[1]), int(npix_x), int(npix_y),
@@ -321,9 +346,9 @@ def dirty2ms_vis(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7
 
 def dirty2ms(uvw, freq, dirty, wgt, pixsize_x, pixsize_y, epsilon=1e-7,
              do_wstacking=True, flip_uw=False, out=None, dirty_strides=None,
-             npix=None, accumulate=False, vis_dtype=torch.complex64):
+             npix=None, accumulate=False, vis_dtype=torch.complex64, precision=None):
     """ducc0.wgridder.dirty2ms semantics on device; returns vis [nrow,nchan]."""
-    _eps_note(epsilon)
+    pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
     dev = uvw.device
     freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
@@ -343,7 +368,8 @@ def dirty2ms(uvw, freq, dirty, wgt, pixsize_x, pixsize_y, epsilon=1e-7,
     _on_gpu(out, "vis out")
     if out.dtype not in (torch.complex64, torch.complex128) or tuple(out.shape) != (nrow, nchan):
         raise ValueError("vis out must be complex [nrow, nchan]")
-    flags = (_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+    flags = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+             | pbits)
     info = _lib.WGridInfo()
     _lib.call(
         "sdp_hip_dirty2ms",

@@ -29,7 +29,7 @@ SEEN = set()  # visibility channels (frequencies) this process computed
 def _oracle_ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, px, py,
                          epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
                          out_strides=None, accumulate=False, sumwt=None, shift_lmn=None,
-                         keep_buckets=False, reuse_buckets=False):
+                         keep_buckets=False, reuse_buckets=False, precision=None):
     assert shift_lmn is None
     SEEN.update(freq.numpy().tolist())
     m = 1.0 - flags.numpy().astype(float)
@@ -51,7 +51,7 @@ def _oracle_ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, 
 
 def _oracle_dirty2ms_vis(uvw, freq, dirty, out, coef, px, py, epsilon=1e-7, do_wstacking=True,
                          flip_uw=False, dirty_strides=None, npix=None, accumulate=False,
-                         shift_lmn=None):
+                         shift_lmn=None, precision=None):
     assert shift_lmn is None and tuple(dirty_strides) == (1, npix[0])
     SEEN.update(freq.numpy().tolist())
     v = orc.dirty2ms_exact(uvw.numpy() * (FLIP if flip_uw else 1.0), freq.numpy(),

@@ -62,7 +62,7 @@ def test_c2_full_invert_against_reference_precision():
     obs, cell = _c2()
     assert obs["nrow"] * 64 == 123_558_400
     out, info = kernels.ms2dirty(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], NPIX, NPIX,
-                                 cell, cell, 1e-12, True, flip_uw=True)
+                                 cell, cell, 1e-7, True, flip_uw=True)
     gpu = out.cpu().numpy()
     uvw = obs["uvw"].cpu().numpy() * FLIP_UW
     freq = obs["freq"].cpu().numpy()
@@ -101,7 +101,7 @@ def test_c2_full_predict_against_reference_precision():
     rng = np.random.default_rng(32)
     img = rng.normal(size=(NPIX, NPIX))
     v, info = kernels.dirty2ms(obs["uvw"], obs["freq"], torch.as_tensor(img, device="cuda:0"),
-                               obs["wgt"], cell, cell, 1e-12, True, flip_uw=True)
+                               obs["wgt"], cell, cell, 1e-7, True, flip_uw=True)
     gpu = v.cpu().numpy()
     uvw = obs["uvw"].cpu().numpy() * FLIP_UW
     freq = obs["freq"].cpu().numpy()
@@ -204,7 +204,7 @@ def test_c4_shard_invert_predict_at_full_size():
     assert nvis == 1_674_444_800
     cell = 0.25 / obs["umax"]
     d, info = kernels.ms2dirty(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], npix, npix, cell,
-                               cell, 1e-12, True, flip_uw=True)
+                               cell, 1e-7, True, flip_uw=True)
     assert info["ngrid_x"] == 2 * npix and info["nplanes"] > 40
     # exact sums at 12 pixels (host copies of the shard: 13.4 GB of c64)
     rng = np.random.default_rng(41)
@@ -219,7 +219,7 @@ def test_c4_shard_invert_predict_at_full_size():
     y = torch.zeros((npix, npix), dtype=torch.float64, device=dev)
     iy = rng.integers(npix // 4, 3 * npix // 4, (2, 4096))
     y[iy[0], iy[1]] = torch.as_tensor(rng.normal(size=4096), device=dev)
-    v, _ = kernels.dirty2ms(obs["uvw"], obs["freq"], y, obs["wgt"], cell, cell, 1e-12, True,
+    v, _ = kernels.dirty2ms(obs["uvw"], obs["freq"], y, obs["wgt"], cell, cell, 1e-7, True,
                             flip_uw=True)
     lhs = float(torch.sum(d * y))
     rhs = 0.0
@@ -235,12 +235,12 @@ def test_c4_shard_invert_predict_at_full_size():
     pt[x0, y0] = 1.0
     l0, m0 = (x0 - npix // 2) * cell, (y0 - npix // 2) * cell
     n0 = math.sqrt(1.0 - l0 * l0 - m0 * m0)
-    vp, _ = kernels.dirty2ms(obs["uvw"], obs["freq"], pt, None, cell, cell, 1e-12, True,
+    vp, _ = kernels.dirty2ms(obs["uvw"], obs["freq"], pt, None, cell, cell, 1e-7, True,
                              flip_uw=True)
     e_amp = 0.0
     for a in range(0, obs["nrow"], 4_000_000):
         e_amp = max(e_amp, float(torch.max(torch.abs(torch.abs(vp[a:a + 4_000_000]) * n0 - 1.0))))
-    dp, _ = kernels.ms2dirty(obs["uvw"], obs["freq"], vp, None, npix, npix, cell, cell, 1e-12,
+    dp, _ = kernels.ms2dirty(obs["uvw"], obs["freq"], vp, None, npix, npix, cell, cell, 1e-7,
                              True, flip_uw=True)
     k = int(torch.argmax(dp))
     peak = float(dp.view(-1)[k]) * n0 * n0 / nvis
@@ -255,7 +255,7 @@ def test_c4_shard_invert_predict_at_full_size():
                                            obs["vis"][:, a:e].contiguous(),
                                            obs["wgt"][:, a:e].contiguous(), npix, npix, cell, cell,
                                            b, first=i == 0, last=i == len(blocks) - 1,
-                                           epsilon=1e-12, flip_uw=True)
+                                           epsilon=1e-7, flip_uw=True)
         assert binfo["nplanes"] == info["nplanes"] and binfo["w0"] == info["w0"]
     e_batch = float(torch.sqrt(torch.mean((db - d) ** 2) / torch.mean(d ** 2)))
     e_bpx = rel_rms(db.cpu().numpy()[px, py], ex)

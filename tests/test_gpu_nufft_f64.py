@@ -1,0 +1,143 @@
+"""GPU parity of the fp64 w-stacking NUFFT (epsilon < 1e-7, the reference's
+default 1e-12 -- ducc0 with double_precision_accumulation, reference
+imaging/ng.py:178, :240-256) against the exact direct sums
+(oracle/nufft_oracle.py, fp64).
+
+Tolerances: epsilon 1e-12 (W = 13) -> relative RMS < 1e-10; epsilon 1e-9
+(W = 10) -> < 1e-7.  precision="fp32" keeps the fp32 NUFFT (W = 8)."""
+
+import numpy as np
+import pytest
+import torch
+
+import nufft_oracle as orc
+from conftest import rel_rms
+
+pytestmark = pytest.mark.gpu
+FLIP_UW = np.array([-1.0, 1.0, -1.0])
+
+
+def T(a, dt=None):
+    return torch.as_tensor(np.asarray(a), device=torch.device("cuda:0"), dtype=dt)
+
+
+def _problem(seed, nrow=400, nchan=3, umax=2000.0, frac=0.45):
+    rng = np.random.default_rng(seed)
+    freq = np.linspace(1.0e9, 1.2e9, nchan)
+    uvw = rng.uniform(-1, 1, (nrow, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw[:, 2] *= 0.6
+    ms = rng.normal(size=(nrow, nchan)) + 1j * rng.normal(size=(nrow, nchan))
+    wgt = rng.uniform(0.5, 1.5, (nrow, nchan))
+    return uvw, freq, ms, wgt, frac / umax
+
+
+@pytest.mark.parametrize("eps,tol,W", [(1e-12, 1e-10, 13), (1e-9, 1e-7, 10)])
+@pytest.mark.parametrize("dow", [False, True])
+@pytest.mark.parametrize("vdt", [torch.complex64, torch.complex128])
+def test_ms2dirty_f64_matches_exact(eps, tol, W, dow, vdt):
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(71)
+    if vdt == torch.complex64:
+        ms = ms.astype(np.complex64).astype(np.complex128)  # the values the GPU reads
+    npx, npy = 64, 48
+    ex = orc.ms2dirty_exact(uvw * FLIP_UW, freq, ms, wgt, npx, npy, cell, cell * 0.9, dow)
+    out, info = kernels.ms2dirty(T(uvw), T(freq), T(ms, vdt), T(wgt), npx, npy, cell, cell * 0.9,
+                                 eps, dow, flip_uw=True)
+    e = rel_rms(out.cpu().numpy(), ex)
+    print(f"\nfp64 invert eps {eps:.0e} W {info['support']} w {dow} {vdt}: rel RMS {e:.2e}")
+    assert info["fp64"] == 1 and info["support"] == W and info["padded"] == 0
+    assert e < tol
+
+
+@pytest.mark.parametrize("eps,tol", [(1e-12, 1e-10), (1e-9, 1e-7)])
+@pytest.mark.parametrize("dow", [False, True])
+@pytest.mark.parametrize("vdt", [torch.complex64, torch.complex128])
+def test_dirty2ms_f64_matches_exact(eps, tol, dow, vdt):
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, _, wgt, cell = _problem(72)
+    rng = np.random.default_rng(73)
+    npx, npy = 64, 48
+    img = rng.normal(size=(npx, npy))
+    ex = orc.dirty2ms_exact(uvw * FLIP_UW, freq, img, wgt, cell, cell * 0.9, dow)
+    v, info = kernels.dirty2ms(T(uvw), T(freq), T(img), T(wgt), cell, cell * 0.9, eps, dow,
+                               flip_uw=True, vis_dtype=vdt)
+    vv = v.cpu().numpy().astype(np.complex128)
+    e = rel_rms(vv, ex)
+    print(f"\nfp64 predict eps {eps:.0e} w {dow} {vdt}: rel RMS {e:.2e}")
+    assert info["fp64"] == 1
+    # a c64 output rounds each visibility to fp32 (~3e-8 relative)
+    assert e < max(tol, 1e-7 if vdt == torch.complex64 else 0.0)
+
+
+def test_f64_adjointness_and_accumulate():
+    """<A x, y> = Re <x, A^H y> to 1e-12; ACCUMULATE adds into the output."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(74, nrow=600)
+    rng = np.random.default_rng(75)
+    d, _ = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), 64, 64, cell, cell, 1e-12, True)
+    y = rng.normal(size=(64, 64))
+    v, _ = kernels.dirty2ms(T(uvw), T(freq), T(y), T(wgt), cell, cell, 1e-12, True,
+                            vis_dtype=torch.complex128)
+    lhs = float(np.sum(d.cpu().numpy() * y))
+    rhs = float(np.sum((np.conj(v.cpu().numpy()) * ms).real))
+    assert abs(lhs - rhs) / abs(lhs) < 1e-12
+    d2 = d.clone()
+    kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), 64, 64, cell, cell, 1e-12, True, out=d2,
+                     accumulate=True)
+    assert rel_rms(d2.cpu().numpy(), 2 * d.cpu().numpy()) < 1e-14
+    v2 = v.clone()
+    kernels.dirty2ms(T(uvw), T(freq), T(y), T(wgt), cell, cell, 1e-12, True, out=v2,
+                     accumulate=True)
+    assert rel_rms(v2.cpu().numpy(), 2 * v.cpu().numpy()) < 1e-14
+
+
+def test_precision_fp32_keeps_the_fp32_path():
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(76)
+    ex = orc.ms2dirty_exact(uvw, freq, ms, wgt, 64, 64, cell, cell, True)
+    out, info = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), 64, 64, cell, cell, 1e-12, True,
+                                 precision="fp32")
+    assert info["fp64"] == 0 and info["support"] == 8
+    assert rel_rms(out.cpu().numpy(), ex) < 5e-6
+
+
+def test_invert_predict_ng_default_epsilon_is_fp64():
+    """invert_ng / predict_ng with the reference's default epsilon (1e-12)
+    run the fp64 NUFFT (with flags and imaging weights): the exact direct
+    sums to 1e-10; precision="fp32" gives the fp32 NUFFT's ~1e-6."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng
+    from gpu_helpers import vis_from_arrays
+    rng = np.random.default_rng(77)
+    nt, nb, nchan = 4, 40, 2
+    freq = np.array([1.0e9, 1.1e9])
+    umax = 1500.0
+    uvw = rng.uniform(-1, 1, (nt, nb, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw[..., 2] *= 0.5
+    shape = (nt, nb, nchan, 1)
+    v = rng.normal(size=shape) + 1j * rng.normal(size=shape)
+    fl = (rng.uniform(size=shape) < 0.1).astype(int)
+    vis = vis_from_arrays(uvw, freq, v, flags=fl, phasecentre=dm.SkyCoord(0.0, -0.6))
+    vis["imaging_weight"] = rng.uniform(0.5, 2.0, shape)
+    npix, cell = 32, 0.4 / umax
+    im = dm.create_image(npix, cell, dm.SkyCoord(0.0, -0.6), frequency=float(freq.mean()),
+                         channel_bandwidth=1e9)
+    w = (np.asarray(vis["imaging_weight"].data) * (1 - fl))[..., 0].reshape(-1, nchan)
+    uv2 = uvw.reshape(-1, 3) * FLIP_UW
+    ex = orc.ms2dirty_exact(uv2, freq, v[..., 0].reshape(-1, nchan), w, npix, npix, cell, cell,
+                            True).T  # RASCIL [y, x]
+    d64, _ = invert_ng(vis, im, normalise=False)
+    d32, _ = invert_ng(vis, im, normalise=False, precision="fp32")
+    e64 = rel_rms(np.asarray(d64["pixels"].data)[0, 0], ex)
+    e32 = rel_rms(np.asarray(d32["pixels"].data)[0, 0], ex)
+    print(f"\ninvert_ng: fp64 {e64:.2e}, fp32 {e32:.2e}")
+    assert e64 < 1e-10 and 1e-9 < e32 < 5e-6
+    model = im.copy(deep=True)
+    model["pixels"].data[...] = rng.normal(size=model["pixels"].data.shape)
+    exv = orc.dirty2ms_exact(uv2, freq, np.asarray(model["pixels"].data)[0, 0].T, None, cell,
+                             cell, True)
+    p64 = np.asarray(predict_ng(vis, model).vis.data)[..., 0].reshape(-1, nchan)
+    p32 = np.asarray(predict_ng(vis, model, precision="fp32").vis.data)[..., 0].reshape(-1, nchan)
+    ep64, ep32 = rel_rms(p64, exv), rel_rms(p32, exv)
+    print(f"predict_ng: fp64 {ep64:.2e}, fp32 {ep32:.2e}")
+    assert ep64 < 1e-10 and 1e-9 < ep32 < 5e-6

@@ -171,17 +171,25 @@ def test_cf_channel_map_checked_like_numpy_indexing():
 
 
 def test_epsilon_below_fp32_floor_is_reported_once(caplog):
+    """epsilon < 1e-7 selects the fp64 NUFFT (no flag bits, no note);
+    precision="fp32" serves it at the fp32 floor (SDP_HIP_FP32) and says so
+    once per process; an unknown precision is refused."""
     import logging
     import torch
-    from ska_sdp_func_python_amd import kernels
+    from ska_sdp_func_python_amd import _lib, kernels
     kernels._eps_warned = False
-    uvw = torch.zeros((4, 3), dtype=torch.float64)
+    assert kernels._prec_bits(1e-12) == 0 and kernels._prec_bits(1e-6, "fp32") == 0
     with caplog.at_level(logging.WARNING, logger="func-python-logger"):
         for _ in range(2):
-            with pytest.raises(ValueError):  # host tensors: rejected after the note
-                kernels.ms2dirty(uvw, torch.ones(1), None, None, 8, 8, 1e-3, 1e-3, 1e-12)
+            assert kernels._prec_bits(1e-12, "fp32") == _lib.SDP_HIP_FP32
     msgs = [r.getMessage() for r in caplog.records if "floor epsilon" in r.getMessage()]
     assert len(msgs) == 1 and "1.0e-12" in msgs[0]
+    with pytest.raises(ValueError):
+        kernels._prec_bits(1e-12, "fp16")
+    uvw = torch.zeros((4, 3), dtype=torch.float64)
+    with pytest.raises(ValueError):  # host tensors are rejected
+        kernels.ms2dirty(uvw, torch.ones(1), None, None, 8, 8, 1e-3, 1e-3, 1e-12,
+                         precision="fp32")
 
 
 def test_balanced_channel_blocks_cover_and_balance():
