@@ -108,7 +108,9 @@ int sdp_hip_set_stage_timing(int enable);
  *          of zero weight are skipped (their visibilities are never read)
  * dirty    f64, element (x, y) at dirty[x*dirty_stride_x + y*dirty_stride_y]
  *          (pass strides (1, nx) to receive RASCIL's transposed image)
- * epsilon  requested accuracy; clamped to the fp32 floor 1e-7 (W <= 8)
+ * epsilon  requested accuracy: >= 1e-7 the fp32 NUFFT (W = ceil(-log10(eps/10)),
+ *          <= 8); below 1e-7 the fp64 NUFFT (W in [9, 16], c128 planes) unless
+ *          flags has SDP_HIP_FP32 (fp32 at its floor, W = 8)
  */
 int sdp_hip_ms2dirty(const double *uvw, int64_t uvw_row_stride,
                      const double *freq, int nchan, int64_t nrow,

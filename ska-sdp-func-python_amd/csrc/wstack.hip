@@ -1229,14 +1229,16 @@ constexpr int kTapBatch = 16;  // records per tap block
 constexpr int kRegCell = 16;  // floats per region cell: 8 planes x re/im
 
 // Work unit of NG groups: 1 (one-cell plans: a chunk of one 2 x 8-cell
-// group) or 16 (large grids: the 16 groups of a sub-sorted 16 x 16-cell
-// coarse item, gridded into one 23 x 23-cell region -- a quarter of the
-// flushed atomics of 16 separate 9 x 15-cell regions; C4's sparse groups,
-// ~120 records each, were bound by those atomics: 121 GB per 1.67 Gvis).
+// group) or 4 (large grids: 2 x pairs x both y halves of a sub-sorted
+// 16 x 16-cell coarse item, gridded into one 11 x 23-cell region -- half
+// the flushed atomics of 4 separate 9 x 15-cell regions; C4's sparse groups,
+// ~120 records each, flushed 121 GB of atomics per 1.67 Gvis one by one).
 template <int NG>
 struct PadUnit {
-    static constexpr int TX = NG == 1 ? 2 : 16, TY = NG == 1 ? 8 : 16;  // cells
-    static constexpr int RGX = TX + 7, RGY = TY + 7;                     // region cells
+    // NG = 1: one 2 x 8-cell group; NG >= 2: NG / 2 x pairs of a sub-sorted
+    // 16x16-cell item, both y halves (groups gi = 2 x pair + y half)
+    static constexpr int TX = NG == 1 ? 2 : NG, TY = NG == 1 ? 8 : 16;  // cells
+    static constexpr int RGX = TX + 7, RGY = TY + 7;                    // region cells
 };
 
 template <int NG>
@@ -1251,7 +1253,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     Geo g, const RecC *__restrict__ recs, const FineItem *__restrict__ items, uint32_t n_items,
     float *__restrict__ grid, int p_lo, int p_hi) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
-    static_assert(NG == 1 || NG == 16, "units of one group or of a 16x16-cell item");
+    static_assert(NG == 1 || NG == 2 || NG == 4 || NG == 8 || NG == 16, "units of 1-16 groups");
+    // (NG = 2, 8, 16 are valid but measured slower on C4; only 1 and 4 are launched)
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int NQ = WS ? W : 1;
     constexpr int kRegX = PadUnit<NG>::RGX, kRegY = PadUnit<NG>::RGY;
@@ -3016,10 +3019,16 @@ static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t 
     const auto r = chunk_items(P, p_lo, p_hi);
     const unsigned n = r.second - r.first;
     if (n == 0) return;
-    if (P.subpad)
-        k_grid_mfma_pad<W, WS, 16><<<n, 64, grid_mfma_pad_lds<16>(), st>>>(
-            P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, n, (float *)P.grid, p_lo, p_hi);
-    else
+    if (P.subpad) {
+        // units of 4 of a coarse item's 16 groups (2 x pairs x 2 y halves,
+        // 4 x 16 cells, an 11 x 23-cell region).  C4 N = 1 gridding: 1 group
+        // per unit 1001 ms, 2: 786, 4: 706, 8: 813, 16: 1078 ms -- larger
+        // units flush fewer atomics (the small groups of C4's sparse cells,
+        // ~120 records each, were bound by them) but hold more LDS per wave
+        const unsigned nu = n * 4u;
+        k_grid_mfma_pad<W, WS, 4><<<nu, 64, grid_mfma_pad_lds<4>(), st>>>(
+            P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo, p_hi);
+    } else
         k_grid_mfma_pad<W, WS, 1><<<n, 64, grid_mfma_pad_lds<1>(), st>>>(
             P.g, reinterpret_cast<const RecC *>(P.recs), P.pt.fitems + r.first, n, (float *)P.grid,
             p_lo, p_hi);
