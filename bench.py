@@ -89,6 +89,12 @@ def parse():
     ap.add_argument("--c4-cpu-chans", type=int, default=2,
                     help="c4: channels in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--c4-traffic", default=os.path.join(ROOT, "profiles", "traffic_c4_k_grid.json"))
+    ap.add_argument("--partition", choices=("chan", "wslab"), default="wslab",
+                    help="c4 with N > 1: 'wslab' -- every rank scans the band and grids the "
+                         "visibilities of its contiguous slab of the band's w planes "
+                         "(parallel.wslab_partition; plane work ~ the band's planes once); "
+                         "'chan' -- cost-balanced contiguous channel blocks, each rank with its "
+                         "own w planes (parallel.balanced_channel_blocks)")
     ap.add_argument("--emulate", default=None, metavar="RANK/WORLD",
                     help="c4 on one GPU: run only rank RANK's block of a WORLD-way partition "
                          "(no collective), to measure per-rank times")
@@ -270,9 +276,10 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
     `sub` returns the line as a dict (the default bench's "c4_n1" object)."""
     from ska_sdp_func_python_amd import kernels, parallel, simulation
     freqs = np.linspace(C4_FLO, C4_FHI, C4_NCHAN)
-    blocks = parallel.balanced_channel_blocks(freqs, world)
+    wslab = args.partition == "wslab" and world > 1  # (N = 1: the whole band, no slab)
+    blocks = [(0, C4_NCHAN)] * world if wslab else parallel.balanced_channel_blocks(freqs, world)
     lo, hi = blocks[rank]
-    obs = simulation.device_observation(C4_NTIMES, 1, C4_FLO, C4_FHI, config="LOW", seed=rank,
+    obs = simulation.device_observation(C4_NTIMES, 1, C4_FLO, C4_FHI, config="LOW", seed=0,
                                         device=dev, nchan_total=C4_NCHAN, channels=[lo])
     uvw, nrow = obs["uvw"], obs["nrow"]
     nb = max(1, -(-(hi - lo) // args.c4_batch),
@@ -283,13 +290,22 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
     cell = 0.25 / obs["umax"]
     freq_all = torch.as_tensor(freqs, device=dev)
     local_freq = freq_all[lo:hi]
-    resident = world >= 4
+    bounds, slab, slabs, layout, hist = None, None, None, None, None
+    if wslab:
+        # the band's plane layout (identical on every rank) and this rank's slab
+        bounds = kernels.merge_bounds(*[kernels.uvw_bounds(uvw, freq_all[a:e]) for a, e in batches])
+        layout = kernels.wstack_layout(bounds, C4_NPIX, C4_NPIX, cell, cell, EPS_REQUESTED, True,
+                                       flip_uw=True)
+        hist = parallel.first_plane_histogram(uvw, freqs, layout)
+        slabs = parallel.wslab_partition(hist, world, layout["support"])
+        slab = slabs[rank]
+    resident = world >= 4 and not wslab
     gen = torch.Generator(device=dev)
     steps = args.extra_steps if sub else args.steps
     warmup = min(args.warmup, 1) if sub else args.warmup
 
     def make_vis(a, e):
-        gen.manual_seed(7919 * rank + a)
+        gen.manual_seed(7919 * (0 if wslab else rank) + a)  # (w slabs: one band, every rank)
         return torch.randn((nrow, e - a), generator=gen, device=dev, dtype=torch.complex64)
 
     store = {(a, e): make_vis(a, e) for a, e in batches} if resident else {}
@@ -299,7 +315,7 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
 
     rel = [(a - lo, e - lo) for a, e in batches]
     out = torch.zeros((C4_NPIX, C4_NPIX), dtype=torch.float64, device=dev)
-    nvis_rank = nrow * (hi - lo)
+    nvis_rank = int(hist[slab[0]:slab[1]].sum()) if wslab else nrow * (hi - lo)
     seg = {"t": 0.0}
 
     class Seg:
@@ -324,7 +340,8 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
     def step(timer):
         out.zero_()
         parallel.invert_batched_shard(uvw, local_freq, vis_of_block, rel, C4_NPIX, cell, EPS_REQUESTED,
-                                      True, flip_uw=True, out=out, timer=timer)
+                                      True, flip_uw=True, out=out, timer=timer, bounds=bounds,
+                                      slab=slab)
 
     def reduce():
         sw = torch.tensor([float(nrow * C4_NCHAN)], dtype=torch.float64, device=dev)
@@ -373,10 +390,17 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
         elapsed = float(t.item())
     ms_step = elapsed / steps * 1e3
     nvis_total = nrow * C4_NCHAN
+    def model_ms(r):
+        if wslab:
+            a, e = slabs[r]
+            return round(parallel.wslab_cost(hist, a, e, layout["support"], float(hist.sum())), 1)
+        return round(parallel.c4_block_cost(freqs[blocks[r][0]:blocks[r][1]]), 1)
+
     if emulated:
-        print(json.dumps({"emulated_rank": rank, "world": world, "block": blocks[rank],
+        print(json.dumps({"emulated_rank": rank, "world": world, "partition": args.partition,
+                          "block": blocks[rank], "slab": slab,
                           "ms_per_step": round(ms_step, 3), "nvis_rank": nvis_rank,
-                          "model_ms": round(parallel.c4_block_cost(freqs[lo:hi]), 1),
+                          "model_ms": model_ms(rank),
                           "stages_ms": {k: round(float(sum(i[k] for i in infos)), 3)
                                         for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
                           "note": "rank's block only; no all-reduce"}), flush=True)
@@ -395,9 +419,11 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
     if os.path.exists(args.c4_traffic):
         with open(args.c4_traffic) as f:
             tr = json.load(f)
-        if tr.get("launches") == len(batches):
-            traffic = tr.get("bytes_per_launch")
-    model = [round(parallel.c4_block_cost(freqs[a:e]), 1) for a, e in blocks]
+        # PMC bytes of all the batch launches of one invert (scripts/pmc_c4.sh),
+        # the same span as `alg` and `kernel_ms_rank0`
+        if tr.get("launches") == len(batches) and world == 1:
+            traffic = tr.get("bytes_per_invert")
+    model = [model_ms(r) for r in range(world)]
     cpu = None
     if world == 1 and args.c4_cpu_chans > 0:
         cpu = c4_cpu_baseline(uvw.cpu().numpy(), freqs, cell, nvis_total, info["nplanes"],
@@ -411,10 +437,15 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
         "config": {"workload": "C4: SKA-LOW 512 stations x 400 times x 256 chan (50-350 MHz) "
                                "= 13.4 Gvis, 8192^2 image, 16384^2 w-stack grid",
                    "nvis_total": nvis_total, "npix": C4_NPIX, "cell_rad": cell,
-                   "channel_blocks": blocks, "model_ms_per_rank": model,
+                   "partition": args.partition if world > 1 else "none",
+                   "channel_blocks": blocks if not wslab else None, "w_slabs": slabs,
+                   "model_ms_per_rank": model,
                    "rank0_batches": len(batches), "inputs_resident": resident,
                    "support": W, "nplanes_rank0": info["nplanes"],
-                   "parallelism": f"channel blocks x{world}, streamed batches, 1 all-reduce"},
+                   "parallelism": (f"w slabs x{world} (each rank scans the band, grids its "
+                                   "slab's first planes), streamed batches, 1 all-reduce"
+                                   if wslab else
+                                   f"channel blocks x{world}, streamed batches, 1 all-reduce")},
         "stages_ms_rank0": {k: round(float(sum(i[k] for i in infos)), 3)
                             for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None,
@@ -427,7 +458,8 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
                      "kernel_ms_rank0": round(ms_grid, 3), "launches": len(batches),
                      "alg_bytes": int(alg),
                      "note": "vis 8 B + uvw 24 B per row per batch + the band's planes written "
-                             "once per invert, over the summed gridding launches",
+                             "once per invert, over the summed gridding launches; traffic = "
+                             "PMC bytes of those launches (profiles/traffic_c4_k_grid.json)",
                      "compute": {"achieved": round(flops / (ms_grid * 1e-3) / 1e12, 2),
                                  "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                                  "frac": round(flops / (ms_grid * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,

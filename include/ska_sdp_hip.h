@@ -60,6 +60,16 @@ extern "C" {
  * histogram exceeds 2^28 keys are refused).  SDP_HIP_FP32 keeps the fp32
  * NUFFT at its floor instead (W = 8, ~1e-6 relative RMS), as before. */
 #define SDP_HIP_FP32 64u
+/* sdp_hip_ms2dirty_batch: grid one w slab of the sequence's plane layout.
+ * `bounds` then holds 8 doubles: the 6 below, then the slab's first planes
+ * [lo, hi) (integers, 0 <= lo < hi; hi is clipped to the layout's first-plane
+ * count, which sdp_hip_wstack_layout reports).  Only visibilities whose first
+ * w plane lies in the slab are gridded -- the others are skipped (tested
+ * before their weights or values are read) -- and only planes lo .. hi + W - 2
+ * are held, transformed and screened.  The dirty images of the slabs of one
+ * layout sum to the full image (multi-GPU w-slab partition).
+ * fp32 NUFFT (epsilon >= 1e-7 or SDP_HIP_FP32) with w-stacking only. */
+#define SDP_HIP_W_SLAB 128u
 
 /* Diagnostics filled by the NUFFT entry points (may be NULL). */
 typedef struct sdp_hip_wgrid_info {
@@ -156,6 +166,18 @@ int sdp_hip_ms2dirty_batch(const double *uvw, int64_t uvw_row_stride,
                            int64_t dirty_stride_x, int64_t dirty_stride_y,
                            void *stream, sdp_hip_wgrid_info *info,
                            char *errbuf, size_t errbuf_len);
+
+/*
+ * sdp_hip_wstack_layout -- the w-plane layout sdp_hip_ms2dirty_batch uses for
+ * `bounds` (6 doubles, as above) and the image geometry, without device work:
+ * info->support, nplanes (first planes = nplanes - support + 1), w0, dw,
+ * ngrid_x/y, fp64.  A w-slab partition (SDP_HIP_W_SLAB) splits the first
+ * planes [0, nplanes - support + 1) between the ranks.
+ */
+int sdp_hip_wstack_layout(const double *bounds, int npix_x, int npix_y,
+                          double pixsize_x, double pixsize_y, double epsilon,
+                          int do_wstacking, unsigned flags, sdp_hip_wgrid_info *info,
+                          char *errbuf, size_t errbuf_len);
 
 /*
  * sdp_hip_ms2dirty_vis -- sdp_hip_ms2dirty with the visibility-side prologue

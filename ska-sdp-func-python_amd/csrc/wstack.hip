@@ -85,6 +85,11 @@ struct Geo {
     // one-cell keys: blocks of bx x 8 cells (bx = 2, 4 or 8; bxs = log2 bx),
     // each bx / 2 groups of 2 x 8 cells, consecutive in the key order
     int bx, bxs;
+    // w slab (SDP_HIP_W_SLAB): this call grids only the visibilities whose
+    // first plane lies in [slab_lo, slab_lo + nps) of the sequence's layout of
+    // nps_all first planes; w0 is then the slab's first plane, and the others
+    // are skipped without being counted as out of bounds
+    int slab, slab_lo, nps_all;
 };
 
 struct __attribute__((aligned(32))) VisRec {
@@ -167,6 +172,7 @@ struct Coord {
     double du, dv, dw;  // the same offsets in fp64 (RecC encoding)
     double w;  // w in wavelengths (sign applied)
     bool ok;
+    bool skip = false;  // w slab: inside the sequence's layout, outside this slab
 };
 
 __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restrict__ uvw,
@@ -202,7 +208,9 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
         c.dw = fp + 1.0 - pw;
         c.fw = (float)c.dw;
         c.p0 = (int)fp + 1;
-        c.ok = c.ok && c.p0 >= 0 && c.p0 < g.nps;
+        const bool in_slab = c.p0 >= 0 && c.p0 < g.nps;
+        c.ok = c.ok && in_slab;
+        if (g.slab) c.skip = !in_slab && (unsigned)(c.p0 + g.slab_lo) < (unsigned)g.nps_all;
         c.p0 = min(max(c.p0, 0), g.nps - 1);
     } else {
         c.p0 = 0;
@@ -210,6 +218,18 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
         c.dw = 0.0;
     }
     return c;
+}
+
+// w slab: the visibility's first plane (computed exactly as vis_coord does)
+// lies in the sequence's layout but outside this call's slab -- tested before
+// anything else of the visibility is read
+__device__ __forceinline__ bool slab_out(const Geo &g, const double *__restrict__ uvw, int64_t rs,
+                                         int64_t row, double f) {
+    const double s = f / kCLight;
+    const double w = g.su * uvw[row * rs + 2] * s;
+    const double pw = (w - g.w0) / g.dw;
+    const int p0 = (int)floor(fmin(fmax(pw - 0.5 * g.W, -2.0), 2.0e9)) + 1;
+    return (p0 < 0 || p0 >= g.nps) && (unsigned)(p0 + g.slab_lo) < (unsigned)g.nps_all;
 }
 
 // p0-major bucket keys: the items of a range of first planes are contiguous.
@@ -469,6 +489,10 @@ __device__ __forceinline__ void bucket_one(const Geo &g, int64_t v, int64_t nvis
         if (valid) {
             row = vg / g.nchan;
             chan = (int)(vg - row * g.nchan);
+            // (a w-slab call's count pass left no rank for the slab's outsiders)
+            if (g.slab && slab_out(g, uvw, uvw_rs, row, freq[chan])) valid = false;
+        }
+        if (valid) {
             wd = eff_weight(wgt, wrs, wcs, x, row, chan);
             wt = (float)wd;
         }
@@ -488,9 +512,14 @@ __device__ __forceinline__ void bucket_one(const Geo &g, int64_t v, int64_t nvis
         c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
     } else {
         double wd = 0.0;
+        bool outside = false;  // w slab: another call's visibility (no rank stored)
         if (valid) {
             row = vg / g.nchan;
             chan = (int)(vg - row * g.nchan);
+            outside = g.slab && slab_out(g, uvw, uvw_rs, row, freq[chan]);
+            valid = !outside;
+        }
+        if (valid) {
             wd = eff_weight(wgt, wrs, wcs, x, row, chan);
             wt = (float)wd;
             valid = x.all || (wt != 0.0f);
@@ -498,14 +527,14 @@ __device__ __forceinline__ void bucket_one(const Geo &g, int64_t v, int64_t nvis
                 c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
                 if (!c.ok) {
                     valid = false;
-                    atomicAdd(nbad, 1ull);
+                    if (!c.skip) atomicAdd(nbad, 1ull);
                 }
             }
         }
         const unsigned key = valid ? coord_key(g, c, row) : 0xffffffffu;
         const unsigned rank = run_reserve<true>(key, valid, counter);
         // only the rank is kept: the scatter pass recomputes the key
-        if (v < nvis) rk[v] = valid ? rank : 0xffffffffu;
+        if (v < nvis && !outside) rk[v] = valid ? rank : 0xffffffffu;
         if (sw_slots) {
             // weight sum: wave reduction, one atomic per wave into a slot
 #pragma unroll
@@ -1227,6 +1256,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 constexpr int kTapRec = 24;    // floats per record row of the tap block
 constexpr int kTapBatch = 16;  // records per tap block
 constexpr int kRegCell = 16;  // floats per region cell: 8 planes x re/im
+// 16-B chunk (plane pair k) of region row y: XOR-swizzled by (y >> 1) & 3
+__device__ __forceinline__ int reg_chunk(int k, int y) { return k ^ ((y >> 1) & 3); }
 
 // Work unit of NG groups: 1 (one-cell plans: a chunk of one 2 x 8-cell
 // group) or 4 (large grids: 2 x pairs x both y halves of a sub-sorted
@@ -1279,8 +1310,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     const float *const kW = blk + (lane >> 4) * kTapRec + 16 + ((lane & 15) >> 1);
     const float *const kC = reinterpret_cast<const float *>(cval) + (lane >> 4) * 2 + (lane & 1);
     // this lane's accumulator slot in a footprint cell (xo, yo) + (kx, ky):
-    // float offset ((xo + 2t + h) * kRegY + yo + (l & 7)) * 16 + 4 (l >> 4)
-    const int acc_lane = ((((lane & 15) >> 3) * kRegY) + (lane & 7)) * kRegCell + 4 * (lane >> 4);
+    // region cell (X, Y) = (xo + 2t + h, yo + (l & 7)), float offset
+    // (X kRegY + Y) 16 + 4 reg_chunk(l >> 4, Y) -- the 16-B chunk of plane pair
+    // k sits at k ^ ((Y >> 1) & 3), so the 8 lanes of a ds_write_b128 group
+    // (consecutive Y) cover all 32 banks (unswizzled: 4-way conflicts, and
+    // 8-way in the flush reads; profiles/r03_k_grid_mfma_pad_v2_pmc.json)
+    const int acc_lane = (((lane & 15) >> 3) * kRegY) * kRegCell;
+    const int acc_y = lane & 7, acc_k = lane >> 4;
     constexpr int acc_t = 2 * kRegY * kRegCell;  // + t N-tiles (two x rows each)
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
@@ -1303,8 +1339,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                 r4[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
 
+        // the accumulators and their base offset (floats) in the region: they
+        // start as zeros bound to a (zero) region slot of this lane, so the
+        // store before every cell's load needs no "first cell" test (a group
+        // that follows re-stores the previous group's last cell: the same values
+        // to the same slot)
         floatx4 acc[4];
-        int cbase = 0;  // the accumulators' base offset (floats) in the region
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+        int cbase = acc_y * kRegCell + acc_lane + 4 * reg_chunk(acc_k, acc_y);
         auto store_cell = [&]() {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
@@ -1323,10 +1366,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             return o;
         };
         auto kmfma = [&](const Ops &o) {
+            // all five operand products first: no VALU-write -> MFMA-read
+            // wait states between the four MFMAs
             const float a = o.w * o.c;
+            float bt[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) bt[t] = o.b[t] * o.v;
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, o.b[t] * o.v, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bt[t], acc[t], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x0002, 5, 0);  // the 5 VALU products
+            __builtin_amdgcn_sched_group_barrier(0x0008, 4, 0);  // then the 4 MFMAs
         };
 
         for (int gi = 0; gi < NG; ++gi) {
@@ -1337,8 +1387,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             const int gxo = NG == 1 ? 0 : 2 * (gi >> 1), gyo = NG == 1 ? 0 : 8 * (gi & 1);
             int cur = -1;  // cell of the accumulators (wave-uniform)
             auto load_cell = [&](int cell) {
-                const int xo = gxo + (cell & 1), yo = gyo + (cell >> 1);
-                cbase = (xo * kRegY + yo) * kRegCell + acc_lane;
+                const int xo = gxo + (cell & 1), y = gyo + (cell >> 1) + acc_y;
+                cbase = (xo * kRegY + y) * kRegCell + acc_lane + 4 * reg_chunk(acc_k, y);
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
                     acc[t] = *reinterpret_cast<const floatx4 *>(reg + cbase + t * acc_t);
@@ -1409,7 +1459,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                     for (int jj = 0; jj < kTapBatch / 4; ++jj) {
                         if (jj < nk) {
                             if ((hchg >> (4 * jj)) & 1ull) {
-                                if (cur >= 0) store_cell();
+                                store_cell();
                                 cur = __builtin_amdgcn_readlane(cj, kTapBatch * h + 4 * jj);
                                 load_cell(cur);
                             }
@@ -1418,14 +1468,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                     }
                 }
             }
-            if (cur >= 0) store_cell();
+            store_cell();
         }
         wave_lds_sync();
 
         // flush: lane l takes float f = i0 + l of a plane's RX x RY cells in
         // the grid's order (x rows of RY cells, re/im interleaved), i.e.
-        // region float (x * kRegY + y) * 16 + 2 q + (f & 1); buffer atomics off
-        // a per-plane descriptor (32-bit offsets); zero floats are skipped
+        // region float (x * kRegY + y) * 16 + 4 reg_chunk(q >> 1, y) +
+        // 2 (q & 1) + (f & 1); the NQ planes' values are read before any
+        // atomic is issued (one LDS wait per 64 floats, not one per plane);
+        // buffer atomics off a per-plane descriptor (32-bit offsets); zero
+        // floats are skipped
         constexpr int FPP = RX * RY * 2;
         const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
 #pragma unroll
@@ -1439,10 +1492,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
             if (gy >= g.ngy) gy -= g.ngy;
             const int voff = ((gx * g.ngy + gy) * 2 + (f & 1)) * (int)sizeof(float);
             const float *src = reg + (xl * kRegY + yl) * kRegCell + (f & 1);
+            float vals[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) vals[q] = src[4 * reg_chunk(q >> 1, yl) + 2 * (q & 1)];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int p = (int)p0 + q;
-                const float val = src[2 * q];
+                const float val = vals[q];
                 if (p >= p_lo && p < p_hi && val != 0.0f) {
                     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                         grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)), 0,
@@ -1547,25 +1603,62 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                 const float v1 = es_tap<W>(rec.fv, tv1, ihw, bl);
                 const float w0 = WS ? es_tap<W>(rec.fw, tu0, ihw, bl) : (kg == 0 ? 1.0f : 0.0f);
                 const float w1 = WS ? es_tap<W>(rec.fw, tu1, ihw, bl) : 0.0f;
+                // tu[2h], tu[2h+1] of the lane's record live in 16-lane row h
+                // (u0, u1): broadcast every row to all four with v_permlane32_swap
+                // + v_permlane16_swap (VALU; the ds_bpermute form put an LDS
+                // round trip between every pair of MFMAs)
                 float tu[8];
+                {
+                    const auto p0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(u0),
+                                                                     __float_as_uint(u0), false, false);
+                    const auto p1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(u1),
+                                                                     __float_as_uint(u1), false, false);
+                    // p[0] = rows (0, 1, 0, 1), p[1] = rows (2, 3, 2, 3)
+                    const auto a0 = __builtin_amdgcn_permlane16_swap(p0[0], p0[0], false, false);
+                    const auto b0 = __builtin_amdgcn_permlane16_swap(p0[1], p0[1], false, false);
+                    const auto a1 = __builtin_amdgcn_permlane16_swap(p1[0], p1[0], false, false);
+                    const auto b1 = __builtin_amdgcn_permlane16_swap(p1[1], p1[1], false, false);
+                    tu[0] = __uint_as_float(a0[0]);
+                    tu[2] = __uint_as_float(a0[1]);
+                    tu[4] = __uint_as_float(b0[0]);
+                    tu[6] = __uint_as_float(b0[1]);
+                    tu[1] = __uint_as_float(a1[0]);
+                    tu[3] = __uint_as_float(a1[1]);
+                    tu[5] = __uint_as_float(b1[0]);
+                    tu[7] = __uint_as_float(b1[1]);
+                }
+                float bt[16];
 #pragma unroll
-                for (int h = 0; h < 4; ++h) {
-                    tu[2 * h] = __shfl(u0, r16 + 16 * h);
-                    tu[2 * h + 1] = __shfl(u1, r16 + 16 * h);
+                for (int s = 0; s < 16; s += 2) {
+                    bt[s] = tu[s >> 1] * v0;
+                    bt[s + 1] = tu[s >> 1] * v1;
                 }
                 floatx4 d0 = floatx4{0.0f, 0.0f, 0.0f, 0.0f}, d1 = d0;
 #pragma unroll
                 for (int s = 0; s < 16; s += 2) {
-                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], tu[s >> 1] * v0, d0, 0, 0, 0);
-                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s + 1], tu[s >> 1] * v1, d1, 0, 0, 0);
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bt[s], d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s + 1], bt[s + 1], d1, 0, 0, 0);
                 }
                 // row 4 kg + i of D = (q = 2 kg + (i >> 1), re/im = i & 1)
                 float sr = w0 * (d0[0] + d1[0]) + w1 * (d0[2] + d1[2]);
                 float si = w0 * (d0[1] + d1[1]) + w1 * (d0[3] + d1[3]);
-                sr += __shfl_xor(sr, 16);
-                si += __shfl_xor(si, 16);
-                sr += __shfl_xor(sr, 32);
-                si += __shfl_xor(si, 32);
+                // sum over the four rows: (row pairs by v_permlane32_swap, then
+                // rows by v_permlane16_swap), every lane gets the total
+                {
+                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(sr),
+                                                                    __float_as_uint(si), false, false);
+                    // r[0] = (sr rows 0,1 | si rows 0,1), r[1] = (sr rows 2,3 | si rows 2,3)
+                    const float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                    // t: rows 0,1 = sr (0+2, 1+3), rows 2,3 = si (0+2, 1+3)
+                    const auto s2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(t),
+                                                                     __float_as_uint(t), false, false);
+                    const float tot = __uint_as_float(s2[0]) + __uint_as_float(s2[1]);
+                    // tot: rows 0,1 = sr total, rows 2,3 = si total
+                    const auto s3 = __builtin_amdgcn_permlane32_swap(__float_as_uint(tot),
+                                                                     __float_as_uint(tot), false, false);
+                    sr = __uint_as_float(s3[0]);  // rows 0,1 of tot -> all rows
+                    si = __uint_as_float(s3[1]);  // rows 2,3 of tot -> all rows
+                }
                 if (kg == 0 && ri < re) {
                     if (vdirect) {
                         vdirect[rec.idx] =
@@ -2519,7 +2612,7 @@ struct BatchSeq {
     int nx = 0, ny = 0, do_w = 0, nplanes = 0;
     double px = 0, py = 0, eps = 0;
     unsigned flip = 0;
-    double b[6] = {0, 0, 0, 0, 0, 0};
+    double b[8] = {0, 0, 0, 0, 0, 0, -1, -1};  // bounds (+ the w slab)
 };
 
 static std::mutex g_kept_mu;
@@ -2591,6 +2684,10 @@ static BatchSeq batch_token(const Plan &P, const Inputs &in) {
     s.eps = in.eps;
     s.flip = in.flags & SDP_HIP_FLIP_UW;
     for (int k = 0; k < 6; ++k) s.b[k] = in.bounds[k];
+    if (in.flags & SDP_HIP_W_SLAB) {
+        s.b[6] = in.bounds[6];
+        s.b[7] = in.bounds[7];
+    }
     return s;
 }
 
@@ -2608,9 +2705,34 @@ static void check_batch_seq(const Plan &P, const Inputs &in, bool first) {
     bool same = cur.nx == t.nx && cur.ny == t.ny && cur.do_w == t.do_w &&
                 cur.nplanes == t.nplanes && cur.px == t.px && cur.py == t.py &&
                 cur.eps == t.eps && cur.flip == t.flip;
-    for (int k = 0; k < 6; ++k) same = same && cur.b[k] == t.b[k];
+    for (int k = 0; k < 8; ++k) same = same && cur.b[k] == t.b[k];
     SDP_REQUIRE(same, "batched invert: every batch of a sequence needs the geometry, epsilon, "
                       "flags and bounds of its first batch");
+}
+
+// w-plane layout of an invert / predict (ducc0's w-stacking geometry): plane
+// spacing dw = 1 / (2 tmax) from the image's largest n - 1, first plane w0 a
+// half support below the smallest w, nplanes covering the largest; nps =
+// distinct first planes.  Shared by plan_geometry and sdp_hip_wstack_layout.
+static void w_layout(const Inputs &in, double wmin, double wmax, Geo &g) {
+    const double lmax = (in.nx / 2) * in.px, mmax = (in.ny / 2) * in.py;
+    const double r2 = std::min(lmax * lmax + mmax * mmax, 1.0);
+    const double tmax = 1.0 - std::sqrt(1.0 - r2);
+    g.do_w = (in.do_w && tmax > 0.0) ? 1 : 0;
+    if (g.do_w) {
+        g.s0 = 0.5 * tmax;
+        g.dw = 1.0 / (2.0 * tmax);
+        g.w0 = wmin - (0.5 * g.W - 0.5) * g.dw;
+        const double pwmax = (wmax - g.w0) / g.dw;
+        g.nplanes = (int)std::floor(pwmax - 0.5 * g.W) + 1 + g.W;
+        g.nps = g.nplanes - g.W + 1;
+    } else {
+        g.s0 = 0.0;
+        g.dw = 1.0;
+        g.w0 = 0.0;
+        g.nplanes = 1;
+        g.nps = 1;
+    }
 }
 
 // Geometry shared by both directions: kernel, padded grid, w planes, bucket
@@ -2678,23 +2800,28 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     SDP_REQUIRE(umax * in.px < 0.5 && vmax * in.py < 0.5,
                 "some uvw coordinates exceed the image's Nyquist limit (|u|*pixsize >= 0.5)");
 
-    const double lmax = (in.nx / 2) * in.px, mmax = (in.ny / 2) * in.py;
-    const double r2 = std::min(lmax * lmax + mmax * mmax, 1.0);
-    const double tmax = 1.0 - std::sqrt(1.0 - r2);
-    g.do_w = (in.do_w && tmax > 0.0) ? 1 : 0;
-    if (g.do_w) {
-        g.s0 = 0.5 * tmax;
-        g.dw = 1.0 / (2.0 * tmax);
-        g.w0 = wmin - (0.5 * g.W - 0.5) * g.dw;
-        const double pwmax = (wmax - g.w0) / g.dw;
-        g.nplanes = (int)std::floor(pwmax - 0.5 * g.W) + 1 + g.W;
-        g.nps = g.nplanes - g.W + 1;
-    } else {
-        g.s0 = 0.0;
-        g.dw = 1.0;
-        g.w0 = 0.0;
-        g.nplanes = 1;
-        g.nps = 1;
+    w_layout(in, wmin, wmax, g);
+    // w slab of the sequence's plane layout (bounds[6], bounds[7]: first
+    // planes [lo, hi)): this call's planes are lo .. hi + W - 2 and its w0 the
+    // slab's first plane, so records, keys, FFTs and screens see only the slab
+    g.slab = 0;
+    g.slab_lo = 0;
+    g.nps_all = g.nps;
+    if (in.flags & SDP_HIP_W_SLAB) {
+        SDP_REQUIRE(in.bounds != nullptr, "SDP_HIP_W_SLAB needs the batch bounds (8 doubles)");
+        SDP_REQUIRE(g.do_w, "SDP_HIP_W_SLAB needs w-stacking");
+        SDP_REQUIRE(grid_mode && !P.f64, "SDP_HIP_W_SLAB is an fp32 invert option");
+        const double lo_d = in.bounds[6], hi_d = in.bounds[7];
+        SDP_REQUIRE(lo_d >= 0.0 && lo_d < hi_d && lo_d == std::floor(lo_d) &&
+                        hi_d == std::floor(hi_d) && lo_d < (double)g.nps,
+                    "w slab: first planes [lo, hi) must be integers with 0 <= lo < hi and lo "
+                    "below the layout's first-plane count");
+        const int lo = (int)lo_d, hi = (int)std::min<double>(hi_d, (double)g.nps);
+        g.slab = 1;
+        g.slab_lo = lo;
+        g.w0 += lo * g.dw;
+        g.nps = hi - lo;
+        g.nplanes = g.nps + g.W - 1;
     }
     // bucket window (origins only: the footprints' halo may leave it).  x
     // (rows) only: the y stride stays ngy, since a compacted y range packs the
@@ -3629,6 +3756,44 @@ int sdp_hip_ms2dirty_batch(const double *uvw, int64_t uvw_row_stride, const doub
         in.x.wgt_f64 = wstack::weight_is_f64(wgt_dtype);
         in.bounds = bounds;
         wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
+    });
+}
+
+int sdp_hip_wstack_layout(const double *bounds, int npix_x, int npix_y, double pixsize_x,
+                          double pixsize_y, double epsilon, int do_wstacking, unsigned flags,
+                          sdp_hip_wgrid_info *info, char *errbuf, size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(bounds != nullptr && info != nullptr, "null pointer argument");
+        SDP_REQUIRE(npix_x > 0 && npix_y > 0 && npix_x % 2 == 0 && npix_y % 2 == 0,
+                    "npix_x and npix_y must be positive and even");
+        SDP_REQUIRE(pixsize_x > 0 && pixsize_y > 0, "pixel sizes must be positive");
+        const double *b = bounds;
+        SDP_REQUIRE(b[0] <= b[1] && b[2] >= 0 && b[3] >= 0 && b[4] > 0 && b[4] <= b[5],
+                    "bounds must be {wmin <= wmax, umax >= 0, vmax >= 0, 0 < fmin <= fmax}");
+        wstack::Inputs in{};
+        in.nx = npix_x;
+        in.ny = npix_y;
+        in.px = pixsize_x;
+        in.py = pixsize_y;
+        in.eps = epsilon;
+        in.do_w = do_wstacking;
+        in.flags = flags;
+        wstack::Geo g{};
+        const bool f64 = epsilon < 1.0e-7 && !(flags & SDP_HIP_FP32);
+        g.W = f64 ? wstack::kernel_support64(epsilon) : wstack::kernel_support(epsilon);
+        const double su = (flags & SDP_HIP_FLIP_UW) ? -1.0 : 1.0;
+        const double h0 = su > 0 ? b[0] : -b[1], h1 = su > 0 ? b[1] : -b[0];
+        const double slo = b[4] / wstack::kCLight, shi = b[5] / wstack::kCLight;
+        wstack::w_layout(in, std::min(h0 * slo, h0 * shi), std::max(h1 * slo, h1 * shi), g);
+        *info = sdp_hip_wgrid_info{};
+        info->support = g.W;
+        info->beta = 2.30 * g.W;
+        info->ngrid_x = ((2 * npix_x + wstack::kGridAlign - 1) / wstack::kGridAlign) * wstack::kGridAlign;
+        info->ngrid_y = ((2 * npix_y + wstack::kGridAlign - 1) / wstack::kGridAlign) * wstack::kGridAlign;
+        info->nplanes = g.nplanes;
+        info->w0 = g.w0;
+        info->dw = g.dw;
+        info->fp64 = f64 ? 1 : 0;
     });
 }
 

@@ -32,6 +32,7 @@ SDP_HIP_BATCH_LAST = 8
 SDP_HIP_KEEP_BUCKETS = 16
 SDP_HIP_REUSE_BUCKETS = 32
 SDP_HIP_FP32 = 64
+SDP_HIP_W_SLAB = 128
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
@@ -87,9 +88,12 @@ SIGNATURES = {
         c_vp, c_int, c_i64, c_i64,                # vis, dtype, strides
         c_vp, c_int, c_i64, c_i64,                # wgt, dtype (f32 / f64), strides
         c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,
-        c_vp,                                     # bounds (host, 6 doubles)
+        c_vp,                                     # bounds (host, 6 doubles; 8 with W_SLAB)
         c_vp, c_i64, c_i64,                       # dirty, strides
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
+    "sdp_hip_wstack_layout": [
+        c_vp, c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,  # bounds, geometry, eps, do_w, flags
+        ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_ms2dirty_vis": [
         c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
         c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # vis, dtype, row/chan/pol strides, npol_vis

@@ -171,14 +171,35 @@ def merge_bounds(*bs):
             max(b[3] for b in bs), min(b[4] for b in bs), max(b[5] for b in bs)]
 
 
+def wstack_layout(bounds, npix_x, npix_y, pixsize_x, pixsize_y, epsilon=1e-7, do_wstacking=True,
+                  flip_uw=False, precision=None):
+    """The w-plane layout an ms2dirty_batch sequence with these ``bounds``
+    uses (sdp_hip_wstack_layout, no device work): dict with support, nplanes,
+    w0, dw and ``nps`` = the first-plane count a w-slab partition splits."""
+    if len(bounds) != 6:
+        raise ValueError("bounds: {wmin, wmax, umax, vmax, fmin, fmax}")
+    bbuf = (ctypes.c_double * 6)(*[float(x) for x in bounds])
+    flags = (_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | _prec_bits(epsilon, precision)
+    info = _lib.WGridInfo()
+    _lib.call("sdp_hip_wstack_layout", ctypes.cast(bbuf, ctypes.c_void_p), int(npix_x),
+              int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
+              int(bool(do_wstacking)), flags, ctypes.byref(info))
+    d = info.as_dict()
+    d["nps"] = d["nplanes"] - d["support"] + 1 if d["nplanes"] > 1 else 1
+    return d
+
+
 def ms2dirty_batch(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y, bounds,
                    first, last, epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
-                   out_strides=None, accumulate=False, precision=None):
+                   out_strides=None, accumulate=False, precision=None, slab=None):
     """One batch of a batched invert (sdp_hip_ms2dirty_batch): the batch is
     gridded into the resident w planes shared by the whole sequence; the
     ``first`` batch zeroes them, the ``last`` runs the FFT and w-screens into
     ``out`` (allocated if None; earlier batches return None).  ``bounds``:
-    merge_bounds over every batch of the sequence."""
+    merge_bounds over every batch of the sequence.  ``slab`` = (lo, hi): grid
+    only the visibilities whose first w plane of the sequence's layout
+    (wstack_layout) lies in [lo, hi), into that slab's planes only
+    (SDP_HIP_W_SLAB; the slabs of one layout sum to the full image)."""
     pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
     dev = uvw.device
@@ -200,9 +221,16 @@ def ms2dirty_batch(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y, bo
             raise ValueError("dirty output must be float64")
     if len(bounds) != 6:
         raise ValueError("bounds: {wmin, wmax, umax, vmax, fmin, fmax}")
-    bbuf = (ctypes.c_double * 6)(*[float(x) for x in bounds])
+    vals = [float(x) for x in bounds]
+    if slab is not None:
+        lo, hi = (int(x) for x in slab)
+        if not 0 <= lo < hi:
+            raise ValueError("slab: first planes (lo, hi) with 0 <= lo < hi")
+        vals += [float(lo), float(hi)]
+    bbuf = (ctypes.c_double * len(vals))(*vals)
     flags = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
-             | (_lib.SDP_HIP_BATCH_FIRST if first else 0) | (_lib.SDP_HIP_BATCH_LAST if last else 0))
+             | (_lib.SDP_HIP_BATCH_FIRST if first else 0) | (_lib.SDP_HIP_BATCH_LAST if last else 0)
+             | (_lib.SDP_HIP_W_SLAB if slab is not None else 0) | pbits)
     info = _lib.WGridInfo()
     _lib.call(
         "sdp_hip_ms2dirty_batch",

@@ -159,8 +159,82 @@ def balanced_channel_blocks(freqs, world, cost=c4_block_cost):
     return sweep(hi_t)
 
 
+# w-slab partition of a band's invert (SDP_HIP_W_SLAB).  Every rank scans the
+# whole band and grids only the visibilities whose first w plane lies in its
+# contiguous slab of the band's plane layout, so it holds, transforms and
+# screens only its slab's planes plus a W - 1 halo: the band's plane work is
+# ~ nps + (world - 1)(W - 1) planes in total, not the sum over channel blocks
+# of each block's own w range.  The image-domain sum of the slabs' images is
+# the full image (each visibility is gridded once; the planes a slab holds
+# are the footprints of its own visibilities).  Cost per rank (ms): gridding
+# + bucketing per gridded visibility, the skip test per scanned visibility,
+# per held plane (zeroing, FFT, w-screen), fixed.
+WSLAB_VIS_MS_PER_G = 99.0    # C4 N = 1: (prep 619 + grid 709 ms) / 13.4 Gvis
+WSLAB_SCAN_MS_PER_G = 4.0    # slab test of the visibilities of other slabs
+WSLAB_PLANE_MS = 1.55        # C4 N = 1: (FFT 97 + screen 11 ms) / 71 planes, + zeroing
+WSLAB_FIXED_MS = 4.2
+
+
+def first_plane_histogram(uvw, freqs, layout, flip_uw=True):
+    """Visibilities per first w plane of ``layout`` (kernels.wstack_layout) over
+    the rows ``uvw`` [nrow, 3] (device, metres) and all ``freqs``: p0 =
+    floor((w f / c - w0) / dw - W / 2) + 1, as the bucketing computes it."""
+    w = uvw[:, 2].to(torch.float64) * (-1.0 if flip_uw else 1.0)
+    nps, W, w0, dw = layout["nps"], layout["support"], layout["w0"], layout["dw"]
+    hist = torch.zeros(nps, dtype=torch.float64, device=uvw.device)
+    for f in np.asarray(freqs, dtype=float):
+        pw = (w * (f / 299792458.0) - w0) / dw
+        p0 = torch.floor(torch.clamp(pw - 0.5 * W, -2.0, 2.0e9)).to(torch.int64) + 1
+        hist += torch.bincount(p0.clamp(0, nps - 1), minlength=nps)[:nps].to(torch.float64)
+    return hist.cpu().numpy()
+
+
+def wslab_cost(hist, lo, hi, W, nvis_total):
+    """Modelled invert time (ms) of the rank holding first planes [lo, hi)."""
+    n = float(np.sum(hist[lo:hi]))
+    return (WSLAB_FIXED_MS + WSLAB_VIS_MS_PER_G * n / 1e9 +
+            WSLAB_SCAN_MS_PER_G * (nvis_total - n) / 1e9 + WSLAB_PLANE_MS * (hi - lo + W - 1))
+
+
+def wslab_partition(hist, world, W):
+    """Contiguous first-plane slabs [(lo, hi)] covering [0, len(hist)) for
+    `world` ranks, minimising the largest modelled cost (bisection on the
+    target with a greedy sweep; every slab holds at least one first plane)."""
+    nps = len(hist)
+    nvis = float(np.sum(hist))
+    if world <= 1 or nps <= 1:
+        return [(0, nps)]
+    world_eff = min(world, nps)
+
+    def sweep(target):
+        slabs, lo = [], 0
+        for r in range(world_eff):
+            hi = lo + 1
+            while hi < nps and nps - hi > world_eff - r - 1 and \
+                    wslab_cost(hist, lo, hi + 1, W, nvis) <= target:
+                hi += 1
+            if r == world_eff - 1:
+                hi = nps
+            slabs.append((lo, hi))
+            lo = hi
+        return slabs
+
+    lo_t, hi_t = 0.0, wslab_cost(hist, 0, nps, W, nvis)
+    for _ in range(60):
+        mid = 0.5 * (lo_t + hi_t)
+        sl = sweep(mid)
+        if max(wslab_cost(hist, a, e, W, nvis) for a, e in sl) <= mid:
+            hi_t = mid
+        else:
+            lo_t = mid
+    slabs = sweep(hi_t)
+    # more ranks than first planes: the extra ranks get empty slabs
+    return slabs + [(nps, nps)] * (world - world_eff)
+
+
 def invert_batched_shard(uvw, freq, vis_of_block, blocks, npix, cell, epsilon=1e-7,
-                         do_wstacking=True, flip_uw=True, out=None, timer=None):
+                         do_wstacking=True, flip_uw=True, out=None, timer=None, bounds=None,
+                         slab=None, batch_fn=None):
     """Invert one rank's channels as a sequence of channel blocks streamed
     through shared resident w planes (kernels.ms2dirty_batch: one plane
     layout from the merged bounds, one FFT pass).  ``vis_of_block(a, e)``
@@ -168,22 +242,51 @@ def invert_batched_shard(uvw, freq, vis_of_block, blocks, npix, cell, epsilon=1e
     or loaded on demand); ``timer`` (optional) is a context-manager factory
     wrapped around each device call so the caller can exclude the input
     staging from its timing.  Unit weights.  Returns the dirty image in
-    RASCIL [y, x] order (unnormalised) accumulated into ``out``."""
+    RASCIL [y, x] order (unnormalised) accumulated into ``out``.  ``bounds``:
+    the sequence's plane layout (default: merged over ``blocks``); ``slab`` =
+    (lo, hi): a w-slab rank's first planes of that layout (wslab_partition),
+    ``blocks`` then covering the whole band."""
     from . import kernels
     dev = uvw.device
     if out is None:
         out = torch.zeros((npix, npix), dtype=torch.float64, device=dev)
-    b = kernels.merge_bounds(*[kernels.uvw_bounds(uvw, freq[a:e]) for a, e in blocks])
+    if slab is not None and slab[0] >= slab[1]:
+        return out  # (an empty slab: more ranks than first planes)
+    b = bounds or kernels.merge_bounds(*[kernels.uvw_bounds(uvw, freq[a:e]) for a, e in blocks])
+    fn = batch_fn or kernels.ms2dirty_batch
     for i, (a, e) in enumerate(blocks):
         vis = vis_of_block(a, e)
         ctx = timer() if timer else _nullctx()
         with ctx:
-            kernels.ms2dirty_batch(uvw, freq[a:e], vis, None, npix, npix, cell, cell, b,
+            fn(uvw, freq[a:e], vis, None, npix, npix, cell, cell, b,
                                    first=i == 0, last=i == len(blocks) - 1, epsilon=epsilon,
                                    do_wstacking=do_wstacking, flip_uw=flip_uw, out=out,
-                                   out_strides=(1, npix), accumulate=True)
+                                   out_strides=(1, npix), accumulate=True, slab=slab)
         del vis
     return out
+
+
+def invert_wslab(uvw, freq, vis_of_block, blocks, npix, cell, epsilon=1e-7, do_wstacking=True,
+                 flip_uw=True, bounds=None, group=None, out=None, timer=None, batch_fn=None):
+    """w-slab multi-GPU invert of one band: every rank streams ALL the band's
+    channel ``blocks`` (the SPMD form in which every rank holds the band, as
+    the API sharding assumes) and grids only its slab of the band's first w
+    planes (wslab_partition over first_plane_histogram: modelled cost
+    balanced), then ONE all-reduce of the image sums the slabs.  Returns
+    (image [y, x] unnormalised, slabs).  ``batch_fn`` replaces
+    kernels.ms2dirty_batch (CPU tests inject the exact-sum oracle)."""
+    from . import kernels
+    rank, world = (dist.get_rank(group), dist.get_world_size(group)) if _dist_on() else (0, 1)
+    b = bounds or kernels.merge_bounds(*[kernels.uvw_bounds(uvw, freq[a:e]) for a, e in blocks])
+    lay = kernels.wstack_layout(b, npix, npix, cell, cell, epsilon, do_wstacking, flip_uw=flip_uw)
+    hist = first_plane_histogram(uvw, freq.detach().cpu().numpy(), lay, flip_uw=flip_uw)
+    slabs = wslab_partition(hist, world, lay["support"])
+    out = invert_batched_shard(uvw, freq, vis_of_block, blocks, npix, cell, epsilon, do_wstacking,
+                               flip_uw, out=out, timer=timer, bounds=b,
+                               slab=slabs[rank] if world > 1 else None, batch_fn=batch_fn)
+    if world > 1:
+        all_reduce_sum(out, group)
+    return out, slabs
 
 
 class _nullctx:

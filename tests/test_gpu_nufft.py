@@ -703,3 +703,58 @@ def test_nan_in_flagged_samples_does_not_reach_the_image(pf, ipf):
     np.testing.assert_allclose(sw_bad, sw_ok, rtol=1e-12)
     for p in range(npol):
         assert rel_rms(d_bad["pixels"].data[0, p], d_ok["pixels"].data[0, p]) < 1e-6, p
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_w_slabs_sum_to_the_full_invert(flip):
+    """SDP_HIP_W_SLAB (the multi-GPU w-slab partition): the dirty images of
+    contiguous first-plane slabs of one plane layout -- each a batched
+    sequence over the whole band that grids only its slab's visibilities into
+    its slab's planes -- sum to the full invert; the slabs' gridded
+    visibilities add up to the total and each holds only its slab's planes
+    (+ W - 1); visibilities outside the layout are still refused."""
+    from ska_sdp_func_python_amd import kernels, parallel
+    uvw, freq, ms, wgt, cell = _problem(24, nrow=3000, nchan=6, umax=6000.0)
+    uvw[:, 2] *= 60.0  # w spans many planes
+    U, F, M, Wt = T(uvw), T(freq), T(ms), T(wgt)
+    blocks = [(0, 2), (2, 4), (4, 6)]
+    b = kernels.merge_bounds(*[kernels.uvw_bounds(U, F[a:e]) for a, e in blocks])
+    full = None
+    for i, (a, e) in enumerate(blocks):
+        full, finfo = kernels.ms2dirty_batch(U, F[a:e], M[:, a:e].contiguous(),
+                                             Wt[:, a:e].contiguous(), 256, 256, cell, cell, b,
+                                             first=i == 0, last=i == 2, epsilon=1e-7,
+                                             flip_uw=flip)
+    lay = kernels.wstack_layout(b, 256, 256, cell, cell, 1e-7, True, flip_uw=flip)
+    assert lay["nplanes"] == finfo["nplanes"] and lay["w0"] == finfo["w0"]
+    nps, W = lay["nps"], lay["support"]
+    assert nps >= 6
+    hist = parallel.first_plane_histogram(U, freq, lay, flip_uw=flip)
+    assert hist.sum() == uvw.shape[0] * freq.size
+    slabs = parallel.wslab_partition(hist, 3, W)
+    assert slabs[0][0] == 0 and slabs[-1][1] == nps
+    assert all(s[1] == t[0] for s, t in zip(slabs, slabs[1:]))
+    total = torch.zeros_like(full)
+    used = 0
+    for lo, hi in slabs + [(nps, nps + 5)]:  # (a slab past the layout grids nothing)
+        if lo >= hi or lo >= nps:
+            continue
+        out = None
+        for i, (a, e) in enumerate(blocks):
+            out, sinfo = kernels.ms2dirty_batch(U, F[a:e], M[:, a:e].contiguous(),
+                                                Wt[:, a:e].contiguous(), 256, 256, cell, cell, b,
+                                                first=i == 0, last=i == 2, epsilon=1e-7,
+                                                flip_uw=flip, slab=(lo, hi))
+            used += sinfo["nvis_used"]
+        assert sinfo["nplanes"] == min(hi, nps) - lo + W - 1
+        assert abs(sinfo["w0"] - (lay["w0"] + lo * lay["dw"])) < 1e-9 * abs(lay["dw"]) * nps
+        total += out
+    assert used == uvw.shape[0] * freq.size
+    assert rel_rms(total.cpu().numpy(), full.cpu().numpy()) < 1e-6
+    exact = orc.ms2dirty_exact(uvw * (FLIP_UW if flip else 1.0), freq, ms, wgt, 256, 256, cell,
+                               cell, True)
+    assert rel_rms(total.cpu().numpy(), exact) < TOL
+    tight = [b[0], 0.5 * (b[0] + b[1]), b[2], b[3], b[4], b[5]]
+    with pytest.raises(ValueError, match="outside"):
+        kernels.ms2dirty_batch(U, F, M, None, 256, 256, cell, cell, tight, first=True, last=True,
+                               epsilon=1e-7, flip_uw=flip, slab=(0, 1))

@@ -203,3 +203,37 @@ def test_balanced_channel_blocks_cover_and_balance():
         assert all(b[i][1] == b[i + 1][0] and b[i][0] < b[i][1] for i in range(world - 1))
         c = [parallel.c4_block_cost(f[a:e]) for a, e in b]
         assert max(c) <= 1.03 * (sum(c) / world)
+
+
+def test_wslab_partition_covers_the_planes_and_balances():
+    """parallel.wslab_partition: contiguous first-plane slabs covering the
+    layout, none empty while there are planes enough, the modelled costs
+    balanced within one plane's worth of work; more ranks than planes leave
+    the extra ranks empty.  first_plane_histogram matches the bucketing's
+    first-plane formula on CPU tensors."""
+    import numpy as np
+    import torch
+    from ska_sdp_func_python_amd import parallel
+    rng = np.random.default_rng(7)
+    hist = rng.gamma(0.6, 1e7, 71)
+    hist[:10] *= 8.0  # the dense low-|w| planes
+    for world in (1, 2, 4, 8):
+        slabs = parallel.wslab_partition(hist, world, 8)
+        assert len(slabs) == world and slabs[0][0] == 0 and slabs[-1][1] == 71
+        assert all(s[1] == t[0] and s[0] < s[1] for s, t in zip(slabs, slabs[1:]))
+        costs = [parallel.wslab_cost(hist, a, e, 8, hist.sum()) for a, e in slabs]
+        best_single = max(parallel.wslab_cost(hist, p, p + 1, 8, hist.sum()) for p in range(71))
+        assert max(costs) <= max(best_single, sum(costs) / world + 3 * parallel.WSLAB_PLANE_MS
+                                 + parallel.WSLAB_VIS_MS_PER_G * hist.max() / 1e9)
+    few = parallel.wslab_partition(np.ones(3), 5, 8)
+    assert few[:3] == [(0, 1), (1, 2), (2, 3)] and few[3:] == [(3, 3), (3, 3)]
+    uvw = torch.as_tensor(rng.normal(size=(500, 3)) * 300.0)
+    freqs = np.array([1.0e8, 1.5e8, 2.0e8])
+    lay = {"nps": 40, "support": 8, "w0": -80.0, "dw": 4.0}
+    h = parallel.first_plane_histogram(uvw, freqs, lay, flip_uw=True)
+    w = -uvw[:, 2].numpy()
+    ref = np.zeros(40)
+    for f in freqs:
+        p0 = np.floor(np.clip((w * f / 299792458.0 + 80.0) / 4.0 - 4.0, -2, 2e9)).astype(int) + 1
+        np.add.at(ref, np.clip(p0, 0, 39), 1)
+    assert np.array_equal(h, ref)
