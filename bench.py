@@ -89,12 +89,13 @@ def parse():
     ap.add_argument("--c4-cpu-chans", type=int, default=2,
                     help="c4: channels in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--c4-traffic", default=os.path.join(ROOT, "profiles", "traffic_c4_k_grid.json"))
-    ap.add_argument("--partition", choices=("chan", "wslab"), default="wslab",
-                    help="c4 with N > 1: 'wslab' -- every rank scans the band and grids the "
-                         "visibilities of its contiguous slab of the band's w planes "
-                         "(parallel.wslab_partition; plane work ~ the band's planes once); "
-                         "'chan' -- cost-balanced contiguous channel blocks, each rank with its "
-                         "own w planes (parallel.balanced_channel_blocks)")
+    ap.add_argument("--partition", choices=("chan", "wslab"), default="chan",
+                    help="c4 with N > 1: 'chan' (default) -- cost-balanced contiguous channel "
+                         "blocks, each rank with its own w planes (parallel."
+                         "balanced_channel_blocks); 'wslab' -- every rank scans the band and "
+                         "grids the visibilities of its contiguous slab of the band's w planes "
+                         "(parallel.wslab_partition; measured 2.6x at N = 8 on C4, whose first "
+                         "plane at w ~ 0 holds 38 %% of the visibilities: DESIGN.md §6)")
     ap.add_argument("--emulate", default=None, metavar="RANK/WORLD",
                     help="c4 on one GPU: run only rank RANK's block of a WORLD-way partition "
                          "(no collective), to measure per-rank times")

@@ -1603,62 +1603,25 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                 const float v1 = es_tap<W>(rec.fv, tv1, ihw, bl);
                 const float w0 = WS ? es_tap<W>(rec.fw, tu0, ihw, bl) : (kg == 0 ? 1.0f : 0.0f);
                 const float w1 = WS ? es_tap<W>(rec.fw, tu1, ihw, bl) : 0.0f;
-                // tu[2h], tu[2h+1] of the lane's record live in 16-lane row h
-                // (u0, u1): broadcast every row to all four with v_permlane32_swap
-                // + v_permlane16_swap (VALU; the ds_bpermute form put an LDS
-                // round trip between every pair of MFMAs)
                 float tu[8];
-                {
-                    const auto p0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(u0),
-                                                                     __float_as_uint(u0), false, false);
-                    const auto p1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(u1),
-                                                                     __float_as_uint(u1), false, false);
-                    // p[0] = rows (0, 1, 0, 1), p[1] = rows (2, 3, 2, 3)
-                    const auto a0 = __builtin_amdgcn_permlane16_swap(p0[0], p0[0], false, false);
-                    const auto b0 = __builtin_amdgcn_permlane16_swap(p0[1], p0[1], false, false);
-                    const auto a1 = __builtin_amdgcn_permlane16_swap(p1[0], p1[0], false, false);
-                    const auto b1 = __builtin_amdgcn_permlane16_swap(p1[1], p1[1], false, false);
-                    tu[0] = __uint_as_float(a0[0]);
-                    tu[2] = __uint_as_float(a0[1]);
-                    tu[4] = __uint_as_float(b0[0]);
-                    tu[6] = __uint_as_float(b0[1]);
-                    tu[1] = __uint_as_float(a1[0]);
-                    tu[3] = __uint_as_float(a1[1]);
-                    tu[5] = __uint_as_float(b1[0]);
-                    tu[7] = __uint_as_float(b1[1]);
-                }
-                float bt[16];
 #pragma unroll
-                for (int s = 0; s < 16; s += 2) {
-                    bt[s] = tu[s >> 1] * v0;
-                    bt[s + 1] = tu[s >> 1] * v1;
+                for (int h = 0; h < 4; ++h) {
+                    tu[2 * h] = __shfl(u0, r16 + 16 * h);
+                    tu[2 * h + 1] = __shfl(u1, r16 + 16 * h);
                 }
                 floatx4 d0 = floatx4{0.0f, 0.0f, 0.0f, 0.0f}, d1 = d0;
 #pragma unroll
                 for (int s = 0; s < 16; s += 2) {
-                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bt[s], d0, 0, 0, 0);
-                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s + 1], bt[s + 1], d1, 0, 0, 0);
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], tu[s >> 1] * v0, d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s + 1], tu[s >> 1] * v1, d1, 0, 0, 0);
                 }
                 // row 4 kg + i of D = (q = 2 kg + (i >> 1), re/im = i & 1)
                 float sr = w0 * (d0[0] + d1[0]) + w1 * (d0[2] + d1[2]);
                 float si = w0 * (d0[1] + d1[1]) + w1 * (d0[3] + d1[3]);
-                // sum over the four rows: (row pairs by v_permlane32_swap, then
-                // rows by v_permlane16_swap), every lane gets the total
-                {
-                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(sr),
-                                                                    __float_as_uint(si), false, false);
-                    // r[0] = (sr rows 0,1 | si rows 0,1), r[1] = (sr rows 2,3 | si rows 2,3)
-                    const float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-                    // t: rows 0,1 = sr (0+2, 1+3), rows 2,3 = si (0+2, 1+3)
-                    const auto s2 = __builtin_amdgcn_permlane16_swap(__float_as_uint(t),
-                                                                     __float_as_uint(t), false, false);
-                    const float tot = __uint_as_float(s2[0]) + __uint_as_float(s2[1]);
-                    // tot: rows 0,1 = sr total, rows 2,3 = si total
-                    const auto s3 = __builtin_amdgcn_permlane32_swap(__float_as_uint(tot),
-                                                                     __float_as_uint(tot), false, false);
-                    sr = __uint_as_float(s3[0]);  // rows 0,1 of tot -> all rows
-                    si = __uint_as_float(s3[1]);  // rows 2,3 of tot -> all rows
-                }
+                sr += __shfl_xor(sr, 16);
+                si += __shfl_xor(si, 16);
+                sr += __shfl_xor(sr, 32);
+                si += __shfl_xor(si, 32);
                 if (kg == 0 && ri < re) {
                     if (vdirect) {
                         vdirect[rec.idx] =
