@@ -91,24 +91,23 @@ def interleaved_channels(nchan_total, rank, world):
 
 # Cost model of one rank's invert of a contiguous channel block of the C4
 # band (SKA-LOW 512 stations x 400 times, 8192^2 image, 16384^2 grid): a
-# least-squares fit (non-negative) to the per-rank times of the 1-, 2-, 4-
-# and 8-way partitions measured on one MI355X
-# (profiles/r02_c4_scaling_salt4.jsonl, bench.py --config c4 --emulate),
-# within 4 % of every measurement:
+# non-negative least-squares fit to the per-rank stage times of the 8-way
+# partition measured on one MI355X with the round-3 kernels
+# (profiles/r03_c4_chan_8way.jsonl, bench.py --config c4 --emulate r/8;
+# residuals within 4 %):
 #   * bucketing + gridding per channel (52.3 Mvis each), piecewise linear in
-#     frequency -- highest in the compact low band, whose uv core
-#     concentrates the histogram atomics;
-#   * 48.8 ms per batch beyond the first (a block streams in batches of at
-#     most C4_MAX_BATCH channels: plan, bucket histogram, sub-sort items);
-#   * 2.34 ms per resident w plane (zeroing, FFT, w-screen), the plane
-#     count growing with the block's top frequency (w range ~ f_hi);
-#   * 4.2 ms fixed.
-C4_CHAN_COST = ((50e6, 7.49), (110e6, 4.14), (170e6, 4.76), (230e6, 4.19), (290e6, 4.82),
-                (350e6, 4.77))
-C4_BATCH_MS = 48.8
+#     frequency (ms at 50, 110, ..., 350 MHz);
+#   * 1.41 ms per resident w plane (zeroing, FFT, w-screen), the plane count
+#     growing with the block's top frequency (w range ~ f_hi) -- the term that
+#     limits strong scaling: at 8 ranks the planes are held 5x over;
+#   * a batch of the stream costs no measurable extra beyond its channels;
+#   * 2.7 ms fixed (plan, all-reduce excluded).
+C4_CHAN_COST = ((50e6, 5.64), (110e6, 4.94), (170e6, 5.28), (230e6, 5.22), (290e6, 5.14),
+                (350e6, 5.87))
+C4_BATCH_MS = 0.0
 C4_MAX_BATCH = 40
-C4_PLANE_MS = 2.34
-C4_FIXED_MS = 4.2
+C4_PLANE_MS = 1.41
+C4_FIXED_MS = 2.7
 C4_PLANES = (0.179e-6, 8.33)  # nplanes ~ a f_hi + b
 
 
