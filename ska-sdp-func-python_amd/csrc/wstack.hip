@@ -1558,19 +1558,34 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
         // staged (both depend only on the item descriptor)
         uint32_t pf = it.b;
         VisRec nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
+        // the region's W planes: every load of the lane issued before the
+        // first LDS store (one memory round trip per item, not one per 64
+        // cells -- the load / wait / store loop cost ~17 serial round trips)
+        // (three rounds of up to 6 loads per lane: the registers of a single
+        // batch of 17 would cost the kernel a wave per SIMD)
+        constexpr int NSTG = (NQ * PS + 63) / 64, NH = (NSTG + 2) / 3;
         wave_lds_sync();  // previous item's reads of the region
-        for (int i = lane; i < NQ * PS; i += 64) {
-            const int q = i / PS;
-            const int p = (int)it.p0 + q;
-            const int rem = i - q * PS;
-            const int xl = rem / RY, yl = rem - (rem / RY) * RY;
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            tile[i] = (p >= p_lo && p < p_hi)
-                          ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
-                          : make_float2(0.0f, 0.0f);
+#pragma unroll
+        for (int k0 = 0; k0 < NSTG; k0 += NH) {
+            float2 stg[NH];
+#pragma unroll
+            for (int k = 0; k < NH; ++k) {
+                const int i = lane + 64 * (k0 + k);
+                const int q = i / PS;
+                const int p = (int)it.p0 + q;
+                const int rem = i - q * PS;
+                const int xl = rem / RY, yl = rem - (rem / RY) * RY;
+                int gx = ibase + xl;
+                if (gx >= g.ngx) gx -= g.ngx;
+                int gy = jbase + yl;
+                if (gy >= g.ngy) gy -= g.ngy;
+                stg[k] = (k0 + k < NSTG && i < NQ * PS && p >= p_lo && p < p_hi)
+                             ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
+                             : make_float2(0.0f, 0.0f);
+            }
+#pragma unroll
+            for (int k = 0; k < NH; ++k)
+                if (k0 + k < NSTG && lane + 64 * (k0 + k) < NQ * PS) tile[lane + 64 * (k0 + k)] = stg[k];
         }
         wave_lds_sync();
 
