@@ -89,13 +89,14 @@ def parse():
     ap.add_argument("--c4-cpu-chans", type=int, default=2,
                     help="c4: channels in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--c4-traffic", default=os.path.join(ROOT, "profiles", "traffic_c4_k_grid.json"))
-    ap.add_argument("--partition", choices=("chan", "wslab"), default="chan",
-                    help="c4 with N > 1: 'chan' (default) -- cost-balanced contiguous channel "
-                         "blocks, each rank with its own w planes (parallel."
-                         "balanced_channel_blocks); 'wslab' -- every rank scans the band and "
-                         "grids the visibilities of its contiguous slab of the band's w planes "
-                         "(parallel.wslab_partition; measured 2.6x at N = 8 on C4, whose first "
-                         "plane at w ~ 0 holds 38 %% of the visibilities: DESIGN.md §6)")
+    ap.add_argument("--partition", choices=("wrow", "chan", "wslab"), default="wrow",
+                    help="c4 with N > 1: 'wrow' (default) -- ranks own contiguous w intervals "
+                         "of the rows and grid all channels of their rows, each with its own "
+                         "w planes (parallel.wrow_partition); 'chan' -- cost-balanced contiguous "
+                         "channel blocks (parallel.balanced_channel_blocks; the top block holds "
+                         "every plane); 'wslab' -- every rank scans the band and grids its slab "
+                         "of the band's w planes (parallel.wslab_partition; 2.6x at N = 8: the "
+                         "w ~ 0 plane holds 38 %% of the visibilities) -- DESIGN.md §6")
     ap.add_argument("--emulate", default=None, metavar="RANK/WORLD",
                     help="c4 on one GPU: run only rank RANK's block of a WORLD-way partition "
                          "(no collective), to measure per-rank times")
@@ -278,12 +279,28 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
     from ska_sdp_func_python_amd import kernels, parallel, simulation
     freqs = np.linspace(C4_FLO, C4_FHI, C4_NCHAN)
     wslab = args.partition == "wslab" and world > 1  # (N = 1: the whole band, no slab)
-    blocks = [(0, C4_NCHAN)] * world if wslab else parallel.balanced_channel_blocks(freqs, world)
+    wrow = args.partition == "wrow" and world > 1
+    blocks = ([(0, C4_NCHAN)] * world if wslab or wrow
+              else parallel.balanced_channel_blocks(freqs, world))
     lo, hi = blocks[rank]
     obs = simulation.device_observation(C4_NTIMES, 1, C4_FLO, C4_FHI, config="LOW", seed=0,
                                         device=dev, nchan_total=C4_NCHAN, channels=[lo])
     uvw, nrow = obs["uvw"], obs["nrow"]
-    nb = max(1, -(-(hi - lo) // args.c4_batch),
+    row_costs = None
+    if wrow:
+        # the rank's rows: a contiguous interval of the rows' w (the imaging
+        # sign, flip_uw), cut by the cost model over the band's plane spacing
+        cell0 = 0.25 / obs["umax"]
+        lay0 = kernels.wstack_layout(kernels.uvw_bounds(uvw, torch.as_tensor(freqs, device=dev)),
+                                     C4_NPIX, C4_NPIX, cell0, cell0, EPS_REQUESTED, True,
+                                     flip_uw=True)
+        order, cuts, row_costs = parallel.wrow_partition((-uvw[:, 2]).cpu().numpy(), freqs, world,
+                                                         lay0["dw"], lay0["support"])
+        rows = torch.as_tensor(order[cuts[rank]:cuts[rank + 1]], device=dev)
+        uvw = uvw[rows].contiguous()
+        nrow = int(rows.numel())
+        del rows
+    nb = max(1, 0 if wrow else -(-(hi - lo) // args.c4_batch),
              math.ceil(nrow * (hi - lo) / (args.c4_batch_gvis * 1e9)))
     cuts = [lo + (hi - lo) * i // nb for i in range(nb + 1)]
     batches = list(zip(cuts[:-1], cuts[1:]))
@@ -300,7 +317,7 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
         hist = parallel.first_plane_histogram(uvw, freqs, layout)
         slabs = parallel.wslab_partition(hist, world, layout["support"])
         slab = slabs[rank]
-    resident = world >= 4 and not wslab
+    resident = world >= 4 and not wslab  # (wrow: ~14 GB of c64 per rank at N = 8)
     gen = torch.Generator(device=dev)
     steps = args.extra_steps if sub else args.steps
     warmup = min(args.warmup, 1) if sub else args.warmup
@@ -392,6 +409,8 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
     ms_step = elapsed / steps * 1e3
     nvis_total = nrow * C4_NCHAN
     def model_ms(r):
+        if wrow:
+            return round(float(row_costs[r]), 1)
         if wslab:
             a, e = slabs[r]
             return round(parallel.wslab_cost(hist, a, e, layout["support"], float(hist.sum())), 1)
@@ -439,6 +458,7 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
                                "= 13.4 Gvis, 8192^2 image, 16384^2 w-stack grid",
                    "nvis_total": nvis_total, "npix": C4_NPIX, "cell_rad": cell,
                    "partition": args.partition if world > 1 else "none",
+                   "rank0_rows": nrow,
                    "channel_blocks": blocks if not wslab else None, "w_slabs": slabs,
                    "model_ms_per_rank": model,
                    "rank0_batches": len(batches), "inputs_resident": resident,
@@ -446,6 +466,8 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
                    "parallelism": (f"w slabs x{world} (each rank scans the band, grids its "
                                    "slab's first planes), streamed batches, 1 all-reduce"
                                    if wslab else
+                                   f"row w-intervals x{world} (all channels of the rank's rows, "
+                                   "own w planes), streamed batches, 1 all-reduce" if wrow else
                                    f"channel blocks x{world}, streamed batches, 1 all-reduce")},
         "stages_ms_rank0": {k: round(float(sum(i[k] for i in infos)), 3)
                             for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},

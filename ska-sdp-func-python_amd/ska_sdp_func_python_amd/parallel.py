@@ -231,6 +231,87 @@ def wslab_partition(hist, world, W):
     return slabs + [(nps, nps)] * (world - world_eff)
 
 
+# Row partition by w (the default C4 strong-scaling partition): ranks own
+# contiguous intervals of the rows' w (metres) and grid ALL channels of their
+# rows, each with its own w-plane layout.  A row's w_lambda over the band is
+# w f / c, so a rank of small-|w| rows holds few planes and a rank of
+# large-|w| rows holds many but gets fewer rows: the cuts balance the cost
+# below.  Plane work is ~2x the single-GPU planes in total at 8 ranks, not
+# ~5x as with channel blocks (whose top-band block holds every plane), and no
+# rank scans visibilities it does not grid (unlike the w-slab partition).
+WROW_VIS_MS_PER_G = 92.0   # C4 N = 1: (prep 614 + grid 620 ms) / 13.4 Gvis
+WROW_PLANE_MS = 1.41       # per held 16384^2 plane (zeroing, FFT, w-screen)
+WROW_FIXED_MS = 3.0
+
+
+def wrow_planes(wa, wb, f_lo, f_hi, dw, W):
+    """Planes a rank holds whose rows' w (metres, sign applied) span [wa, wb]
+    over frequencies [f_lo, f_hi]: its w_lambda range / dw plus the support."""
+    c = 299792458.0
+    lo = wa * (f_hi if wa < 0 else f_lo) / c
+    hi = wb * (f_hi if wb > 0 else f_lo) / c
+    return (hi - lo) / dw + W
+
+
+def wrow_partition(w, freqs, world, dw, W, vis_ms_per_g=WROW_VIS_MS_PER_G,
+                   plane_ms=WROW_PLANE_MS, fixed_ms=WROW_FIXED_MS):
+    """Contiguous w intervals of the rows for `world` ranks minimising the
+    largest modelled cost (ms): rows x channels x vis cost + held planes x
+    plane cost + fixed (bisection on the target, greedy sweep with a binary
+    search per rank).  ``w``: the rows' w in metres with the imaging sign
+    convention applied (numpy).  Returns (order, cuts, costs): rank r owns
+    rows order[cuts[r]:cuts[r + 1]]."""
+    w = np.asarray(w, dtype=float)
+    order = np.argsort(w, kind="stable")
+    ws = w[order]
+    n = ws.size
+    f = np.asarray(freqs, dtype=float)
+    f_lo, f_hi, nch = float(f.min()), float(f.max()), f.size
+
+    def cost(i, j):
+        if j <= i:
+            return 0.0
+        return (vis_ms_per_g * (j - i) * nch / 1e9 +
+                plane_ms * wrow_planes(ws[i], ws[j - 1], f_lo, f_hi, dw, W) + fixed_ms)
+
+    if world <= 1 or n == 0:
+        return order, [0, n], [cost(0, n)]
+
+    def sweep(target):
+        cuts, i = [0], 0
+        for r in range(world):
+            if i >= n:
+                cuts.append(n)
+                continue
+            if r == world - 1:
+                cuts.append(n)
+                i = n
+                continue
+            a, b = i + 1, n
+            if cost(i, a) > target:
+                return None
+            while a < b:
+                m = (a + b + 1) // 2
+                if cost(i, m) <= target:
+                    a = m
+                else:
+                    b = m - 1
+            cuts.append(a)
+            i = a
+        return cuts if cost(cuts[-2], n) <= target else None
+
+    lo_t, hi_t = 0.0, cost(0, n)
+    best = [0] * world + [n]
+    for _ in range(60):
+        mid = 0.5 * (lo_t + hi_t)
+        c = sweep(mid)
+        if c is not None:
+            hi_t, best = mid, c
+        else:
+            lo_t = mid
+    return order, best, [cost(a, e) for a, e in zip(best[:-1], best[1:])]
+
+
 def invert_batched_shard(uvw, freq, vis_of_block, blocks, npix, cell, epsilon=1e-7,
                          do_wstacking=True, flip_uw=True, out=None, timer=None, bounds=None,
                          slab=None, batch_fn=None):
@@ -330,6 +411,30 @@ def invert_sharded(uvw, freq, vis, wgt, npix, cell, epsilon=1e-7, do_wstacking=T
         else:
             out.zero_()
     return out, sumwt
+
+
+def invert_wrow(uvw, freq, vis, wgt, npix, cell, epsilon=1e-7, do_wstacking=True, flip_uw=True,
+                normalise=True, group=None, grid_fn=None, out=None, layout=None):
+    """Row partition by w (wrow_partition): every rank holds the full [nrow,
+    nchan] arrays (the SPMD form of the API sharding), grids ALL channels of
+    its interval of the rows' w into its own w-plane layout, and one
+    all-reduce of the image and sumwt combines the ranks.  ``layout``
+    (support, dw) defaults to kernels.wstack_layout over the full band.
+    Returns (dirty [y, x], sumwt, (order, cuts))."""
+    from . import kernels
+    rank, world = (dist.get_rank(group), dist.get_world_size(group)) if _dist_on() else (0, 1)
+    if layout is None:
+        b = kernels.uvw_bounds(uvw, freq)
+        layout = kernels.wstack_layout(b, npix, npix, cell, cell, epsilon, do_wstacking,
+                                       flip_uw=flip_uw)
+    w = uvw[:, 2].detach().to("cpu", torch.float64).numpy() * (-1.0 if flip_uw else 1.0)
+    order, cuts, _ = wrow_partition(w, freq.detach().cpu().numpy(), world, layout["dw"],
+                                    layout["support"])
+    rows = torch.as_tensor(order[cuts[rank]:cuts[rank + 1]], device=uvw.device)
+    sub = lambda t: None if t is None else t[rows].contiguous()  # noqa: E731
+    img, sw = invert_sharded(sub(uvw), freq, sub(vis), sub(wgt), npix, cell, epsilon,
+                             do_wstacking, flip_uw, normalise, group, grid_fn, out)
+    return img, sw, (order, cuts)
 
 
 def _dist_on():

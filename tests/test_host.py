@@ -237,3 +237,26 @@ def test_wslab_partition_covers_the_planes_and_balances():
         p0 = np.floor(np.clip((w * f / 299792458.0 + 80.0) / 4.0 - 4.0, -2, 2e9)).astype(int) + 1
         np.add.at(ref, np.clip(p0, 0, 39), 1)
     assert np.array_equal(h, ref)
+
+
+def test_wrow_partition_covers_the_rows_and_balances():
+    """parallel.wrow_partition: rank r owns rows order[cuts[r]:cuts[r+1]], a
+    contiguous interval of w; the intervals cover all rows, the modelled
+    costs are balanced, and the small-|w| ranks hold fewer planes."""
+    import numpy as np
+    from ska_sdp_func_python_amd import parallel
+    rng = np.random.default_rng(3)
+    w = np.concatenate([rng.normal(0, 30.0, 200000), rng.normal(0, 800.0, 40000)])
+    f = np.linspace(50e6, 350e6, 256)
+    for world in (1, 2, 4, 8):
+        order, cuts, costs = parallel.wrow_partition(w, f, world, 1734.0, 8)
+        assert len(cuts) == world + 1 and cuts[0] == 0 and cuts[-1] == w.size
+        assert all(a <= b for a, b in zip(cuts, cuts[1:]))
+        ws = w[order]
+        assert np.all(np.diff(ws) >= 0)
+        if world > 1:
+            assert max(costs) < 1.1 * min(costs) + 2 * parallel.WROW_PLANE_MS
+            pl = [parallel.wrow_planes(ws[a], ws[e - 1], f.min(), f.max(), 1734.0, 8)
+                  for a, e in zip(cuts[:-1], cuts[1:])]
+            mid = world // 2
+            assert pl[mid] <= max(pl[0], pl[-1])
