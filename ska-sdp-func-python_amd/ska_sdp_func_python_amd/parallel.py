@@ -239,8 +239,14 @@ def wslab_partition(hist, world, W):
 # below.  Plane work is ~2x the single-GPU planes in total at 8 ranks, not
 # ~5x as with channel blocks (whose top-band block holds every plane), and no
 # rank scans visibilities it does not grid (unlike the w-slab partition).
-WROW_VIS_MS_PER_G = 92.0   # C4 N = 1: (prep 614 + grid 620 ms) / 13.4 Gvis
-WROW_PLANE_MS = 1.41       # per held 16384^2 plane (zeroing, FFT, w-screen)
+# Per-visibility cost (bucketing + gridding) grows with the row's |w| -- the
+# long baselines fill sparse cells whose regions flush more atomics per
+# record: (65.1 + 53.7 sqrt(|w| / max|w|)) ms per Gvis, a least-squares fit
+# to the 8-way emulation (profiles/r03_c4_wrow_8way.jsonl, rms 6 ms/Gvis);
+# planes 1.49 ms each.
+WROW_VIS_MS_PER_G = 65.1
+WROW_VIS_W_MS_PER_G = 53.7
+WROW_PLANE_MS = 1.49
 WROW_FIXED_MS = 3.0
 
 
@@ -254,11 +260,12 @@ def wrow_planes(wa, wb, f_lo, f_hi, dw, W):
 
 
 def wrow_partition(w, freqs, world, dw, W, vis_ms_per_g=WROW_VIS_MS_PER_G,
-                   plane_ms=WROW_PLANE_MS, fixed_ms=WROW_FIXED_MS):
+                   vis_w_ms_per_g=WROW_VIS_W_MS_PER_G, plane_ms=WROW_PLANE_MS,
+                   fixed_ms=WROW_FIXED_MS):
     """Contiguous w intervals of the rows for `world` ranks minimising the
-    largest modelled cost (ms): rows x channels x vis cost + held planes x
-    plane cost + fixed (bisection on the target, greedy sweep with a binary
-    search per rank).  ``w``: the rows' w in metres with the imaging sign
+    largest modelled cost (ms): the rows' channels x a vis cost rising with
+    sqrt(|w| / max|w|) + held planes x plane cost + fixed (bisection on the
+    target, greedy sweep with a binary search per rank).  ``w``: the rows' w in metres with the imaging sign
     convention applied (numpy).  Returns (order, cuts, costs): rank r owns
     rows order[cuts[r]:cuts[r + 1]]."""
     w = np.asarray(w, dtype=float)
@@ -267,11 +274,15 @@ def wrow_partition(w, freqs, world, dw, W, vis_ms_per_g=WROW_VIS_MS_PER_G,
     n = ws.size
     f = np.asarray(freqs, dtype=float)
     f_lo, f_hi, nch = float(f.min()), float(f.max()), f.size
+    wmax = float(np.max(np.abs(ws))) if n else 1.0
+    # prefix sums of the per-row vis cost (ms)
+    row_ms = (vis_ms_per_g + vis_w_ms_per_g * np.sqrt(np.abs(ws) / max(wmax, 1e-300))) * nch / 1e9
+    pre = np.concatenate([[0.0], np.cumsum(row_ms)])
 
     def cost(i, j):
         if j <= i:
             return 0.0
-        return (vis_ms_per_g * (j - i) * nch / 1e9 +
+        return (pre[j] - pre[i] +
                 plane_ms * wrow_planes(ws[i], ws[j - 1], f_lo, f_hi, dw, W) + fixed_ms)
 
     if world <= 1 or n == 0:

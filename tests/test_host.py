@@ -249,7 +249,9 @@ def test_wrow_partition_covers_the_rows_and_balances():
     w = np.concatenate([rng.normal(0, 30.0, 200000), rng.normal(0, 800.0, 40000)])
     f = np.linspace(50e6, 350e6, 256)
     for world in (1, 2, 4, 8):
-        order, cuts, costs = parallel.wrow_partition(w, f, world, 1734.0, 8)
+        # (vis costs scaled x1000: the 240k rows stand for a C4-sized band)
+        order, cuts, costs = parallel.wrow_partition(w, f, world, 1734.0, 8, vis_ms_per_g=65.1e3,
+                                                     vis_w_ms_per_g=53.7e3)
         assert len(cuts) == world + 1 and cuts[0] == 0 and cuts[-1] == w.size
         assert all(a <= b for a, b in zip(cuts, cuts[1:]))
         ws = w[order]
