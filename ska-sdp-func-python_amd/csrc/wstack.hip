@@ -2843,8 +2843,20 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.grp = g.sub == kTileCell ? kGroupCell : 1;
     g.salt = 1;
     if (g.sub == kTileCoarse) {
-        const int sv = env_int("SDP_HIP_SALT", 4);
-        g.salt = (sv >= 1 && sv <= 64 && (sv & (sv - 1)) == 0) ? sv : 4;
+        // salt: as many counters per bucket as 2^28 counters allow (64 at
+        // most, 4 at least): a call whose visibilities crowd into few first
+        // planes -- a rank of the row-by-w partition holding the dense uv
+        // core -- spreads its hot buckets' serial atomics over 64 counters
+        // (such a 4-way rank: count + scatter 317 -> 208 ms at salt 32); the
+        // full C4 band (63 first planes) keeps 4 (salt 1 / 2 / 4 / 8 / 16
+        // measured within 1 % there, profiles/r03_c4_knobs.txt)
+        const int sv = env_int("SDP_HIP_SALT", 0);
+        if (sv >= 1 && sv <= 64 && (sv & (sv - 1)) == 0) {
+            g.salt = sv;
+        } else {
+            g.salt = 64;
+            while (g.salt > 4 && (double)g.ntiles * g.nps * g.salt > 268435456.0) g.salt >>= 1;
+        }
         while (g.salt > 1 && (double)g.ntiles * g.nps * g.salt >= 1.0e9) g.salt >>= 1;
     }
     SDP_REQUIRE((double)g.ntiles * g.nps * g.salt < 4.0e9, "too many (plane, tile) buckets");
