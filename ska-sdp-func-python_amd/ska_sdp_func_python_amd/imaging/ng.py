@@ -27,8 +27,12 @@ drop-in use: the reference call, unchanged, on each rank), the visibility
 channels are split into contiguous blocks balanced by the measured cost
 model (parallel.balanced_channel_blocks).  invert_ng grids only its block
 and combines the partial images and weight sums with one all-reduce each
-(the reference's only exchange point, before normalise_sumwt); predict_ng
-predicts its block and all-gathers the channel blocks.  Every rank returns
+(the reference's only exchange point, before normalise_sumwt); an MFS invert
+with w-stacking instead splits the ROWS into contiguous intervals of w
+(parallel.wrow_partition: a rank of small-|w| rows holds few w planes, where
+a channel block at the top of a wide band holds them all; SDP_HIP_SHARD=chan
+keeps channel blocks); predict_ng predicts its block and all-gathers the
+channel blocks.  Every rank returns
 the reference's full result.  ``shard=False`` (or SDP_HIP_SHARD=0) computes
 everything on each rank.
 Kwargs ``epsilon`` (default 1e-12), ``do_wstacking`` (True), ``threads``
@@ -56,6 +60,19 @@ def _vis_to_im(model, freq):
 
 def _pixsize(model):
     return float(np.abs(np.radians(model.image_acc.wcs.wcs.cdelt[0])))
+
+
+def _rank_rows(uvw, freq, npix, pixsize, epsilon, precision, shard):
+    """This rank's rows of an MFS w-stacked invert: an interval of the rows'
+    w (RASCIL's sign, u and w negated) cut by parallel.wrow_partition over
+    the band's plane spacing (kernels.wstack_layout)."""
+    b = [float(uvw[:, 2].min()), float(uvw[:, 2].max()), float(uvw[:, 0].abs().max()),
+         float(uvw[:, 1].abs().max()), float(np.min(freq)), float(np.max(freq))]
+    lay = kernels.wstack_layout(b, npix, npix, pixsize, pixsize, epsilon, True, flip_uw=True,
+                                precision=precision)
+    order, cuts, _ = parallel.wrow_partition(-uvw[:, 2].cpu().numpy(), freq, shard[1], lay["dw"],
+                                             lay["support"])
+    return torch.as_tensor(order[cuts[shard[0]]:cuts[shard[0] + 1]], device=uvw.device)
 
 
 def predict_ng(bvis, model, **kwargs):
@@ -166,40 +183,54 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     freq = np.asarray(sbvis.frequency.data, dtype=float)
     nrows, nbaselines, vnchan, vnpol = sbvis.vis.shape
     nrow = nrows * nbaselines
-    # this rank's visibility channels [lo, hi) (all of them unsharded)
+    # this rank's visibility channels [lo, hi) (all of them unsharded), or
+    # for an MFS w-stacked invert its rows (an interval of w, all channels)
     lo, hi = 0, vnchan
-    if shard:
+    mfs = nchan == 1 and vnchan > 1
+    uvw = _device.to_dev(sbvis.uvw.data, torch.float64, dev).reshape(nrow, 3).contiguous()
+    rows = None
+    if shard and mfs and do_wstacking and parallel.shard_mode() != "chan":
+        rows = _rank_rows(uvw, freq, nx, _pixsize(im), epsilon, precision, shard)
+    elif shard:
         lo, hi = parallel.balanced_channel_blocks(freq, shard[1])[shard[0]]
     nloc = hi - lo
+
+    def local(arr, dtype=None):
+        # the rank's slice: rows gathered on the host before the copy when
+        # the Visibility is host-resident (only 1/N of it crosses PCIe)
+        a = arr[:, :, lo:hi]
+        if rows is None:
+            return _device.to_dev(a, dtype, dev).reshape(nrow, nloc, vnpol)
+        a = a.reshape((nrow,) + tuple(a.shape[2:]))
+        if isinstance(a, np.ndarray):
+            return _device.to_dev(a[rows.cpu().numpy()], dtype, dev)
+        return _device.to_dev(a, dtype, dev)[rows]
 
     # The Visibility's own arrays, read in place by the fused prologue of
     # sdp_hip_ms2dirty_vis: flag masking (ng.py:191, :202), the pol-frame
     # conversion (ng.py:193-198) as one matrix row per image pol, f64 weights
     # and the weight sums (ng.py:258, :289) -- no O(Nvis) passes here.
-    flags = _device.to_dev(sbvis.flags.data[:, :, lo:hi], None, dev)
+    flags = local(sbvis.flags.data)
     if flags.dtype not in kernels._FLAG_DT:
         flags = flags.to(torch.int64)
-    flags = flags.reshape(nrow, nloc, vnpol)
-    wgt = _device.to_dev(sbvis.imaging_weight.data[:, :, lo:hi], None, dev)
+    wgt = local(sbvis.imaging_weight.data)
     if wgt.dtype not in (torch.float32, torch.float64):
         wgt = wgt.to(torch.float64)
-    wgt = wgt.reshape(nrow, nloc, vnpol)
     ms = None
     if not dopsf:
-        ms = _device.to_dev(sbvis.vis.data[:, :, lo:hi], None, dev)
+        ms = local(sbvis.vis.data)
         if ms.dtype not in (torch.complex64, torch.complex128):
             ms = ms.to(torch.complex128)
-        ms = ms.reshape(nrow, nloc, vnpol)
     conv = pol_conversion_matrix(bvis.visibility_acc.polarisation_frame,
                                  im.image_acc.polarisation_frame)
-    uvw = _device.to_dev(sbvis.uvw.data, torch.float64, dev).reshape(nrow, 3).contiguous()
+    if rows is not None:
+        uvw = uvw[rows].contiguous()
     freq_t = _device.to_dev(freq[lo:hi], torch.float64, dev)
 
     npixdirty = nx
     pixsize = _pixsize(im)
     sumwt_d = torch.zeros((nchan, npol), dtype=torch.float64, device=dev)
     vis_to_im = _vis_to_im(model, freq)
-    mfs = nchan == 1 and vnchan > 1
 
     # the image pols of one channel range share one bucketing: the first pol
     # keeps it, the others only re-run the value pass (SDP_HIP_REUSE_BUCKETS)

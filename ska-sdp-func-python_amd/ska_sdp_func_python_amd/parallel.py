@@ -15,6 +15,14 @@ import torch
 import torch.distributed as dist
 
 
+def shard_mode():
+    """SDP_HIP_SHARD: "0" off, "chan" channel blocks everywhere, else (the
+    default) rows by w for MFS w-stacked inverts and channel blocks for the
+    rest."""
+    import os
+    return os.environ.get("SDP_HIP_SHARD", "1")
+
+
 def shard_info(kwargs=None):
     """(rank, world, group) when the reference-shaped API (invert_ng,
     predict_ng, solve_gaintable) should shard its work across the ranks of

@@ -1,8 +1,9 @@
 """CPU, world_size 2 over gloo: the reference-shaped API itself -- invert_ng
 and predict_ng -- sharding a replicated Visibility across ranks when
-torch.distributed is initialised (imaging/ng.py: channel blocks from
-parallel.balanced_channel_blocks, one all-reduce of image + sumwt for
-invert, an all-gather of the channel blocks for predict).  Every rank must
+torch.distributed is initialised (imaging/ng.py: rows split into intervals
+of w for an MFS invert, channel blocks from parallel.balanced_channel_blocks
+otherwise; one all-reduce of image + sumwt for invert, an all-gather of the
+channel blocks for predict).  Every rank must
 return the unsharded result.
 
 There is no GPU here, so inside the test processes the two HIP entry points
@@ -24,6 +25,7 @@ import nufft_oracle as orc
 
 FLIP = np.array([-1.0, 1.0, -1.0])
 SEEN = set()  # visibility channels (frequencies) this process computed
+ROWS = set()  # rows (their u) this process gridded
 
 
 def _oracle_ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, px, py,
@@ -32,6 +34,7 @@ def _oracle_ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, 
                          keep_buckets=False, reuse_buckets=False, precision=None):
     assert shift_lmn is None
     SEEN.update(freq.numpy().tolist())
+    ROWS.update(np.round(uvw.numpy()[:, 0], 6).tolist())
     m = 1.0 - flags.numpy().astype(float)
     w = wgt.numpy() * m[..., pol]
     if vis is None:
@@ -111,7 +114,7 @@ def _worker(rank, world, port, kind, q):
     _patch()
     try:
         out = _run(kind)
-        q.put((rank, out, sorted(SEEN)))
+        q.put((rank, out, sorted(SEEN), sorted(ROWS)))
     finally:
         dist.destroy_process_group()
 
@@ -133,9 +136,14 @@ def test_reference_api_shards_across_ranks(kind, monkeypatch):
     for p in procs:
         p.join(timeout=60)
     assert len(res) == 2
-    # the ranks computed disjoint channel blocks that cover the band
-    seen = [set(s) for _, _, s in res]
-    assert seen[0] and seen[1] and not (seen[0] & seen[1]) and len(seen[0] | seen[1]) == 5
-    for _, out, _ in res:
+    if kind == "invert_mfs":
+        # an MFS w-stacked invert splits the rows (intervals of w, all channels)
+        rows = [set(r) for _, _, _, r in res]
+        assert rows[0] and rows[1] and not (rows[0] & rows[1]) and len(rows[0] | rows[1]) == 36
+    else:
+        # the ranks computed disjoint channel blocks that cover the band
+        seen = [set(s) for _, _, s, _ in res]
+        assert seen[0] and seen[1] and not (seen[0] & seen[1]) and len(seen[0] | seen[1]) == 5
+    for _, out, _, _ in res:
         for a, b in zip(out, ref):
             np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)

@@ -143,8 +143,9 @@ def copy_vis(v):
 
 def test_api_sharding_two_ranks_one_gpu():
     """invert_ng / predict_ng / solve_gaintable with torch.distributed
-    initialised (2 ranks, gloo, one GPU): the sharded call (channel blocks +
-    all-reduce / all-gather; gain-row blocks + all-gather + whole-table
+    initialised (2 ranks, gloo, one GPU): the sharded call (rows split by w
+    for an MFS invert, channel blocks otherwise, + all-reduce / all-gather;
+    gain-row blocks + all-gather + whole-table
     normalisation) equals the unsharded one on every rank.  Tolerance 1e-5
     relative RMS for the NUFFT (each rank's w-plane layout follows its own
     channels), 1e-12 for sumwt and 1e-9 for the gains (same solves)."""
