@@ -70,6 +70,13 @@ extern "C" {
  * layout sum to the full image (multi-GPU w-slab partition).
  * fp32 NUFFT (epsilon >= 1e-7 or SDP_HIP_FP32) with w-stacking only. */
 #define SDP_HIP_W_SLAB 128u
+/* sdp_hip_ms2dirty / _vis / sdp_hip_dirty2ms / _vis: use the second set of
+ * scratch buffers (planes, records, histograms, FFT plans, auxiliary stream).
+ * A caller that alternates it between two streams can have two calls in
+ * flight at once -- the next call's bucketing runs while the previous one
+ * grids and transforms.  Not with KEEP/REUSE_BUCKETS, the batch flags or
+ * W_SLAB. */
+#define SDP_HIP_SLOT1 256u
 
 /* Diagnostics filled by the NUFFT entry points (may be NULL). */
 typedef struct sdp_hip_wgrid_info {

@@ -162,9 +162,18 @@ class Workspace {
     std::map<std::pair<int, std::string>, Buf> bufs_;
 };
 
+// Workspace slot of the calling NUFFT (0, or 1 under SDP_HIP_SLOT1): a second
+// set of every named buffer, so that two inverts issued on two streams can
+// run overlapped without sharing scratch memory.
+inline int &ws_slot() {
+    static thread_local int s = 0;
+    return s;
+}
+inline std::string ws_name(const std::string &name) { return ws_slot() ? name + "#1" : name; }
+
 template <class T>
 T *scratch(const std::string &name, size_t count) {
-    return static_cast<T *>(Workspace::get().buffer(name, count * sizeof(T)));
+    return static_cast<T *>(Workspace::get().buffer(ws_name(name), count * sizeof(T)));
 }
 
 inline hipStream_t as_stream(void *s) { return static_cast<hipStream_t>(s); }

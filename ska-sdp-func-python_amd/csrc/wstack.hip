@@ -2347,11 +2347,12 @@ static const double *phi_table(int W, double beta, hipStream_t stream) {
 static hipfftHandle fft_plan_1d(int n, int stride, int dist, int batch, hipStream_t stream,
                                bool f64 = false) {
     static std::mutex mu;
-    static std::map<std::tuple<int, int, int, int, int, int>, hipfftHandle> plans;
+    static std::map<std::tuple<int, int, int, int, int, int, int>, hipfftHandle> plans;
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_tuple(dev, n, stride, dist, batch, f64 ? 1 : 0);
+    // (one plan per workspace slot: a plan's stream and work area are its own)
+    const auto key = std::make_tuple(dev, n, stride, dist, batch, f64 ? 1 : 0, ws_slot());
     auto itp = plans.find(key);
     hipfftHandle h;
     if (itp == plans.end()) {
@@ -2511,9 +2512,11 @@ static size_t grid_budget_bytes(size_t need_other) {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)8 << 30;
     Workspace &ws = Workspace::get();
-    const size_t held_planes = ws.held("grid") + ws.held("spec") + ws.held("spec_in");
-    const size_t held_other = ws.held("recs") + ws.held("key_rank") + ws.held("degrid_acc") +
-                              ws.held("recs_pad") + ws.held("rec_cls");
+    const size_t held_planes =
+        ws.held(ws_name("grid")) + ws.held(ws_name("spec")) + ws.held(ws_name("spec_in"));
+    const size_t held_other = ws.held(ws_name("recs")) + ws.held(ws_name("key_rank")) +
+                              ws.held(ws_name("degrid_acc")) + ws.held(ws_name("recs_pad")) +
+                              ws.held(ws_name("rec_cls"));
     const size_t avail = free_b + held_planes + held_other;
     const size_t reserve = std::max<size_t>((size_t)6 << 30, total_b / 16);
     const size_t need = need_other + reserve;
@@ -2525,6 +2528,7 @@ static hipStream_t aux_stream() {
     static std::map<int, hipStream_t> streams;
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
+    dev = 2 * dev + ws_slot();  // one per workspace slot
     std::lock_guard<std::mutex> lk(mu);
     auto it = streams.find(dev);
     if (it != streams.end()) return it->second;
@@ -2553,7 +2557,7 @@ static float2 *band_input(const Plan &P, hipStream_t st) {
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(mu);
-    BandState &b = states[dev];
+    BandState &b = states[2 * dev + ws_slot()];
     if (b.ptr != buf || b.elems < elems || b.lo != P.row_lo || b.hi != P.row_hi || b.ny != g.ny ||
         b.ngx != g.ngx) {
         SDP_HIP_CHECK(hipMemsetAsync(buf, 0, elems * sizeof(float2), st));
@@ -2651,7 +2655,7 @@ static Plan reuse_buckets(const Inputs &in) {
 static BatchSeq batch_token(const Plan &P, const Inputs &in) {
     BatchSeq s;
     s.valid = true;
-    s.epoch = Workspace::get().epoch("grid");
+    s.epoch = Workspace::get().epoch(ws_name("grid"));
     s.grid = P.grid;
     s.nx = in.nx;
     s.ny = in.ny;
@@ -2894,18 +2898,18 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // buffers of the other kind of plan are freed, not left cached: the plane
     // budget below counts the held record buffers as reusable
     if (!P.subpad) {
-        Workspace::get().drop("recs_pad");
-        Workspace::get().drop("rec_cls");
+        Workspace::get().drop(ws_name("recs_pad"));
+        Workspace::get().drop(ws_name("rec_cls"));
     }
-    if (grid_mode) Workspace::get().drop("degrid_acc");
+    if (grid_mode) Workspace::get().drop(ws_name("degrid_acc"));
     {
         // a record buffer held much larger than this plan needs (a predict's
         // 32-B records before a large-grid invert's 16-B ones) is freed too:
         // kept, its surplus would be counted as free but stay allocated
         const size_t want = (size_t)std::max<int64_t>(nvis, 1) *
                             (P.f64 ? sizeof(VisRec64) : P.subpad ? sizeof(RecC) : sizeof(VisRec));
-        if (Workspace::get().held("recs") > want + want / 4 + ((size_t)256 << 20))
-            Workspace::get().drop("recs");
+        if (Workspace::get().held(ws_name("recs")) > want + want / 4 + ((size_t)256 << 20))
+            Workspace::get().drop(ws_name("recs"));
     }
     const size_t need_other =
         (size_t)((double)nvis * (rec_bytes + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2)))) +
@@ -3440,11 +3444,26 @@ static int weight_is_f64(int wgt_dtype) {
     return wgt_dtype == SDP_HIP_F64 ? 1 : 0;
 }
 
+// The call's workspace slot (SDP_HIP_SLOT1), reset on every exit.
+struct SlotGuard {
+    explicit SlotGuard(unsigned flags) {
+        const bool one = flags & SDP_HIP_SLOT1;
+        SDP_REQUIRE(!one || !(flags & (SDP_HIP_KEEP_BUCKETS | SDP_HIP_REUSE_BUCKETS |
+                                       SDP_HIP_BATCH_FIRST | SDP_HIP_BATCH_LAST |
+                                       SDP_HIP_W_SLAB)),
+                    "SDP_HIP_SLOT1 cannot be combined with kept / reused buckets, batches or "
+                    "w slabs");
+        ws_slot() = one ? 1 : 0;
+    }
+    ~SlotGuard() { ws_slot() = 0; }
+};
+
 static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
                      sdp_hip_wgrid_info *info, hipStream_t st) {
     SDP_REQUIRE(in.vis == nullptr || in.vis_dtype == SDP_HIP_C64 ||
                     in.vis_dtype == SDP_HIP_C128,
                 "vis must be complex64 or complex128");
+    SlotGuard slot(in.flags);
     StageTimer tm(st);
     tm.mark();
     const bool keep = in.flags & SDP_HIP_KEEP_BUCKETS, reuse = in.flags & SDP_HIP_REUSE_BUCKETS;
@@ -3550,6 +3569,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
                      sdp_hip_wgrid_info *info, hipStream_t st, const OutConv &oc = OutConv{}) {
     SDP_REQUIRE(in.vis_dtype == SDP_HIP_C64 || in.vis_dtype == SDP_HIP_C128,
                 "vis must be complex64 or complex128");
+    SlotGuard slot(in.flags);
     StageTimer tm(st);
     tm.mark();
     Plan P = plan_geometry(in, false, st);

@@ -33,6 +33,7 @@ SDP_HIP_KEEP_BUCKETS = 16
 SDP_HIP_REUSE_BUCKETS = 32
 SDP_HIP_FP32 = 64
 SDP_HIP_W_SLAB = 128
+SDP_HIP_SLOT1 = 256
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int

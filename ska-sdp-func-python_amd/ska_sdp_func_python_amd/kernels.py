@@ -114,13 +114,15 @@ def _check_uvw(uvw):
 
 def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
              epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
-             out_strides=None, accumulate=False, precision=None):
+             out_strides=None, accumulate=False, precision=None, slot=0):
     """ducc0.wgridder.ms2dirty semantics on device.
 
     uvw [nrow,3] f64, freq [nchan] f64, vis [nrow,nchan] c64/c128 (or None
     for unit visibilities), wgt [nrow,nchan] f32 (or None).  Returns the
     f64 dirty image [npix_x, npix_y] (or writes ``out`` with
     ``out_strides`` = (stride_x, stride_y) in elements) and an info dict.
+    ``slot=1`` uses the library's second scratch set (SDP_HIP_SLOT1): calls
+    alternated between two streams and slots overlap on the device.
     """
     pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
@@ -141,7 +143,7 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y,
     if out.dtype != torch.float64:
         raise ValueError("dirty output must be float64")
     flags = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
-             | pbits)
+             | (_lib.SDP_HIP_SLOT1 if slot else 0) | pbits)
     info = _lib.WGridInfo()
     _lib.call(
         "sdp_hip_ms2dirty",

@@ -424,11 +424,9 @@ def invert_sharded(uvw, freq, vis, wgt, npix, cell, epsilon=1e-7, do_wstacking=T
         dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
         dist.all_reduce(sumwt, op=dist.ReduceOp.SUM, group=group)
     if normalise:
-        s = float(sumwt.item())
-        if s > 0:
-            out /= s
-        else:
-            out.zero_()
+        # on the device (no host sync, so calls on two streams can overlap):
+        # image / sumwt, or zeros when sumwt is 0 (normalise_sumwt)
+        out.mul_(torch.where(sumwt > 0, 1.0 / sumwt, torch.zeros_like(sumwt)))
     return out, sumwt
 
 

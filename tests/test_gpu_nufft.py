@@ -785,3 +785,43 @@ def test_row_partition_by_w_sums_to_the_full_invert():
     assert rel_rms(total.cpu().numpy(), full.cpu().numpy()) < 1e-6
     exact = orc.ms2dirty_exact(uvw * FLIP_UW, freq, ms, wgt, 256, 256, cell, cell, True)
     assert rel_rms(total.cpu().numpy(), exact) < TOL
+
+
+def test_two_slots_on_two_streams_overlap_correctly():
+    """SDP_HIP_SLOT1: inverts alternated between two streams and the library's
+    two scratch slots (the pipelined bench) -- different problems in flight at
+    once -- each equal to its own single call; slot 1 refuses batches."""
+    from ska_sdp_func_python_amd import kernels
+    probs = [_problem(30 + k, nrow=3000, nchan=4, umax=5000.0) for k in range(2)]
+    dev = torch.device("cuda:0")
+    refs = []
+    for uvw, freq, ms, wgt, cell in probs:
+        r, _ = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), 256, 256, cell, cell, 1e-7, True)
+        refs.append(r.cpu().numpy())
+    streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+    args = [(T(uvw), T(freq), T(ms), T(wgt), cell) for uvw, freq, ms, wgt, cell in probs]
+    torch.cuda.synchronize()
+    outs = [[], []]
+    for rep in range(3):
+        for j in (0, 1):
+            U, F, M, Wt, cell = args[j]
+            with torch.cuda.stream(streams[j]):
+                o, _ = kernels.ms2dirty(U, F, M, Wt, 256, 256, cell, cell, 1e-7, True, slot=j)
+            outs[j].append(o)
+    torch.cuda.synchronize()
+    for j in (0, 1):
+        for o in outs[j]:
+            assert rel_rms(o.cpu().numpy(), refs[j]) < 1e-6
+    U, F, M, Wt, cell = args[0]
+    b = kernels.uvw_bounds(U, F)
+    import ctypes
+    with pytest.raises(ValueError, match="SLOT1"):
+        bbuf = (ctypes.c_double * 6)(*b)
+        info = kernels._lib.WGridInfo()
+        kernels._lib.call("sdp_hip_ms2dirty_batch", kernels._ptr(U), U.stride(0), kernels._ptr(F),
+                          F.shape[0], U.shape[0], kernels._ptr(M), kernels._lib.SDP_HIP_C64,
+                          M.stride(0), M.stride(1), None, kernels._lib.SDP_HIP_F32, 0, 0, 256, 256,
+                          cell, cell, 1e-7, 1,
+                          kernels._lib.SDP_HIP_SLOT1 | kernels._lib.SDP_HIP_BATCH_FIRST,
+                          ctypes.cast(bbuf, ctypes.c_void_p), None, 0, 0,
+                          kernels._stream(dev), ctypes.byref(info))
