@@ -36,6 +36,7 @@
 #include <cstdlib>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -1331,12 +1332,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         int ibase, jbase;
         group_origin(g, (int)it.tile, ibase, jbase);
         const uint32_t p0 = it.p0;
+        // the first group's first 64 records are requested before the region
+        // is zeroed (the load's latency under the LDS stores)
+        RecC nx;
+        if (it.b < it.e) nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
 
         wave_lds_sync();  // the previous item's flush reads of the region
         {
+            constexpr int kZ = kRegX * kRegY * kRegCell / 4;  // float4s
             float4 *r4 = reinterpret_cast<float4 *>(reg);
-            for (int i = lane; i < kRegX * kRegY * kRegCell / 4; i += 64)
-                r4[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+            for (int i = 0; i < kZ / 64; ++i) r4[lane + 64 * i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (kZ % 64 && lane < kZ % 64)
+                r4[lane + 64 * (kZ / 64)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
 
         // the accumulators and their base offset (floats) in the region: they
@@ -1394,7 +1402,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
                     acc[t] = *reinterpret_cast<const floatx4 *>(reg + cbase + t * acc_t);
             };
 
-            RecC nx = recs[min(rb + (uint32_t)lane, re - 1)];
+            if (gi > 0) nx = recs[min(rb + (uint32_t)lane, re - 1)];  // (group 0: above)
             for (uint32_t b0 = rb; b0 < re; b0 += 64) {
                 const RecC my = nx;
                 if (b0 + 64 < re) nx = recs[min(b0 + 64 + (uint32_t)lane, re - 1)];
@@ -1525,14 +1533,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 // One wave per work item (a chunk of a group of 16 cells, a 2 x 8-cell
 // region whose W planes are staged in LDS once).  The record factor
 // wgt * exp(-2 pi i w s0) is applied and the visibility written in place
-// (vdirect), or the raw sum added to acc[record] for k_finalize.
-template <int W, bool WS>
+// (VD: out = the visibilities), or the raw sum added to out[record] for
+// k_finalize.  Every lane stores, without a branch: lanes past the batch's
+// records write to a per-block slot of `sink` (a skipped store left the
+// loop-top wait for the prefetched records at vmcnt(0), i.e. behind the
+// previous batch's store), and the 4 lanes of a record write the same value.
+constexpr int kDegridSinkBlocks = 4096;  // sink slots (x 64 lanes)
+template <int W, bool WS, bool VD>
 __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restrict__ recs,
                                                     uint32_t n_items,
                                                     const FineItem *__restrict__ fitems,
                                                     const float2 *__restrict__ grid, int p_lo,
-                                                    int p_hi, float2 *__restrict__ acc,
-                                                    float2 *__restrict__ vdirect) {
+                                                    int p_hi, float2 *__restrict__ out,
+                                                    float2 *__restrict__ sink) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
@@ -1607,11 +1620,18 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                            : 0.0f;
             }
             for (uint32_t b0 = rb; b0 < re; b0 += 16) {
+                // pf == b0 always: a cell's batches end at its last record and
+                // the next non-empty cell starts there (an empty cell has
+                // b == e), so the prefetched batch is this one (a reload path
+                // here left the loop's record wait at vmcnt(0))
                 const uint32_t ri = b0 + (uint32_t)r16;
-                if (pf != b0) nxt = recs[min(ri, it.e - 1)];  // (wave-uniform; not expected)
                 const VisRec rec = nxt;
                 pf = min(b0 + 16, re);
                 nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
+                // the next batch's loads issue here, a whole batch before the
+                // loop-carried copy that waits for them (scheduled freely they
+                // sank under the MFMAs, ~50 instructions from that wait)
+                __builtin_amdgcn_sched_barrier(0);
                 const float u0 = es_tap<W>(rec.fu, tu0, ihw, bl);
                 const float u1 = es_tap<W>(rec.fu, tu1, ihw, bl);
                 const float v0 = es_tap<W>(rec.fv, tv0, ihw, bl);
@@ -1637,17 +1657,16 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                 si += __shfl_xor(si, 16);
                 sr += __shfl_xor(sr, 32);
                 si += __shfl_xor(si, 32);
-                if (kg == 0 && ri < re) {
-                    if (vdirect) {
-                        vdirect[rec.idx] =
-                            make_float2(rec.cre * sr - rec.cim * si, rec.cre * si + rec.cim * sr);
-                    } else {
-                        float2 *dst = acc + ri;
-                        float2 v = *dst;
-                        v.x += sr;
-                        v.y += si;
-                        *dst = v;
-                    }
+                float2 *const dump = sink + (blockIdx.x & (kDegridSinkBlocks - 1)) * 64 + lane;
+                if constexpr (VD) {
+                    float2 *const dst = ri < re ? out + rec.idx : dump;
+                    *dst = make_float2(rec.cre * sr - rec.cim * si, rec.cre * si + rec.cim * sr);
+                } else {
+                    float2 *const dst = ri < re ? out + ri : dump;
+                    float2 v = *dst;
+                    v.x += sr;
+                    v.y += si;
+                    *dst = v;
                 }
             }
         }
@@ -3230,6 +3249,20 @@ static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
     return launch_grid_mfma_fi<W, false>(P, p_lo, p_hi, st);
 }
 
+// the degridder's store sink (kDegridSinkBlocks x 64 float2 per device,
+// allocated once, never read)
+static float2 *degrid_sink() {
+    static float2 *sinks[64] = {};
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    SDP_REQUIRE(dev >= 0 && dev < 64, "device index out of range");
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!sinks[dev])
+        SDP_HIP_CHECK(hipMalloc(&sinks[dev], (size_t)kDegridSinkBlocks * 64 * sizeof(float2)));
+    return sinks[dev];
+}
+
 template <int W, bool WS>
 static void launch_degrid_mfma(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
     const size_t lds = (size_t)(WS ? W : 1) * (2 + W - 1) * (8 + W - 1) * sizeof(float2);
@@ -3238,8 +3271,13 @@ static void launch_degrid_mfma(const Plan &P, int p_lo, int p_hi, float2 *acc, h
     const unsigned per = P.subsort ? 16u : 1u;
     const unsigned n = per * (r.second - r.first);
     if (n == 0) return;
-    k_degrid_mfma<W, WS><<<n, 64, lds, st>>>(P.g, P.recs, n, P.pt.fitems + per * (size_t)r.first,
-                                             P.grid, p_lo, p_hi, acc, P.vdirect);
+    float2 *const sink = degrid_sink();
+    if (P.vdirect)
+        k_degrid_mfma<W, WS, true><<<n, 64, lds, st>>>(
+            P.g, P.recs, n, P.pt.fitems + per * (size_t)r.first, P.grid, p_lo, p_hi, P.vdirect, sink);
+    else
+        k_degrid_mfma<W, WS, false><<<n, 64, lds, st>>>(
+            P.g, P.recs, n, P.pt.fitems + per * (size_t)r.first, P.grid, p_lo, p_hi, acc, sink);
 }
 
 template <int W>
