@@ -1254,6 +1254,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 // 88 % of the LDS cycles in conflicts, profiles/r02_k_grid_mfma_pad_pmc.json).
 // The block's (up to) 4 K-steps are unrolled with compile-time LDS offsets.
 // The region tile is flushed once per item with buffer float atomics.
+// buffer offset past any plane (planes are < 2^32 - 16 bytes): an atomic
+// issued there is dropped by the buffer range check
+constexpr int kDropOff = -16;
 constexpr int kTapRec = 24;    // floats per record row of the tap block
 constexpr int kTapBatch = 16;  // records per tap block
 constexpr int kRegCell = 16;  // floats per region cell: 8 planes x re/im
@@ -1486,9 +1489,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         // 2 (q & 1) + (f & 1); the NQ planes' values are read before any
         // atomic is issued (one LDS wait per 64 floats, not one per plane);
         // buffer atomics off a per-plane descriptor (32-bit offsets); zero
-        // floats are skipped
+        // floats are dropped by the range check
         constexpr int FPP = RX * RY * 2;
         const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
+        // one buffer descriptor per plane (scalar registers); a plane outside
+        // [p_lo, p_hi) gets an empty range, and a zero float an offset past
+        // the plane, so the buffer range check drops those atomics: no branch
+        __amdgpu_buffer_rsrc_t prs[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int p = (int)p0 + q;
+            const bool in = p >= p_lo && p < p_hi;
+            prs[q] = __builtin_amdgcn_make_buffer_rsrc(
+                in ? grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)) : grid, 0,
+                in ? (int)plane_bytes : 0, 0x00020000);
+        }
 #pragma unroll
         for (int i0 = 0; i0 < FPP; i0 += 64) {
             const int f = i0 + lane;
@@ -1504,16 +1519,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 #pragma unroll
             for (int q = 0; q < NQ; ++q) vals[q] = src[4 * reg_chunk(q >> 1, yl) + 2 * (q & 1)];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int p = (int)p0 + q;
-                const float val = vals[q];
-                if (p >= p_lo && p < p_hi && val != 0.0f) {
-                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                        grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)), 0,
-                        (int)plane_bytes, 0x00020000);
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, rs, voff, 0, 0);
-                }
-            }
+            for (int q = 0; q < NQ; ++q)
+                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+                    vals[q], prs[q], vals[q] != 0.0f ? voff : kDropOff, 0, 0);
         }
     }
 }
