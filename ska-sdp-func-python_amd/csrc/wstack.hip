@@ -1642,22 +1642,29 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                 __builtin_amdgcn_sched_barrier(0);
                 const float u0 = es_tap<W>(rec.fu, tu0, ihw, bl);
                 const float u1 = es_tap<W>(rec.fu, tu1, ihw, bl);
-                const float v0 = es_tap<W>(rec.fv, tv0, ihw, bl);
-                const float v1 = es_tap<W>(rec.fv, tv1, ihw, bl);
-                const float w0 = WS ? es_tap<W>(rec.fw, tu0, ihw, bl) : (kg == 0 ? 1.0f : 0.0f);
-                const float w1 = WS ? es_tap<W>(rec.fw, tu1, ihw, bl) : 0.0f;
                 float tu[8];
 #pragma unroll
                 for (int h = 0; h < 4; ++h) {
                     tu[2 * h] = __shfl(u0, r16 + 16 * h);
                     tu[2 * h + 1] = __shfl(u1, r16 + 16 * h);
                 }
+                // all 8 tap broadcasts in flight before the v / w taps are
+                // evaluated under them (interleaved with the MFMAs each
+                // waited for its own round trip)
+                __builtin_amdgcn_sched_barrier(0);
+                const float v0 = es_tap<W>(rec.fv, tv0, ihw, bl);
+                const float v1 = es_tap<W>(rec.fv, tv1, ihw, bl);
+                const float w0 = WS ? es_tap<W>(rec.fw, tu0, ihw, bl) : (kg == 0 ? 1.0f : 0.0f);
+                const float w1 = WS ? es_tap<W>(rec.fw, tu1, ihw, bl) : 0.0f;
                 floatx4 d0 = floatx4{0.0f, 0.0f, 0.0f, 0.0f}, d1 = d0;
 #pragma unroll
                 for (int s = 0; s < 16; s += 2) {
                     d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], tu[s >> 1] * v0, d0, 0, 0, 0);
                     d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s + 1], tu[s >> 1] * v1, d1, 0, 0, 0);
                 }
+                // (the loop-carried copy of the prefetched records, and its
+                // wait, stay below the MFMAs)
+                __builtin_amdgcn_sched_barrier(0);
                 // row 4 kg + i of D = (q = 2 kg + (i >> 1), re/im = i & 1)
                 float sr = w0 * (d0[0] + d1[0]) + w1 * (d0[2] + d1[2]);
                 float si = w0 * (d0[1] + d1[1]) + w1 * (d0[3] + d1[3]);
