@@ -92,8 +92,12 @@ def parse():
     ap.add_argument("--c4-cpu-chans", type=int, default=2,
                     help="c4: channels in the cpu_baseline sample (0 = skip)")
     ap.add_argument("--c4-traffic", default=os.path.join(ROOT, "profiles", "traffic_c4_k_grid.json"))
-    ap.add_argument("--partition", choices=("wrow", "chan", "wslab"), default="wrow",
-                    help="c4 with N > 1: 'wrow' (default) -- ranks own contiguous w intervals "
+    ap.add_argument("--partition", choices=("auto", "wrow", "chan", "wslab"), default="auto",
+                    help="c4 with N > 1: 'auto' (default) -- 'chan' at N = 2, 'wrow' at N >= 4 "
+                         "(the faster of the two per world size on the one-GPU emulation: "
+                         "2-way chan 1.89x vs wrow 1.78x, 4-way wrow 3.71x vs chan 3.35x, "
+                         "8-way wrow 7.53x vs chan 5.36x; profiles/r03_c4_chan_24way.jsonl, "
+                         "r03_c4_wrow_scaling_final_summary.txt); 'wrow' -- ranks own contiguous w intervals "
                          "of the rows and grid all channels of their rows, each with its own "
                          "w planes (parallel.wrow_partition); 'chan' -- cost-balanced contiguous "
                          "channel blocks (parallel.balanced_channel_blocks; the top block holds "
@@ -281,6 +285,8 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
     `sub` returns the line as a dict (the default bench's "c4_n1" object)."""
     from ska_sdp_func_python_amd import kernels, parallel, simulation
     freqs = np.linspace(C4_FLO, C4_FHI, C4_NCHAN)
+    if args.partition == "auto":
+        args.partition = "chan" if world <= 2 else "wrow"
     wslab = args.partition == "wslab" and world > 1  # (N = 1: the whole band, no slab)
     wrow = args.partition == "wrow" and world > 1
     blocks = ([(0, C4_NCHAN)] * world if wslab or wrow
