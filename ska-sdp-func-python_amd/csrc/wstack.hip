@@ -2436,7 +2436,7 @@ static T *pinned_host(size_t off, size_t count) {
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(mu);
-    char *&b = bufs[dev];
+    char *&b = bufs[2 * dev + ws_slot()];  // one per workspace slot
     if (!b) SDP_HIP_CHECK(hipHostMalloc((void **)&b, kBytes, hipHostMallocDefault));
     return reinterpret_cast<T *>(b + off);
 }
@@ -2577,7 +2577,7 @@ static hipStream_t aux_stream() {
 // so the zeros are kept across calls: the buffer is cleared only when it is
 // (re)allocated or the band / shape changes.
 struct BandState {
-    float2 *ptr = nullptr;
+    uint64_t epoch = 0;  // the allocation (Workspace epoch) the zeros were written to
     size_t elems = 0;
     int lo = -1, hi = -1, ny = 0, ngx = 0;
 };
@@ -2588,14 +2588,17 @@ static float2 *band_input(const Plan &P, hipStream_t st) {
     const Geo &g = P.g;
     const size_t elems = (size_t)P.fft_planes * g.ny * g.ngx * (cbytes(P) / sizeof(float2));
     float2 *buf = scratch<float2>("spec_in", elems);
+    // the buffer's allocation identity, not its address: a release and a
+    // new allocation at the same address leaves unzeroed memory behind
+    const uint64_t ep = Workspace::get().epoch(ws_name("spec_in"));
     int dev = 0;
     SDP_HIP_CHECK(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(mu);
     BandState &b = states[2 * dev + ws_slot()];
-    if (b.ptr != buf || b.elems < elems || b.lo != P.row_lo || b.hi != P.row_hi || b.ny != g.ny ||
+    if (b.epoch != ep || b.elems < elems || b.lo != P.row_lo || b.hi != P.row_hi || b.ny != g.ny ||
         b.ngx != g.ngx) {
         SDP_HIP_CHECK(hipMemsetAsync(buf, 0, elems * sizeof(float2), st));
-        b = BandState{buf, elems, P.row_lo, P.row_hi, g.ny, g.ngx};
+        b = BandState{ep, elems, P.row_lo, P.row_hi, g.ny, g.ngx};
     }
     return buf;
 }
@@ -2761,8 +2764,14 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     SDP_REQUIRE(in.nchan > 0 && in.nrow >= 0, "nchan must be positive");
     SDP_REQUIRE(in.nrow * (int64_t)in.nchan < (int64_t)0xffffffffll,
                 "more than 2^32 visibilities per call");
-    drop_kept_buckets();  // a fresh plan re-uses the bucketing scratch
-    if (!in.bounds) drop_batch_seq();  // and may overwrite a batch sequence's planes
+    // a fresh plan re-uses the bucketing scratch and may overwrite a batch
+    // sequence's planes -- those of its own slot: kept buckets and batch
+    // sequences exist in slot 0 only, and a slot-1 plan uses the '#1'
+    // buffers, so it leaves them valid
+    if (ws_slot() == 0) {
+        drop_kept_buckets();
+        if (!in.bounds) drop_batch_seq();
+    }
     Plan P;
     Geo &g = P.g;
     P.f64 = in.eps < 1.0e-7 && !(in.flags & SDP_HIP_FP32);

@@ -18,13 +18,14 @@ The point-source sums (:99-107) are formed on the device; the reference's
 dense [nants, nants] matrix (:108-114) is replaced by a canonical packed
 baseline order (kernels.canonical_baselines).
 
-Multi-GPU: with torch.distributed initialised (more than
-one rank, every rank calling with the same inputs) each rank forms the sums
-and solves a contiguous block of the gain rows, with no collective in the
-solve; one all-gather assembles the table on every rank, and the
-mean/median normalisation (:135-143) then runs over the whole table as in
-the reference.  ``shard=False`` (a keyword beyond the reference's) or
-SDP_HIP_SHARD=0 solves every row on every rank.
+Multi-GPU, opt-in with ``shard=True`` (a keyword beyond
+the reference's) or SDP_HIP_SHARD=1: with torch.distributed initialised
+(more than one rank, every rank calling with the same inputs, which is
+checked first) each rank forms the sums and solves a contiguous block of the
+gain rows, with no collective in the solve; one all-gather assembles the
+table on every rank, and the mean/median normalisation (:135-143) then runs
+over the whole table as in the reference.  By default every rank solves its
+own call.
 """
 
 import logging
@@ -54,7 +55,7 @@ def _windows(vis_time, gain_table):
 
 def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=200, tol=1e-6,
                     crosspol=False, normalise_gains="mean", jones_type="T", timeslice=None,
-                    shard=True):
+                    shard=None):
     if modelvis is not None:
         mv = modelvis.vis.data
         mx = float(mv.abs().max()) if isinstance(mv, torch.Tensor) else float(np.max(np.abs(mv)))
@@ -93,6 +94,9 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
     # this rank's gain rows [r0, r1) (all of them unsharded)
     nrow_g = len(present)
     sh = parallel.shard_info({"shard": shard})
+    parallel.check_replicated(sh, [v, m, w, np.asarray(vis.time.data, dtype=float),
+                                  tuple(gain_table["gain"].data.shape)],
+                              "solve_gaintable")
     rblocks = [(0, nrow_g)]
     r0, r1 = 0, nrow_g
     if sh:

@@ -21,11 +21,13 @@ Mirrors reference ``src/ska_sdp_func_python/imaging/ng.py``:
 
 The image transpose (:102, :257) is folded into the C ABI's output strides.
 
-Multi-GPU: when torch.distributed is initialised with more
-than one rank and every rank calls with the same Visibility and model (the
-drop-in use: the reference call, unchanged, on each rank), the visibility
-channels are split into contiguous blocks balanced by the measured cost
-model (parallel.balanced_channel_blocks).  invert_ng grids only its block
+Multi-GPU, opt-in with ``shard=True`` (a keyword beyond
+the reference's) or SDP_HIP_SHARD=1: when torch.distributed is initialised
+with more than one rank and every rank calls with the same Visibility and
+model (checked first: parallel.check_replicated raises ValueError on every
+rank otherwise), the visibility channels are split into contiguous blocks
+balanced by the measured cost model (parallel.balanced_channel_blocks).
+Without it every rank computes its own call, as the reference does.  invert_ng grids only its block
 and combines the partial images and weight sums with one all-reduce each
 (the reference's only exchange point, before normalise_sumwt); an MFS invert
 with w-stacking instead splits the ROWS into contiguous intervals of w
@@ -33,8 +35,7 @@ with w-stacking instead splits the ROWS into contiguous intervals of w
 a channel block at the top of a wide band holds them all; SDP_HIP_SHARD=chan
 keeps channel blocks); predict_ng predicts its block and all-gathers the
 channel blocks.  Every rank returns
-the reference's full result.  ``shard=False`` (or SDP_HIP_SHARD=0) computes
-everything on each rank.
+the reference's full result.
 Kwargs ``epsilon`` (default 1e-12), ``do_wstacking`` (True), ``threads``
 and ``verbosity`` are accepted as in the reference; ``threads`` is ignored
 (one GPU per process).  epsilon < 1e-7 runs the fp64 NUFFT (as ducc0 with
@@ -93,6 +94,7 @@ def predict_ng(bvis, model, **kwargs):
     uvw = _device.to_dev(bvis.uvw.data, torch.float64, dev).reshape(nrows * nbaselines, 3)
     uvw = torch.nan_to_num(uvw).contiguous()
     shard = parallel.shard_info(kwargs)
+    parallel.check_replicated(shard, [uvw, freq, model["pixels"].data], "predict_ng")
     blocks = [(0, vnchan)]
     lo, hi = 0, vnchan
     if shard:
@@ -188,6 +190,9 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     lo, hi = 0, vnchan
     mfs = nchan == 1 and vnchan > 1
     uvw = _device.to_dev(sbvis.uvw.data, torch.float64, dev).reshape(nrow, 3).contiguous()
+    parallel.check_replicated(
+        shard, [uvw, freq, sbvis.imaging_weight.data, None if dopsf else sbvis.vis.data,
+                model["pixels"].data.shape], "invert_ng")
     rows = None
     if shard and mfs and do_wstacking and parallel.shard_mode() != "chan":
         rows = _rank_rows(uvw, freq, nx, _pixsize(im), epsilon, precision, shard)

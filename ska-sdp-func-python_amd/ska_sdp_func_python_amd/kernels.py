@@ -78,14 +78,18 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
-def _alloc(shape, dtype, dev):
+def _alloc(shape, dtype, dev, may_release=True):
     """torch.empty on the device; when the caching allocator cannot serve it
     because the library's workspace holds the memory (cached w planes and
     records of an earlier large call), the workspace is released and the
-    allocation retried once (the w planes are re-made on the next call)."""
+    allocation retried once (the w planes are re-made on the next call).
+    ``may_release=False`` (a batched invert past its first batch, whose
+    resident planes hold the earlier batches' work) re-raises instead."""
     try:
         return torch.empty(shape, dtype=dtype, device=dev)
     except torch.OutOfMemoryError:
+        if not may_release:
+            raise
         release_workspace()
         torch.cuda.empty_cache()
         return torch.empty(shape, dtype=dtype, device=dev)
@@ -214,7 +218,9 @@ def ms2dirty_batch(uvw, freq, vis, wgt, npix_x, npix_y, pixsize_x, pixsize_y, bo
     _check_wgt(wgt, nrow, nchan)
     if last:
         if out is None:
-            out = _alloc((npix_x, npix_y), torch.float64, dev)
+            # (never auto-release the workspace here: past the first batch it
+            # holds the sequence's resident planes)
+            out = _alloc((npix_x, npix_y), torch.float64, dev, may_release=first)
             out_strides = (npix_y, 1)
         elif out_strides is None:
             out_strides = out.stride()

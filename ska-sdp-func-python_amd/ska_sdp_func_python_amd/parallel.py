@@ -16,25 +16,32 @@ import torch.distributed as dist
 
 
 def shard_mode():
-    """SDP_HIP_SHARD: "0" off, "chan" channel blocks everywhere, else (the
-    default) rows by w for MFS w-stacked inverts and channel blocks for the
-    rest."""
+    """SDP_HIP_SHARD: unset / "0" off, "chan" channel blocks everywhere, any
+    other value rows by w for MFS w-stacked inverts and channel blocks for
+    the rest."""
     import os
-    return os.environ.get("SDP_HIP_SHARD", "1")
+    return os.environ.get("SDP_HIP_SHARD", "0")
 
 
 def shard_info(kwargs=None):
     """(rank, world, group) when the reference-shaped API (invert_ng,
     predict_ng, solve_gaintable) should shard its work across the ranks of
-    the default process group: torch.distributed initialised with more than
-    one rank, every rank calling with the same (replicated) inputs.  Each rank
-    then computes its share and one collective combines the shares, so every
-    rank returns the reference's full result.  Disabled by the kwarg
-    ``shard=False`` or SDP_HIP_SHARD=0 (each rank then computes everything)."""
+    the default process group.
+
+    Sharding is OPT-IN: the kwarg ``shard=True`` (beyond the reference's
+    signature) or SDP_HIP_SHARD=1 / chan, with torch.distributed initialised
+    over more than one rank and every rank calling with the same (replicated)
+    inputs.  Each rank then computes its share and one collective combines
+    the shares, so every rank returns the reference's full result.  By
+    default each rank computes its own call independently, as the reference
+    does: ranks of a data-parallel pipeline pass different data.  The
+    entry points check replication with :func:`check_replicated` before they
+    split anything."""
     import os
-    if kwargs is not None and kwargs.get("shard", True) is False:
-        return None
-    if os.environ.get("SDP_HIP_SHARD", "1") == "0":
+    want = None if kwargs is None else kwargs.get("shard")
+    if want is None:
+        want = os.environ.get("SDP_HIP_SHARD", "0") not in ("", "0")
+    if not want:
         return None
     if not (dist.is_available() and dist.is_initialized()):
         return None
@@ -42,6 +49,54 @@ def shard_info(kwargs=None):
     if world <= 1:
         return None
     return dist.get_rank(), world, None
+
+
+def _fingerprint(arrays):
+    """float64 vector: per array its shape, element count and (for numbers)
+    the sums of its values and of their magnitudes, in a fixed order."""
+    out = []
+    for a in arrays:
+        if a is None:
+            out += [-1.0]
+            continue
+        t = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a))
+        out += [float(t.dim())] + [float(s) for s in t.shape]
+        if t.numel() == 0:
+            continue
+        if t.is_complex():
+            t = torch.view_as_real(t)
+        t = t.to(torch.float64)
+        out += [float(t.sum()), float(t.abs().sum())]
+    return torch.tensor(out, dtype=torch.float64)
+
+
+def check_replicated(shard, arrays, what):
+    """Raise ValueError on EVERY rank unless every rank of ``shard`` passed
+    the same arrays (shapes, element sums and magnitude sums agree): a
+    sharded call splits one replicated problem, and ranks that pass their
+    own data would otherwise combine unrelated partial results (or hang in
+    a collective of mismatched shapes).  One small all-reduce pair."""
+    if not shard:
+        return
+    fp = _fingerprint(arrays)
+    dev = torch.device("cpu")
+    if dist.get_backend(shard[2]) != "gloo":  # RCCL takes device tensors only
+        dev = torch.device("cuda", torch.cuda.current_device())
+    fp = fp.to(dev)
+    # the fingerprints' lengths first: a shape mismatch changes the length
+    n = torch.tensor([float(len(fp)), -float(len(fp))], dtype=torch.float64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=shard[2])
+    same = float(n[0]) == -float(n[1])
+    if same:
+        hi = fp.clone()
+        lo = -fp
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=shard[2])
+        dist.all_reduce(lo, op=dist.ReduceOp.MAX, group=shard[2])
+        same = bool(torch.equal(hi, -lo))
+    if not same:
+        raise ValueError(f"{what}: shard=True needs the same inputs on every rank (the ranks "
+                         "passed different visibilities, models or tables); call without "
+                         "sharding to process each rank's own data")
 
 
 def _host_staged(group, t):

@@ -1,6 +1,6 @@
 """CPU, world_size 2 over gloo: the reference-shaped API itself -- invert_ng
-and predict_ng -- sharding a replicated Visibility across ranks when
-torch.distributed is initialised (imaging/ng.py: rows split into intervals
+and predict_ng -- sharding a replicated Visibility across ranks when asked to
+(shard=True) with torch.distributed initialised (imaging/ng.py: rows split into intervals
 of w for an MFS invert, channel blocks from parallel.balanced_channel_blocks
 otherwise; one all-reduce of image + sumwt for invert, an all-gather of the
 channel blocks for predict).  Every rank must
@@ -76,10 +76,10 @@ def _patch():
     kernels.dirty2ms_vis = _oracle_dirty2ms_vis
 
 
-def _case(kind):
+def _case(kind, seed=51):
     from ska_sdp_func_python_amd import datamodels as dm
     from gpu_helpers import vis_from_arrays
-    rng = np.random.default_rng(51)
+    rng = np.random.default_rng(seed)
     nt, nb, nchan = 3, 12, 5
     freq = np.linspace(1.0e9, 1.2e9, nchan)
     umax = 1200.0
@@ -98,25 +98,43 @@ def _case(kind):
     return vis, im
 
 
-def _run(kind):
+def _run(kind, seed=51, **kw):
     from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng
-    vis, im = _case(kind)
+    vis, im = _case(kind, seed)
     if kind == "predict":
-        return (np.asarray(predict_ng(vis, im).vis.data),)
-    d, sw = invert_ng(vis, im, normalise=True)
+        return (np.asarray(predict_ng(vis, im, **kw).vis.data),)
+    d, sw = invert_ng(vis, im, normalise=True, **kw)
     return np.asarray(d["pixels"].data), np.asarray(sw)
 
 
-def _worker(rank, world, port, kind, q):
+def _worker(rank, world, port, kind, q, shard=True, own_data=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     _patch()
     try:
-        out = _run(kind)
+        kw = {} if shard is None else {"shard": shard}
+        try:
+            out = _run(kind, 51 + (rank if own_data else 0), **kw)
+        except ValueError as e:
+            out = ("ValueError", str(e))
         q.put((rank, out, sorted(SEEN), sorted(ROWS)))
     finally:
         dist.destroy_process_group()
+
+
+def _spawn(kind, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + int(np.random.default_rng().integers(0, 300))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, q), kwargs=kw) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert len(res) == 2
+    return res
 
 
 @pytest.mark.parametrize("kind", ["invert_mfs", "invert_cube", "predict"])
@@ -126,16 +144,7 @@ def test_reference_api_shards_across_ranks(kind, monkeypatch):
     monkeypatch.setattr(kernels, "ms2dirty_vis", _oracle_ms2dirty_vis)
     monkeypatch.setattr(kernels, "dirty2ms_vis", _oracle_dirty2ms_vis)
     ref = _run(kind)  # this process: no process group, so unsharded
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = 29600 + int(np.random.default_rng().integers(0, 300))
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=180) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-    assert len(res) == 2
+    res = _spawn(kind, shard=True)
     if kind == "invert_mfs":
         # an MFS w-stacked invert splits the rows (intervals of w, all channels)
         rows = [set(r) for _, _, _, r in res]
@@ -147,3 +156,23 @@ def test_reference_api_shards_across_ranks(kind, monkeypatch):
     for _, out, _, _ in res:
         for a, b in zip(out, ref):
             np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
+
+
+def test_default_is_per_rank_and_mismatched_shards_raise(monkeypatch):
+    """Without shard=True every rank computes its own call (a data-parallel
+    pipeline passes each rank its own data, as with the reference); with
+    shard=True ranks that pass different data get ValueError on every rank
+    instead of an image combined from unrelated partial results."""
+    from ska_sdp_func_python_amd import _device, kernels
+    monkeypatch.setattr(_device, "device", lambda: torch.device("cpu"))
+    monkeypatch.setattr(kernels, "ms2dirty_vis", _oracle_ms2dirty_vis)
+    monkeypatch.setattr(kernels, "dirty2ms_vis", _oracle_dirty2ms_vis)
+    refs = [_run("invert_mfs", 51 + r) for r in range(2)]
+    res = _spawn("invert_mfs", shard=None, own_data=True)
+    for rank, out, _, rows in res:
+        assert len(rows) == 36  # every row of its own observation
+        for a, b in zip(out, refs[rank]):
+            np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
+    res = _spawn("invert_mfs", shard=True, own_data=True)
+    for _, out, _, _ in res:
+        assert out[0] == "ValueError" and "same inputs" in out[1]

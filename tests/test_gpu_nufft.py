@@ -825,3 +825,22 @@ def test_two_slots_on_two_streams_overlap_correctly():
                           kernels._lib.SDP_HIP_SLOT1 | kernels._lib.SDP_HIP_BATCH_FIRST,
                           ctypes.cast(bbuf, ctypes.c_void_p), None, 0, 0,
                           kernels._stream(dev), ctypes.byref(info))
+
+
+def test_invert_after_workspace_release_is_unchanged():
+    """The band-only x-FFT input keeps its zeros across calls: after
+    release_workspace a new allocation (possibly at the same address, holding
+    stale data) must be cleared again (band state keyed by the allocation's
+    workspace epoch, not its address)."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(21, nrow=2000, nchan=4, umax=4000.0)
+    args = (T(uvw), T(freq), T(ms), T(wgt), 256, 256, cell, cell, 1e-7, True)
+    a, _ = kernels.ms2dirty(*args)
+    kernels.release_workspace()
+    # dirty the freed memory so that a re-allocation at the same address sees garbage
+    junk = torch.full((64 << 20,), float("nan"), device=dev())
+    del junk
+    torch.cuda.empty_cache()
+    b, _ = kernels.ms2dirty(*args)
+    assert torch.isfinite(b).all()
+    assert rel_rms(b.cpu().numpy(), a.cpu().numpy()) < 1e-6

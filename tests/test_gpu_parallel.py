@@ -77,7 +77,7 @@ def test_solve_gains_sharded_normalises(norm):
 # the reference-shaped API sharding across ranks (imaging/ng.py,
 # calibration/solvers.py), two processes on one MI355X over gloo (device
 # tensors host-staged for the collectives): each rank checks its sharded
-# result against the unsharded call (shard=False) through the same kernels
+# result (shard=True) against the unsharded call through the same kernels
 # ---------------------------------------------------------------------------
 def _api_case():
     from ska_sdp_func_python_amd import datamodels as dm
@@ -111,11 +111,11 @@ def _api_worker(rank, world, port, q):
         from ska_sdp_func_python_amd.calibration import solve_gaintable
         from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng
         vis, im, model = _api_case()
-        d1, s1 = invert_ng(vis, im)
+        d1, s1 = invert_ng(vis, im, shard=True)
         d0, s0 = invert_ng(vis, im, shard=False)
         e_inv = rel_rms(d1["pixels"].data, d0["pixels"].data)
         e_sw = float(np.max(np.abs(np.asarray(s1) - np.asarray(s0)) / np.abs(np.asarray(s0))))
-        p1 = predict_ng(vis, model).vis.data
+        p1 = predict_ng(vis, model, shard=True).vis.data
         p0 = predict_ng(vis, model, shard=False).vis.data
         e_pred = rel_rms(p1, p0)
         # gain solve: 5 gain rows over the 6 times split 3 / 2 across the ranks
@@ -126,7 +126,7 @@ def _api_worker(rank, world, port, q):
         bl = np.asarray(cv.baselines.data)
         cv["vis"].data[...] = (g[:, bl[:, 0]] * np.conj(g[:, bl[:, 1]]))[..., None]
         gt1 = solve_gaintable(copy_vis(cv), phase_only=False, normalise_gains="mean",
-                              jones_type="B")
+                              jones_type="B", shard=True)
         gt0 = solve_gaintable(copy_vis(cv), phase_only=False, normalise_gains="mean",
                               jones_type="B", shard=False)
         e_gain = float(np.max(np.abs(np.asarray(gt1["gain"].data) - np.asarray(gt0["gain"].data))))
