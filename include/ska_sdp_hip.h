@@ -97,6 +97,8 @@ typedef struct sdp_hip_wgrid_info {
     int padded;           /* invert: gridded on cells padded to 4 records
                              (k_grid_mfma_pad; 0: k_grid_mfma)              */
     int fp64;             /* the fp64 NUFFT ran (epsilon < 1e-7)            */
+    int tiled;            /* one-cell buckets from the two-level (64x64-cell
+                             bin, then cell) LDS-histogram sort             */
 } sdp_hip_wgrid_info;
 
 /* Library/ABI version and a device probe. */

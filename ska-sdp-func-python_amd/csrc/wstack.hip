@@ -91,6 +91,10 @@ struct Geo {
     // nps_all first planes; w0 is then the slab's first plane, and the others
     // are skipped without being counted as out of bounds
     int slab, slab_lo, nps_all;
+    // two-level bucketing of one-cell keys (tiled = 1): the window is cut into
+    // tlx x tly bins of 64 x 64 cells per first plane (nbins in all); the
+    // keys of a bin are contiguous (bin-major, 4096 per bin)
+    int tiled, tlx, tly, nbins;
 };
 
 struct __attribute__((aligned(32))) VisRec {
@@ -236,7 +240,24 @@ __device__ __forceinline__ bool slab_out(const Geo &g, const double *__restrict_
 // p0-major bucket keys: the items of a range of first planes are contiguous.
 // One-cell keys inside a plane: block (x-major), x pair in the block, y, x
 // parity -- 16 consecutive keys are a group of 2 x 8 cells.
+// Two-level (tiled) one-cell keys: bin = (first plane, 64 x 64-cell tile of
+// the window), then inside the bin: x pair (32), y block of 8 (8), and the
+// cell of the 2 x 8-cell group, (y & 7) * 2 + (x & 1) -- 16 consecutive keys
+// are again one group, 256 groups per bin.
+constexpr int kTile = 64;
+constexpr int kBinCells = kTile * kTile;
+__device__ __forceinline__ unsigned tiled_key(const Geo &g, const Coord &c) {
+    const int ic = c.ic0 - g.wx0, jc = c.jc0 - g.wy0;
+    const int tile = (ic >> 6) * g.tly + (jc >> 6);
+    const int lx = ic & 63, ly = jc & 63;
+    const unsigned local = ((unsigned)(((lx >> 1) << 3) | (ly >> 3)) << 4) |
+                           (unsigned)((ly & 7) << 1) | (unsigned)(lx & 1);
+    return ((unsigned)c.p0 * (unsigned)(g.tlx * g.tly) + (unsigned)tile) * (unsigned)kBinCells +
+           local;
+}
+
 __device__ __forceinline__ unsigned coord_key(const Geo &g, const Coord &c, int64_t row) {
+    if (g.tiled) return tiled_key(g, c);
     const int ic = c.ic0 - g.wx0, jc = c.jc0 - g.wy0;
     const int tile =
         g.sub == kTileCell
@@ -942,6 +963,13 @@ __global__ __launch_bounds__(kSubThreads) void k_subsort_pad(Geo g, const Item *
 // first cell (centred grid) of 16-key group `gi` (index inside its first
 // plane) of a one-cell plan: block gi / (bx / 2), x pair gi % (bx / 2)
 __device__ __forceinline__ void group_origin(const Geo &g, int gi, int &ib, int &jb) {
+    if (g.tiled) {  // bin-major: 256 groups per 64 x 64-cell tile, x pair major
+        const int tile = gi >> 8, gt = gi & 255;
+        const int tx = tile / g.tly, ty = tile - tx * g.tly;
+        ib = g.wx0 + tx * kTile + 2 * (gt >> 3);
+        jb = g.wy0 + ty * kTile + 8 * (gt & 7);
+        return;
+    }
     const int ppb = g.bx >> 1;
     const int blk = gi / ppb, xp = gi - blk * ppb;
     const int nby = g.wny >> 3;
@@ -2062,6 +2090,578 @@ __global__ void k_bucket_f64(Geo g, int64_t nvis, const double *__restrict__ uvw
     recs[pos] = rec;
 }
 
+// ------------------------------------------------------------------------
+// Two-level bucketing of one-cell plans (Geo::tiled).  The one-cell
+// histogram of the single-level path takes one returning global atomic per
+// run of equal cells (C2: 60 M for 123.6 M visibilities, serialised on the
+// uv core's hot cells).  Here no per-cell global atomic exists:
+//   k_t_count     per workgroup (a contiguous range of visibilities) an LDS
+//                 histogram over the nbins 64 x 64-cell bins; one returning
+//                 atomic per (workgroup, non-empty bin) reserves the
+//                 workgroup's slice of each bin
+//   k_t_bins      one workgroup: bin bases (scan), the bins' chunks of
+//                 records (<= 64 per bin, >= kTChunk records each) and the
+//                 non-empty bin list
+//   k_t_scatter   the value pass: the record (RecC / VisRec / VisRec64) and
+//                 its cell in the bin (u16) written in bin order, ranks from
+//                 LDS cursors (one LDS atomic per run of equal bins)
+//   k_t_cellcount per chunk an LDS histogram over the bin's 4096 cells
+//   k_t_cellcol   per (bin, cell): the count prefix over the bin's chunks
+//                 (in place), the total, and the bin's padded-record / item
+//                 sums (packed, one 64-bit atomic per 256 cells)
+//   k_t_binscan   one workgroup: record and item bases of the bins, the
+//                 metadata the host reads (the only host sync)
+//   k_t_cellfin   per bin: cell bases, pad records, FineItem work items
+//   k_t_final     per chunk: records moved to their cell (LDS cursors
+//                 seeded with the cell base + the chunk's prefix)
+// The writes of the two scatter passes land in runs inside the few bins /
+// cells a workgroup touches at a time, not at random addresses.
+constexpr int kMaxBins = 16384;    // LDS histogram of the first level (64 KiB)
+constexpr int kTThreads = 1024;
+constexpr unsigned kTChunk = 32768;  // records per second-level chunk (at least)
+constexpr unsigned kTMaxChunksPerBin = 64;
+
+struct TChunk {
+    uint32_t bin, b, e, pad;
+};
+
+// consecutive lanes with equal `key` form a run; its head lane adds the run
+// length to ctr[key] (LDS); with kRet every lane of a valid run gets its slot
+template <bool kRet>
+__device__ __forceinline__ unsigned lds_run_add(unsigned key, bool valid, unsigned *ctr) {
+    const int lane = threadIdx.x & 63;
+    const unsigned k = valid ? key : 0xffffffffu;
+    const unsigned prev = __shfl_up(k, 1);
+    const bool start = (lane == 0) || (prev != k);
+    const unsigned long long B = __ballot(start);
+    const unsigned long long above = (lane == 63) ? 0ull : (B & ~((2ull << lane) - 1ull));
+    const int end = above ? (__ffsll((long long)above) - 1) : 64;
+    unsigned base = 0;
+    if (valid && start) base = atomicAdd(&ctr[k], (unsigned)(end - lane));
+    if (!kRet) return 0;
+    const unsigned long long upto = (lane == 63) ? B : (B & ((2ull << lane) - 1ull));
+    const int head = 63 - __clzll((long long)upto);
+    const unsigned hb = __shfl(base, head);
+    return hb + (unsigned)(lane - head);
+}
+
+// The visibility's classification, shared bit for bit by the count and the
+// value pass: weight (flag-masked), in-slab test, fp64 coordinates, and
+// whether it is bucketed.  v < 2^32 (the plan refuses larger calls).
+struct TPoint {
+    int64_t row;
+    int chan;
+    double wd;  // effective weight (0 outside the call's w slab)
+    Coord c;
+    bool in;
+};
+
+template <bool kCount>
+__device__ __forceinline__ TPoint t_point(const Geo &g, int64_t v, int64_t vend,
+                                          const double *__restrict__ uvw, int64_t rs,
+                                          const double *__restrict__ freq,
+                                          const void *__restrict__ wgt, int64_t wrs, int64_t wcs,
+                                          const VisExtra &x, unsigned long long *nbad) {
+    TPoint p;
+    p.in = false;
+    p.wd = 0.0;
+    p.row = 0;
+    p.chan = 0;
+    p.c.ok = false;
+    if (v >= vend) return p;
+    const uint32_t v32 = (uint32_t)v, r32 = v32 / (uint32_t)g.nchan;
+    p.row = r32;
+    p.chan = (int)(v32 - r32 * (uint32_t)g.nchan);
+    if (g.slab && slab_out(g, uvw, rs, p.row, freq[p.chan])) return p;
+    p.wd = eff_weight(wgt, wrs, wcs, x, p.row, p.chan);
+    if (!(x.all || (float)p.wd != 0.0f)) return p;
+    p.c = vis_coord(g, uvw, rs, p.row, freq[p.chan]);
+    if (!p.c.ok) {
+        if (kCount && !p.c.skip) atomicAdd(nbad, 1ull);
+        return p;
+    }
+    p.in = true;
+    return p;
+}
+
+// weight sum of the workgroup's visibilities: wave reduction, one fp64
+// atomic per wave into the call's slots (k_sum_slots folds them)
+__device__ __forceinline__ void t_weight_sum(double ws, double *sw_slots) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ws += __shfl_xor(ws, o, 64);
+    if ((threadIdx.x & 63) == 0 && ws != 0.0)
+        atomicAdd(&sw_slots[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) &
+                            (kSumSlots - 1)],
+                  ws);
+}
+
+__global__ __launch_bounds__(kTThreads) void k_t_count(Geo g, int64_t nvis, int64_t vpw,
+                                                       const double *__restrict__ uvw, int64_t rs,
+                                                       const double *__restrict__ freq,
+                                                       const void *__restrict__ wgt, int64_t wrs,
+                                                       int64_t wcs, VisExtra x, double *sw_slots,
+                                                       unsigned *__restrict__ binc,
+                                                       unsigned *__restrict__ m1,
+                                                       unsigned long long *nbad) {
+    extern __shared__ unsigned hist[];
+    const int nb = g.nbins;
+    for (int b = threadIdx.x; b < nb; b += kTThreads) hist[b] = 0u;
+    __syncthreads();
+    const int64_t v0 = (int64_t)blockIdx.x * vpw, v1 = min(nvis, v0 + vpw);
+    double ws = 0.0;
+    for (int64_t base = v0; base < v1; base += kTThreads) {
+        const TPoint p = t_point<true>(g, base + threadIdx.x, v1, uvw, rs, freq, wgt, wrs, wcs, x,
+                                       nbad);
+        ws += p.wd;
+        lds_run_add<false>(p.in ? tiled_key(g, p.c) >> 12 : 0u, p.in, hist);
+    }
+    if (sw_slots) t_weight_sum(ws, sw_slots);
+    __syncthreads();
+    // the workgroup's slice of every non-empty bin (its offset inside the bin)
+    unsigned *row = m1 + (size_t)blockIdx.x * nb;
+    for (int b = threadIdx.x; b < nb; b += kTThreads) {
+        const unsigned c = hist[b];
+        row[b] = c ? atomicAdd(&binc[b], c) : 0u;
+    }
+}
+
+// 1024-thread exclusive scan helper (hipcub block scan)
+template <class T>
+using TBlockScan = hipcub::BlockScan<T, kTThreads>;
+
+// one workgroup: bin bases, chunks, non-empty bins.  Thread t owns bins
+// [t * per, t * per + per).  binbase[nb] = total records; nbl[0] = number of
+// non-empty bins, nbl[1 + k] = the k-th; meta_ch[0] = number of chunks.
+__global__ __launch_bounds__(kTThreads) void k_t_bins(int nb, const unsigned *__restrict__ binc,
+                                                      unsigned *__restrict__ binbase,
+                                                      unsigned *__restrict__ chbase,
+                                                      unsigned *__restrict__ nchb,
+                                                      unsigned *__restrict__ nbl,
+                                                      TChunk *__restrict__ chunks,
+                                                      unsigned *__restrict__ meta_ch) {
+    __shared__ typename TBlockScan<unsigned>::TempStorage tmp;
+    const int per = (nb + kTThreads - 1) / kTThreads;
+    const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+    unsigned rec = 0, nch = 0, nne = 0;
+    auto chunk_size = [](unsigned n) {
+        const unsigned big = (n + kTMaxChunksPerBin - 1) / kTMaxChunksPerBin;
+        return big > kTChunk ? big : kTChunk;
+    };
+    for (int b = b0; b < b1; ++b) {
+        const unsigned n = binc[b];
+        rec += n;
+        if (n) {
+            const unsigned cs = chunk_size(n);
+            nch += (n + cs - 1) / cs;
+            ++nne;
+        }
+    }
+    unsigned rec_x, nch_x, nne_x, rec_t, nch_t, nne_t;
+    TBlockScan<unsigned>(tmp).ExclusiveSum(rec, rec_x, rec_t);
+    __syncthreads();
+    TBlockScan<unsigned>(tmp).ExclusiveSum(nch, nch_x, nch_t);
+    __syncthreads();
+    TBlockScan<unsigned>(tmp).ExclusiveSum(nne, nne_x, nne_t);
+    for (int b = b0; b < b1; ++b) {
+        const unsigned n = binc[b];
+        binbase[b] = rec_x;
+        chbase[b] = nch_x;
+        unsigned k = 0;
+        if (n) {
+            const unsigned cs = chunk_size(n);
+            k = (n + cs - 1) / cs;
+            for (unsigned j = 0; j < k; ++j) {
+                TChunk t;
+                t.bin = (uint32_t)b;
+                t.b = rec_x + j * cs;
+                t.e = rec_x + min(n, (j + 1) * cs);
+                t.pad = 0u;
+                chunks[nch_x + j] = t;
+            }
+            nbl[1 + nne_x++] = (unsigned)b;
+        }
+        nchb[b] = k;
+        rec_x += n;
+        nch_x += k;
+    }
+    if (threadIdx.x == kTThreads - 1) {
+        binbase[nb] = rec_t;
+        nbl[0] = nne_t;
+        meta_ch[0] = nch_t;
+    }
+}
+
+// Record writers of the value pass (the fields bucket_one / k_bucket_f64
+// write for the single-level path, computed the same way).
+template <class VT, bool kGrid>
+__device__ __forceinline__ void t_value32(const Geo &g, const VisExtra &x,
+                                          const double *__restrict__ uvw, int64_t rs,
+                                          const double *__restrict__ freq, const VT *vis,
+                                          int64_t vrs, int64_t vcs, const TPoint &p, float &cr,
+                                          float &ci) {
+    const float wt = (float)p.wd;
+    cr = wt;
+    ci = 0.0f;
+    if (kGrid) {
+        const float2 xv = (vis && wt != 0.0f) ? eff_vis(vis, vrs, vcs, x, p.row, p.chan)
+                                              : make_float2(1.0f, 0.0f);
+        cr = wt != 0.0f ? xv.x * wt : 0.0f;
+        ci = wt != 0.0f ? xv.y * wt : 0.0f;
+    }
+    if (g.do_w || x.shift) {
+        double ph = g.do_w ? p.c.w * g.s0 : 0.0;
+        if (x.shift) {
+            const double *u = uvw + p.row * rs;
+            ph += (u[0] * x.sl + u[1] * x.sm + u[2] * x.sn) * (freq[p.chan] / kCLight);
+        }
+        ph -= rint(ph);
+        float sn, cs;
+        sincospif((float)(2.0 * ph), &sn, &cs);
+        if (!kGrid) sn = -sn;
+        const float r_ = cr * cs - ci * sn, i_ = cr * sn + ci * cs;
+        cr = r_;
+        ci = i_;
+    }
+}
+
+// KIND 0: RecC (4-padded invert), 1: VisRec (fp32 predict), 2: VisRec64
+template <int KIND>
+struct TRec;
+template <>
+struct TRec<0> {
+    using type = RecC;
+};
+template <>
+struct TRec<1> {
+    using type = VisRec;
+};
+template <>
+struct TRec<2> {
+    using type = VisRec64;
+};
+
+template <class VT, int KIND, bool kGrid>
+__device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x,
+                                        const double *__restrict__ uvw, int64_t rs,
+                                        const double *__restrict__ freq, const VT *vis,
+                                        int64_t vrs, int64_t vcs, const TPoint &p, int64_t vg,
+                                        void *out, unsigned pos) {
+    if constexpr (KIND == 2) {
+        double cr = p.wd, ci = 0.0;
+        if (kGrid) {
+            const double2 xv = (vis && p.wd != 0.0) ? eff_vis_d(vis, vrs, vcs, x, p.row, p.chan)
+                                                    : make_double2(1.0, 0.0);
+            cr = p.wd != 0.0 ? xv.x * p.wd : 0.0;
+            ci = p.wd != 0.0 ? xv.y * p.wd : 0.0;
+        }
+        if (g.do_w || x.shift) {
+            double ph = g.do_w ? p.c.w * g.s0 : 0.0;
+            if (x.shift) {
+                const double *u = uvw + p.row * rs;
+                ph += (u[0] * x.sl + u[1] * x.sm + u[2] * x.sn) * (freq[p.chan] / kCLight);
+            }
+            ph -= rint(ph);
+            double sn, cs;
+            sincospi(2.0 * ph, &sn, &cs);
+            if (!kGrid) sn = -sn;
+            const double r_ = cr * cs - ci * sn, i_ = cr * sn + ci * cs;
+            cr = r_;
+            ci = i_;
+        }
+        VisRec64 rec;
+        rec.cre = cr;
+        rec.cim = ci;
+        rec.du = p.c.du;
+        rec.dv = p.c.dv;
+        rec.dw = p.c.dw;
+        rec.ij = (uint32_t)p.c.ic0 | ((uint32_t)p.c.jc0 << 16);
+        rec.p0 = (uint32_t)p.c.p0;
+        rec.idx = (uint32_t)vg;
+        rec.pad = 0u;
+        static_cast<VisRec64 *>(out)[pos] = rec;
+    } else {
+        float cr, ci;
+        t_value32<VT, kGrid>(g, x, uvw, rs, freq, vis, vrs, vcs, p, cr, ci);
+        if constexpr (KIND == 0) {
+            const double base = 1.0 - 0.5 * g.W;
+            const uint32_t qu = fix_frac(base - p.c.du, 21), qv = fix_frac(base - p.c.dv, 21);
+            const uint32_t qw = g.do_w ? fix_frac(base - p.c.dw, 22) : 0u;
+            RecC rc;
+            rc.cre = cr;
+            rc.cim = ci;
+            rc.lo = qu | (qv << 21);
+            rc.hi = (qv >> 11) | (qw << 10);
+            static_cast<RecC *>(out)[pos] = rc;
+        } else {
+            VisRec rec;
+            rec.cre = cr;
+            rec.cim = ci;
+            rec.fu = p.c.fu;
+            rec.fv = p.c.fv;
+            rec.fw = p.c.fw;
+            rec.ij = (uint32_t)p.c.ic0 | ((uint32_t)p.c.jc0 << 16);
+            rec.p0 = (uint32_t)p.c.p0;
+            rec.idx = (uint32_t)vg;
+            static_cast<VisRec *>(out)[pos] = rec;
+        }
+    }
+}
+
+template <class VT, int KIND, bool kGrid>
+__global__ __launch_bounds__(kTThreads) void k_t_scatter(
+    Geo g, int64_t nvis, int64_t vpw, const double *__restrict__ uvw, int64_t rs,
+    const double *__restrict__ freq, const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
+    const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x, double *sw_slots,
+    const unsigned *__restrict__ binbase, const unsigned *__restrict__ m1, void *__restrict__ out,
+    uint16_t *__restrict__ lkey) {
+    extern __shared__ unsigned cur[];
+    const int nb = g.nbins;
+    const unsigned *row = m1 + (size_t)blockIdx.x * nb;
+    for (int b = threadIdx.x; b < nb; b += kTThreads) cur[b] = binbase[b] + row[b];
+    __syncthreads();
+    const int64_t v0 = (int64_t)blockIdx.x * vpw, v1 = min(nvis, v0 + vpw);
+    double ws = 0.0;
+    for (int64_t base = v0; base < v1; base += kTThreads) {
+        const int64_t v = base + threadIdx.x;
+        const TPoint p = t_point<false>(g, v, v1, uvw, rs, freq, wgt, wrs, wcs, x, nullptr);
+        ws += p.wd;
+        const unsigned key = p.in ? tiled_key(g, p.c) : 0u;
+        const unsigned pos = lds_run_add<true>(key >> 12, p.in, cur);
+        if (p.in) {
+            t_write<VT, KIND, kGrid>(g, x, uvw, rs, freq, vis, vrs, vcs, p, v, out, pos);
+            lkey[pos] = (uint16_t)(key & (kBinCells - 1));
+        }
+    }
+    if (sw_slots) t_weight_sum(ws, sw_slots);
+}
+
+// per chunk: its records' cell histogram (M2 row of kBinCells counts)
+__global__ __launch_bounds__(kTThreads) void k_t_cellcount(const TChunk *__restrict__ chunks,
+                                                           const unsigned *__restrict__ meta_ch,
+                                                           const uint16_t *__restrict__ lkey,
+                                                           unsigned *__restrict__ m2) {
+    __shared__ unsigned h[kBinCells];
+    const unsigned n = meta_ch[0];
+    for (unsigned c = blockIdx.x; c < n; c += gridDim.x) {
+        for (int i = threadIdx.x; i < kBinCells; i += kTThreads) h[i] = 0u;
+        __syncthreads();
+        const TChunk t = chunks[c];
+        for (uint32_t i0 = t.b; i0 < t.e; i0 += kTThreads) {
+            const uint32_t i = i0 + threadIdx.x;
+            const bool ok = i < t.e;
+            lds_run_add<false>(ok ? (unsigned)lkey[i] : 0u, ok, h);
+        }
+        __syncthreads();
+        uint4 *dst = reinterpret_cast<uint4 *>(m2 + (size_t)c * kBinCells);
+        const uint4 *src = reinterpret_cast<const uint4 *>(h);
+        for (int i = threadIdx.x; i < kBinCells / 4; i += kTThreads) dst[i] = src[i];
+        __syncthreads();
+    }
+}
+
+// per (non-empty bin, 256-cell slice), one thread per cell: the exclusive
+// prefix of the cell's counts over the bin's chunks (in place in M2), the
+// cell total T, and into binsum[bin] the slice's (padded records << 32 |
+// items) -- a group of 16 cells is 16 consecutive lanes; its items are its
+// padded records in chunks of `chunk`
+template <bool PAD>
+__global__ __launch_bounds__(256) void k_t_cellcol(const unsigned *__restrict__ nbl,
+                                                   const unsigned *__restrict__ chbase,
+                                                   const unsigned *__restrict__ nchb,
+                                                   unsigned *__restrict__ m2,
+                                                   unsigned *__restrict__ tot, unsigned chunk,
+                                                   unsigned long long *__restrict__ binsum,
+                                                   unsigned *__restrict__ npad) {
+    __shared__ unsigned long long red[4];
+    __shared__ unsigned redp[4];
+    const unsigned nwork = nbl[0] * (kBinCells / 256);
+    for (unsigned w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const unsigned b = nbl[1 + w / (kBinCells / 256)];
+        const int cell = (int)(w % (kBinCells / 256)) * 256 + threadIdx.x;
+        const unsigned c0 = chbase[b], nc = nchb[b];
+        unsigned *q = m2 + (size_t)c0 * kBinCells + cell;
+        unsigned run = 0;
+        unsigned k = 0;
+        for (; k + 8 <= nc; k += 8) {
+            unsigned v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = q[(size_t)(k + j) * kBinCells];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                q[(size_t)(k + j) * kBinCells] = run;
+                run += v[j];
+            }
+        }
+        for (; k < nc; ++k) {
+            const unsigned v = q[(size_t)k * kBinCells];
+            q[(size_t)k * kBinCells] = run;
+            run += v;
+        }
+        tot[(size_t)b * kBinCells + cell] = run;
+        const unsigned pd = PAD ? (run + 3u) & ~3u : run;
+        unsigned gt = pd;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) gt += __shfl_xor(gt, o, 64);
+        unsigned long long r =
+            ((unsigned long long)pd << 32) |
+            (unsigned long long)((threadIdx.x & 15) == 0 ? (gt + chunk - 1) / chunk : 0u);
+        unsigned pads = pd - run;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            r += __shfl_xor(r, o, 64);
+            pads += __shfl_xor(pads, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            red[threadIdx.x >> 6] = r;
+            redp[threadIdx.x >> 6] = pads;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long t = red[0] + red[1] + red[2] + red[3];
+            if (t) atomicAdd(&binsum[b], t);
+            const unsigned tp = redp[0] + redp[1] + redp[2] + redp[3];
+            if (tp) atomicAdd(npad, tp);
+        }
+        __syncthreads();
+    }
+}
+
+// one workgroup: exclusive scan of the bins' (padded records << 32 | items)
+// -> bofs; the metadata the host reads: {nbad lo, nbad hi, gridded records,
+// items, first item of each first plane [nps + 1], padded records}
+__global__ __launch_bounds__(kTThreads) void k_t_binscan(
+    int nb, int bins_per_plane, int nps, const unsigned long long *__restrict__ binsum,
+    const unsigned *__restrict__ binbase, const unsigned long long *__restrict__ nbad,
+    unsigned long long *__restrict__ bofs, unsigned *__restrict__ meta) {
+    __shared__ typename TBlockScan<unsigned long long>::TempStorage tmp;
+    const int per = (nb + kTThreads - 1) / kTThreads;
+    const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+    unsigned long long s = 0;
+    for (int b = b0; b < b1; ++b) s += binsum[b];
+    unsigned long long x, t;
+    TBlockScan<unsigned long long>(tmp).ExclusiveSum(s, x, t);
+    for (int b = b0; b < b1; ++b) {
+        bofs[b] = x;
+        x += binsum[b];
+    }
+    if (threadIdx.x == kTThreads - 1) bofs[nb] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        meta[0] = (unsigned)(*nbad & 0xffffffffull);
+        meta[1] = (unsigned)(*nbad >> 32);
+        meta[2] = binbase[nb];
+        meta[3] = (unsigned)(t & 0xffffffffull);
+        meta[5 + nps] = (unsigned)(t >> 32);
+    }
+    for (int p = threadIdx.x; p <= nps; p += kTThreads)
+        meta[4 + p] = (unsigned)((p < nps ? bofs[(size_t)p * bins_per_plane] : t) & 0xffffffffull);
+}
+
+// per non-empty bin, thread = one of its 256 groups of 16 cells: cell bases
+// (cbase, absolute record index), zero pad records behind each cell's
+// records (RecC, PAD), and the group's FineItems (chunks of `chunk` padded
+// records, each with the 16 cell ends)
+template <bool PAD>
+__global__ __launch_bounds__(256) void k_t_cellfin(const Geo g, const unsigned *__restrict__ nbl,
+                                                   const unsigned *__restrict__ tot,
+                                                   const unsigned long long *__restrict__ bofs,
+                                                   unsigned chunk, unsigned *__restrict__ cbase,
+                                                   RecC *__restrict__ recs,
+                                                   FineItem *__restrict__ items) {
+    __shared__ typename hipcub::BlockScan<unsigned long long, 256>::TempStorage tmp;
+    const unsigned nne = nbl[0];
+    const int tpp = g.tlx * g.tly;
+    for (unsigned w = blockIdx.x; w < nne; w += gridDim.x) {
+        const unsigned b = nbl[1 + w];
+        const int gi = threadIdx.x;
+        const uint4 *t4 = reinterpret_cast<const uint4 *>(tot + (size_t)b * kBinCells + gi * 16);
+        unsigned n[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = t4[q];
+            n[4 * q] = v.x;
+            n[4 * q + 1] = v.y;
+            n[4 * q + 2] = v.z;
+            n[4 * q + 3] = v.w;
+        }
+        unsigned G = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) G += PAD ? (n[j] + 3u) & ~3u : n[j];
+        const unsigned it = (G + chunk - 1) / chunk;
+        unsigned long long x;
+        hipcub::BlockScan<unsigned long long, 256>(tmp).ExclusiveSum(
+            ((unsigned long long)G << 32) | it, x);
+        const unsigned long long bo = bofs[b];
+        const unsigned base = (unsigned)(bo >> 32) + (unsigned)(x >> 32);
+        const unsigned ib = (unsigned)bo + (unsigned)x;
+        FineItem f;
+        unsigned run = base;
+        unsigned st[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            st[j] = run;
+            const unsigned r = PAD ? (n[j] + 3u) & ~3u : n[j];
+            if (PAD && r != n[j]) {
+                RecC z;
+                z.cre = z.cim = 0.0f;
+                z.lo = z.hi = 0u;
+                for (unsigned i = run + n[j]; i < run + r; ++i) recs[i] = z;
+            }
+            run += r;
+            f.o[j] = run;
+        }
+        uint4 *cb = reinterpret_cast<uint4 *>(cbase + (size_t)b * kBinCells + gi * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cb[q] = make_uint4(st[4 * q], st[4 * q + 1], st[4 * q + 2], st[4 * q + 3]);
+        f.p0 = b / (unsigned)tpp;
+        f.tile = (b - f.p0 * (unsigned)tpp) * 256u + (unsigned)gi;
+        for (unsigned s = 0; s < it; ++s) {
+            f.b = base + s * chunk;
+            f.e = min(run, f.b + chunk);
+            items[ib + s] = f;
+        }
+        __syncthreads();  // (tmp reused by the next bin)
+    }
+}
+
+// per chunk: each record to its cell, at the cell base + the chunk's prefix
+// + its rank among the chunk's records of that cell (LDS cursors)
+template <int KIND>
+__global__ __launch_bounds__(kTThreads) void k_t_final(const TChunk *__restrict__ chunks,
+                                                       const unsigned *__restrict__ meta_ch,
+                                                       const uint16_t *__restrict__ lkey,
+                                                       const unsigned *__restrict__ m2,
+                                                       const unsigned *__restrict__ cbase,
+                                                       const void *__restrict__ in,
+                                                       void *__restrict__ out) {
+    using R = typename TRec<KIND>::type;
+    constexpr int NW = (int)(sizeof(R) / sizeof(uint4));
+    __shared__ unsigned cur[kBinCells];
+    const unsigned n = meta_ch[0];
+    for (unsigned c = blockIdx.x; c < n; c += gridDim.x) {
+        const TChunk t = chunks[c];
+        const unsigned *pre = m2 + (size_t)c * kBinCells;
+        const unsigned *cb = cbase + (size_t)t.bin * kBinCells;
+        for (int i = threadIdx.x; i < kBinCells; i += kTThreads) cur[i] = cb[i] + pre[i];
+        __syncthreads();
+        for (uint32_t i0 = t.b; i0 < t.e; i0 += kTThreads) {
+            const uint32_t i = i0 + threadIdx.x;
+            const bool ok = i < t.e;
+            uint4 r[NW];
+            if (ok) {
+#pragma unroll
+                for (int k = 0; k < NW; ++k) r[k] = reinterpret_cast<const uint4 *>(in)[(size_t)i * NW + k];
+            }
+            const unsigned pos = lds_run_add<true>(ok ? (unsigned)lkey[i] : 0u, ok, cur);
+            if (ok) {
+#pragma unroll
+                for (int k = 0; k < NW; ++k) reinterpret_cast<uint4 *>(out)[(size_t)pos * NW + k] = r[k];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 template <int W, bool WS>
 constexpr size_t grid_f64_lds() {
     return (size_t)(WS ? W : 1) * (W + 1) * (W + 7) * sizeof(double2) +
@@ -2482,6 +3082,17 @@ struct Part {
     // host copies (read_part_meta)
     int64_t nrec = 0, nitems = 0;
     std::vector<unsigned> p0_items;
+    // two-level (tiled) plans: see k_t_count .. k_t_final
+    int t_g1 = 0;          // workgroups of the count / value passes
+    int64_t t_vpw = 0;     // visibilities per such workgroup
+    unsigned t_maxch = 0;  // bound on the second-level chunks
+    unsigned *t_binc = nullptr, *t_binbase = nullptr, *t_chbase = nullptr, *t_nchb = nullptr;
+    unsigned *t_nbl = nullptr, *t_m1 = nullptr, *t_m2 = nullptr, *t_tot = nullptr;
+    unsigned *t_cbase = nullptr, *t_meta_ch = nullptr, *t_npad = nullptr;
+    TChunk *t_chunks = nullptr;
+    unsigned long long *t_binsum = nullptr, *t_bofs = nullptr;
+    uint16_t *t_lkey = nullptr;
+    void *t_a = nullptr;  // records in bin order (the value pass's output)
 };
 
 struct Plan {
@@ -2550,7 +3161,8 @@ static size_t grid_budget_bytes(size_t need_other) {
         ws.held(ws_name("grid")) + ws.held(ws_name("spec")) + ws.held(ws_name("spec_in"));
     const size_t held_other = ws.held(ws_name("recs")) + ws.held(ws_name("key_rank")) +
                               ws.held(ws_name("degrid_acc")) + ws.held(ws_name("recs_pad")) +
-                              ws.held(ws_name("rec_cls"));
+                              ws.held(ws_name("rec_cls")) + ws.held(ws_name("recs_a")) +
+                              ws.held(ws_name("rec_lkey")) + ws.held(ws_name("t_m2"));
     const size_t avail = free_b + held_planes + held_other;
     const size_t reserve = std::max<size_t>((size_t)6 << 30, total_b / 16);
     const size_t need = need_other + reserve;
@@ -2848,21 +3460,48 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         g.nps = hi - lo;
         g.nplanes = g.nps + g.W - 1;
     }
-    // bucket window (origins only: the footprints' halo may leave it).  x
-    // (rows) only: the y stride stays ngy, since a compacted y range packs the
-    // hot histogram counters of the uv core closer together and measured 2x
-    // slower count-pass atomics on C2
-    {
-        const double amax = umax * in.px * g.ngx;
-        const int reach = (int)std::ceil(amax + 0.5 * g.W) + 2;
-        int lo = (g.ngx / 2 - reach) & ~(kGridAlign - 1);
-        int hi = ((g.ngx / 2 + reach + kGridAlign - 1) / kGridAlign) * kGridAlign;
-        if (lo <= 0 || hi >= g.ngx) {
+    // bucket window (origins only: the footprints' halo may leave it): the
+    // `al`-aligned cell range [ng/2 - reach, ng/2 + reach), or the whole
+    // (al-rounded) axis when that reaches an edge
+    auto window = [&](double m, int ng, int al, int &w0, int &wn) {
+        const int reach = (int)std::ceil(m + 0.5 * g.W) + 2;
+        int lo = (ng / 2 - reach) & ~(al - 1);
+        int hi = ((ng / 2 + reach + al - 1) / al) * al;
+        if (lo <= 0 || hi >= ng) {
             lo = 0;
-            hi = g.ngx;
+            hi = ((ng + al - 1) / al) * al;
         }
-        g.wx0 = lo;
-        g.wnx = hi - lo;
+        w0 = lo;
+        wn = hi - lo;
+    };
+    const double amax = umax * in.px * g.ngx, bmax = vmax * in.py * g.ngy;
+    // two-level bucketing (k_t_*): one-cell keys in 64 x 64-cell bins, while
+    // the bins of the window fit the first level's LDS histogram (C2: 2 first
+    // planes x 59 x 61 bins); SDP_HIP_BUCKET2=0 selects the single-level
+    // one-cell histogram below (A/B and tests)
+    g.tiled = 0;
+    g.tlx = g.tly = g.nbins = 0;
+    if (env_int("SDP_HIP_BUCKET2", 1) != 0 && env_int("SDP_HIP_BUCKET", 0) != kTileCoarse) {
+        int x0, nx_, y0, ny_;
+        window(amax, g.ngx, kTile, x0, nx_);
+        window(bmax, g.ngy, kTile, y0, ny_);
+        const int64_t nbins = (int64_t)(nx_ / kTile) * (ny_ / kTile) * g.nps;
+        if (nbins <= kMaxBins) {
+            g.tiled = 1;
+            g.wx0 = x0;
+            g.wnx = nx_;
+            g.wy0 = y0;
+            g.wny = ny_;
+            g.tlx = nx_ / kTile;
+            g.tly = ny_ / kTile;
+            g.nbins = (int)nbins;
+        }
+    }
+    if (!g.tiled) {
+        // x (rows) only: the y stride stays ngy, since a compacted y range
+        // packs the hot histogram counters of the uv core closer together and
+        // measured 2x slower count-pass atomics on C2
+        window(amax, g.ngx, kGridAlign, g.wx0, g.wnx);
         g.wy0 = 0;
         g.wny = g.ngy;
     }
@@ -2872,7 +3511,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // SDP_HIP_BUCKET=16 forces the latter (tests of the large-grid path)
     {
         const int64_t cell = (int64_t)g.wnx * g.wny * g.nps;
-        g.sub = cell <= kMaxCellKeys ? kTileCell : kTileCoarse;
+        g.sub = (g.tiled || cell <= kMaxCellKeys) ? kTileCell : kTileCoarse;
         if (env_int("SDP_HIP_BUCKET", 0) == kTileCoarse) g.sub = kTileCoarse;
     }
     g.nty = g.wny / g.sub;
@@ -2935,15 +3574,23 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // (k_subsort_pad; budgeted at 1.35x -- C4's top channels pad to <= 1.5x
     // one channel at a time, less over a batch of channels)
     P.subpad = grid_mode && g.sub == kTileCoarse && env_int("SDP_HIP_SUBSORT_PAD", 1) != 0;
-    const double rec_bytes = P.f64      ? sizeof(VisRec64)
-                             : P.subpad ? sizeof(RecC) + 1 + 1.35 * sizeof(RecC)
-                                        : sizeof(VisRec);
+    // two-level plans: the bin-ordered records + their cell keys, then the
+    // final (for the invert 4-padded, ~1.05x) copy
+    const double tiled_rec = P.f64 ? sizeof(VisRec64) : grid_mode ? sizeof(RecC) : sizeof(VisRec);
+    const double rec_bytes = g.tiled     ? 2.1 * tiled_rec + sizeof(uint16_t) - sizeof(unsigned)
+                             : P.f64     ? sizeof(VisRec64)
+                             : P.subpad  ? sizeof(RecC) + 1 + 1.35 * sizeof(RecC)
+                                         : sizeof(VisRec);
     // buffers of the other kind of plan are freed, not left cached: the plane
     // budget below counts the held record buffers as reusable
     if (!P.subpad) {
         Workspace::get().drop(ws_name("recs_pad"));
         Workspace::get().drop(ws_name("rec_cls"));
     }
+    for (const char *n : {"recs_a", "rec_lkey", "t_m1", "t_m2", "t_tot", "t_cbase"})
+        if (!g.tiled) Workspace::get().drop(ws_name(n));
+    for (const char *n : {"key_rank", "hist", "offs", "gsum", "gofs"})
+        if (g.tiled) Workspace::get().drop(ws_name(n));
     if (grid_mode) Workspace::get().drop(ws_name("degrid_acc"));
     {
         // a record buffer held much larger than this plan needs (a predict's
@@ -2954,10 +3601,12 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         if (Workspace::get().held(ws_name("recs")) > want + want / 4 + ((size_t)256 << 20))
             Workspace::get().drop(ws_name("recs"));
     }
+    const size_t hist_bytes =
+        g.tiled ? ((size_t)nvis / kTChunk + 2 * (size_t)g.nbins + 512) * kBinCells * sizeof(unsigned)
+                : (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned);
     const size_t need_other =
         (size_t)((double)nvis * (rec_bytes + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2)))) +
-        (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned) +
-        (size_t)P.fft_planes * spec_plane;
+        hist_bytes + (size_t)P.fft_planes * spec_plane;
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
     P.chunk_planes = std::min(cp, g.nplanes);
     P.fft_planes = std::min(P.fft_planes, P.chunk_planes);
@@ -2980,6 +3629,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     P.pad4 = grid_mode && g.sub == kTileCell && !P.f64;
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
     P.pt.nvis = nvis;
+    if (g.tiled) return P;  // (records: bucket_tiled, once their padded count is known)
     P.recs = P.f64      ? scratch<VisRec>("recs", 2 * std::max<int64_t>(nvis, 1))  // VisRec64
              : P.subpad ? scratch<VisRec>("recs", (std::max<int64_t>(nvis, 1) + 1) / 2 + 1)  // RecC
                         : scratch<VisRec>("recs", std::max<int64_t>(nvis, 1));
@@ -3336,6 +3986,7 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
     info->bucket = P.g.sub;
     info->padded = (P.pad4 || P.subpad) ? 1 : 0;
     info->fp64 = P.f64 ? 1 : 0;
+    info->tiled = P.g.tiled;
     info->grid_launches = (P.g.nplanes + P.chunk_planes - 1) / P.chunk_planes;
 }
 
@@ -3449,6 +4100,160 @@ static void screen_adj(const Plan &P, const double *dirty, int64_t sx, int64_t s
     SDP_HIP_CHECK(hipGetLastError());
 }
 
+static int cu_count() {
+    static std::mutex mu;
+    static std::map<int, int> cus;
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cus.find(dev);
+    if (it != cus.end()) return it->second;
+    int n = 0;
+    SDP_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    cus[dev] = std::max(n, 1);
+    return cus[dev];
+}
+
+// Two-level bucketing of a tiled one-cell plan (k_t_count .. k_t_final):
+// the count pass, bins, value pass, cell counts and bases, then (one host
+// sync: the metadata, which sizes the final record array) the cell bases,
+// pads, work items and the move of every record to its cell.  The weight
+// sums go to `slots` (count pass; value pass when values_only).  values_only
+// (SDP_HIP_REUSE_BUCKETS): the kept plan's bins, chunks and cell bases are
+// valid, so only the value pass and the final move run.
+static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st,
+                         bool values_only, const std::function<void()> &after_clear,
+                         double *slots) {
+    const Geo &g = P.g;
+    Part &pt = P.pt;
+    const int nb = g.nbins;
+    const int kind = P.f64 ? 2 : (grid_mode ? 0 : 1);
+    const size_t rsz = kind == 2 ? sizeof(VisRec64) : kind == 0 ? sizeof(RecC) : sizeof(VisRec);
+    const int64_t nvis = pt.nvis;
+    const size_t lds_bins = (size_t)nb * sizeof(unsigned);
+    if (!values_only) {
+        pt.t_g1 = 2 * cu_count();
+        pt.t_vpw = std::max<int64_t>(kTThreads, (nvis + pt.t_g1 - 1) / pt.t_g1);
+        pt.t_vpw = (pt.t_vpw + 63) / 64 * 64;
+        pt.t_g1 = (int)std::max<int64_t>(1, (nvis + pt.t_vpw - 1) / pt.t_vpw);
+        pt.t_maxch = (unsigned)std::min<int64_t>((int64_t)nb * kTMaxChunksPerBin,
+                                                 nvis / kTChunk + nb) + 1;
+        pt.t_binc = scratch<unsigned>("t_binc", nb);
+        pt.t_binbase = scratch<unsigned>("t_binbase", nb + 1);
+        pt.t_chbase = scratch<unsigned>("t_chbase", nb);
+        pt.t_nchb = scratch<unsigned>("t_nchb", nb);
+        pt.t_nbl = scratch<unsigned>("t_nbl", nb + 1);
+        pt.t_meta_ch = scratch<unsigned>("t_meta_ch", 2);
+        pt.t_npad = scratch<unsigned>("t_npad", 1);
+        pt.t_chunks = scratch<TChunk>("t_chunks", pt.t_maxch);
+        pt.t_binsum = scratch<unsigned long long>("t_binsum", nb);
+        pt.t_bofs = scratch<unsigned long long>("t_bofs", nb + 1);
+        pt.t_m1 = scratch<unsigned>("t_m1", (size_t)pt.t_g1 * nb);
+        pt.t_m2 = scratch<unsigned>("t_m2", (size_t)pt.t_maxch * kBinCells);
+        pt.t_tot = scratch<unsigned>("t_tot", (size_t)nb * kBinCells);
+        pt.t_cbase = scratch<unsigned>("t_cbase", (size_t)nb * kBinCells);
+        pt.t_lkey = scratch<uint16_t>("rec_lkey", std::max<int64_t>(nvis, 1));
+        pt.t_a = scratch<char>("recs_a", (size_t)std::max<int64_t>(nvis, 1) * rsz);
+        pt.nbad = scratch<unsigned long long>("nbad", 1);
+        pt.meta = scratch<unsigned>("meta", g.nps + 6);
+        SDP_HIP_CHECK(hipMemsetAsync(pt.t_binc, 0, nb * sizeof(unsigned), st));
+        SDP_HIP_CHECK(hipMemsetAsync(pt.t_binsum, 0, nb * sizeof(unsigned long long), st));
+        SDP_HIP_CHECK(hipMemsetAsync(pt.nbad, 0, sizeof(unsigned long long), st));
+        SDP_HIP_CHECK(hipMemsetAsync(pt.t_npad, 0, sizeof(unsigned), st));
+        if (after_clear) after_clear();
+    }
+    const int cus = cu_count();
+    const unsigned gch = std::min<unsigned>(pt.t_maxch, 4u * (unsigned)cus);
+    auto scatter = [&](double *sl) {
+        auto go = [&](auto vt_tag, auto kind_tag, auto grid_tag) {
+            using VT = typename decltype(vt_tag)::type;
+            constexpr int K = decltype(kind_tag)::value;
+            constexpr bool G = decltype(grid_tag)::value;
+            k_t_scatter<VT, K, G><<<pt.t_g1, kTThreads, lds_bins, st>>>(
+                g, nvis, pt.t_vpw, in.uvw, in.uvw_rs, in.freq,
+                G ? static_cast<const VT *>(in.vis) : nullptr, in.vrs, in.vcs, in.wgt, in.wrs,
+                in.wcs, in.x, sl, pt.t_binbase, pt.t_m1, pt.t_a, pt.t_lkey);
+        };
+        auto by_kind = [&](auto vt_tag) {
+            if (kind == 2) {
+                if (grid_mode) go(vt_tag, std::integral_constant<int, 2>{}, std::true_type{});
+                else go(vt_tag, std::integral_constant<int, 2>{}, std::false_type{});
+            } else if (kind == 0) {
+                go(vt_tag, std::integral_constant<int, 0>{}, std::true_type{});
+            } else {
+                go(vt_tag, std::integral_constant<int, 1>{}, std::false_type{});
+            }
+        };
+        if (in.vis_dtype == SDP_HIP_C128) by_kind(TypeTag<double2>{});
+        else by_kind(TypeTag<float2>{});
+    };
+    auto final_move = [&] {
+        if (kind == 2)
+            k_t_final<2><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
+                                                     pt.t_cbase, pt.t_a, P.recs);
+        else if (kind == 0)
+            k_t_final<0><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
+                                                     pt.t_cbase, pt.t_a, P.recs);
+        else
+            k_t_final<1><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
+                                                     pt.t_cbase, pt.t_a, P.recs);
+        SDP_HIP_CHECK(hipGetLastError());
+    };
+    if (values_only) {
+        if (nvis > 0) {
+            scatter(slots);
+            final_move();
+        }
+        return;
+    }
+    if (nvis > 0)
+        k_t_count<<<pt.t_g1, kTThreads, lds_bins, st>>>(g, nvis, pt.t_vpw, in.uvw, in.uvw_rs,
+                                                        in.freq, in.wgt, in.wrs, in.wcs, in.x,
+                                                        slots, pt.t_binc, pt.t_m1, pt.nbad);
+    k_t_bins<<<1, kTThreads, 0, st>>>(nb, pt.t_binc, pt.t_binbase, pt.t_chbase, pt.t_nchb,
+                                      pt.t_nbl, pt.t_chunks, pt.t_meta_ch);
+    if (nvis > 0) scatter(nullptr);
+    k_t_cellcount<<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2);
+    const unsigned gcol = (unsigned)std::min<int64_t>((int64_t)nb * (kBinCells / 256), 8192);
+    if (P.pad4)
+        k_t_cellcol<true><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_chbase, pt.t_nchb, pt.t_m2,
+                                                pt.t_tot, P.chunk, pt.t_binsum, pt.t_npad);
+    else
+        k_t_cellcol<false><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_chbase, pt.t_nchb, pt.t_m2,
+                                                 pt.t_tot, P.chunk, pt.t_binsum, pt.t_npad);
+    k_t_binscan<<<1, kTThreads, 0, st>>>(nb, g.tlx * g.tly, g.nps, pt.t_binsum, pt.t_binbase,
+                                         pt.nbad, pt.t_bofs, pt.meta);
+    SDP_HIP_CHECK(hipGetLastError());
+    if (slots) k_sum_slots<<<1, 64, 0, st>>>(slots, in.x.sumwt);
+    // the metadata (one sync): out-of-grid check, record / item counts, the
+    // first item of each first plane, the padded record total
+    const int nps = g.nps;
+    const size_t per = (size_t)nps + 6;
+    unsigned *m = pinned_host<unsigned>(64, per);
+    SDP_HIP_CHECK(hipMemcpyAsync(m, pt.meta, per * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    SDP_HIP_CHECK(hipStreamSynchronize(st));
+    const unsigned long long nbad = (unsigned long long)m[0] | ((unsigned long long)m[1] << 32);
+    SDP_REQUIRE(nbad == 0,
+                "visibilities outside the padded grid (or, in a batched invert, outside the "
+                "sequence's bounds)");
+    pt.nrec = m[2];
+    pt.nitems = m[3];
+    pt.p0_items.assign(m + 4, m + 4 + nps + 1);
+    const size_t ntot = (size_t)m[5 + nps];
+    P.recs = reinterpret_cast<VisRec *>(scratch<char>("recs", (ntot + 1) * rsz));
+    pt.fitems = scratch<FineItem>("fitems", (size_t)pt.nitems + 1);
+    const unsigned gfin = (unsigned)std::min(nb, 4096);
+    if (P.pad4)
+        k_t_cellfin<true><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
+                                                pt.t_cbase, reinterpret_cast<RecC *>(P.recs),
+                                                pt.fitems);
+    else
+        k_t_cellfin<false><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
+                                                 pt.t_cbase, nullptr, pt.fitems);
+    if (nvis > 0) final_move();
+    SDP_HIP_CHECK(hipGetLastError());
+}
+
 // Bucketing with the fused weight sum (slots zeroed before the count pass,
 // folded into *sumwt after it), then the metadata read back by the host.
 // `after_clear` runs once the histogram clearing is queued (work put on
@@ -3457,6 +4262,10 @@ static void bucket_all(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st
                        const std::function<void()> &after_clear = nullptr) {
     double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
     if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
+    if (P.g.tiled) {  // (reads its metadata itself)
+        bucket_tiled(P, in, grid_mode, st, false, after_clear, slots);
+        return;
+    }
     bucket_part(P, in, grid_mode, st, false, after_clear);
     if (slots) k_sum_slots<<<1, 64, 0, st>>>(slots, in.x.sumwt);
     read_part_meta(P, st);
@@ -3533,7 +4342,10 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     SDP_REQUIRE(in.bounds == nullptr || !(keep || reuse),
                 "batched inverts do not keep or reuse bucketings");
     Inputs inx = in;
-    inx.x.all = keep;
+    // a kept bucketing holds every in-grid visibility (zero weights add exact
+    // zeros); its reuse classifies them the same way (the two-level value
+    // pass re-derives the bin ranks from that classification)
+    inx.x.all = keep || reuse;
     Plan P = reuse ? reuse_buckets(in) : plan_geometry(inx, true, st);
     const Geo &g = P.g;
     // batched invert: planes zeroed by the first batch, FFT + screens by the
@@ -3565,7 +4377,8 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
         // value pass only (weight sums included)
         double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
         if (slots) SDP_HIP_CHECK(hipMemsetAsync(slots, 0, kSumSlots * sizeof(double), st));
-        bucket_part(P, inx, true, st, true);
+        if (P.g.tiled) bucket_tiled(P, inx, true, st, true, nullptr, slots);
+        else bucket_part(P, inx, true, st, true);
         if (slots) k_sum_slots<<<1, 64, 0, st>>>(slots, in.x.sumwt);
     } else {
         bucket_all(P, inx, true, st, start_zero);

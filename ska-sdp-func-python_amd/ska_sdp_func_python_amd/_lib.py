@@ -64,6 +64,7 @@ class WGridInfo(ctypes.Structure):
         ("grid_launches", c_int),
         ("padded", c_int),
         ("fp64", c_int),
+        ("tiled", c_int),
     ]
 
     def as_dict(self):

@@ -35,15 +35,18 @@ def _problem(seed, nrow=300, nchan=3, umax=2000.0, frac=0.45):
     return uvw, freq, ms, wgt, frac / umax
 
 
-@pytest.fixture(params=["fine", "coarse"])
+@pytest.fixture(params=["fine", "fine1", "coarse"])
 def bucket(request, monkeypatch):
-    """Both bucketings: one-cell buckets (4-padded for the invert's MFMA
-    gridder, plain for the MFMA degridder), the default at these sizes, and
-    16x16-cell buckets sub-sorted by cell per work item (the path of very
-    large grids such as C4's 16384^2 x 70 planes, forced here by
-    SDP_HIP_BUCKET=16)."""
+    """Every bucketing: one-cell buckets (4-padded for the invert's MFMA
+    gridder, plain for the MFMA degridder) from the two-level LDS-histogram
+    sort (k_t_*, the default at these sizes), the same buckets from the
+    single-level global histogram (SDP_HIP_BUCKET2=0), and 16x16-cell buckets
+    sub-sorted by cell per work item (the path of very large grids such as
+    C4's 16384^2 x 70 planes, forced here by SDP_HIP_BUCKET=16)."""
     if request.param == "coarse":
         monkeypatch.setenv("SDP_HIP_BUCKET", "16")
+    if request.param == "fine1":
+        monkeypatch.setenv("SDP_HIP_BUCKET2", "0")
     return request.param
 
 
@@ -60,6 +63,7 @@ def test_ms2dirty_matches_exact(dow, vdt, flip, bucket):
                                  cell * 0.9, 1e-7, dow, flip_uw=flip)
     assert info["support"] == 8
     assert info["bucket"] == (16 if bucket == "coarse" else 1)
+    assert info["tiled"] == (1 if bucket == "fine" else 0)
     assert info["padded"] == 1  # invert: k_grid_mfma_pad on 4-padded cells
     assert info["grid_launches"] == 1
     assert rel_rms(out.cpu().numpy(), ex) < TOL
