@@ -43,7 +43,9 @@ double_precision_accumulation); ``precision="fp32"`` (beyond the reference)
 serves such requests with the fp32 NUFFT at its floor (W = 8, ~1e-6).
 """
 
+import contextlib
 import logging
+import os
 
 import numpy as np
 import torch
@@ -61,6 +63,17 @@ def _vis_to_im(model, freq):
 
 def _pixsize(model):
     return float(np.abs(np.radians(model.image_acc.wcs.wcs.cdelt[0])))
+
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """The second stream of a pipelined invert (one per device)."""
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(dev)
+    return s
 
 
 def _rank_rows(uvw, freq, npix, pixsize, epsilon, precision, shard):
@@ -237,11 +250,30 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     sumwt_d = torch.zeros((nchan, npol), dtype=torch.float64, device=dev)
     vis_to_im = _vis_to_im(model, freq)
 
-    # the image pols of one channel range share one bucketing: the first pol
-    # keeps it, the others only re-run the value pass (SDP_HIP_REUSE_BUCKETS)
-    share = npol > 1 and not dopsf
+    # the (pol, channel) images the reference loops over (ng.py:236-289): all
+    # pols of the band for MFS, channel-major per visibility channel else
+    # (each image is independent, so the order does not matter)
+    if mfs:
+        calls = [(pol, slice(0, nloc), 0) for pol in range(npol if nloc > 0 else 0)]
+    else:
+        calls = [(pol, slice(vchan - lo, vchan - lo + 1), int(vis_to_im[vchan]))
+                 for vchan in range(lo, hi) for pol in range(npol)]
+    grid_calls = [c for c in calls if not (dopsf and c[0] != 0)]
+    # Two or more NUFFT calls are pipelined: consecutive calls alternate
+    # between two streams and the library's two scratch slots, so call k+1's
+    # bucketing runs under call k's gridding and FFT (SDP_HIP_OVERLAP=0: one
+    # stream).  Otherwise the image pols of one channel range share one
+    # bucketing: the first pol keeps it, the others re-run only the value pass
+    # (SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS).
+    overlap = len(grid_calls) > 1 and dev.type == "cuda" and \
+        os.environ.get("SDP_HIP_OVERLAP", "1") != "0"
+    share = npol > 1 and not dopsf and not overlap
+    main = torch.cuda.current_stream(dev) if overlap else None
+    side = _side_stream(dev) if overlap else None
+    if overlap:
+        side.wait_stream(main)
 
-    def grid_pol(pol, chans, ichan):
+    def grid_pol(pol, chans, ichan, k):
         sw = sumwt_d[ichan, pol:pol + 1]
         if dopsf and pol != 0:
             # PSF: pol 0 holds unit visibilities, the others are zero and are
@@ -250,24 +282,25 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
             sw += (wgt[:, chans, pol].to(torch.float64) * m).sum()
             return
         coef = None if (dopsf or conv is None) else conv[pol]
-        _, info = kernels.ms2dirty_vis(
-            uvw, freq_t[chans], None if dopsf else ms[:, chans, :], pol, wgt[:, chans, pol],
-            flags[:, chans, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
-            do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
-            accumulate=True, sumwt=sw, shift_lmn=lmn, keep_buckets=share and pol == 0,
-            reuse_buckets=share and pol > 0, precision=precision)
+        ctx = torch.cuda.stream(side if k % 2 else main) if overlap else contextlib.nullcontext()
+        with ctx:
+            _, info = kernels.ms2dirty_vis(
+                uvw, freq_t[chans], None if dopsf else ms[:, chans, :], pol, wgt[:, chans, pol],
+                flags[:, chans, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
+                do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
+                accumulate=True, sumwt=sw, shift_lmn=lmn, keep_buckets=share and pol == 0,
+                reuse_buckets=share and pol > 0, precision=precision,
+                slot=(k % 2) if overlap else 0)
         if verbosity:
             log.info("invert_ng: %s", info)
 
-    if mfs:
-        for pol in range(npol if nloc > 0 else 0):
-            grid_pol(pol, slice(0, nloc), 0)
-    else:
-        # channel-major (the reference loops pol-major, ng.py:259-289; each
-        # (pol, chan) image is independent, so the order does not matter)
-        for vchan in range(lo, hi):
-            for pol in range(npol):
-                grid_pol(pol, slice(vchan - lo, vchan - lo + 1), int(vis_to_im[vchan]))
+    k = 0
+    for pol, chans, ichan in calls:
+        grid_pol(pol, chans, ichan, k)
+        if not (dopsf and pol != 0):
+            k += 1
+    if overlap:
+        main.wait_stream(side)
     if shard:
         # the one exchange: partial images and weight sums of the ranks'
         # channel blocks (before normalise_sumwt, ng.py:292)

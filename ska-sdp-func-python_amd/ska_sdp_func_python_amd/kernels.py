@@ -266,7 +266,7 @@ _FLAG_DT = {torch.int64: 8, torch.int32: 4, torch.int8: 1, torch.uint8: 1, torch
 def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_x, pixsize_y,
                  epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None, out_strides=None,
                  accumulate=False, sumwt=None, shift_lmn=None, keep_buckets=False,
-                 reuse_buckets=False, precision=None):
+                 reuse_buckets=False, precision=None, slot=0):
     """ms2dirty with invert_ng's visibility prologue fused in
     (sdp_hip_ms2dirty_vis): ``vis`` [nrow, nchan, npol_vis] complex (any
     strides, read in place; None = unit visibilities), ``flags`` the same
@@ -278,7 +278,9 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
     ``keep_buckets`` buckets every in-grid visibility and keeps the bucketing
     on the device; a following call with ``reuse_buckets`` and the same uvw,
     freq and geometry (another image pol) runs only the value pass, gridding
-    and FFT (SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS)."""
+    and FFT (SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS).  ``slot=1`` uses
+    the library's second scratch set (SDP_HIP_SLOT1; not with kept / reused
+    buckets): calls alternated between two streams and slots overlap."""
     pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
     dev = uvw.device
@@ -321,7 +323,7 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
     bits = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
             | pbits)
     bits |= (_lib.SDP_HIP_KEEP_BUCKETS if keep_buckets else 0) | \
-        (_lib.SDP_HIP_REUSE_BUCKETS if reuse_buckets else 0)
+        (_lib.SDP_HIP_REUSE_BUCKETS if reuse_buckets else 0) | (_lib.SDP_HIP_SLOT1 if slot else 0)
     info = _lib.WGridInfo()
     _lib.call(
         "sdp_hip_ms2dirty_vis",

@@ -31,7 +31,7 @@ ROWS = set()  # rows (their u) this process gridded
 def _oracle_ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, px, py,
                          epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
                          out_strides=None, accumulate=False, sumwt=None, shift_lmn=None,
-                         keep_buckets=False, reuse_buckets=False, precision=None):
+                         keep_buckets=False, reuse_buckets=False, precision=None, slot=0):
     assert shift_lmn is None
     SEEN.update(freq.numpy().tolist())
     ROWS.update(np.round(uvw.numpy()[:, 0], 6).tolist())
