@@ -53,6 +53,8 @@ FP32_PEAK_TFLOPS = 157.3       # fp32 vector (packed FMA) peak
 NCHAN_PER_GPU, NTIMES, NPIX = 64, 100, 4096
 F_LO, F_HI = 0.95e9, 1.76e9
 EPS_REQUESTED = 1e-7  # the fp32 NUFFT, W = 8 (epsilon < 1e-7 selects fp64)
+EPS_REFERENCE = 1e-12  # invert_ng's default (ng.py:178): the fp64 NUFFT, W = 13
+FP64_PEAK_TFLOPS = 78.6       # fp64 vector = fp64 matrix peak on gfx950
 
 
 def parse():
@@ -219,6 +221,124 @@ def api_rates(args, obs, cell):
             "host_visibility_Mvis_s": round(nvis / t_host / 1e6, 1),
             "note": "reference-shaped invert_ng on a c128/f64/int64 Visibility; the host "
                     "figure includes the H2D copies of ~5 GB (PCIe-inclusive) and the image D2H"}
+
+
+def _timed_calls(fn, steps, warmup, dev):
+    """Wall time of `steps` calls of fn (after `warmup`), one stream, then one
+    more call with the C ABI's stage timing on (HIP events around every
+    stage on the launch stream) for its stage times."""
+    from ska_sdp_func_python_amd import kernels
+    kernels.set_stage_timing(False)
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / steps
+    kernels.set_stage_timing(True)
+    infos = [fn()[1] for _ in range(2)]
+    kernels.set_stage_timing(False)
+    return el, infos[-1]
+
+
+def c2_predict_and_fp64(args, obs, cell, dev, cpu):
+    """Two more C2 objects (SURVEY.md §8 a2 and the reference's default
+    precision), each with its own roofline and CPU baseline:
+
+    * c2_predict -- dirty2ms (predict_ng's NUFFT, ng.py:95-129) of a random
+      4096^2 model onto the 123.6 Mvis at epsilon 1e-7 (fp32, W = 8);
+      roofline of the degridder k_degrid_mfma: the same algorithmic bytes as
+      the gridder (12.375 B per visibility + the planes read once);
+      cpu_baseline = oracle/wgrid_cpu.c dirty2ms (fp32, W = 8).
+    * c2_fp64 -- ms2dirty at the reference's default epsilon 1e-12 (ng.py:178,
+      double_precision_accumulation=True): the fp64 NUFFT (W = 13, c128
+      planes, fp64 taps); roofline of k_grid_f64 against HBM and against the
+      fp64 peak (4 W^3 flops per visibility); cpu_baseline = the fp64
+      variant of the C2 CPU baseline (same restatement at W = 13)."""
+    from ska_sdp_func_python_amd import kernels
+    nvis = obs["nrow"] * obs["freq"].shape[0]
+    nchan = obs["freq"].shape[0]
+    g = torch.Generator(device=dev)
+    g.manual_seed(77)
+    img = torch.randn((args.npix, args.npix), generator=g, device=dev, dtype=torch.float64)
+    vout = torch.empty((obs["nrow"], nchan), dtype=torch.complex64, device=dev)
+
+    def pred():
+        return kernels.dirty2ms(obs["uvw"], obs["freq"], img, None, cell, cell, EPS_REQUESTED,
+                                True, flip_uw=True, out=vout)
+    el, info = _timed_calls(pred, args.steps, 2, dev)
+    alg = nvis * (8 + 4 + 24.0 / nchan) + info["nplanes"] * info["ngrid_x"] * info["ngrid_y"] * 8
+    kms = info["ms_grid"] / max(1, info["grid_launches"])
+    ach = alg / max(1, info["grid_launches"]) / (kms * 1e-3) / 1e9
+    pcpu = None
+    if args.cpu_chans > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import wgrid_cpu
+        nch = max(1, args.cpu_chans // 2)
+        idx = np.linspace(0, nchan - 1, nch).round().astype(int)
+        uvw_h = obs["uvw"].cpu().numpy() * np.array([-1.0, 1.0, -1.0])
+        f_h = obs["freq"].cpu().numpy()[idx]
+        threads = cpu["cores"] if cpu else min(16, len(os.sched_getaffinity(0)))
+        t0 = time.perf_counter()
+        _, tg, tf = wgrid_cpu.dirty2ms(uvw_h, f_h, img.cpu().numpy(), None, cell, cell,
+                                       EPS_REQUESTED, True, nthreads=threads, precision="single")
+        wall = time.perf_counter() - t0
+        t_full = (wall - tf) * nvis / (uvw_h.shape[0] * nch) + tf
+        pcpu = {"value": round(nvis / t_full / 1e6, 4), "unit": "Mvis/s", "cores": threads,
+                "kind": "port",
+                "sample": f"oracle/wgrid_cpu.c dirty2ms (fp32, W=8) on {nch} of {nchan} channels "
+                          f"({uvw_h.shape[0] * nch / 1e6:.2f} Mvis): {wall:.1f} s wall, {tf:.1f} s "
+                          "FFT+screen; degridding scaled to all visibilities + FFT/screen once"}
+    predict = {
+        "metric": "Mvis/s degridded (predict, 8k^2 w-stack grid)", "value": round(nvis / el / 1e6, 3),
+        "unit": "Mvis/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": round(el * 1e3, 3),
+        "higher_is_better": True, "dtype": "f32",
+        "config": {"workload": "C2 predict: dirty2ms of a 4096^2 model onto 123.6 Mvis, 8192^2 "
+                               "w-stack grid, epsilon 1e-7 (W = 8)", "nplanes": info["nplanes"]},
+        "stages_ms": {k: round(float(info[k]), 3) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": f"k_degrid_mfma<{info['support']},true>", "kernel_ms": round(kms, 4),
+                     "alg_bytes_per_launch": int(alg / max(1, info["grid_launches"]))},
+        "cpu_baseline": pcpu}
+    del vout
+    out = torch.empty((args.npix, args.npix), dtype=torch.float64, device=dev)
+
+    def inv64():
+        return kernels.ms2dirty(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], args.npix, args.npix,
+                                cell, cell, EPS_REFERENCE, True, flip_uw=True, out=out)
+    el, info = _timed_calls(inv64, max(2, args.extra_steps), 1, dev)
+    W = info["support"]
+    alg = nvis * (8 + 4 + 24.0 / nchan) + info["nplanes"] * info["ngrid_x"] * info["ngrid_y"] * 16
+    kms = info["ms_grid"] / max(1, info["grid_launches"])
+    ach = alg / max(1, info["grid_launches"]) / (kms * 1e-3) / 1e9
+    tfl = nvis * 4 * W ** 3 / (info["ms_grid"] * 1e-3) / 1e12
+    c64 = None
+    if cpu and len(cpu.get("variants", [])) > 1:
+        v = cpu["variants"][1]
+        c64 = {"value": v["value"], "unit": "Mvis/s", "cores": v["cores"], "kind": "port",
+               "sample": "oracle/wgrid_cpu.c at the reference's precision (fp64, W = "
+                         f"{v['support']}, {v['nplanes']} planes), {v['sample']}"}
+    fp64 = {
+        "metric": METRIC + " at the reference's default epsilon 1e-12 (fp64 NUFFT)",
+        "value": round(nvis / el / 1e6, 3), "unit": "Mvis/s", "n_gpus": 1,
+        "steps": max(2, args.extra_steps), "ms_per_step": round(el * 1e3, 3),
+        "higher_is_better": True, "dtype": "f64",
+        "config": {"workload": "C2 invert at epsilon 1e-12: 123.6 Mvis, 4096^2 image, 8192^2 "
+                               "w-stack grid", "support": W, "nplanes": info["nplanes"],
+                   "epsilon_requested": EPS_REFERENCE, "fp64": info["fp64"]},
+        "stages_ms": {k: round(float(info[k]), 3) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
+        "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": f"k_grid_f64<{W},true>", "kernel_ms": round(kms, 4),
+                     "alg_bytes_per_launch": int(alg / max(1, info["grid_launches"])),
+                     "compute": {"achieved": round(tfl, 2), "peak": FP64_PEAK_TFLOPS,
+                                 "unit": "TFLOP/s", "frac": round(tfl / FP64_PEAK_TFLOPS, 4),
+                                 "note": "4 W^3 fp64 flops per visibility"}},
+        "cpu_baseline": c64}
+    return {"c2_predict": predict, "c2_fp64": fp64}
 
 
 # ---------------------------------------------------------------------------
@@ -866,6 +986,7 @@ def main():
 
     extra = {}
     if world == 1 and not args.no_extra:
+        extra.update(c2_predict_and_fp64(args, obs, cell, dev, cpu))
         # the other configurations, each timed on its own (free the C2 inputs
         # first: the whole-band C4 needs ~250 GB of HBM)
         del obs
