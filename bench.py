@@ -830,7 +830,7 @@ def run_c5(args, world, rank, dev, sub=False):
         "value": round(nsub / (elapsed / steps), 1), "unit": "solves/s",
         "n_gpus": world, "steps": steps, "warmup": warmup,
         "ms_per_step": round(elapsed / steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "f64 (c128 gains)",
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64 arithmetic, x/w fp32 storage (c128 gains)",
         "data": "synthetic: true gains lognormal(0, 0.1) x exp(i N(0, 0.1)) per (time, station, "
                 "chan), x_b = g_a1 conj(g_a2), unit weights, generated on device per batch "
                 "outside the timed segments",

@@ -275,6 +275,139 @@ def test_c4_shard_invert_predict_at_full_size():
     assert e_px < TOL
 
 
+def _c4_band(dev):
+    """C4's rows (SKA-LOW 512 stations x 400 times, uvw resident), the band's
+    256 frequencies and the cell -- bench.py run_c4's setup."""
+    from ska_sdp_func_python_amd import simulation
+    obs = simulation.device_observation(400, 1, 50e6, 350e6, config="LOW", device=dev,
+                                        nchan_total=256, channels=[0])
+    del obs["vis"], obs["wgt"]
+    return obs["uvw"], obs["nrow"], np.linspace(50e6, 350e6, 256), 0.25 / obs["umax"]
+
+
+def _point_vis(uvw, freq, l0, m0, rows=2_000_000):
+    """Visibilities of a unit point source at (l0, m0) in the ducc0 frame of
+    an invert with flip_uw (u, w negated): dirty[x0, y0] = sum(w) / n0."""
+    n0 = math.sqrt(1.0 - l0 * l0 - m0 * m0)
+    out = torch.empty((uvw.shape[0], freq.shape[0]), dtype=torch.complex64, device=uvw.device)
+    s = freq.to(torch.float64)[None, :] / 299792458.0
+    for a in range(0, uvw.shape[0], rows):
+        u = uvw[a:a + rows]
+        d = (-u[:, 0:1] * l0 + u[:, 1:2] * m0 + u[:, 2:3] * (n0 - 1.0)) * s
+        d = d - torch.round(d)
+        out[a:a + rows] = torch.polar(torch.ones_like(d), -2.0 * math.pi * d).to(torch.complex64)
+    return out
+
+
+def _c4_streamed_checks(tag, uvw, freqs, batches, vis_of, npix, cell, npx=6, seed=90):
+    """The streamed (sdp_hip_ms2dirty_batch) invert of `batches` against
+    exact direct sums at sampled pixels (accumulated per batch on the host),
+    adjointness <A x, y> = Re <x, A^H y> over every visibility, and a unit
+    point source (peak pixel and value sum(w)/n0)."""
+    import wgrid_cpu
+    from ska_sdp_func_python_amd import kernels, parallel
+    dev = uvw.device
+    f_all = torch.as_tensor(freqs, device=dev)
+    nvis = uvw.shape[0] * sum(e - a for a, e in batches)
+    d = parallel.invert_batched_shard(uvw, f_all, vis_of, batches, npix, cell, 1e-7, True,
+                                      flip_uw=True)  # RASCIL [y, x]
+    print(f"\n{tag}: streamed invert of {nvis / 1e9:.2f} Gvis in {len(batches)} batches done",
+          flush=True)
+    rng = np.random.default_rng(seed)
+    px = np.concatenate([[npix // 2], rng.integers(npix // 8, 7 * npix // 8, npx - 1)])
+    py = np.concatenate([[npix // 2 - 3], rng.integers(npix // 8, 7 * npix // 8, npx - 1)])
+    uvw_h = uvw.cpu().numpy() * FLIP_UW
+    ex = np.zeros(npx)
+    for i, (a, e) in enumerate(batches):
+        vis_h = vis_of(a, e).cpu().numpy()
+        ex += wgrid_cpu.exact_pixels(uvw_h, freqs[a:e], vis_h, None, npix, npix, cell, cell, True,
+                                     px, py, nthreads=_threads())
+        del vis_h
+        print(f"{tag}: exact pixels, batch {i + 1}/{len(batches)}", flush=True)
+    e_px = rel_rms(d.cpu().numpy()[py, px], ex)
+    # adjointness: a random sparse model (ducc0 [x, y]) degridded batch by batch
+    y = torch.zeros((npix, npix), dtype=torch.float64, device=dev)
+    iy = rng.integers(npix // 4, 3 * npix // 4, (2, 4096))
+    y[iy[0], iy[1]] = torch.as_tensor(rng.normal(size=4096), device=dev)
+    lhs = float(torch.sum(d.T * y))
+    rhs = 0.0
+    for a, e in batches:
+        v, _ = kernels.dirty2ms(uvw, f_all[a:e], y, None, cell, cell, 1e-7, True, flip_uw=True)
+        x = vis_of(a, e)
+        for r in range(0, uvw.shape[0], 4_000_000):
+            rhs += float(torch.sum((v[r:r + 4_000_000].to(torch.complex128).conj()
+                                    * x[r:r + 4_000_000].to(torch.complex128)).real))
+        del v, x
+    e_adj = abs(lhs - rhs) / abs(lhs)
+    # unit point source off the phase centre
+    x0, y0 = npix // 2 + 1200, npix // 2 - 700
+    l0, m0 = (x0 - npix // 2) * cell, (y0 - npix // 2) * cell
+    n0 = math.sqrt(1.0 - l0 * l0 - m0 * m0)
+    dp = parallel.invert_batched_shard(uvw, f_all,
+                                       lambda a, e: _point_vis(uvw, f_all[a:e], l0, m0), batches,
+                                       npix, cell, 1e-7, True, flip_uw=True)
+    k = int(torch.argmax(dp))
+    peak = float(dp.view(-1)[k]) * n0 / nvis
+    print(f"{tag}: exact pixels rel-RMS {e_px:.2e}; adjointness {e_adj:.2e}; point source peak "
+          f"at (y, x) {(k // npix, k % npix)} value n0/sum(w) x {peak:.8f}", flush=True)
+    assert e_px < TOL
+    assert e_adj < 5e-6
+    assert (k // npix, k % npix) == (y0, x0)
+    assert abs(peak - 1.0) < 1e-5
+
+
+@pytest.mark.timeout(1800)
+def test_c4_full_band_streamed_as_benchmarked():
+    """The c4_n1 object's exact form: all 256 channels of the SKA-LOW band
+    (13.4 Gvis) streamed through sdp_hip_ms2dirty_batch in bench.py's 8
+    channel batches (generated on device per batch, run_c4's seeds) into the
+    band's 71 resident 16384^2 planes, against exact sums, adjointness and a
+    point source -- the reference's per-channel loop (ng.py:259-289) gridded
+    as one streamed invert."""
+    dev = torch.device("cuda:0")
+    uvw, nrow, freqs, cell = _c4_band(dev)
+    nb = max(-(-256 // 40), math.ceil(nrow * 256 / 1.8e9))
+    assert nb == 8
+    cuts = [256 * i // nb for i in range(nb + 1)]
+    batches = list(zip(cuts[:-1], cuts[1:]))
+    gen = torch.Generator(device=dev)
+
+    def vis_of(a, e):
+        gen.manual_seed(a)
+        return torch.randn((nrow, e - a), generator=gen, device=dev, dtype=torch.complex64)
+
+    _c4_streamed_checks("C4 full band", uvw, freqs, batches, vis_of, 8192, cell, npx=4)
+
+
+@pytest.mark.timeout(1500)
+def test_c4_largest_w_rank_of_the_8way_row_partition():
+    """Rank 7 of bench.py's default 8-GPU C4 partition (rows by w,
+    parallel.wrow_partition: the interval of the largest |w|, all 256
+    channels, its own plane layout) at full size, as run_c4 streams it."""
+    from ska_sdp_func_python_amd import kernels, parallel
+    dev = torch.device("cuda:0")
+    uvw, nrow, freqs, cell = _c4_band(dev)
+    f_all = torch.as_tensor(freqs, device=dev)
+    lay = kernels.wstack_layout(kernels.uvw_bounds(uvw, f_all), 8192, 8192, cell, cell, 1e-7, True,
+                                flip_uw=True)
+    order, cuts, _ = parallel.wrow_partition((-uvw[:, 2]).cpu().numpy(), freqs, 8, lay["dw"],
+                                             lay["support"])
+    rows = torch.as_tensor(order[cuts[7]:cuts[8]], device=dev)
+    u7 = uvw[rows].contiguous()
+    del uvw, rows
+    n7 = u7.shape[0]
+    nb = max(1, math.ceil(n7 * 256 / 1.8e9))
+    cb = [256 * i // nb for i in range(nb + 1)]
+    batches = list(zip(cb[:-1], cb[1:]))
+    gen = torch.Generator(device=dev)
+
+    def vis_of(a, e):
+        gen.manual_seed(7919 * 7 + a)
+        return torch.randn((n7, e - a), generator=gen, device=dev, dtype=torch.complex64)
+
+    _c4_streamed_checks(f"C4 wrow rank 7/8 ({n7} rows)", u7, freqs, batches, vis_of, 8192, cell)
+
+
 # ---------------------------------------------------------------------------
 # C5: StefCal 512 stations x 256 channels x 1000 times
 # ---------------------------------------------------------------------------
