@@ -180,13 +180,15 @@ struct Coord {
     bool skip = false;  // w slab: inside the sequence's layout, outside this slab
 };
 
-__device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restrict__ uvw,
-                                           int64_t rs, int64_t row, double f) {
+// the visibility's grid coordinates from its row's uvw (metres) and its
+// frequency
+__device__ __forceinline__ Coord vis_coord_v(const Geo &g, double um, double vm, double wm,
+                                             double f) {
     Coord c;
     const double s = f / kCLight;
-    const double u = g.su * uvw[row * rs] * s;
-    const double v = uvw[row * rs + 1] * s;
-    c.w = g.su * uvw[row * rs + 2] * s;
+    const double u = g.su * um * s;
+    const double v = vm * s;
+    c.w = g.su * wm * s;
     const double a = u * g.px * g.ngx;
     const double b = v * g.py * g.ngy;
     c.ok = fabs(a) < (double)g.ngx && fabs(b) < (double)g.ngy;
@@ -225,9 +227,22 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
     return c;
 }
 
+__device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restrict__ uvw,
+                                           int64_t rs, int64_t row, double f) {
+    return vis_coord_v(g, uvw[row * rs], uvw[row * rs + 1], uvw[row * rs + 2], f);
+}
+
 // w slab: the visibility's first plane (computed exactly as vis_coord does)
 // lies in the sequence's layout but outside this call's slab -- tested before
 // anything else of the visibility is read
+__device__ __forceinline__ bool slab_out_v(const Geo &g, double wm, double f) {
+    const double s = f / kCLight;
+    const double w = g.su * wm * s;
+    const double pw = (w - g.w0) / g.dw;
+    const int p0 = (int)floor(fmin(fmax(pw - 0.5 * g.W, -2.0), 2.0e9)) + 1;
+    return (p0 < 0 || p0 >= g.nps) && (unsigned)(p0 + g.slab_lo) < (unsigned)g.nps_all;
+}
+
 __device__ __forceinline__ bool slab_out(const Geo &g, const double *__restrict__ uvw, int64_t rs,
                                          int64_t row, double f) {
     const double s = f / kCLight;
@@ -2100,15 +2115,17 @@ __global__ void k_bucket_f64(Geo g, int64_t nvis, const double *__restrict__ uvw
 //                 atomic per (workgroup, non-empty bin) reserves the
 //                 workgroup's slice of each bin
 //   k_t_bins      one workgroup: bin bases (scan), the bins' chunks of
-//                 records (<= 64 per bin, >= kTChunk records each) and the
+//                 kTChunk records, segments of kTSeg chunks, and the
 //                 non-empty bin list
 //   k_t_scatter   the value pass: the record (RecC / VisRec / VisRec64) and
 //                 its cell in the bin (u16) written in bin order, ranks from
 //                 LDS cursors (one LDS atomic per run of equal bins)
 //   k_t_cellcount per chunk an LDS histogram over the bin's 4096 cells
-//   k_t_cellcol   per (bin, cell): the count prefix over the bin's chunks
-//                 (in place), the total, and the bin's padded-record / item
-//                 sums (packed, one 64-bit atomic per 256 cells)
+//   k_t_segscan   per (segment, cell): the count prefix over the segment's
+//                 chunks (in place) and the segment total
+//   k_t_cellcol   per (bin, cell): the prefix over the bin's segments (in
+//                 place), the total, and the bin's padded-record / item sums
+//                 (packed, one 64-bit atomic per 256 cells)
 //   k_t_binscan   one workgroup: record and item bases of the bins, the
 //                 metadata the host reads (the only host sync)
 //   k_t_cellfin   per bin: cell bases, pad records, FineItem work items
@@ -2117,12 +2134,18 @@ __global__ void k_bucket_f64(Geo g, int64_t nvis, const double *__restrict__ uvw
 // The writes of the two scatter passes land in runs inside the few bins /
 // cells a workgroup touches at a time, not at random addresses.
 constexpr int kMaxBins = 16384;    // LDS histogram of the first level (64 KiB)
-constexpr int kTThreads = 1024;
-constexpr unsigned kTChunk = 32768;  // records per second-level chunk (at least)
-constexpr unsigned kTMaxChunksPerBin = 64;
+constexpr int kTThreads = 1024;     // second-level kernels, bin scans
+constexpr int kT1Threads = 512;     // count and value passes (VGPR-limited occupancy)
+constexpr unsigned kTChunk = 32768;  // records per second-level chunk
+constexpr unsigned kTSeg = 16;       // chunks per segment of the cells' column prefix
+constexpr int kTU = 2;               // visibilities per lane in flight (count / value pass)
+constexpr int kTU2 = 4;              // records per lane in flight (cell count / final move)
 
 struct TChunk {
-    uint32_t bin, b, e, pad;
+    uint32_t bin, b, e, seg;  // records [b, e) of `bin`; `seg`: its prefix segment
+};
+struct TSeg {
+    uint32_t c0, nc, pad0, pad1;  // chunks [c0, c0 + nc) of one bin
 };
 
 // consecutive lanes with equal `key` form a run; its head lane adds the run
@@ -2145,9 +2168,41 @@ __device__ __forceinline__ unsigned lds_run_add(unsigned key, bool valid, unsign
     return hb + (unsigned)(lane - head);
 }
 
-// The visibility's classification, shared bit for bit by the count and the
-// value pass: weight (flag-masked), in-slab test, fp64 coordinates, and
-// whether it is bucketed.  v < 2^32 (the plan refuses larger calls).
+// A visibility in two phases, so that a lane's kTU visibilities issue all
+// their loads before any of them is used: t_load (uvw of the row, frequency,
+// flag-masked weight) and t_classify (in-slab test, fp64 coordinates,
+// bucketed or not) -- bit-identical in the count and the value pass.
+// v < 2^32 (the plan refuses larger calls).
+struct TLoad {
+    uint32_t row, chan;
+    double um, vm, wm, f, wd;
+    bool live;
+};
+
+__device__ __forceinline__ TLoad t_load(const Geo &g, int64_t v, int64_t vend,
+                                        const double *__restrict__ uvw, int64_t rs,
+                                        const double *__restrict__ freq,
+                                        const void *__restrict__ wgt, int64_t wrs, int64_t wcs,
+                                        const VisExtra &x) {
+    TLoad L;
+    L.live = v < vend;
+    const uint32_t v32 = L.live ? (uint32_t)v : 0u, r32 = v32 / (uint32_t)g.nchan;
+    L.row = r32;
+    L.chan = v32 - r32 * (uint32_t)g.nchan;
+    L.um = L.vm = L.wm = 0.0;
+    L.f = 1.0;
+    L.wd = 0.0;
+    if (L.live) {
+        const double *p = uvw + (int64_t)L.row * rs;
+        L.um = p[0];
+        L.vm = p[1];
+        L.wm = p[2];
+        L.f = freq[L.chan];
+        L.wd = eff_weight(wgt, wrs, wcs, x, L.row, L.chan);
+    }
+    return L;
+}
+
 struct TPoint {
     int64_t row;
     int chan;
@@ -2157,25 +2212,19 @@ struct TPoint {
 };
 
 template <bool kCount>
-__device__ __forceinline__ TPoint t_point(const Geo &g, int64_t v, int64_t vend,
-                                          const double *__restrict__ uvw, int64_t rs,
-                                          const double *__restrict__ freq,
-                                          const void *__restrict__ wgt, int64_t wrs, int64_t wcs,
-                                          const VisExtra &x, unsigned long long *nbad) {
+__device__ __forceinline__ TPoint t_classify(const Geo &g, const TLoad &L, const VisExtra &x,
+                                             unsigned long long *nbad) {
     TPoint p;
     p.in = false;
     p.wd = 0.0;
-    p.row = 0;
-    p.chan = 0;
+    p.row = L.row;
+    p.chan = (int)L.chan;
     p.c.ok = false;
-    if (v >= vend) return p;
-    const uint32_t v32 = (uint32_t)v, r32 = v32 / (uint32_t)g.nchan;
-    p.row = r32;
-    p.chan = (int)(v32 - r32 * (uint32_t)g.nchan);
-    if (g.slab && slab_out(g, uvw, rs, p.row, freq[p.chan])) return p;
-    p.wd = eff_weight(wgt, wrs, wcs, x, p.row, p.chan);
+    if (!L.live) return p;
+    if (g.slab && slab_out_v(g, L.wm, L.f)) return p;
+    p.wd = L.wd;
     if (!(x.all || (float)p.wd != 0.0f)) return p;
-    p.c = vis_coord(g, uvw, rs, p.row, freq[p.chan]);
+    p.c = vis_coord_v(g, L.um, L.vm, L.wm, L.f);
     if (!p.c.ok) {
         if (kCount && !p.c.skip) atomicAdd(nbad, 1ull);
         return p;
@@ -2195,7 +2244,7 @@ __device__ __forceinline__ void t_weight_sum(double ws, double *sw_slots) {
                   ws);
 }
 
-__global__ __launch_bounds__(kTThreads) void k_t_count(Geo g, int64_t nvis, int64_t vpw,
+__global__ __launch_bounds__(kT1Threads) void k_t_count(Geo g, int64_t nvis, int64_t vpw,
                                                        const double *__restrict__ uvw, int64_t rs,
                                                        const double *__restrict__ freq,
                                                        const void *__restrict__ wgt, int64_t wrs,
@@ -2205,21 +2254,28 @@ __global__ __launch_bounds__(kTThreads) void k_t_count(Geo g, int64_t nvis, int6
                                                        unsigned long long *nbad) {
     extern __shared__ unsigned hist[];
     const int nb = g.nbins;
-    for (int b = threadIdx.x; b < nb; b += kTThreads) hist[b] = 0u;
+    for (int b = threadIdx.x; b < nb; b += kT1Threads) hist[b] = 0u;
     __syncthreads();
     const int64_t v0 = (int64_t)blockIdx.x * vpw, v1 = min(nvis, v0 + vpw);
     double ws = 0.0;
-    for (int64_t base = v0; base < v1; base += kTThreads) {
-        const TPoint p = t_point<true>(g, base + threadIdx.x, v1, uvw, rs, freq, wgt, wrs, wcs, x,
-                                       nbad);
-        ws += p.wd;
-        lds_run_add<false>(p.in ? tiled_key(g, p.c) >> 12 : 0u, p.in, hist);
+    for (int64_t base = v0; base < v1; base += (int64_t)kT1Threads * kTU) {
+        TLoad L[kTU];
+#pragma unroll
+        for (int u = 0; u < kTU; ++u)
+            L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, freq, wgt, wrs, wcs,
+                          x);
+#pragma unroll
+        for (int u = 0; u < kTU; ++u) {
+            const TPoint p = t_classify<true>(g, L[u], x, nbad);
+            ws += p.wd;
+            lds_run_add<false>(p.in ? tiled_key(g, p.c) >> 12 : 0u, p.in, hist);
+        }
     }
     if (sw_slots) t_weight_sum(ws, sw_slots);
     __syncthreads();
     // the workgroup's slice of every non-empty bin (its offset inside the bin)
     unsigned *row = m1 + (size_t)blockIdx.x * nb;
-    for (int b = threadIdx.x; b < nb; b += kTThreads) {
+    for (int b = threadIdx.x; b < nb; b += kT1Threads) {
         const unsigned c = hist[b];
         row[b] = c ? atomicAdd(&binc[b], c) : 0u;
     }
@@ -2229,100 +2285,91 @@ __global__ __launch_bounds__(kTThreads) void k_t_count(Geo g, int64_t nvis, int6
 template <class T>
 using TBlockScan = hipcub::BlockScan<T, kTThreads>;
 
-// one workgroup: bin bases, chunks, non-empty bins.  Thread t owns bins
+// one workgroup: bin bases, the bins' chunks of kTChunk records and their
+// prefix segments of kTSeg chunks, the non-empty bins.  Thread t owns bins
 // [t * per, t * per + per).  binbase[nb] = total records; nbl[0] = number of
-// non-empty bins, nbl[1 + k] = the k-th; meta_ch[0] = number of chunks.
+// non-empty bins, nbl[1 + k] = the k-th; meta_ch = {chunks, segments}.
 __global__ __launch_bounds__(kTThreads) void k_t_bins(int nb, const unsigned *__restrict__ binc,
                                                       unsigned *__restrict__ binbase,
-                                                      unsigned *__restrict__ chbase,
-                                                      unsigned *__restrict__ nchb,
+                                                      unsigned *__restrict__ segb,
+                                                      unsigned *__restrict__ nsegb,
                                                       unsigned *__restrict__ nbl,
                                                       TChunk *__restrict__ chunks,
+                                                      TSeg *__restrict__ segs,
                                                       unsigned *__restrict__ meta_ch) {
     __shared__ typename TBlockScan<unsigned>::TempStorage tmp;
     const int per = (nb + kTThreads - 1) / kTThreads;
     const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
-    unsigned rec = 0, nch = 0, nne = 0;
-    auto chunk_size = [](unsigned n) {
-        const unsigned big = (n + kTMaxChunksPerBin - 1) / kTMaxChunksPerBin;
-        return big > kTChunk ? big : kTChunk;
-    };
+    unsigned rec = 0, nch = 0, nsg = 0, nne = 0;
     for (int b = b0; b < b1; ++b) {
         const unsigned n = binc[b];
         rec += n;
-        if (n) {
-            const unsigned cs = chunk_size(n);
-            nch += (n + cs - 1) / cs;
-            ++nne;
-        }
+        const unsigned k = (n + kTChunk - 1) / kTChunk;
+        nch += k;
+        nsg += (k + kTSeg - 1) / kTSeg;
+        nne += n ? 1u : 0u;
     }
-    unsigned rec_x, nch_x, nne_x, rec_t, nch_t, nne_t;
+    unsigned rec_x, nch_x, nsg_x, nne_x, rec_t, nch_t, nsg_t, nne_t;
     TBlockScan<unsigned>(tmp).ExclusiveSum(rec, rec_x, rec_t);
     __syncthreads();
     TBlockScan<unsigned>(tmp).ExclusiveSum(nch, nch_x, nch_t);
     __syncthreads();
+    TBlockScan<unsigned>(tmp).ExclusiveSum(nsg, nsg_x, nsg_t);
+    __syncthreads();
     TBlockScan<unsigned>(tmp).ExclusiveSum(nne, nne_x, nne_t);
     for (int b = b0; b < b1; ++b) {
         const unsigned n = binc[b];
+        const unsigned k = (n + kTChunk - 1) / kTChunk, ks = (k + kTSeg - 1) / kTSeg;
         binbase[b] = rec_x;
-        chbase[b] = nch_x;
-        unsigned k = 0;
-        if (n) {
-            const unsigned cs = chunk_size(n);
-            k = (n + cs - 1) / cs;
-            for (unsigned j = 0; j < k; ++j) {
-                TChunk t;
-                t.bin = (uint32_t)b;
-                t.b = rec_x + j * cs;
-                t.e = rec_x + min(n, (j + 1) * cs);
-                t.pad = 0u;
-                chunks[nch_x + j] = t;
-            }
-            nbl[1 + nne_x++] = (unsigned)b;
+        segb[b] = nsg_x;
+        nsegb[b] = ks;
+        for (unsigned j = 0; j < k; ++j) {
+            TChunk t;
+            t.bin = (uint32_t)b;
+            t.b = rec_x + j * kTChunk;
+            t.e = rec_x + min(n, (j + 1) * kTChunk);
+            t.seg = nsg_x + j / kTSeg;
+            chunks[nch_x + j] = t;
         }
-        nchb[b] = k;
+        for (unsigned j = 0; j < ks; ++j) {
+            TSeg sg;
+            sg.c0 = nch_x + j * kTSeg;
+            sg.nc = min(k - j * kTSeg, kTSeg);
+            sg.pad0 = sg.pad1 = 0u;
+            segs[nsg_x + j] = sg;
+        }
+        if (n) nbl[1 + nne_x++] = (unsigned)b;
         rec_x += n;
         nch_x += k;
+        nsg_x += ks;
     }
     if (threadIdx.x == kTThreads - 1) {
         binbase[nb] = rec_t;
         nbl[0] = nne_t;
         meta_ch[0] = nch_t;
+        meta_ch[1] = nsg_t;
     }
 }
 
-// Record writers of the value pass (the fields bucket_one / k_bucket_f64
-// write for the single-level path, computed the same way).
-template <class VT, bool kGrid>
-__device__ __forceinline__ void t_value32(const Geo &g, const VisExtra &x,
-                                          const double *__restrict__ uvw, int64_t rs,
-                                          const double *__restrict__ freq, const VT *vis,
-                                          int64_t vrs, int64_t vcs, const TPoint &p, float &cr,
-                                          float &ci) {
-    const float wt = (float)p.wd;
-    cr = wt;
-    ci = 0.0f;
-    if (kGrid) {
-        const float2 xv = (vis && wt != 0.0f) ? eff_vis(vis, vrs, vcs, x, p.row, p.chan)
-                                              : make_float2(1.0f, 0.0f);
-        cr = wt != 0.0f ? xv.x * wt : 0.0f;
-        ci = wt != 0.0f ? xv.y * wt : 0.0f;
-    }
-    if (g.do_w || x.shift) {
-        double ph = g.do_w ? p.c.w * g.s0 : 0.0;
-        if (x.shift) {
-            const double *u = uvw + p.row * rs;
-            ph += (u[0] * x.sl + u[1] * x.sm + u[2] * x.sn) * (freq[p.chan] / kCLight);
+// the visibility's value (phase 1 of the value pass: loads only)
+template <class VT, int KIND, bool kGrid>
+struct TVal {
+    using type = typename std::conditional<KIND == 2, double2, float2>::type;
+    __device__ static __forceinline__ type load(const VT *vis, int64_t vrs, int64_t vcs,
+                                                const VisExtra &x, const TLoad &L) {
+        type xv;
+        xv.x = 1;
+        xv.y = 0;
+        if constexpr (kGrid) {
+            if constexpr (KIND == 2) {
+                if (vis && L.live && L.wd != 0.0) xv = eff_vis_d(vis, vrs, vcs, x, L.row, L.chan);
+            } else {
+                if (vis && L.live && (float)L.wd != 0.0f) xv = eff_vis(vis, vrs, vcs, x, L.row, L.chan);
+            }
         }
-        ph -= rint(ph);
-        float sn, cs;
-        sincospif((float)(2.0 * ph), &sn, &cs);
-        if (!kGrid) sn = -sn;
-        const float r_ = cr * cs - ci * sn, i_ = cr * sn + ci * cs;
-        cr = r_;
-        ci = i_;
+        return xv;
     }
-}
+};
 
 // KIND 0: RecC (4-padded invert), 1: VisRec (fp32 predict), 2: VisRec64
 template <int KIND>
@@ -2340,27 +2387,25 @@ struct TRec<2> {
     using type = VisRec64;
 };
 
-template <class VT, int KIND, bool kGrid>
-__device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x,
-                                        const double *__restrict__ uvw, int64_t rs,
-                                        const double *__restrict__ freq, const VT *vis,
-                                        int64_t vrs, int64_t vcs, const TPoint &p, int64_t vg,
-                                        void *out, unsigned pos) {
+// Record writers of the value pass: the fields bucket_one / k_bucket_f64
+// write for the single-level path, computed the same way.
+template <int KIND, bool kGrid, class XV>
+__device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x, const TLoad &L,
+                                        const TPoint &p, XV xv, void *out, unsigned pos) {
+    double ph = 0.0;
+    const bool rot = g.do_w || x.shift;
+    if (rot) {
+        ph = g.do_w ? p.c.w * g.s0 : 0.0;
+        if (x.shift) ph += (L.um * x.sl + L.vm * x.sm + L.wm * x.sn) * (L.f / kCLight);
+        ph -= rint(ph);
+    }
     if constexpr (KIND == 2) {
         double cr = p.wd, ci = 0.0;
         if (kGrid) {
-            const double2 xv = (vis && p.wd != 0.0) ? eff_vis_d(vis, vrs, vcs, x, p.row, p.chan)
-                                                    : make_double2(1.0, 0.0);
             cr = p.wd != 0.0 ? xv.x * p.wd : 0.0;
             ci = p.wd != 0.0 ? xv.y * p.wd : 0.0;
         }
-        if (g.do_w || x.shift) {
-            double ph = g.do_w ? p.c.w * g.s0 : 0.0;
-            if (x.shift) {
-                const double *u = uvw + p.row * rs;
-                ph += (u[0] * x.sl + u[1] * x.sm + u[2] * x.sn) * (freq[p.chan] / kCLight);
-            }
-            ph -= rint(ph);
+        if (rot) {
             double sn, cs;
             sincospi(2.0 * ph, &sn, &cs);
             if (!kGrid) sn = -sn;
@@ -2376,12 +2421,24 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x,
         rec.dw = p.c.dw;
         rec.ij = (uint32_t)p.c.ic0 | ((uint32_t)p.c.jc0 << 16);
         rec.p0 = (uint32_t)p.c.p0;
-        rec.idx = (uint32_t)vg;
+        rec.idx = (uint32_t)(L.row * (uint32_t)g.nchan + L.chan);
         rec.pad = 0u;
         static_cast<VisRec64 *>(out)[pos] = rec;
     } else {
-        float cr, ci;
-        t_value32<VT, kGrid>(g, x, uvw, rs, freq, vis, vrs, vcs, p, cr, ci);
+        const float wt = (float)p.wd;
+        float cr = wt, ci = 0.0f;
+        if (kGrid) {
+            cr = wt != 0.0f ? xv.x * wt : 0.0f;
+            ci = wt != 0.0f ? xv.y * wt : 0.0f;
+        }
+        if (rot) {
+            float sn, cs;
+            sincospif((float)(2.0 * ph), &sn, &cs);
+            if (!kGrid) sn = -sn;
+            const float r_ = cr * cs - ci * sn, i_ = cr * sn + ci * cs;
+            cr = r_;
+            ci = i_;
+        }
         if constexpr (KIND == 0) {
             const double base = 1.0 - 0.5 * g.W;
             const uint32_t qu = fix_frac(base - p.c.du, 21), qv = fix_frac(base - p.c.dv, 21);
@@ -2401,35 +2458,46 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x,
             rec.fw = p.c.fw;
             rec.ij = (uint32_t)p.c.ic0 | ((uint32_t)p.c.jc0 << 16);
             rec.p0 = (uint32_t)p.c.p0;
-            rec.idx = (uint32_t)vg;
+            rec.idx = L.row * (uint32_t)g.nchan + L.chan;
             static_cast<VisRec *>(out)[pos] = rec;
         }
     }
 }
 
 template <class VT, int KIND, bool kGrid>
-__global__ __launch_bounds__(kTThreads) void k_t_scatter(
+__global__ __launch_bounds__(kT1Threads) void k_t_scatter(
     Geo g, int64_t nvis, int64_t vpw, const double *__restrict__ uvw, int64_t rs,
     const double *__restrict__ freq, const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
     const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x, double *sw_slots,
     const unsigned *__restrict__ binbase, const unsigned *__restrict__ m1, void *__restrict__ out,
     uint16_t *__restrict__ lkey) {
+    using V = TVal<VT, KIND, kGrid>;
     extern __shared__ unsigned cur[];
     const int nb = g.nbins;
     const unsigned *row = m1 + (size_t)blockIdx.x * nb;
-    for (int b = threadIdx.x; b < nb; b += kTThreads) cur[b] = binbase[b] + row[b];
+    for (int b = threadIdx.x; b < nb; b += kT1Threads) cur[b] = binbase[b] + row[b];
     __syncthreads();
     const int64_t v0 = (int64_t)blockIdx.x * vpw, v1 = min(nvis, v0 + vpw);
     double ws = 0.0;
-    for (int64_t base = v0; base < v1; base += kTThreads) {
-        const int64_t v = base + threadIdx.x;
-        const TPoint p = t_point<false>(g, v, v1, uvw, rs, freq, wgt, wrs, wcs, x, nullptr);
-        ws += p.wd;
-        const unsigned key = p.in ? tiled_key(g, p.c) : 0u;
-        const unsigned pos = lds_run_add<true>(key >> 12, p.in, cur);
-        if (p.in) {
-            t_write<VT, KIND, kGrid>(g, x, uvw, rs, freq, vis, vrs, vcs, p, v, out, pos);
-            lkey[pos] = (uint16_t)(key & (kBinCells - 1));
+    for (int64_t base = v0; base < v1; base += (int64_t)kT1Threads * kTU) {
+        TLoad L[kTU];
+        typename V::type xv[kTU];
+#pragma unroll
+        for (int u = 0; u < kTU; ++u) {
+            L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, freq, wgt, wrs, wcs,
+                          x);
+            xv[u] = V::load(vis, vrs, vcs, x, L[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kTU; ++u) {
+            const TPoint p = t_classify<false>(g, L[u], x, nullptr);
+            ws += p.wd;
+            const unsigned key = p.in ? tiled_key(g, p.c) : 0u;
+            const unsigned pos = lds_run_add<true>(key >> 12, p.in, cur);
+            if (p.in) {
+                t_write<KIND, kGrid>(g, x, L[u], p, xv[u], out, pos);
+                lkey[pos] = (uint16_t)(key & (kBinCells - 1));
+            }
         }
     }
     if (sw_slots) t_weight_sum(ws, sw_slots);
@@ -2446,10 +2514,15 @@ __global__ __launch_bounds__(kTThreads) void k_t_cellcount(const TChunk *__restr
         for (int i = threadIdx.x; i < kBinCells; i += kTThreads) h[i] = 0u;
         __syncthreads();
         const TChunk t = chunks[c];
-        for (uint32_t i0 = t.b; i0 < t.e; i0 += kTThreads) {
-            const uint32_t i = i0 + threadIdx.x;
-            const bool ok = i < t.e;
-            lds_run_add<false>(ok ? (unsigned)lkey[i] : 0u, ok, h);
+        for (uint32_t i0 = t.b; i0 < t.e; i0 += kTThreads * kTU2) {
+            unsigned k[kTU2];
+#pragma unroll
+            for (int u = 0; u < kTU2; ++u) {
+                const uint32_t i = i0 + u * kTThreads + threadIdx.x;
+                k[u] = i < t.e ? (unsigned)lkey[i] : 0xffffu;
+            }
+#pragma unroll
+            for (int u = 0; u < kTU2; ++u) lds_run_add<false>(k[u], k[u] != 0xffffu, h);
         }
         __syncthreads();
         uint4 *dst = reinterpret_cast<uint4 *>(m2 + (size_t)c * kBinCells);
@@ -2459,16 +2532,42 @@ __global__ __launch_bounds__(kTThreads) void k_t_cellcount(const TChunk *__restr
     }
 }
 
+// per (segment of <= kTSeg chunks of one bin, 256-cell slice), one thread
+// per cell: the exclusive prefix of the cell's counts over the segment's
+// chunks (in place in M2) and the segment total (S)
+__global__ __launch_bounds__(256) void k_t_segscan(const TSeg *__restrict__ segs,
+                                                   const unsigned *__restrict__ meta_ch,
+                                                   unsigned *__restrict__ m2,
+                                                   unsigned *__restrict__ stot) {
+    const unsigned nwork = meta_ch[1] * (kBinCells / 256);
+    for (unsigned w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const unsigned sg = w / (kBinCells / 256);
+        const int cell = (int)(w % (kBinCells / 256)) * 256 + threadIdx.x;
+        const TSeg t = segs[sg];
+        unsigned *q = m2 + (size_t)t.c0 * kBinCells + cell;
+        unsigned v[kTSeg];
+#pragma unroll
+        for (unsigned j = 0; j < kTSeg; ++j) v[j] = j < t.nc ? q[(size_t)j * kBinCells] : 0u;
+        unsigned run = 0;
+#pragma unroll
+        for (unsigned j = 0; j < kTSeg; ++j) {
+            if (j < t.nc) q[(size_t)j * kBinCells] = run;
+            run += v[j];
+        }
+        stot[(size_t)sg * kBinCells + cell] = run;
+    }
+}
+
 // per (non-empty bin, 256-cell slice), one thread per cell: the exclusive
-// prefix of the cell's counts over the bin's chunks (in place in M2), the
+// prefix of the segment totals over the bin's segments (in place in S), the
 // cell total T, and into binsum[bin] the slice's (padded records << 32 |
 // items) -- a group of 16 cells is 16 consecutive lanes; its items are its
 // padded records in chunks of `chunk`
 template <bool PAD>
 __global__ __launch_bounds__(256) void k_t_cellcol(const unsigned *__restrict__ nbl,
-                                                   const unsigned *__restrict__ chbase,
-                                                   const unsigned *__restrict__ nchb,
-                                                   unsigned *__restrict__ m2,
+                                                   const unsigned *__restrict__ segb,
+                                                   const unsigned *__restrict__ nsegb,
+                                                   unsigned *__restrict__ stot,
                                                    unsigned *__restrict__ tot, unsigned chunk,
                                                    unsigned long long *__restrict__ binsum,
                                                    unsigned *__restrict__ npad) {
@@ -2478,11 +2577,11 @@ __global__ __launch_bounds__(256) void k_t_cellcol(const unsigned *__restrict__ 
     for (unsigned w = blockIdx.x; w < nwork; w += gridDim.x) {
         const unsigned b = nbl[1 + w / (kBinCells / 256)];
         const int cell = (int)(w % (kBinCells / 256)) * 256 + threadIdx.x;
-        const unsigned c0 = chbase[b], nc = nchb[b];
-        unsigned *q = m2 + (size_t)c0 * kBinCells + cell;
+        const unsigned s0 = segb[b], ns = nsegb[b];
+        unsigned *q = stot + (size_t)s0 * kBinCells + cell;
         unsigned run = 0;
         unsigned k = 0;
-        for (; k + 8 <= nc; k += 8) {
+        for (; k + 8 <= ns; k += 8) {
             unsigned v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = q[(size_t)(k + j) * kBinCells];
@@ -2492,7 +2591,7 @@ __global__ __launch_bounds__(256) void k_t_cellcol(const unsigned *__restrict__ 
                 run += v[j];
             }
         }
-        for (; k < nc; ++k) {
+        for (; k < ns; ++k) {
             const unsigned v = q[(size_t)k * kBinCells];
             q[(size_t)k * kBinCells] = run;
             run += v;
@@ -2612,7 +2711,8 @@ __global__ __launch_bounds__(256) void k_t_cellfin(const Geo g, const unsigned *
         }
         uint4 *cb = reinterpret_cast<uint4 *>(cbase + (size_t)b * kBinCells + gi * 16);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) cb[q] = make_uint4(st[4 * q], st[4 * q + 1], st[4 * q + 2], st[4 * q + 3]);
+        for (int q = 0; q < 4; ++q)
+            cb[q] = make_uint4(st[4 * q], st[4 * q + 1], st[4 * q + 2], st[4 * q + 3]);
         f.p0 = b / (unsigned)tpp;
         f.tile = (b - f.p0 * (unsigned)tpp) * 256u + (unsigned)gi;
         for (unsigned s = 0; s < it; ++s) {
@@ -2624,13 +2724,15 @@ __global__ __launch_bounds__(256) void k_t_cellfin(const Geo g, const unsigned *
     }
 }
 
-// per chunk: each record to its cell, at the cell base + the chunk's prefix
-// + its rank among the chunk's records of that cell (LDS cursors)
+// per chunk: each record to its cell, at the cell base + the segment's
+// prefix + the chunk's prefix inside its segment + its rank among the
+// chunk's records of that cell (LDS cursors)
 template <int KIND>
 __global__ __launch_bounds__(kTThreads) void k_t_final(const TChunk *__restrict__ chunks,
                                                        const unsigned *__restrict__ meta_ch,
                                                        const uint16_t *__restrict__ lkey,
                                                        const unsigned *__restrict__ m2,
+                                                       const unsigned *__restrict__ stot,
                                                        const unsigned *__restrict__ cbase,
                                                        const void *__restrict__ in,
                                                        void *__restrict__ out) {
@@ -2638,24 +2740,36 @@ __global__ __launch_bounds__(kTThreads) void k_t_final(const TChunk *__restrict_
     constexpr int NW = (int)(sizeof(R) / sizeof(uint4));
     __shared__ unsigned cur[kBinCells];
     const unsigned n = meta_ch[0];
+    const uint4 *src = reinterpret_cast<const uint4 *>(in);
+    uint4 *dst = reinterpret_cast<uint4 *>(out);
     for (unsigned c = blockIdx.x; c < n; c += gridDim.x) {
         const TChunk t = chunks[c];
         const unsigned *pre = m2 + (size_t)c * kBinCells;
+        const unsigned *sp = stot + (size_t)t.seg * kBinCells;
         const unsigned *cb = cbase + (size_t)t.bin * kBinCells;
-        for (int i = threadIdx.x; i < kBinCells; i += kTThreads) cur[i] = cb[i] + pre[i];
+        for (int i = threadIdx.x; i < kBinCells; i += kTThreads) cur[i] = cb[i] + sp[i] + pre[i];
         __syncthreads();
-        for (uint32_t i0 = t.b; i0 < t.e; i0 += kTThreads) {
-            const uint32_t i = i0 + threadIdx.x;
-            const bool ok = i < t.e;
-            uint4 r[NW];
-            if (ok) {
+        for (uint32_t i0 = t.b; i0 < t.e; i0 += kTThreads * kTU2) {
+            uint4 r[kTU2][NW];
+            unsigned k[kTU2];
 #pragma unroll
-                for (int k = 0; k < NW; ++k) r[k] = reinterpret_cast<const uint4 *>(in)[(size_t)i * NW + k];
+            for (int u = 0; u < kTU2; ++u) {
+                const uint32_t i = i0 + u * kTThreads + threadIdx.x;
+                k[u] = 0xffffu;
+                if (i < t.e) {
+                    k[u] = lkey[i];
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) r[u][q] = src[(size_t)i * NW + q];
+                }
             }
-            const unsigned pos = lds_run_add<true>(ok ? (unsigned)lkey[i] : 0u, ok, cur);
-            if (ok) {
 #pragma unroll
-                for (int k = 0; k < NW; ++k) reinterpret_cast<uint4 *>(out)[(size_t)pos * NW + k] = r[k];
+            for (int u = 0; u < kTU2; ++u) {
+                const bool ok = k[u] != 0xffffu;
+                const unsigned pos = lds_run_add<true>(k[u], ok, cur);
+                if (ok) {
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) dst[(size_t)pos * NW + q] = r[u][q];
+                }
             }
         }
         __syncthreads();
@@ -3086,10 +3200,12 @@ struct Part {
     int t_g1 = 0;          // workgroups of the count / value passes
     int64_t t_vpw = 0;     // visibilities per such workgroup
     unsigned t_maxch = 0;  // bound on the second-level chunks
-    unsigned *t_binc = nullptr, *t_binbase = nullptr, *t_chbase = nullptr, *t_nchb = nullptr;
+    unsigned t_maxseg = 0;  // bound on their prefix segments
+    unsigned *t_binc = nullptr, *t_binbase = nullptr, *t_segb = nullptr, *t_nsegb = nullptr;
     unsigned *t_nbl = nullptr, *t_m1 = nullptr, *t_m2 = nullptr, *t_tot = nullptr;
-    unsigned *t_cbase = nullptr, *t_meta_ch = nullptr, *t_npad = nullptr;
+    unsigned *t_cbase = nullptr, *t_meta_ch = nullptr, *t_npad = nullptr, *t_stot = nullptr;
     TChunk *t_chunks = nullptr;
+    TSeg *t_segs = nullptr;
     unsigned long long *t_binsum = nullptr, *t_bofs = nullptr;
     uint16_t *t_lkey = nullptr;
     void *t_a = nullptr;  // records in bin order (the value pass's output)
@@ -3587,7 +3703,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         Workspace::get().drop(ws_name("recs_pad"));
         Workspace::get().drop(ws_name("rec_cls"));
     }
-    for (const char *n : {"recs_a", "rec_lkey", "t_m1", "t_m2", "t_tot", "t_cbase"})
+    for (const char *n : {"recs_a", "rec_lkey", "t_m1", "t_m2", "t_tot", "t_cbase", "t_stot"})
         if (!g.tiled) Workspace::get().drop(ws_name(n));
     for (const char *n : {"key_rank", "hist", "offs", "gsum", "gofs"})
         if (g.tiled) Workspace::get().drop(ws_name(n));
@@ -3602,7 +3718,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
             Workspace::get().drop(ws_name("recs"));
     }
     const size_t hist_bytes =
-        g.tiled ? ((size_t)nvis / kTChunk + 2 * (size_t)g.nbins + 512) * kBinCells * sizeof(unsigned)
+        g.tiled ? ((size_t)nvis / kTChunk + 4 * (size_t)g.nbins + 512) * kBinCells * sizeof(unsigned)
                 : (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned);
     const size_t need_other =
         (size_t)((double)nvis * (rec_bytes + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2)))) +
@@ -4132,16 +4248,18 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     const int64_t nvis = pt.nvis;
     const size_t lds_bins = (size_t)nb * sizeof(unsigned);
     if (!values_only) {
-        pt.t_g1 = 2 * cu_count();
-        pt.t_vpw = std::max<int64_t>(kTThreads, (nvis + pt.t_g1 - 1) / pt.t_g1);
+        pt.t_g1 = 4 * cu_count();
+        pt.t_vpw = std::max<int64_t>(kT1Threads, (nvis + pt.t_g1 - 1) / pt.t_g1);
         pt.t_vpw = (pt.t_vpw + 63) / 64 * 64;
         pt.t_g1 = (int)std::max<int64_t>(1, (nvis + pt.t_vpw - 1) / pt.t_vpw);
-        pt.t_maxch = (unsigned)std::min<int64_t>((int64_t)nb * kTMaxChunksPerBin,
-                                                 nvis / kTChunk + nb) + 1;
+        pt.t_maxch = (unsigned)(nvis / kTChunk + nb + 1);
+        pt.t_maxseg = (unsigned)(nvis / ((int64_t)kTChunk * kTSeg) + nb + 1);
         pt.t_binc = scratch<unsigned>("t_binc", nb);
         pt.t_binbase = scratch<unsigned>("t_binbase", nb + 1);
-        pt.t_chbase = scratch<unsigned>("t_chbase", nb);
-        pt.t_nchb = scratch<unsigned>("t_nchb", nb);
+        pt.t_segb = scratch<unsigned>("t_segb", nb);
+        pt.t_nsegb = scratch<unsigned>("t_nsegb", nb);
+        pt.t_segs = scratch<TSeg>("t_segs", pt.t_maxseg);
+        pt.t_stot = scratch<unsigned>("t_stot", (size_t)pt.t_maxseg * kBinCells);
         pt.t_nbl = scratch<unsigned>("t_nbl", nb + 1);
         pt.t_meta_ch = scratch<unsigned>("t_meta_ch", 2);
         pt.t_npad = scratch<unsigned>("t_npad", 1);
@@ -4169,7 +4287,7 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
             using VT = typename decltype(vt_tag)::type;
             constexpr int K = decltype(kind_tag)::value;
             constexpr bool G = decltype(grid_tag)::value;
-            k_t_scatter<VT, K, G><<<pt.t_g1, kTThreads, lds_bins, st>>>(
+            k_t_scatter<VT, K, G><<<pt.t_g1, kT1Threads, lds_bins, st>>>(
                 g, nvis, pt.t_vpw, in.uvw, in.uvw_rs, in.freq,
                 G ? static_cast<const VT *>(in.vis) : nullptr, in.vrs, in.vcs, in.wgt, in.wrs,
                 in.wcs, in.x, sl, pt.t_binbase, pt.t_m1, pt.t_a, pt.t_lkey);
@@ -4190,13 +4308,13 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     auto final_move = [&] {
         if (kind == 2)
             k_t_final<2><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
-                                                     pt.t_cbase, pt.t_a, P.recs);
+                                                     pt.t_stot, pt.t_cbase, pt.t_a, P.recs);
         else if (kind == 0)
             k_t_final<0><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
-                                                     pt.t_cbase, pt.t_a, P.recs);
+                                                     pt.t_stot, pt.t_cbase, pt.t_a, P.recs);
         else
             k_t_final<1><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
-                                                     pt.t_cbase, pt.t_a, P.recs);
+                                                     pt.t_stot, pt.t_cbase, pt.t_a, P.recs);
         SDP_HIP_CHECK(hipGetLastError());
     };
     if (values_only) {
@@ -4207,19 +4325,22 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         return;
     }
     if (nvis > 0)
-        k_t_count<<<pt.t_g1, kTThreads, lds_bins, st>>>(g, nvis, pt.t_vpw, in.uvw, in.uvw_rs,
+        k_t_count<<<pt.t_g1, kT1Threads, lds_bins, st>>>(g, nvis, pt.t_vpw, in.uvw, in.uvw_rs,
                                                         in.freq, in.wgt, in.wrs, in.wcs, in.x,
                                                         slots, pt.t_binc, pt.t_m1, pt.nbad);
-    k_t_bins<<<1, kTThreads, 0, st>>>(nb, pt.t_binc, pt.t_binbase, pt.t_chbase, pt.t_nchb,
-                                      pt.t_nbl, pt.t_chunks, pt.t_meta_ch);
+    k_t_bins<<<1, kTThreads, 0, st>>>(nb, pt.t_binc, pt.t_binbase, pt.t_segb, pt.t_nsegb,
+                                      pt.t_nbl, pt.t_chunks, pt.t_segs, pt.t_meta_ch);
     if (nvis > 0) scatter(nullptr);
     k_t_cellcount<<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2);
+    const unsigned gseg =
+        (unsigned)std::min<int64_t>((int64_t)pt.t_maxseg * (kBinCells / 256), 8192);
+    k_t_segscan<<<gseg, 256, 0, st>>>(pt.t_segs, pt.t_meta_ch, pt.t_m2, pt.t_stot);
     const unsigned gcol = (unsigned)std::min<int64_t>((int64_t)nb * (kBinCells / 256), 8192);
     if (P.pad4)
-        k_t_cellcol<true><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_chbase, pt.t_nchb, pt.t_m2,
+        k_t_cellcol<true><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_segb, pt.t_nsegb, pt.t_stot,
                                                 pt.t_tot, P.chunk, pt.t_binsum, pt.t_npad);
     else
-        k_t_cellcol<false><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_chbase, pt.t_nchb, pt.t_m2,
+        k_t_cellcol<false><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_segb, pt.t_nsegb, pt.t_stot,
                                                  pt.t_tot, P.chunk, pt.t_binsum, pt.t_npad);
     k_t_binscan<<<1, kTThreads, 0, st>>>(nb, g.tlx * g.tly, g.nps, pt.t_binsum, pt.t_binbase,
                                          pt.nbad, pt.t_bofs, pt.meta);
