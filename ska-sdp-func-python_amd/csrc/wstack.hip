@@ -2660,12 +2660,12 @@ __global__ __launch_bounds__(kTThreads) void k_t_binscan(
 // (cbase, absolute record index), zero pad records behind each cell's
 // records (RecC, PAD), and the group's FineItems (chunks of `chunk` padded
 // records, each with the 16 cell ends)
-template <bool PAD>
+template <bool PAD, int KIND>
 __global__ __launch_bounds__(256) void k_t_cellfin(const Geo g, const unsigned *__restrict__ nbl,
                                                    const unsigned *__restrict__ tot,
                                                    const unsigned long long *__restrict__ bofs,
                                                    unsigned chunk, unsigned *__restrict__ cbase,
-                                                   RecC *__restrict__ recs,
+                                                   void *__restrict__ recs,
                                                    FineItem *__restrict__ items) {
     __shared__ typename hipcub::BlockScan<unsigned long long, 256>::TempStorage tmp;
     const unsigned nne = nbl[0];
@@ -2701,10 +2701,20 @@ __global__ __launch_bounds__(256) void k_t_cellfin(const Geo g, const unsigned *
             st[j] = run;
             const unsigned r = PAD ? (n[j] + 3u) & ~3u : n[j];
             if (PAD && r != n[j]) {
-                RecC z;
-                z.cre = z.cim = 0.0f;
-                z.lo = z.hi = 0u;
-                for (unsigned i = run + n[j]; i < run + r; ++i) recs[i] = z;
+                // zero-valued pads with in-range offsets (finite taps): RecC
+                // fractions 0 (offset 1 - W/2), or VisRec64 offsets 1 - W/2
+                if constexpr (KIND == 2) {
+                    VisRec64 z;
+                    z.cre = z.cim = 0.0;
+                    z.du = z.dv = z.dw = 1.0 - 0.5 * g.W;
+                    z.ij = z.p0 = z.idx = z.pad = 0u;
+                    for (unsigned i = run + n[j]; i < run + r; ++i) static_cast<VisRec64 *>(recs)[i] = z;
+                } else {
+                    RecC z;
+                    z.cre = z.cim = 0.0f;
+                    z.lo = z.hi = 0u;
+                    for (unsigned i = run + n[j]; i < run + r; ++i) static_cast<RecC *>(recs)[i] = z;
+                }
             }
             run += r;
             f.o[j] = run;
@@ -2910,6 +2920,157 @@ __global__ __launch_bounds__(64) void k_grid_f64(Geo g, const VisRec64 *__restri
             double *dst = grid + 2 * ((size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy);
             if (v.x != 0.0) atomicAdd(dst, v.x);
             if (v.y != 0.0) atomicAdd(dst + 1, v.y);
+        }
+    }
+}
+
+// fp64 MFMA gridder (invert at epsilon < 1e-7) on 4-padded cells (the
+// two-level bucketing pads VisRec64 cells to a multiple of 4 records for it,
+// SDP_HIP_F64_MFMA).  A cell's records share their footprint origin, so its
+// contribution is one GEMM on v_mfma_f64_16x16x4_f64 (exact fp64 FMAs):
+//     C[(kx, ky), (q, re/im)] += sum_r tu_r[kx] tv_r[ky] * tw_r[q] c_r
+// A = the W^2 separable (u, v) taps (ceil(W^2 / 16) M-tiles), B = the w taps
+// x value (2 W columns: one N-tile per wave -- W = 13: 2 waves, 26 of 32
+// columns), K = 4 records of one cell.  Per K-step each wave issues MT
+// independent MFMAs, with 2 MT fp64 tap products and one B product as its
+// VALU work.  Accumulators are region-resident: loaded from the item's LDS
+// region tile [x][y][(q, re/im)] (fp64) when a cell starts and stored back
+// when it ends; the two waves own disjoint columns, so no barrier is needed
+// at cell changes.  The 16-record tap block ([record][tu | tv | tw | c]) is
+// computed once by both waves; the region is flushed per item with fp64
+// global atomics (zeros skipped), as k_grid_f64.
+template <int W, bool WS>
+constexpr int f64m_waves() {
+    return (2 * (WS ? W : 1) + 15) / 16;
+}
+template <int W, bool WS>
+constexpr size_t grid_f64m_lds() {
+    return (size_t)(W + 1) * (W + 7) * 2 * (WS ? W : 1) * sizeof(double) + 64 * sizeof(double) +
+           (size_t)kTap64 * (3 * W + 2) * sizeof(double);
+}
+typedef double doublex4 __attribute__((ext_vector_type(4)));
+
+template <int W, bool WS>
+__global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64_mfma(
+    Geo g, const VisRec64 *__restrict__ recs, const FineItem *__restrict__ items,
+    uint32_t n_items, double *__restrict__ grid, int p_lo, int p_hi) {
+    constexpr int NQ = WS ? W : 1, NC = 2 * NQ, NW = f64m_waves<W, WS>();
+    constexpr int MT = (W * W + 15) / 16, RX = W + 1, RY = W + 7, RS = RX * RY * NC;
+    constexpr int TR = 3 * W + 2, NTH = 64 * NW;
+    extern __shared__ __attribute__((aligned(16))) double smd[];
+    double *const reg = smd;        // [RX][RY][NC]
+    double *const dummy = smd + RS;  // sink of the accumulator rows / columns outside the GEMM
+    double *const tap = dummy + 64;  // [kTap64][TR]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const double ihw = 2.0 / W, beta = (double)g.beta;
+    // this lane's accumulator column (q, re/im) and B operand
+    const int col = wv * 16 + (lane & 15);
+    const bool colok = col < NC;
+    const int bq = 2 * W + (colok ? col >> 1 : 0), bc = 3 * W + (col & 1);
+    // accumulator element i of M-tile mt: tap row (lane >> 4) + 4 i -> its
+    // region offset (doubles, relative to the cell's origin) or -1
+    int tofs[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int t = mt * 16 + (lane >> 4) + 4 * i, kx = t / W, ky = t - kx * W;
+            tofs[mt][i] = (t < W * W && colok) ? (kx * RY + ky) * NC + col : -1;
+        }
+    // A operand of M-tile mt: tap (lane & 15) + 16 mt of record lane >> 4
+    int au[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int t = mt * 16 + (lane & 15), kx = t / W, ky = t - kx * W;
+        au[mt] = t < W * W ? kx | ((W + ky) << 8) : -1;
+    }
+    const int rk = lane >> 4;
+    const size_t plane_elems = (size_t)g.ngx * g.ngy;
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        uint32_t bnd[kGroupCell];
+        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
+        if (it.b >= it.e) continue;
+        int ibase, jbase;
+        group_origin(g, (int)it.tile, ibase, jbase);
+        __syncthreads();  // the previous item's flush reads of the region
+        for (int i = threadIdx.x; i < RS; i += NTH) reg[i] = 0.0;
+        doublex4 acc[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = doublex4{0.0, 0.0, 0.0, 0.0};
+        int cur = -1;
+        auto store_cell = [&](int cell) {
+            const int cb = ((cell & 1) * RY + (cell >> 1)) * NC;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    double *d = tofs[mt][i] >= 0 ? reg + cb + tofs[mt][i] : dummy + lane;
+                    *d = acc[mt][i];
+                }
+        };
+        auto load_cell = [&](int cell) {
+            const int cb = ((cell & 1) * RY + (cell >> 1)) * NC;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[mt][i] = tofs[mt][i] >= 0 ? reg[cb + tofs[mt][i]] : 0.0;
+        };
+        for (uint32_t b0 = it.b; b0 < it.e; b0 += kTap64) {
+            __syncthreads();  // the region zeroing / previous block's tap reads
+            const int nb = (int)min((uint32_t)kTap64, it.e - b0);  // (a multiple of 4)
+            for (int t = threadIdx.x; t < nb * TR; t += NTH) {
+                const int r = t / TR, k = t - r * TR;
+                const VisRec64 *R = recs + b0 + r;
+                double tv;
+                if (k >= 3 * W) {
+                    tv = k == 3 * W ? R->cre : R->cim;
+                } else {
+                    const int ax = k / W, j = k - ax * W;
+                    if (ax == 2 && !WS) tv = j == 0 ? 1.0 : 0.0;
+                    else tv = es_tap64(ax == 0 ? R->du : (ax == 1 ? R->dv : R->dw), j, ihw, beta);
+                }
+                tap[t] = tv;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int kk = 0; kk < kTap64 / 4; ++kk) {
+                if (4 * kk >= nb) break;
+                const uint32_t ri = b0 + 4u * (uint32_t)kk;
+                int cell = 0;
+#pragma unroll
+                for (int c = 0; c < kGroupCell - 1; ++c) cell += ri >= bnd[c] ? 1 : 0;
+                if (cell != cur) {
+                    if (cur >= 0) store_cell(cur);
+                    cur = cell;
+                    load_cell(cur);
+                }
+                const double *T = tap + (4 * kk + rk) * TR;
+                const double bop = colok ? T[bq] * T[bc] : 0.0;
+                double aop[MT];
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    aop[mt] = au[mt] >= 0 ? T[au[mt] & 0xff] * T[au[mt] >> 8] : 0.0;
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+                    acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[mt], bop, acc[mt], 0, 0, 0);
+            }
+        }
+        if (cur >= 0) store_cell(cur);
+        __syncthreads();
+        for (int i = threadIdx.x; i < RS; i += NTH) {
+            const double v = reg[i];
+            if (v == 0.0) continue;
+            const int c = i % NC, cell = i / NC;
+            const int p = (int)it.p0 + (c >> 1);
+            if (p < p_lo || p >= p_hi) continue;
+            const int xl = cell / RY, yl = cell - xl * RY;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            atomicAdd(grid + 2 * ((size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy) + (c & 1),
+                      v);
         }
     }
 }
@@ -3221,6 +3382,7 @@ struct Plan {
     uint8_t *cls = nullptr;          // subpad: each RecC record's cell in its bucket
     RecC *recs_pad = nullptr;        // subpad: the 4-padded, cell-ordered records
     bool pad4 = false;               // one-cell buckets padded to 4 records (k_grid_mfma_pad)
+    bool pad64 = false;              // fp64 invert: VisRec64 cells padded to 4 (k_grid_f64_mfma)
     float2 *vdirect = nullptr;       // dirty2ms: the degridder writes c64 vis in place
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
@@ -3743,6 +3905,9 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // (k_grid_mfma_pad); the padded record count is read back before the
     // scatter (one host sync)
     P.pad4 = grid_mode && g.sub == kTileCell && !P.f64;
+    // fp64 invert on the two-level bucketing: VisRec64 cells padded to 4 for
+    // the MFMA gridder (SDP_HIP_F64_MFMA=0: the VALU gridder, unpadded)
+    P.pad64 = grid_mode && g.tiled && P.f64 && env_int("SDP_HIP_F64_MFMA", 1) != 0;
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
     P.pt.nvis = nvis;
     if (g.tiled) return P;  // (records: bucket_tiled, once their padded count is known)
@@ -4011,10 +4176,29 @@ static void launch_degrid_f64(const Plan &P, int p_lo, int p_hi, VT *vis, int64_
         default: CALL(16); break; \
     }
 
+template <int W, bool WS>
+static void launch_grid_f64_mfma(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
+    const auto r = chunk_items(P, p_lo, p_hi);
+    const unsigned n = r.second - r.first;
+    if (n == 0) return;
+    static const bool attr = [] {  // dynamic LDS above 64 KiB (W >= 14)
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_grid_f64_mfma<W, WS>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)grid_f64m_lds<W, WS>()));
+        return true;
+    }();
+    (void)attr;
+    k_grid_f64_mfma<W, WS><<<n, 64 * f64m_waves<W, WS>(), grid_f64m_lds<W, WS>(), st>>>(
+        P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
+        reinterpret_cast<double *>(P.grid), p_lo, p_hi);
+}
+
 static void grid_f64(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
-#define SDP_G64(WW)                                                          \
-    (P.g.do_w ? launch_grid_f64<WW, true>(P, p_lo, p_hi, st)                 \
-              : launch_grid_f64<WW, false>(P, p_lo, p_hi, st))
+#define SDP_G64(WW)                                                                    \
+    (P.pad64 ? (P.g.do_w ? launch_grid_f64_mfma<WW, true>(P, p_lo, p_hi, st)          \
+                         : launch_grid_f64_mfma<WW, false>(P, p_lo, p_hi, st))        \
+             : (P.g.do_w ? launch_grid_f64<WW, true>(P, p_lo, p_hi, st)               \
+                         : launch_grid_f64<WW, false>(P, p_lo, p_hi, st)))
     SDP_W64_DISPATCH(P.g.W, SDP_G64);
 #undef SDP_G64
 }
@@ -4100,7 +4284,7 @@ static void fill_info(const Plan &P, sdp_hip_wgrid_info *info) {
     info->nitems = P.pt.nitems;
     info->plane_chunk = P.chunk_planes;
     info->bucket = P.g.sub;
-    info->padded = (P.pad4 || P.subpad) ? 1 : 0;
+    info->padded = (P.pad4 || P.subpad || P.pad64) ? 1 : 0;
     info->fp64 = P.f64 ? 1 : 0;
     info->tiled = P.g.tiled;
     info->grid_launches = (P.g.nplanes + P.chunk_planes - 1) / P.chunk_planes;
@@ -4336,7 +4520,7 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         (unsigned)std::min<int64_t>((int64_t)pt.t_maxseg * (kBinCells / 256), 8192);
     k_t_segscan<<<gseg, 256, 0, st>>>(pt.t_segs, pt.t_meta_ch, pt.t_m2, pt.t_stot);
     const unsigned gcol = (unsigned)std::min<int64_t>((int64_t)nb * (kBinCells / 256), 8192);
-    if (P.pad4)
+    if (P.pad4 || P.pad64)
         k_t_cellcol<true><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_segb, pt.t_nsegb, pt.t_stot,
                                                 pt.t_tot, P.chunk, pt.t_binsum, pt.t_npad);
     else
@@ -4365,12 +4549,14 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     pt.fitems = scratch<FineItem>("fitems", (size_t)pt.nitems + 1);
     const unsigned gfin = (unsigned)std::min(nb, 4096);
     if (P.pad4)
-        k_t_cellfin<true><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
-                                                pt.t_cbase, reinterpret_cast<RecC *>(P.recs),
-                                                pt.fitems);
+        k_t_cellfin<true, 0><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
+                                                   pt.t_cbase, P.recs, pt.fitems);
+    else if (P.pad64)
+        k_t_cellfin<true, 2><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
+                                                   pt.t_cbase, P.recs, pt.fitems);
     else
-        k_t_cellfin<false><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
-                                                 pt.t_cbase, nullptr, pt.fitems);
+        k_t_cellfin<false, 1><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
+                                                    pt.t_cbase, nullptr, pt.fitems);
     if (nvis > 0) final_move();
     SDP_HIP_CHECK(hipGetLastError());
 }

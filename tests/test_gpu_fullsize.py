@@ -64,6 +64,12 @@ def test_c2_full_invert_against_reference_precision():
     out, info = kernels.ms2dirty(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], NPIX, NPIX,
                                  cell, cell, 1e-7, True, flip_uw=True)
     gpu = out.cpu().numpy()
+    # the reference's default precision on the GPU: epsilon 1e-12, the fp64
+    # NUFFT (W = 13, the same algorithm as the oracle) -- equal to 1e-10
+    out, info64 = kernels.ms2dirty(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], NPIX, NPIX,
+                                   cell, cell, 1e-12, True, flip_uw=True)
+    assert info64["fp64"] == 1 and info64["support"] == 13
+    gpu64 = out.cpu().numpy()
     uvw = obs["uvw"].cpu().numpy() * FLIP_UW
     freq = obs["freq"].cpu().numpy()
     ms = obs["vis"].cpu().numpy()
@@ -85,12 +91,17 @@ def test_c2_full_invert_against_reference_precision():
                                 nthreads=_threads())
     e_ref = rel_rms(ref[px, py], ex)
     e_gpu = rel_rms(gpu[px, py], ex)
+    err64 = rel_rms(gpu64, ref)
+    e_gpu64 = rel_rms(gpu64[px, py], ex)
     print(f"\nC2 full invert (123.6 Mvis, W_gpu={info['support']}, planes={info['nplanes']}): "
           f"rel-RMS GPU vs fp64 W=13 oracle {err:.3e}; at 48 exact pixels: GPU {e_gpu:.3e}, "
-          f"oracle {e_ref:.3e} (oracle grid {tg:.1f} s, fft {tf:.1f} s)")
+          f"oracle {e_ref:.3e} (oracle grid {tg:.1f} s, fft {tf:.1f} s); GPU fp64 (epsilon "
+          f"1e-12, {info64['nplanes']} planes) vs oracle {err64:.3e}, at the exact pixels "
+          f"{e_gpu64:.3e}")
     assert e_ref < 1e-9
     assert e_gpu < TOL
     assert err < TOL
+    assert err64 < 1e-10 and e_gpu64 < 1e-9
 
 
 @pytest.mark.timeout(900)
@@ -103,6 +114,11 @@ def test_c2_full_predict_against_reference_precision():
     v, info = kernels.dirty2ms(obs["uvw"], obs["freq"], torch.as_tensor(img, device="cuda:0"),
                                obs["wgt"], cell, cell, 1e-7, True, flip_uw=True)
     gpu = v.cpu().numpy()
+    del v
+    v, _ = kernels.dirty2ms(obs["uvw"], obs["freq"], torch.as_tensor(img, device="cuda:0"),
+                            obs["wgt"], cell, cell, 1e-12, True, flip_uw=True,
+                            vis_dtype=torch.complex128)
+    gpu64 = v.cpu().numpy()
     uvw = obs["uvw"].cpu().numpy() * FLIP_UW
     freq = obs["freq"].cpu().numpy()
     wgt = obs["wgt"].cpu().numpy()
@@ -116,12 +132,14 @@ def test_c2_full_predict_against_reference_precision():
     ex = wgrid_cpu.exact_rows(uvw, freq, img, rows, cell, cell, True, nthreads=_threads())
     e_ref = rel_rms(ref[rows], ex)
     e_gpu = rel_rms(gpu[rows], ex)
+    err64 = rel_rms(gpu64, ref)
     print(f"\nC2 full predict (123.6 Mvis, W_gpu={info['support']}): rel-RMS GPU vs fp64 W=13 "
           f"oracle {err:.3e}; 24 exact rows x 64 chans: GPU {e_gpu:.3e}, oracle {e_ref:.3e} "
-          f"(oracle degrid {tg:.1f} s, fft {tf:.1f} s)")
+          f"(oracle degrid {tg:.1f} s, fft {tf:.1f} s); GPU fp64 vs oracle {err64:.3e}")
     assert e_ref < 1e-9
     assert e_gpu < TOL
     assert err < TOL
+    assert err64 < 1e-10
 
 
 # ---------------------------------------------------------------------------
