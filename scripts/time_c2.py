@@ -1,5 +1,5 @@
 """C2 invert and predict wall times (median of --reps after a warm-up), for
-A/B of library variants: python scripts/time_c2.py [--reps N]."""
+A/B of library variants: python scripts/time_c2.py [--reps N] [--eps E]."""
 import argparse
 import json
 import os
@@ -16,6 +16,7 @@ from ska_sdp_func_python_amd import kernels, simulation  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=7)
+ap.add_argument("--eps", type=float, default=1e-7, help="1e-7: fp32 NUFFT; 1e-12: fp64")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 obs = simulation.device_observation(100, 64, 0.95e9, 1.76e9, config="MID", seed=0, device=dev)
@@ -30,9 +31,9 @@ for name in ("invert", "predict"):
         t0 = time.perf_counter()
         if name == "invert":
             _, info = kernels.ms2dirty(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], 4096, 4096,
-                                       cell, cell, 1e-12, True, flip_uw=True)
+                                       cell, cell, a.eps, True, flip_uw=True)
         else:
-            _, info = kernels.dirty2ms(obs["uvw"], obs["freq"], img, obs["wgt"], cell, cell, 1e-12,
+            _, info = kernels.dirty2ms(obs["uvw"], obs["freq"], img, obs["wgt"], cell, cell, a.eps,
                                        True, flip_uw=True)
         torch.cuda.synchronize()
         if i:
