@@ -460,6 +460,14 @@ def _host(a):
 class Visibility(Dataset):
     """Visibility with dims [time, baseline, frequency, polarisation]."""
 
+    def groupby(self, coord, squeeze=False):
+        """xarray's ``groupby("time", squeeze=False)`` as the sky-model
+        drivers use it: (time, one-time-sample Visibility) pairs."""
+        if coord != "time":
+            raise ValueError(f"groupby: only 'time' is supported, not {coord}")
+        times = np.asarray(self._vars["time"])
+        return list(zip(times.tolist(), visibility_time_slices(self)))
+
     @classmethod
     def constructor(cls, frequency=None, channel_bandwidth=None, phasecentre=None,
                     configuration=None, uvw=None, time=None, vis=None, weight=None,

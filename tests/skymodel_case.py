@@ -1,0 +1,53 @@
+"""The sky-model driver case shared by tests/test_gpu_skymodel.py and the
+reference-executed fixture generator (tests/golden/make_golden.py,
+make_skymodel): a seeded SKA-LOW-like observation, a 128^2 stokesI model
+image with a few bright pixels, four point components, a mask, a B-jones
+gain table and a Gaussian 'primary beam' image."""
+
+import math
+
+import numpy as np
+
+
+def _setup(seed=3):
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd import simulation
+    rng = np.random.default_rng(seed)
+    pc = dm.SkyCoord(math.radians(15.0), math.radians(-45.0))
+    vis = simulation.make_visibility("LOW", nants=24, ntimes=4, nchan=3, f_lo=1.0e8, f_hi=1.1e8,
+                                     ha_span_h=1.0, phasecentre=pc)
+    npix = 128
+    cell = 0.5 / (2 * simulation.max_uv_lambda(vis))
+    f = np.asarray(vis.frequency.data)
+    im = dm.create_image(npix, cell, pc, frequency=float(f.mean()), channel_bandwidth=1e8)
+    px = np.zeros((1, 1, npix, npix))
+    for _ in range(6):
+        px[0, 0, rng.integers(40, 88), rng.integers(40, 88)] = rng.uniform(0.5, 2.0)
+    im["pixels"].data = px
+    comps = []
+    for _ in range(4):
+        x, y = rng.uniform(30, 98, 2)
+        d = dm.pixel_to_skycoord(x, y, im.image_acc.wcs, origin=1)
+        comps.append(dm.SkyComponent(d, f, flux=rng.uniform(1, 3, (3, 1)),
+                                     polarisation_frame=dm.PolarisationFrame("stokesI")))
+    mask = im.copy(deep=True)
+    mpx = np.ones((1, 1, npix, npix))
+    mpx[..., :, :24] = 0.0
+    mpx[..., 100:, :] = 0.5
+    mask["pixels"].data = mpx
+    gt = dm.create_gaintable_from_visibility(vis, jones_type="B")
+    gt["gain"].data = (rng.normal(1.0, 0.1, gt["gain"].data.shape)
+                       * np.exp(1j * rng.normal(0, 0.3, gt["gain"].data.shape)))
+    sm = dm.SkyModel(image=im, components=comps, gaintable=gt, mask=mask)
+    return vis, sm, cell
+
+
+def _pb(im):
+    """A Gaussian 'primary beam' image over the model image."""
+    npix = im["pixels"].data.shape[-1]
+    y, x = np.mgrid[:npix, :npix] - npix // 2
+    beam = im.copy(deep=True)
+    beam["pixels"].data = np.exp(-(x ** 2 + y ** 2) / (2 * 40.0 ** 2))[None, None]
+    return beam
+
+

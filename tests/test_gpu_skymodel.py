@@ -17,52 +17,11 @@ import calops_oracle as co
 import nufft_oracle as orc
 import ref_oracle as ro
 from conftest import rel_rms
+from skymodel_case import _pb, _setup
 
 pytestmark = pytest.mark.gpu
 FLIP_UW = np.array([-1.0, 1.0, -1.0])
 TOL = 5e-6
-
-
-def _setup(seed=3):
-    from ska_sdp_func_python_amd import datamodels as dm
-    from ska_sdp_func_python_amd import simulation
-    rng = np.random.default_rng(seed)
-    pc = dm.SkyCoord(math.radians(15.0), math.radians(-45.0))
-    vis = simulation.make_visibility("LOW", nants=24, ntimes=4, nchan=3, f_lo=1.0e8, f_hi=1.1e8,
-                                     ha_span_h=1.0, phasecentre=pc)
-    npix = 128
-    cell = 0.5 / (2 * simulation.max_uv_lambda(vis))
-    f = np.asarray(vis.frequency.data)
-    im = dm.create_image(npix, cell, pc, frequency=float(f.mean()), channel_bandwidth=1e8)
-    px = np.zeros((1, 1, npix, npix))
-    for _ in range(6):
-        px[0, 0, rng.integers(40, 88), rng.integers(40, 88)] = rng.uniform(0.5, 2.0)
-    im["pixels"].data = px
-    comps = []
-    for _ in range(4):
-        x, y = rng.uniform(30, 98, 2)
-        d = dm.pixel_to_skycoord(x, y, im.image_acc.wcs, origin=1)
-        comps.append(dm.SkyComponent(d, f, flux=rng.uniform(1, 3, (3, 1)),
-                                     polarisation_frame=dm.PolarisationFrame("stokesI")))
-    mask = im.copy(deep=True)
-    mpx = np.ones((1, 1, npix, npix))
-    mpx[..., :, :24] = 0.0
-    mpx[..., 100:, :] = 0.5
-    mask["pixels"].data = mpx
-    gt = dm.create_gaintable_from_visibility(vis, jones_type="B")
-    gt["gain"].data = (rng.normal(1.0, 0.1, gt["gain"].data.shape)
-                       * np.exp(1j * rng.normal(0, 0.3, gt["gain"].data.shape)))
-    sm = dm.SkyModel(image=im, components=comps, gaintable=gt, mask=mask)
-    return vis, sm, cell
-
-
-def _pb(im):
-    """A Gaussian 'primary beam' image over the model image."""
-    npix = im["pixels"].data.shape[-1]
-    y, x = np.mgrid[:npix, :npix] - npix // 2
-    beam = im.copy(deep=True)
-    beam["pixels"].data = np.exp(-(x ** 2 + y ** 2) / (2 * 40.0 ** 2))[None, None]
-    return beam
 
 
 def _beam_fluxes(comps, beam_px, wcs):
@@ -154,3 +113,42 @@ def test_skymodel_calibrate_invert(use_pb):
     assert rel_rms(np.asarray(res[0]["pixels"].data)[0, 0], sd / maxwt) < TOL
     np.testing.assert_allclose(np.asarray(res[1]["pixels"].data)[0, 0], np.sqrt(np.sqrt(sf / maxwt)),
                                rtol=1e-12)
+
+
+def test_drivers_and_ng_wrappers_match_the_reference_execution():
+    """The HIP sky-model drivers and invert_ng / predict_ng against
+    tests/golden/skymodel.npz: the reference's own skymodel_imaging.py,
+    imaging.py, ng.py, dft.py and apply_gaintable executed on this case
+    (make_golden.make_skymodel), with ducc0's NUFFT evaluated as its exact
+    direct sums (ducc0 absent).  Tolerance 5e-6 (the fp32 NUFFT term)."""
+    from conftest import golden
+    from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng
+    from ska_sdp_func_python_amd.sky_model import (skymodel_calibrate_invert,
+                                                   skymodel_predict_calibrate)
+    ref = golden("skymodel.npz")
+    vis, sm, cell = _setup()
+    beam = _pb(sm.image)
+    assert abs(cell - float(ref["cell"])) < 1e-15
+    for use_pb in (False, True):
+        out = skymodel_predict_calibrate(vis, sm, context="ng", docal=True, inverse=True,
+                                         get_pb=(lambda v, im: beam) if use_pb else None)
+        e = rel_rms(np.asarray(out.vis.data), ref[f"predict_pb{int(use_pb)}"])
+        print(f"\nskymodel_predict_calibrate pb={use_pb}: {e:.2e}")
+        assert e < TOL
+    vis, sm, cell = _setup(seed=5)
+    vis["vis"].data = ref["invert_vis"]
+    for use_pb in (False, True):
+        d, w = skymodel_calibrate_invert(vis, sm, context="ng", docal=True,
+                                         get_pb=(lambda v, im: beam) if use_pb else None)
+        e = rel_rms(np.asarray(d["pixels"].data), ref[f"invert_pb{int(use_pb)}_dirty"])
+        ww = np.asarray(w["pixels"].data) if hasattr(w, "image_acc") else np.asarray(w)
+        print(f"skymodel_calibrate_invert pb={use_pb}: {e:.2e}")
+        assert e < TOL
+        np.testing.assert_allclose(ww, ref[f"invert_pb{int(use_pb)}_weights"], rtol=1e-12)
+    d, sw = invert_ng(vis, sm.image)
+    e = rel_rms(np.asarray(d["pixels"].data), ref["invert_ng_dirty"])
+    np.testing.assert_allclose(np.asarray(sw), ref["invert_ng_sumwt"], rtol=1e-12)
+    p = predict_ng(vis, sm.image)
+    ep = rel_rms(np.asarray(p.vis.data), ref["predict_ng_vis"])
+    print(f"invert_ng {e:.2e}, predict_ng {ep:.2e}")
+    assert e < TOL and ep < TOL
