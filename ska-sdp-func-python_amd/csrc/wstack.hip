@@ -95,6 +95,7 @@ struct Geo {
     // tlx x tly bins of 64 x 64 cells per first plane (nbins in all); the
     // keys of a bin are contiguous (bin-major, 4096 per bin)
     int tiled, tlx, tly, nbins;
+    double inv_nchan;  // 1 / nchan (the two-level passes' row = v / nchan)
 };
 
 struct __attribute__((aligned(32))) VisRec {
@@ -183,9 +184,8 @@ struct Coord {
 // the visibility's grid coordinates from its row's uvw (metres) and its
 // frequency
 __device__ __forceinline__ Coord vis_coord_v(const Geo &g, double um, double vm, double wm,
-                                             double f) {
+                                             double s) {
     Coord c;
-    const double s = f / kCLight;
     const double u = g.su * um * s;
     const double v = vm * s;
     c.w = g.su * wm * s;
@@ -198,10 +198,13 @@ __device__ __forceinline__ Coord vis_coord_v(const Geo &g, double um, double vm,
     c.dv = fb + 1.0 - b;
     c.fu = (float)c.du;
     c.fv = (float)c.dv;
-    const int ic = ((int)fa + 1 + g.ngx / 2) % g.ngx;
-    const int jc = ((int)fb + 1 + g.ngy / 2) % g.ngy;
-    c.ic0 = ic < 0 ? ic + g.ngx : ic;
-    c.jc0 = jc < 0 ? jc + g.ngy : jc;
+    // (fa + 1 + ng/2) mod ng: |a| < ng puts it in (-ng, 2 ng), so one
+    // conditional add or subtract is the modulo (no integer division)
+    int ic = (int)fa + 1 + g.ngx / 2, jc = (int)fb + 1 + g.ngy / 2;
+    ic = ic >= g.ngx ? ic - g.ngx : (ic < 0 ? ic + g.ngx : ic);
+    jc = jc >= g.ngy ? jc - g.ngy : (jc < 0 ? jc + g.ngy : jc);
+    c.ic0 = ic;
+    c.jc0 = jc;
     // the footprint origin must lie in the bucket window and the first plane
     // in [0, nps): always so when the geometry comes from these
     // visibilities' own extremes (a margin of >= 2 cells / half a plane), but
@@ -229,14 +232,13 @@ __device__ __forceinline__ Coord vis_coord_v(const Geo &g, double um, double vm,
 
 __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restrict__ uvw,
                                            int64_t rs, int64_t row, double f) {
-    return vis_coord_v(g, uvw[row * rs], uvw[row * rs + 1], uvw[row * rs + 2], f);
+    return vis_coord_v(g, uvw[row * rs], uvw[row * rs + 1], uvw[row * rs + 2], f / kCLight);
 }
 
 // w slab: the visibility's first plane (computed exactly as vis_coord does)
 // lies in the sequence's layout but outside this call's slab -- tested before
 // anything else of the visibility is read
-__device__ __forceinline__ bool slab_out_v(const Geo &g, double wm, double f) {
-    const double s = f / kCLight;
+__device__ __forceinline__ bool slab_out_v(const Geo &g, double wm, double s) {
     const double w = g.su * wm * s;
     const double pw = (w - g.w0) / g.dw;
     const int p0 = (int)floor(fmin(fmax(pw - 0.5 * g.W, -2.0), 2.0e9)) + 1;
@@ -2136,7 +2138,7 @@ __global__ void k_bucket_f64(Geo g, int64_t nvis, const double *__restrict__ uvw
 constexpr int kMaxBins = 16384;    // LDS histogram of the first level (64 KiB)
 constexpr int kTThreads = 1024;     // second-level kernels, bin scans
 constexpr int kT1Threads = 512;     // count and value passes (VGPR-limited occupancy)
-constexpr unsigned kTChunk = 32768;  // records per second-level chunk
+constexpr unsigned kTChunk = 131072;  // records per second-level chunk
 constexpr unsigned kTSeg = 16;       // chunks per segment of the cells' column prefix
 constexpr int kTU = 2;               // visibilities per lane in flight (count / value pass)
 constexpr int kTU2 = 4;              // records per lane in flight (cell count / final move)
@@ -2175,32 +2177,43 @@ __device__ __forceinline__ unsigned lds_run_add(unsigned key, bool valid, unsign
 // v < 2^32 (the plan refuses larger calls).
 struct TLoad {
     uint32_t row, chan;
-    double um, vm, wm, f, wd;
+    double um, vm, wm, s, wd;  // s = frequency / c (fsc[chan]: the same division as vis_coord)
     bool live;
 };
 
 __device__ __forceinline__ TLoad t_load(const Geo &g, int64_t v, int64_t vend,
                                         const double *__restrict__ uvw, int64_t rs,
-                                        const double *__restrict__ freq,
+                                        const double *__restrict__ fsc,
                                         const void *__restrict__ wgt, int64_t wrs, int64_t wcs,
                                         const VisExtra &x) {
     TLoad L;
     L.live = v < vend;
-    const uint32_t v32 = L.live ? (uint32_t)v : 0u, r32 = v32 / (uint32_t)g.nchan;
+    const uint32_t v32 = L.live ? (uint32_t)v : 0u, nc = (uint32_t)g.nchan;
+    // row = v / nchan through the fp64 reciprocal (exact to one step, then
+    // corrected), not an integer division
+    uint32_t r32 = (uint32_t)((double)v32 * g.inv_nchan);
+    if ((uint64_t)r32 * nc > v32) --r32;
+    else if ((uint64_t)(r32 + 1u) * nc <= v32) ++r32;
     L.row = r32;
-    L.chan = v32 - r32 * (uint32_t)g.nchan;
+    L.chan = v32 - r32 * nc;
     L.um = L.vm = L.wm = 0.0;
-    L.f = 1.0;
+    L.s = 1.0;
     L.wd = 0.0;
     if (L.live) {
         const double *p = uvw + (int64_t)L.row * rs;
         L.um = p[0];
         L.vm = p[1];
         L.wm = p[2];
-        L.f = freq[L.chan];
+        L.s = fsc[L.chan];
         L.wd = eff_weight(wgt, wrs, wcs, x, L.row, L.chan);
     }
     return L;
+}
+
+// frequency / c per channel (the division vis_coord performs per visibility)
+__global__ void k_fscale(const double *__restrict__ freq, int nchan, double *__restrict__ fsc) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < nchan) fsc[c] = freq[c] / kCLight;
 }
 
 struct TPoint {
@@ -2221,10 +2234,10 @@ __device__ __forceinline__ TPoint t_classify(const Geo &g, const TLoad &L, const
     p.chan = (int)L.chan;
     p.c.ok = false;
     if (!L.live) return p;
-    if (g.slab && slab_out_v(g, L.wm, L.f)) return p;
+    if (g.slab && slab_out_v(g, L.wm, L.s)) return p;
     p.wd = L.wd;
     if (!(x.all || (float)p.wd != 0.0f)) return p;
-    p.c = vis_coord_v(g, L.um, L.vm, L.wm, L.f);
+    p.c = vis_coord_v(g, L.um, L.vm, L.wm, L.s);
     if (!p.c.ok) {
         if (kCount && !p.c.skip) atomicAdd(nbad, 1ull);
         return p;
@@ -2246,7 +2259,7 @@ __device__ __forceinline__ void t_weight_sum(double ws, double *sw_slots) {
 
 __global__ __launch_bounds__(kT1Threads) void k_t_count(Geo g, int64_t nvis, int64_t vpw,
                                                        const double *__restrict__ uvw, int64_t rs,
-                                                       const double *__restrict__ freq,
+                                                       const double *__restrict__ fsc,
                                                        const void *__restrict__ wgt, int64_t wrs,
                                                        int64_t wcs, VisExtra x, double *sw_slots,
                                                        unsigned *__restrict__ binc,
@@ -2262,7 +2275,7 @@ __global__ __launch_bounds__(kT1Threads) void k_t_count(Geo g, int64_t nvis, int
         TLoad L[kTU];
 #pragma unroll
         for (int u = 0; u < kTU; ++u)
-            L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, freq, wgt, wrs, wcs,
+            L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, fsc, wgt, wrs, wcs,
                           x);
 #pragma unroll
         for (int u = 0; u < kTU; ++u) {
@@ -2396,7 +2409,7 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x, const T
     const bool rot = g.do_w || x.shift;
     if (rot) {
         ph = g.do_w ? p.c.w * g.s0 : 0.0;
-        if (x.shift) ph += (L.um * x.sl + L.vm * x.sm + L.wm * x.sn) * (L.f / kCLight);
+        if (x.shift) ph += (L.um * x.sl + L.vm * x.sm + L.wm * x.sn) * L.s;
         ph -= rint(ph);
     }
     if constexpr (KIND == 2) {
@@ -2467,7 +2480,7 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x, const T
 template <class VT, int KIND, bool kGrid>
 __global__ __launch_bounds__(kT1Threads) void k_t_scatter(
     Geo g, int64_t nvis, int64_t vpw, const double *__restrict__ uvw, int64_t rs,
-    const double *__restrict__ freq, const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
+    const double *__restrict__ fsc, const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
     const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x, double *sw_slots,
     const unsigned *__restrict__ binbase, const unsigned *__restrict__ m1, void *__restrict__ out,
     uint16_t *__restrict__ lkey) {
@@ -2484,7 +2497,7 @@ __global__ __launch_bounds__(kT1Threads) void k_t_scatter(
         typename V::type xv[kTU];
 #pragma unroll
         for (int u = 0; u < kTU; ++u) {
-            L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, freq, wgt, wrs, wcs,
+            L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, fsc, wgt, wrs, wcs,
                           x);
             xv[u] = V::load(vis, vrs, vcs, x, L[u]);
         }
@@ -2569,10 +2582,8 @@ __global__ __launch_bounds__(256) void k_t_cellcol(const unsigned *__restrict__ 
                                                    const unsigned *__restrict__ nsegb,
                                                    unsigned *__restrict__ stot,
                                                    unsigned *__restrict__ tot, unsigned chunk,
-                                                   unsigned long long *__restrict__ binsum,
-                                                   unsigned *__restrict__ npad) {
+                                                   unsigned long long *__restrict__ binsum) {
     __shared__ unsigned long long red[4];
-    __shared__ unsigned redp[4];
     const unsigned nwork = nbl[0] * (kBinCells / 256);
     for (unsigned w = blockIdx.x; w < nwork; w += gridDim.x) {
         const unsigned b = nbl[1 + w / (kBinCells / 256)];
@@ -2604,22 +2615,15 @@ __global__ __launch_bounds__(256) void k_t_cellcol(const unsigned *__restrict__ 
         unsigned long long r =
             ((unsigned long long)pd << 32) |
             (unsigned long long)((threadIdx.x & 15) == 0 ? (gt + chunk - 1) / chunk : 0u);
-        unsigned pads = pd - run;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            r += __shfl_xor(r, o, 64);
-            pads += __shfl_xor(pads, o, 64);
-        }
-        if ((threadIdx.x & 63) == 0) {
-            red[threadIdx.x >> 6] = r;
-            redp[threadIdx.x >> 6] = pads;
-        }
+        for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = r;
         __syncthreads();
         if (threadIdx.x == 0) {
+            // (one atomic per 256 cells of a bin: the padded total needs no
+            // chip-wide counter -- same-address atomics serialise at ~10 ns)
             const unsigned long long t = red[0] + red[1] + red[2] + red[3];
             if (t) atomicAdd(&binsum[b], t);
-            const unsigned tp = redp[0] + redp[1] + redp[2] + redp[3];
-            if (tp) atomicAdd(npad, tp);
         }
         __syncthreads();
     }
@@ -3364,11 +3368,12 @@ struct Part {
     unsigned t_maxseg = 0;  // bound on their prefix segments
     unsigned *t_binc = nullptr, *t_binbase = nullptr, *t_segb = nullptr, *t_nsegb = nullptr;
     unsigned *t_nbl = nullptr, *t_m1 = nullptr, *t_m2 = nullptr, *t_tot = nullptr;
-    unsigned *t_cbase = nullptr, *t_meta_ch = nullptr, *t_npad = nullptr, *t_stot = nullptr;
+    unsigned *t_cbase = nullptr, *t_meta_ch = nullptr, *t_stot = nullptr;
     TChunk *t_chunks = nullptr;
     TSeg *t_segs = nullptr;
     unsigned long long *t_binsum = nullptr, *t_bofs = nullptr;
     uint16_t *t_lkey = nullptr;
+    double *t_fsc = nullptr;  // frequency / c per channel
     void *t_a = nullptr;  // records in bin order (the value pass's output)
 };
 
@@ -3678,6 +3683,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.py = in.py;
     g.su = (in.flags & SDP_HIP_FLIP_UW) ? -1.0 : 1.0;
     g.nchan = in.nchan;
+    g.inv_nchan = 1.0 / in.nchan;
     g.nrow = in.nrow;
 
     // uvw and frequency extremes (device) -> host, or the batch sequence's
@@ -4446,7 +4452,6 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         pt.t_stot = scratch<unsigned>("t_stot", (size_t)pt.t_maxseg * kBinCells);
         pt.t_nbl = scratch<unsigned>("t_nbl", nb + 1);
         pt.t_meta_ch = scratch<unsigned>("t_meta_ch", 2);
-        pt.t_npad = scratch<unsigned>("t_npad", 1);
         pt.t_chunks = scratch<TChunk>("t_chunks", pt.t_maxch);
         pt.t_binsum = scratch<unsigned long long>("t_binsum", nb);
         pt.t_bofs = scratch<unsigned long long>("t_bofs", nb + 1);
@@ -4455,15 +4460,16 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         pt.t_tot = scratch<unsigned>("t_tot", (size_t)nb * kBinCells);
         pt.t_cbase = scratch<unsigned>("t_cbase", (size_t)nb * kBinCells);
         pt.t_lkey = scratch<uint16_t>("rec_lkey", std::max<int64_t>(nvis, 1));
+        pt.t_fsc = scratch<double>("t_fscale", g.nchan);
         pt.t_a = scratch<char>("recs_a", (size_t)std::max<int64_t>(nvis, 1) * rsz);
         pt.nbad = scratch<unsigned long long>("nbad", 1);
         pt.meta = scratch<unsigned>("meta", g.nps + 6);
         SDP_HIP_CHECK(hipMemsetAsync(pt.t_binc, 0, nb * sizeof(unsigned), st));
         SDP_HIP_CHECK(hipMemsetAsync(pt.t_binsum, 0, nb * sizeof(unsigned long long), st));
         SDP_HIP_CHECK(hipMemsetAsync(pt.nbad, 0, sizeof(unsigned long long), st));
-        SDP_HIP_CHECK(hipMemsetAsync(pt.t_npad, 0, sizeof(unsigned), st));
         if (after_clear) after_clear();
     }
+    k_fscale<<<grid1d(g.nchan, 256), 256, 0, st>>>(in.freq, g.nchan, pt.t_fsc);
     const int cus = cu_count();
     const unsigned gch = std::min<unsigned>(pt.t_maxch, 4u * (unsigned)cus);
     auto scatter = [&](double *sl) {
@@ -4472,7 +4478,7 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
             constexpr int K = decltype(kind_tag)::value;
             constexpr bool G = decltype(grid_tag)::value;
             k_t_scatter<VT, K, G><<<pt.t_g1, kT1Threads, lds_bins, st>>>(
-                g, nvis, pt.t_vpw, in.uvw, in.uvw_rs, in.freq,
+                g, nvis, pt.t_vpw, in.uvw, in.uvw_rs, pt.t_fsc,
                 G ? static_cast<const VT *>(in.vis) : nullptr, in.vrs, in.vcs, in.wgt, in.wrs,
                 in.wcs, in.x, sl, pt.t_binbase, pt.t_m1, pt.t_a, pt.t_lkey);
         };
@@ -4510,7 +4516,7 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     }
     if (nvis > 0)
         k_t_count<<<pt.t_g1, kT1Threads, lds_bins, st>>>(g, nvis, pt.t_vpw, in.uvw, in.uvw_rs,
-                                                        in.freq, in.wgt, in.wrs, in.wcs, in.x,
+                                                        pt.t_fsc, in.wgt, in.wrs, in.wcs, in.x,
                                                         slots, pt.t_binc, pt.t_m1, pt.nbad);
     k_t_bins<<<1, kTThreads, 0, st>>>(nb, pt.t_binc, pt.t_binbase, pt.t_segb, pt.t_nsegb,
                                       pt.t_nbl, pt.t_chunks, pt.t_segs, pt.t_meta_ch);
@@ -4522,10 +4528,10 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     const unsigned gcol = (unsigned)std::min<int64_t>((int64_t)nb * (kBinCells / 256), 8192);
     if (P.pad4 || P.pad64)
         k_t_cellcol<true><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_segb, pt.t_nsegb, pt.t_stot,
-                                                pt.t_tot, P.chunk, pt.t_binsum, pt.t_npad);
+                                                pt.t_tot, P.chunk, pt.t_binsum);
     else
         k_t_cellcol<false><<<gcol, 256, 0, st>>>(pt.t_nbl, pt.t_segb, pt.t_nsegb, pt.t_stot,
-                                                 pt.t_tot, P.chunk, pt.t_binsum, pt.t_npad);
+                                                 pt.t_tot, P.chunk, pt.t_binsum);
     k_t_binscan<<<1, kTThreads, 0, st>>>(nb, g.tlx * g.tly, g.nps, pt.t_binsum, pt.t_binbase,
                                          pt.nbad, pt.t_bofs, pt.meta);
     SDP_HIP_CHECK(hipGetLastError());
