@@ -3062,18 +3062,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
         }
         if (cur >= 0) store_cell(cur);
         __syncthreads();
-        for (int i = threadIdx.x; i < RS; i += NTH) {
-            const double v = reg[i];
-            if (v == 0.0) continue;
-            const int c = i % NC, cell = i / NC;
-            const int p = (int)it.p0 + (c >> 1);
-            if (p < p_lo || p >= p_hi) continue;
+        // flush in the planes' own order: consecutive lanes take consecutive
+        // doubles of one plane's region rows (re/im interleaved, RY cells of
+        // a row contiguous), so a wave's atomics cover a few contiguous
+        // segments instead of 64 addresses in 26 different planes
+        constexpr int FPP = RX * RY * 2;  // doubles per plane of the region
+        for (int i = threadIdx.x; i < NQ * FPP; i += NTH) {
+            const int q = i / FPP, f = i - q * FPP, cell = f >> 1;
+            const double v = reg[cell * NC + 2 * q + (f & 1)];
+            const int p = (int)it.p0 + q;
+            if (v == 0.0 || p < p_lo || p >= p_hi) continue;
             const int xl = cell / RY, yl = cell - xl * RY;
             int gx = ibase + xl;
             if (gx >= g.ngx) gx -= g.ngx;
             int gy = jbase + yl;
             if (gy >= g.ngy) gy -= g.ngy;
-            atomicAdd(grid + 2 * ((size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy) + (c & 1),
+            atomicAdd(grid + 2 * ((size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy) + (f & 1),
                       v);
         }
     }
