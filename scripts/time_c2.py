@@ -42,5 +42,6 @@ for name in ("invert", "predict"):
     kernels.set_stage_timing(False)
     res[name] = {"ms": round(1e3 * float(np.median(ts)), 3),
                  **{k: round(float(np.median([x[k] for x in infos])), 3)
-                    for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")}}
+                    for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
+                 **{k: infos[-1][k] for k in ("support", "nplanes", "nitems", "nvis_used")}}
 print(json.dumps(res))

@@ -96,6 +96,11 @@ struct Geo {
     // keys of a bin are contiguous (bin-major, 4096 per bin)
     int tiled, tlx, tly, nbins;
     double inv_nchan;  // 1 / nchan (the two-level passes' row = v / nchan)
+    // folded per-visibility factors (geo_factors): a = u_m s kax, b = v_m s
+    // kby, fractional plane pw = w_m s kpw - kpw0 of the FULL layout (a w
+    // slab subtracts its first plane as an integer, so slabs partition the
+    // visibilities exactly) -- no fp64 division per visibility
+    double kax, kby, kpw, kpw0;
 };
 
 struct __attribute__((aligned(32))) VisRec {
@@ -186,11 +191,10 @@ struct Coord {
 __device__ __forceinline__ Coord vis_coord_v(const Geo &g, double um, double vm, double wm,
                                              double s) {
     Coord c;
-    const double u = g.su * um * s;
-    const double v = vm * s;
-    c.w = g.su * wm * s;
-    const double a = u * g.px * g.ngx;
-    const double b = v * g.py * g.ngy;
+    const double ws = wm * s;
+    c.w = g.su * ws;
+    const double a = (um * s) * g.kax;
+    const double b = (vm * s) * g.kby;
     c.ok = fabs(a) < (double)g.ngx && fabs(b) < (double)g.ngy;
     if (!c.ok) return c;
     const double fa = floor(a - 0.5 * g.W), fb = floor(b - 0.5 * g.W);
@@ -213,11 +217,11 @@ __device__ __forceinline__ Coord vis_coord_v(const Geo &g, double um, double vm,
     c.ok = (unsigned)(c.ic0 - g.wx0) < (unsigned)g.wnx &&
            (unsigned)(c.jc0 - g.wy0) < (unsigned)g.wny;
     if (g.do_w) {
-        const double pw = (c.w - g.w0) / g.dw;
+        const double pw = fma(ws, g.kpw, -g.kpw0);
         const double fp = floor(fmin(fmax(pw - 0.5 * g.W, -2.0), 2.0e9));
         c.dw = fp + 1.0 - pw;
         c.fw = (float)c.dw;
-        c.p0 = (int)fp + 1;
+        c.p0 = (int)fp + 1 - g.slab_lo;
         const bool in_slab = c.p0 >= 0 && c.p0 < g.nps;
         c.ok = c.ok && in_slab;
         if (g.slab) c.skip = !in_slab && (unsigned)(c.p0 + g.slab_lo) < (unsigned)g.nps_all;
@@ -239,19 +243,14 @@ __device__ __forceinline__ Coord vis_coord(const Geo &g, const double *__restric
 // lies in the sequence's layout but outside this call's slab -- tested before
 // anything else of the visibility is read
 __device__ __forceinline__ bool slab_out_v(const Geo &g, double wm, double s) {
-    const double w = g.su * wm * s;
-    const double pw = (w - g.w0) / g.dw;
-    const int p0 = (int)floor(fmin(fmax(pw - 0.5 * g.W, -2.0), 2.0e9)) + 1;
+    const double pw = fma(wm * s, g.kpw, -g.kpw0);
+    const int p0 = (int)floor(fmin(fmax(pw - 0.5 * g.W, -2.0), 2.0e9)) + 1 - g.slab_lo;
     return (p0 < 0 || p0 >= g.nps) && (unsigned)(p0 + g.slab_lo) < (unsigned)g.nps_all;
 }
 
 __device__ __forceinline__ bool slab_out(const Geo &g, const double *__restrict__ uvw, int64_t rs,
                                          int64_t row, double f) {
-    const double s = f / kCLight;
-    const double w = g.su * uvw[row * rs + 2] * s;
-    const double pw = (w - g.w0) / g.dw;
-    const int p0 = (int)floor(fmin(fmax(pw - 0.5 * g.W, -2.0), 2.0e9)) + 1;
-    return (p0 < 0 || p0 >= g.nps) && (unsigned)(p0 + g.slab_lo) < (unsigned)g.nps_all;
+    return slab_out_v(g, uvw[row * rs + 2], f / kCLight);
 }
 
 // p0-major bucket keys: the items of a range of first planes are contiguous.
@@ -2790,6 +2789,111 @@ __global__ __launch_bounds__(kTThreads) void k_t_final(const TChunk *__restrict_
     }
 }
 
+// k_t_final with the batch's writes coalesced: each batch of NB records is
+// counting-sorted by cell in LDS (batch histogram, block scan, staging), then
+// written out in that order, so a cell's records of the batch leave as one
+// contiguous run instead of lane-scattered 16-byte stores.  LDS: cursors and
+// batch counts (kBinCells each), the staged records and their destinations.
+template <int KIND, int NB>
+constexpr size_t t_final_lds() {
+    return (size_t)2 * kBinCells * sizeof(unsigned) + (size_t)NB * sizeof(unsigned) +
+           (size_t)NB * sizeof(typename TRec<KIND>::type);
+}
+
+template <int KIND, int NB>
+__global__ __launch_bounds__(kTThreads) void k_t_final_s(const TChunk *__restrict__ chunks,
+                                                         const unsigned *__restrict__ meta_ch,
+                                                         const uint16_t *__restrict__ lkey,
+                                                         const unsigned *__restrict__ m2,
+                                                         const unsigned *__restrict__ stot,
+                                                         const unsigned *__restrict__ cbase,
+                                                         const void *__restrict__ in,
+                                                         void *__restrict__ out) {
+    using R = typename TRec<KIND>::type;
+    constexpr int NW = (int)(sizeof(R) / sizeof(uint4));
+    constexpr int U = NB / kTThreads;
+    constexpr int CPT = kBinCells / kTThreads;  // cells per thread (4)
+    static_assert(NB % kTThreads == 0 && CPT == 4, "k_t_final_s batch shape");
+    __shared__ typename TBlockScan<unsigned>::TempStorage tmp;
+    extern __shared__ __attribute__((aligned(16))) unsigned fsm[];
+    unsigned *const cur = fsm;
+    unsigned *const cnt = fsm + kBinCells;
+    unsigned *const sdst = cnt + kBinCells;
+    uint4 *const stg = reinterpret_cast<uint4 *>(sdst + NB);
+    const unsigned n = meta_ch[0];
+    const uint4 *src = reinterpret_cast<const uint4 *>(in);
+    uint4 *dst = reinterpret_cast<uint4 *>(out);
+    const int c0 = threadIdx.x * CPT;
+    for (int j = 0; j < CPT; ++j) cnt[c0 + j] = 0u;
+    for (unsigned c = blockIdx.x; c < n; c += gridDim.x) {
+        const TChunk t = chunks[c];
+        {
+            const uint4 pv = reinterpret_cast<const uint4 *>(m2 + (size_t)c * kBinCells)[threadIdx.x];
+            const uint4 sv =
+                reinterpret_cast<const uint4 *>(stot + (size_t)t.seg * kBinCells)[threadIdx.x];
+            const uint4 bv =
+                reinterpret_cast<const uint4 *>(cbase + (size_t)t.bin * kBinCells)[threadIdx.x];
+            reinterpret_cast<uint4 *>(cur)[threadIdx.x] =
+                make_uint4(pv.x + sv.x + bv.x, pv.y + sv.y + bv.y, pv.z + sv.z + bv.z,
+                           pv.w + sv.w + bv.w);
+        }
+        __syncthreads();
+        for (uint32_t i0 = t.b; i0 < t.e; i0 += NB) {
+            uint4 r[U][NW];
+            unsigned k[U], rk[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = i0 + u * kTThreads + threadIdx.x;
+                k[u] = 0xffffu;
+                if (i < t.e) {
+                    k[u] = lkey[i];
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) r[u][q] = src[(size_t)i * NW + q];
+                }
+            }
+            // rank of each record among the batch's records of its cell
+#pragma unroll
+            for (int u = 0; u < U; ++u) rk[u] = lds_run_add<true>(k[u], k[u] != 0xffffu, cnt);
+            __syncthreads();
+            unsigned h[CPT], s = 0;
+#pragma unroll
+            for (int j = 0; j < CPT; ++j) {
+                h[j] = cnt[c0 + j];
+                s += h[j];
+            }
+            unsigned x;
+            TBlockScan<unsigned>(tmp).ExclusiveSum(s, x);
+#pragma unroll
+            for (int j = 0; j < CPT; ++j) {
+                cnt[c0 + j] = x;  // the cell's first staging slot
+                x += h[j];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (k[u] != 0xffffu) {
+                    const unsigned slot = cnt[k[u]] + rk[u];
+                    sdst[slot] = cur[k[u]] + rk[u];
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) stg[slot * NW + q] = r[u][q];
+                }
+            }
+            __syncthreads();
+            const int nb = (int)min((uint32_t)NB, t.e - i0);
+            for (int j = threadIdx.x; j < nb * NW; j += kTThreads) {
+                const int rec = j / NW, q = j - rec * NW;
+                dst[(size_t)sdst[rec] * NW + q] = stg[j];
+            }
+#pragma unroll
+            for (int j = 0; j < CPT; ++j) {
+                cur[c0 + j] += h[j];
+                cnt[c0 + j] = 0u;
+            }
+            __syncthreads();
+        }
+    }
+}
+
 template <int W, bool WS>
 constexpr size_t grid_f64_lds() {
     return (size_t)(WS ? W : 1) * (W + 1) * (W + 7) * sizeof(double2) +
@@ -2928,67 +3032,123 @@ __global__ __launch_bounds__(64) void k_grid_f64(Geo g, const VisRec64 *__restri
     }
 }
 
-// fp64 MFMA gridder (invert at epsilon < 1e-7) on 4-padded cells (the
-// two-level bucketing pads VisRec64 cells to a multiple of 4 records for it,
-// SDP_HIP_F64_MFMA).  A cell's records share their footprint origin, so its
-// contribution is one GEMM on v_mfma_f64_16x16x4_f64 (exact fp64 FMAs):
+// fp64 MFMA kernels (epsilon < 1e-7, W <= 16) on one-cell buckets.
+//
+// Taps.  The ES kernel's W taps of an offset f (s = f + W/2 in (0, 1]) are
+// evaluated as W polynomials of degree kPoly64 in t = 2 s - 1 (Horner, the
+// coefficients uniform across lanes: scalar loads of a per-W table fitted on
+// the host at Chebyshev nodes, es_poly64_table), interior taps within ~1e-14
+// of the kernel; the two edge taps, where the kernel's sqrt(1 - x^2) is not
+// analytic, are evaluated exactly.  One lane computes all taps of one
+// (record, axis) pair of a 16-record block: a few hundred FMAs where the
+// per-tap exp/sqrt cost ~3x more.
+constexpr int kPoly64 = 12;
+constexpr int kPolyStride = 16;  // table [kPoly64 + 1][kPolyStride]
+constexpr int kBlk64 = 16;       // records per tap block
+
+// taps j in [j0, j1) of the pair's offset f into dst[j]
+template <int W>
+__device__ __forceinline__ void es_taps_poly(double f, int j0, int j1, const double *__restrict__ pc,
+                                             double ihw, double beta, double *dst) {
+    const double t = 2.0 * (f + 0.5 * W) - 1.0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        if (j < j0 || j >= j1) continue;
+        double v;
+        if (j == 0 || j == W - 1) {
+            v = es_tap64(f, j, ihw, beta);
+        } else {
+            v = pc[kPoly64 * kPolyStride + j];
+#pragma unroll
+            for (int d = kPoly64 - 1; d >= 0; --d) v = fma(v, t, pc[d * kPolyStride + j]);
+        }
+        dst[j] = v;
+    }
+}
+
+// The tap block of nb <= kBlk64 records (b0 ..): [record][tu | tv | tw |
+// cre, cim] rows of TR = 3 W + 2 doubles.  `part` / `nparts`: this wave's
+// share of each pair's taps (the gridder's two waves split them in halves).
+template <int W, bool WS>
+__device__ __forceinline__ void stage_block64(const VisRec64 *__restrict__ recs, uint32_t b0, int nb,
+                                              double *tap, const double *__restrict__ pc,
+                                              double ihw, double beta, int lane, int part,
+                                              int nparts) {
+    constexpr int TR = 3 * W + 2;
+    const int hw = (W + nparts - 1) / nparts, j0 = part * hw, j1 = min(W, j0 + hw);
+    if (lane < 3 * kBlk64) {
+        const int r = lane / 3, ax = lane - 3 * r;
+        if (r < nb) {
+            const VisRec64 *R = recs + b0 + r;
+            double *dst = tap + r * TR + ax * W;
+            if (ax == 2 && !WS) {
+                for (int j = j0; j < j1; ++j) dst[j] = j == 0 ? 1.0 : 0.0;
+            } else {
+                const double f = ax == 0 ? R->du : (ax == 1 ? R->dv : R->dw);
+                es_taps_poly<W>(f, j0, j1, pc, ihw, beta, dst);
+            }
+        }
+    } else if (part == 0 && lane - 3 * kBlk64 < nb) {
+        const int r = lane - 3 * kBlk64;
+        const VisRec64 *R = recs + b0 + r;
+        tap[r * TR + 3 * W] = R->cre;
+        tap[r * TR + 3 * W + 1] = R->cim;
+    }
+}
+
+// fp64 MFMA gridder (invert) on 4-padded cells (the two-level bucketing pads
+// VisRec64 cells to a multiple of 4 records, SDP_HIP_F64_MFMA).  A cell's
+// records share their footprint origin, so its contribution is one GEMM on
+// v_mfma_f64_16x16x4_f64 (exact fp64 FMAs):
 //     C[(kx, ky), (q, re/im)] += sum_r tu_r[kx] tv_r[ky] * tw_r[q] c_r
-// A = the W^2 separable (u, v) taps (ceil(W^2 / 16) M-tiles), B = the w taps
-// x value (2 W columns: one N-tile per wave -- W = 13: 2 waves, 26 of 32
-// columns), K = 4 records of one cell.  Per K-step each wave issues MT
-// independent MFMAs, with 2 MT fp64 tap products and one B product as its
-// VALU work.  Accumulators are region-resident: loaded from the item's LDS
-// region tile [x][y][(q, re/im)] (fp64) when a cell starts and stored back
-// when it ends; the two waves own disjoint columns, so no barrier is needed
-// at cell changes.  The 16-record tap block ([record][tu | tv | tw | c]) is
-// computed once by both waves; the region is flushed per item with fp64
-// global atomics (zeros skipped), as k_grid_f64.
+// M-tile kx (W tiles) holds the rows ky = 0..15 (ky >= W: A = 0), N = the
+// 2 NQ (q, re/im) columns (one 16-column tile per wave), K = 4 records of
+// the cell.  Lane (row (lane >> 4) + 4 i, column lane & 15) of tile kx sits
+// in the item's LDS region [x][y][column] at a compile-time offset from one
+// per-lane base, so a cell change is 4 W stores and 4 W loads with
+// immediate offsets.  Rows ky >= W add exact zeros to region cells of the
+// same wave's columns (an identity update: the region is RY = 8 + 15 rows
+// deep); columns >= 2 NQ are never stored.  The region is zeroed per item
+// and flushed once with fp64 global atomics (zeros skipped) in plane order.
 template <int W, bool WS>
 constexpr int f64m_waves() {
     return (2 * (WS ? W : 1) + 15) / 16;
 }
 template <int W, bool WS>
+constexpr int f64m_ry() {
+    return 8 + 15;
+}
+template <int W, bool WS>
 constexpr size_t grid_f64m_lds() {
-    return (size_t)(W + 1) * (W + 7) * 2 * (WS ? W : 1) * sizeof(double) + 64 * sizeof(double) +
-           (size_t)kTap64 * (3 * W + 2) * sizeof(double);
+    return (size_t)(W + 1) * f64m_ry<W, WS>() * 2 * (WS ? W : 1) * sizeof(double) +
+           (size_t)kBlk64 * (3 * W + 2) * sizeof(double);
 }
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
 template <int W, bool WS>
 __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64_mfma(
     Geo g, const VisRec64 *__restrict__ recs, const FineItem *__restrict__ items,
-    uint32_t n_items, double *__restrict__ grid, int p_lo, int p_hi) {
+    uint32_t n_items, double *__restrict__ grid, int p_lo, int p_hi,
+    const double *__restrict__ pc) {
+    static_assert(W <= 16, "one M-tile of 16 rows per kx");
     constexpr int NQ = WS ? W : 1, NC = 2 * NQ, NW = f64m_waves<W, WS>();
-    constexpr int MT = (W * W + 15) / 16, RX = W + 1, RY = W + 7, RS = RX * RY * NC;
+    constexpr int RX = W + 1, RY = f64m_ry<W, WS>(), RS = RX * RY * NC;
     constexpr int TR = 3 * W + 2, NTH = 64 * NW;
     extern __shared__ __attribute__((aligned(16))) double smd[];
-    double *const reg = smd;        // [RX][RY][NC]
-    double *const dummy = smd + RS;  // sink of the accumulator rows / columns outside the GEMM
-    double *const tap = dummy + 64;  // [kTap64][TR]
+    double *const reg = smd;       // [RX][RY][NC]
+    double *const tap = smd + RS;  // [kBlk64][TR]
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const double ihw = 2.0 / W, beta = (double)g.beta;
-    // this lane's accumulator column (q, re/im) and B operand
     const int col = wv * 16 + (lane & 15);
     const bool colok = col < NC;
+    // B operand: tw[q] c[re/im] of record (lane >> 4); A: tu[kx] tv[ky]
     const int bq = 2 * W + (colok ? col >> 1 : 0), bc = 3 * W + (col & 1);
-    // accumulator element i of M-tile mt: tap row (lane >> 4) + 4 i -> its
-    // region offset (doubles, relative to the cell's origin) or -1
-    int tofs[MT][4];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int t = mt * 16 + (lane >> 4) + 4 * i, kx = t / W, ky = t - kx * W;
-            tofs[mt][i] = (t < W * W && colok) ? (kx * RY + ky) * NC + col : -1;
-        }
-    // A operand of M-tile mt: tap (lane & 15) + 16 mt of record lane >> 4
-    int au[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int t = mt * 16 + (lane & 15), kx = t / W, ky = t - kx * W;
-        au[mt] = t < W * W ? kx | ((W + ky) << 8) : -1;
-    }
+    const int ky = lane & 15;
+    const bool kyok = ky < W;
     const int rk = lane >> 4;
+    // accumulator (kx, i) of a cell at region cell (cx, cy): element
+    // ((cx + kx) RY + cy + rk + 4 i) NC + col
+    const int lbase = rk * NC + col;
     const size_t plane_elems = (size_t)g.ngx * g.ngy;
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
         uint32_t bnd[kGroupCell];
@@ -2998,87 +3158,202 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
         group_origin(g, (int)it.tile, ibase, jbase);
         __syncthreads();  // the previous item's flush reads of the region
         for (int i = threadIdx.x; i < RS; i += NTH) reg[i] = 0.0;
-        doublex4 acc[MT];
+        doublex4 acc[W];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = doublex4{0.0, 0.0, 0.0, 0.0};
-        int cur = -1;
-        auto store_cell = [&](int cell) {
-            const int cb = ((cell & 1) * RY + (cell >> 1)) * NC;
+        for (int kx = 0; kx < W; ++kx) acc[kx] = doublex4{0.0, 0.0, 0.0, 0.0};
+        int cur = -1, cb = 0;
+        auto store_cell = [&]() {
+            if (colok) {
+                double *d = reg + cb + lbase;
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+                for (int kx = 0; kx < W; ++kx)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    double *d = tofs[mt][i] >= 0 ? reg + cb + tofs[mt][i] : dummy + lane;
-                    *d = acc[mt][i];
-                }
+                    for (int i = 0; i < 4; ++i) d[kx * RY * NC + 4 * i * NC] = acc[kx][i];
+            }
         };
         auto load_cell = [&](int cell) {
-            const int cb = ((cell & 1) * RY + (cell >> 1)) * NC;
+            cb = ((cell & 1) * RY + (cell >> 1)) * NC;
+            const double *s = reg + cb + lbase;
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+            for (int kx = 0; kx < W; ++kx)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    acc[mt][i] = tofs[mt][i] >= 0 ? reg[cb + tofs[mt][i]] : 0.0;
+                for (int i = 0; i < 4; ++i) acc[kx][i] = s[kx * RY * NC + 4 * i * NC];
         };
-        for (uint32_t b0 = it.b; b0 < it.e; b0 += kTap64) {
+        for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlk64) {
             __syncthreads();  // the region zeroing / previous block's tap reads
-            const int nb = (int)min((uint32_t)kTap64, it.e - b0);  // (a multiple of 4)
-            for (int t = threadIdx.x; t < nb * TR; t += NTH) {
-                const int r = t / TR, k = t - r * TR;
-                const VisRec64 *R = recs + b0 + r;
-                double tv;
-                if (k >= 3 * W) {
-                    tv = k == 3 * W ? R->cre : R->cim;
-                } else {
-                    const int ax = k / W, j = k - ax * W;
-                    if (ax == 2 && !WS) tv = j == 0 ? 1.0 : 0.0;
-                    else tv = es_tap64(ax == 0 ? R->du : (ax == 1 ? R->dv : R->dw), j, ihw, beta);
-                }
-                tap[t] = tv;
-            }
+            const int nb = (int)min((uint32_t)kBlk64, it.e - b0);  // (a multiple of 4)
+            stage_block64<W, WS>(recs, b0, nb, tap, pc, ihw, beta, lane, wv, NW);
             __syncthreads();
 #pragma unroll
-            for (int kk = 0; kk < kTap64 / 4; ++kk) {
+            for (int kk = 0; kk < kBlk64 / 4; ++kk) {
                 if (4 * kk >= nb) break;
                 const uint32_t ri = b0 + 4u * (uint32_t)kk;
                 int cell = 0;
 #pragma unroll
                 for (int c = 0; c < kGroupCell - 1; ++c) cell += ri >= bnd[c] ? 1 : 0;
                 if (cell != cur) {
-                    if (cur >= 0) store_cell(cur);
+                    if (cur >= 0) store_cell();
                     cur = cell;
                     load_cell(cur);
                 }
                 const double *T = tap + (4 * kk + rk) * TR;
-                const double bop = colok ? T[bq] * T[bc] : 0.0;
-                double aop[MT];
+                const double bop = T[bq] * T[bc];
+                const double tv = kyok ? T[W + ky] : 0.0;
+                double aop[W];
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    aop[mt] = au[mt] >= 0 ? T[au[mt] & 0xff] * T[au[mt] >> 8] : 0.0;
+                for (int kx = 0; kx < W; ++kx) aop[kx] = T[kx] * tv;
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    acc[mt] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[mt], bop, acc[mt], 0, 0, 0);
+                for (int kx = 0; kx < W; ++kx)
+                    acc[kx] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[kx], bop, acc[kx], 0, 0, 0);
             }
         }
-        if (cur >= 0) store_cell(cur);
+        if (cur >= 0) store_cell();
         __syncthreads();
         // flush in the planes' own order: consecutive lanes take consecutive
-        // doubles of one plane's region rows (re/im interleaved, RY cells of
-        // a row contiguous), so a wave's atomics cover a few contiguous
-        // segments instead of 64 addresses in 26 different planes
-        constexpr int FPP = RX * RY * 2;  // doubles per plane of the region
+        // doubles of one plane's region rows (re/im interleaved), so a wave's
+        // atomics cover a few contiguous segments
+        constexpr int RYV = 8 + W - 1;  // rows a footprint reaches
+        constexpr int FPP = RX * RYV * 2;  // doubles per plane of the region
         for (int i = threadIdx.x; i < NQ * FPP; i += NTH) {
             const int q = i / FPP, f = i - q * FPP, cell = f >> 1;
-            const double v = reg[cell * NC + 2 * q + (f & 1)];
+            const int xl = cell / RYV, yl = cell - xl * RYV;
+            const double v = reg[(xl * RY + yl) * NC + 2 * q + (f & 1)];
             const int p = (int)it.p0 + q;
             if (v == 0.0 || p < p_lo || p >= p_hi) continue;
-            const int xl = cell / RY, yl = cell - xl * RY;
             int gx = ibase + xl;
             if (gx >= g.ngx) gx -= g.ngx;
             int gy = jbase + yl;
             if (gy >= g.ngy) gy -= g.ngy;
             atomicAdd(grid + 2 * ((size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy) + (f & 1),
                       v);
+        }
+    }
+}
+
+// fp64 MFMA degridder (predict), the adjoint GEMM per block of <= 16
+// records of one cell:
+//     P[(q, re/im), r] = sum_(kx, ky) G[(kx, ky), (q, re/im)] tu_r[kx] tv_r[ky]
+// M = the 2 NQ (q, re/im) rows (<= 2 tiles), N = 16 records, K = the taps
+// in steps of 4 rows ky (ky >= W: B = 0), then V_r = c_r sum_q tw_r[q]
+// P[q, r] (lane-local plus two cross-lane adds).  The item's region of the
+// planes is staged in LDS once ([x][y][(q, re/im)], rows ky >= W zero) and
+// shared read-only by the workgroup's waves, each of which takes every NW-th
+// 16-record block of the item's cells (no barriers between blocks).
+constexpr int kDeg64Waves = 8;
+template <int W, bool WS>
+constexpr size_t degrid_f64m_lds() {
+    return (size_t)(W + 1) * 23 * 2 * (WS ? W : 1) * sizeof(double) +
+           (size_t)kDeg64Waves * kBlk64 * (3 * W + 2) * sizeof(double);
+}
+
+template <int W, bool WS, class VT>
+__global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
+    Geo g, const VisRec64 *__restrict__ recs, const FineItem *__restrict__ items,
+    uint32_t n_items, const double2 *__restrict__ grid, int p_lo, int p_hi, VT *vis, int64_t vrs,
+    int64_t vcs, int accumulate, OutConv oc, const double *__restrict__ pc) {
+    static_assert(W <= 16, "K-steps of 4 rows ky < 16");
+    constexpr int NQ = WS ? W : 1, NC = 2 * NQ, MT = (NC + 15) / 16;
+    constexpr int RX = W + 1, RY = 23, RS = RX * RY * NC, TR = 3 * W + 2;
+    constexpr int NTH = 64 * kDeg64Waves;
+    extern __shared__ __attribute__((aligned(16))) double smd[];
+    double *const reg = smd;  // [RX][RY][NC]
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double *const tap = smd + RS + wv * kBlk64 * TR;  // this wave's tap block
+    const double ihw = 2.0 / W, beta = (double)g.beta;
+    const int rn = lane & 15, gk = lane >> 4;  // B column (record), K row
+    const size_t plane_elems = (size_t)g.ngx * g.ngy;
+    const bool plain = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
+    // A operand of M-tile m at tap (kx, 4 s + gk): region element
+    // (kx RY + cy + 4 s + gk) NC + 16 m + rn of the cell's origin (cx, cy)
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        uint32_t bnd[kGroupCell];
+        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
+        if (it.b >= it.e) continue;
+        int ibase, jbase;
+        group_origin(g, (int)it.tile, ibase, jbase);
+        __syncthreads();  // the previous item's region reads
+        for (int i = threadIdx.x; i < RS; i += NTH) {
+            const int cell = i / NC, c = i - cell * NC, q = c >> 1;
+            const int xl = cell / RY, yl = cell - xl * RY;
+            const int p = (int)it.p0 + q;
+            double v = 0.0;
+            if (yl < 8 + W - 1 && p >= p_lo && p < p_hi) {
+                int gx = ibase + xl;
+                if (gx >= g.ngx) gx -= g.ngx;
+                int gy = jbase + yl;
+                if (gy >= g.ngy) gy -= g.ngy;
+                const double *src = reinterpret_cast<const double *>(
+                    grid + (size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy);
+                v = src[c & 1];
+            }
+            reg[i] = v;
+        }
+        __syncthreads();
+        // the item's blocks: cell c's records [s_c, e_c) in blocks of 16
+        uint32_t cs = it.b;
+        int blk = 0;
+        for (int c = 0; c < kGroupCell; ++c) {
+            const uint32_t ce = max(cs, c < kGroupCell - 1 ? min(bnd[c], it.e) : it.e);
+            for (uint32_t b0 = cs; b0 < ce; b0 += kBlk64, ++blk) {
+                if (blk % kDeg64Waves != wv) continue;
+                const int nb = (int)min((uint32_t)kBlk64, ce - b0);
+                stage_block64<W, WS>(recs, b0, nb, tap, pc, ihw, beta, lane, 0, 1);
+                wave_lds_sync();
+                const double *T = tap + rn * TR;  // this lane's record (B column)
+                const bool rok = rn < nb;
+                const double *G = reg + ((c & 1) * RY + (c >> 1)) * NC + gk * NC + rn;
+                doublex4 acc[MT];
+#pragma unroll
+                for (int m = 0; m < MT; ++m) acc[m] = doublex4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kx = 0; kx < W; ++kx) {
+                    const double tu = rok ? T[kx] : 0.0;
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const int ky = 4 * s + gk;
+                        const double tv = T[W + min(ky, W - 1)];
+                        const double bop = ky < W ? tu * tv : 0.0;
+#pragma unroll
+                        for (int m = 0; m < MT; ++m) {
+                            const double gv = G[(kx * RY + 4 * s) * NC + 16 * m];
+                            const double aop = 16 * m + rn < NC ? gv : 0.0;
+                            acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop, acc[m], 0, 0, 0);
+                        }
+                    }
+                }
+                // lane holds rows 16 m + gk + 4 i of column rn: (q, re/im) =
+                // ((16 m + gk + 4 i) >> 1, gk & 1)
+                double part = 0.0;
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = 16 * m + gk + 4 * i;
+                        if (row < NC) part = fma(acc[m][i], T[2 * W + (row >> 1)], part);
+                    }
+                part += __shfl_xor(part, 32, 64);  // gk and gk ^ 2: the same component
+                const double pim = __shfl_xor(part, 16, 64);
+                if (gk == 0 && rok) {
+                    const double sr = part, si = pim;
+                    const double cr = T[3 * W], ci = T[3 * W + 1];
+                    const double xr = cr * sr - ci * si, xi = cr * si + ci * sr;
+                    const uint32_t idx = recs[b0 + rn].idx;
+                    const int64_t row = idx / (uint32_t)g.nchan;
+                    const int chan = (int)(idx - row * g.nchan);
+                    VT *pv_ = vis + row * vrs + chan * vcs;
+                    if (plain) {
+                        store_vis_d(pv_, xr, xi, accumulate);
+                    } else {
+                        for (int k = 0; k < oc.npv; ++k) {
+                            if (oc.cre[k] == 0.0 && oc.cim[k] == 0.0) continue;
+                            store_vis_d(pv_ + k * oc.vps, oc.cre[k] * xr - oc.cim[k] * xi,
+                                        oc.cre[k] * xi + oc.cim[k] * xr, accumulate);
+                        }
+                    }
+                }
+                wave_lds_sync();  // the block's tap reads before the next staging
+            }
+            cs = ce;
         }
     }
 }
@@ -3392,6 +3667,7 @@ struct Plan {
     RecC *recs_pad = nullptr;        // subpad: the 4-padded, cell-ordered records
     bool pad4 = false;               // one-cell buckets padded to 4 records (k_grid_mfma_pad)
     bool pad64 = false;              // fp64 invert: VisRec64 cells padded to 4 (k_grid_f64_mfma)
+    bool mfma64 = false;             // fp64 predict on k_degrid_f64_mfma (one-cell buckets)
     float2 *vdirect = nullptr;       // dirty2ms: the degridder writes c64 vis in place
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
@@ -3641,7 +3917,7 @@ static void w_layout(const Inputs &in, double wmin, double wmax, Geo &g) {
         g.s0 = 0.5 * tmax;
         g.dw = 1.0 / (2.0 * tmax);
         g.w0 = wmin - (0.5 * g.W - 0.5) * g.dw;
-        const double pwmax = (wmax - g.w0) / g.dw;
+        const double pwmax = std::fma(wmax, 1.0 / g.dw, -(g.w0 * (1.0 / g.dw)));
         g.nplanes = (int)std::floor(pwmax - 0.5 * g.W) + 1 + g.W;
         g.nps = g.nplanes - g.W + 1;
     } else {
@@ -3651,6 +3927,16 @@ static void w_layout(const Inputs &in, double wmin, double wmax, Geo &g) {
         g.nplanes = 1;
         g.nps = 1;
     }
+}
+
+// the folded per-visibility factors of vis_coord_v (the full layout's
+// plane origin: call before a w slab moves w0)
+static void geo_factors(Geo &g) {
+    const double idw = 1.0 / g.dw;
+    g.kax = g.su * g.px * g.ngx;
+    g.kby = g.py * g.ngy;
+    g.kpw = g.su * idw;
+    g.kpw0 = g.w0 * idw;
 }
 
 // Geometry shared by both directions: kernel, padded grid, w planes, bucket
@@ -3726,6 +4012,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
                 "some uvw coordinates exceed the image's Nyquist limit (|u|*pixsize >= 0.5)");
 
     w_layout(in, wmin, wmax, g);
+    geo_factors(g);
     // w slab of the sequence's plane layout (bounds[6], bounds[7]: first
     // planes [lo, hi)): this call's planes are lo .. hi + W - 2 and its w0 the
     // slab's first plane, so records, keys, FFTs and screens see only the slab
@@ -3766,10 +4053,15 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // two-level bucketing (k_t_*): one-cell keys in 64 x 64-cell bins, while
     // the bins of the window fit the first level's LDS histogram (C2: 2 first
     // planes x 59 x 61 bins); SDP_HIP_BUCKET2=0 selects the single-level
-    // one-cell histogram below (A/B and tests)
+    // one-cell histogram below (A/B and tests).  Not for the fp32 predict:
+    // its 32-byte records make the second move cost more than the
+    // single-level count pass's atomics save (C2 prep 7.3 vs 5.3 ms); =2
+    // forces it there too (tests)
     g.tiled = 0;
     g.tlx = g.tly = g.nbins = 0;
-    if (env_int("SDP_HIP_BUCKET2", 1) != 0 && env_int("SDP_HIP_BUCKET", 0) != kTileCoarse) {
+    const int b2 = env_int("SDP_HIP_BUCKET2", 1);
+    if (b2 != 0 && (grid_mode || P.f64 || b2 == 2) &&
+        env_int("SDP_HIP_BUCKET", 0) != kTileCoarse) {
         int x0, nx_, y0, ny_;
         window(amax, g.ngx, kTile, x0, nx_);
         window(bmax, g.ngy, kTile, y0, ny_);
@@ -3918,6 +4210,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // fp64 invert on the two-level bucketing: VisRec64 cells padded to 4 for
     // the MFMA gridder (SDP_HIP_F64_MFMA=0: the VALU gridder, unpadded)
     P.pad64 = grid_mode && g.tiled && P.f64 && env_int("SDP_HIP_F64_MFMA", 1) != 0;
+    P.mfma64 = !grid_mode && g.sub == kTileCell && P.f64 && env_int("SDP_HIP_F64_MFMA", 1) != 0;
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
     P.pt.nvis = nvis;
     if (g.tiled) return P;  // (records: bucket_tiled, once their padded count is known)
@@ -4186,6 +4479,65 @@ static void launch_degrid_f64(const Plan &P, int p_lo, int p_hi, VT *vis, int64_
         default: CALL(16); break; \
     }
 
+// The fp64 kernels' tap polynomials (es_taps_poly) for support W and shape
+// beta: per tap j, the interpolant of exp(beta (sqrt(1 - x^2) - 1)), x =
+// (s - W/2 + j) 2 / W, at the kPoly64 + 1 Chebyshev nodes of s in [0, 1],
+// as monomial coefficients in t = 2 s - 1 ([d][j], long double sums).  One
+// device table per (device, W), built on first use.
+static const double *es_poly64_table(int W, double beta, hipStream_t st) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, double *> tabs;
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair(dev, W);
+    auto it = tabs.find(key);
+    if (it != tabs.end()) return it->second;
+    constexpr int N = kPoly64 + 1;
+    std::vector<double> tab((size_t)N * kPolyStride, 0.0);
+    const long double pi = 3.141592653589793238462643383279502884L;
+    for (int j = 0; j < W; ++j) {
+        // values at the nodes t_k = cos(pi (k + 1/2) / N)
+        long double fv[N], cheb[N];
+        for (int k = 0; k < N; ++k) {
+            const long double t = std::cos(pi * (k + 0.5L) / N), s = 0.5L * (t + 1.0L);
+            const long double x = (s - 0.5L * W + j) * 2.0L / W, y = 1.0L - x * x;
+            fv[k] = y > 0 ? std::exp((long double)beta * (std::sqrt(y) - 1.0L)) : 0.0L;
+        }
+        for (int d = 0; d < N; ++d) {
+            long double a = 0;
+            for (int k = 0; k < N; ++k) a += fv[k] * std::cos(pi * d * (k + 0.5L) / N);
+            cheb[d] = a * (d == 0 ? 1.0L : 2.0L) / N;
+        }
+        // Chebyshev -> monomial: T_0 = 1, T_1 = t, T_{n+1} = 2 t T_n - T_{n-1}
+        long double mono[N] = {}, tm1[N] = {}, t0[N] = {}, t1[N] = {};
+        t0[0] = 1;
+        t1[1] = 1;
+        for (int d = 0; d < N; ++d) {
+            const long double *T = d == 0 ? t0 : t1;
+            for (int e = 0; e < N; ++e) mono[e] += cheb[d] * T[e];
+            if (d >= 1) {
+                long double nx[N] = {};
+                for (int e = 0; e + 1 < N; ++e) nx[e + 1] += 2 * t1[e];
+                for (int e = 0; e < N; ++e) nx[e] -= t0[e];
+                for (int e = 0; e < N; ++e) {
+                    t0[e] = t1[e];
+                    t1[e] = nx[e];
+                }
+            }
+        }
+        (void)tm1;
+        for (int d = 0; d < N; ++d) tab[(size_t)d * kPolyStride + j] = (double)mono[d];
+    }
+    double *dptr = nullptr;
+    SDP_HIP_CHECK(hipMalloc(&dptr, tab.size() * sizeof(double)));
+    SDP_HIP_CHECK(hipMemcpyAsync(dptr, tab.data(), tab.size() * sizeof(double),
+                                 hipMemcpyHostToDevice, st));
+    SDP_HIP_CHECK(hipStreamSynchronize(st));
+    tabs[key] = dptr;
+    return dptr;
+}
+
 template <int W, bool WS>
 static void launch_grid_f64_mfma(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
     const auto r = chunk_items(P, p_lo, p_hi);
@@ -4200,7 +4552,27 @@ static void launch_grid_f64_mfma(const Plan &P, int p_lo, int p_hi, hipStream_t 
     (void)attr;
     k_grid_f64_mfma<W, WS><<<n, 64 * f64m_waves<W, WS>(), grid_f64m_lds<W, WS>(), st>>>(
         P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
-        reinterpret_cast<double *>(P.grid), p_lo, p_hi);
+        reinterpret_cast<double *>(P.grid), p_lo, p_hi, es_poly64_table(W, P.g.beta, st));
+}
+
+template <int W, bool WS, class VT>
+static void launch_degrid_f64_mfma(const Plan &P, int p_lo, int p_hi, VT *vis, int64_t vrs,
+                                   int64_t vcs, int accumulate, const OutConv &oc,
+                                   hipStream_t st) {
+    const auto r = chunk_items(P, p_lo, p_hi);
+    const unsigned n = r.second - r.first;
+    if (n == 0) return;
+    static const bool attr = [] {  // dynamic LDS above 64 KiB
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_degrid_f64_mfma<W, WS, VT>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)degrid_f64m_lds<W, WS>()));
+        return true;
+    }();
+    (void)attr;
+    k_degrid_f64_mfma<W, WS, VT><<<n, 64 * kDeg64Waves, degrid_f64m_lds<W, WS>(), st>>>(
+        P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
+        reinterpret_cast<const double2 *>(P.grid), p_lo, p_hi, vis, vrs, vcs, accumulate, oc,
+        es_poly64_table(W, P.g.beta, st));
 }
 
 static void grid_f64(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
@@ -4217,8 +4589,17 @@ template <class VT>
 static void degrid_f64(const Plan &P, int p_lo, int p_hi, VT *vis, int64_t vrs, int64_t vcs,
                        int accumulate, const OutConv &oc, hipStream_t st) {
 #define SDP_D64(WW)                                                                        \
-    (P.g.do_w ? launch_degrid_f64<WW, true, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, st) \
-              : launch_degrid_f64<WW, false, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, st))
+    (P.mfma64                                                                              \
+         ? (P.g.do_w                                                                       \
+                ? launch_degrid_f64_mfma<WW, true, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, \
+                                                       oc, st)                             \
+                : launch_degrid_f64_mfma<WW, false, VT>(P, p_lo, p_hi, vis, vrs, vcs,       \
+                                                        accumulate, oc, st))               \
+         : (P.g.do_w                                                                       \
+                ? launch_degrid_f64<WW, true, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, \
+                                                  st)                                      \
+                : launch_degrid_f64<WW, false, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, \
+                                                   st)))
     SDP_W64_DISPATCH(P.g.W, SDP_D64);
 #undef SDP_D64
 }
@@ -4499,16 +4880,47 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         if (in.vis_dtype == SDP_HIP_C128) by_kind(TypeTag<double2>{});
         else by_kind(TypeTag<float2>{});
     };
+    // SDP_HIP_TFINAL: 1 (default) batches staged through 64 KiB of LDS, 2
+    // through 32 KiB (two workgroups per CU), 0 the unstaged move
+    static const int tfinal = env_int("SDP_HIP_TFINAL", 1);
+    auto staged = [&](auto kind_tag, auto nb_tag) {
+        constexpr int K = decltype(kind_tag)::value, NB = decltype(nb_tag)::value;
+        constexpr size_t lds = t_final_lds<K, NB>();
+        static const bool attr = [] {  // dynamic LDS above 64 KiB
+            SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_t_final_s<K, NB>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)t_final_lds<K, NB>()));
+            return true;
+        }();
+        (void)attr;
+        k_t_final_s<K, NB><<<gch, kTThreads, lds, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
+                                                         pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
+                                                         P.recs);
+    };
     auto final_move = [&] {
-        if (kind == 2)
-            k_t_final<2><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
-                                                     pt.t_stot, pt.t_cbase, pt.t_a, P.recs);
-        else if (kind == 0)
-            k_t_final<0><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
-                                                     pt.t_stot, pt.t_cbase, pt.t_a, P.recs);
-        else
-            k_t_final<1><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey, pt.t_m2,
-                                                     pt.t_stot, pt.t_cbase, pt.t_a, P.recs);
+        using I = std::integral_constant<int, 0>;
+        if (tfinal == 0) {
+            if (kind == 2)
+                k_t_final<2><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
+                                                         pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
+                                                         P.recs);
+            else if (kind == 0)
+                k_t_final<0><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
+                                                         pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
+                                                         P.recs);
+            else
+                k_t_final<1><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
+                                                         pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
+                                                         P.recs);
+        } else if (tfinal == 2) {
+            if (kind == 2) staged(std::integral_constant<int, 2>{}, std::integral_constant<int, 1024>{});
+            else if (kind == 0) staged(I{}, std::integral_constant<int, 2048>{});
+            else staged(std::integral_constant<int, 1>{}, std::integral_constant<int, 1024>{});
+        } else {
+            if (kind == 2) staged(std::integral_constant<int, 2>{}, std::integral_constant<int, 1024>{});
+            else if (kind == 0) staged(I{}, std::integral_constant<int, 4096>{});
+            else staged(std::integral_constant<int, 1>{}, std::integral_constant<int, 2048>{});
+        }
         SDP_HIP_CHECK(hipGetLastError());
     };
     if (values_only) {

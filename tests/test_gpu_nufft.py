@@ -39,10 +39,13 @@ def _problem(seed, nrow=300, nchan=3, umax=2000.0, frac=0.45):
 def bucket(request, monkeypatch):
     """Every bucketing: one-cell buckets (4-padded for the invert's MFMA
     gridder, plain for the MFMA degridder) from the two-level LDS-histogram
-    sort (k_t_*, the default at these sizes), the same buckets from the
-    single-level global histogram (SDP_HIP_BUCKET2=0), and 16x16-cell buckets
-    sub-sorted by cell per work item (the path of very large grids such as
-    C4's 16384^2 x 70 planes, forced here by SDP_HIP_BUCKET=16)."""
+    sort (k_t_*, the invert's default at these sizes; forced for the predict
+    too by SDP_HIP_BUCKET2=2), the same buckets from the single-level global
+    histogram (SDP_HIP_BUCKET2=0, the fp32 predict's default), and 16x16-cell
+    buckets sub-sorted by cell per work item (the path of very large grids
+    such as C4's 16384^2 x 70 planes, forced here by SDP_HIP_BUCKET=16)."""
+    if request.param == "fine":
+        monkeypatch.setenv("SDP_HIP_BUCKET2", "2")
     if request.param == "coarse":
         monkeypatch.setenv("SDP_HIP_BUCKET", "16")
     if request.param == "fine1":

@@ -62,7 +62,7 @@ def test_ms2dirty_f64_matches_exact(eps, tol, W, dow, vdt, gridder):
 @pytest.mark.parametrize("eps,tol", [(1e-12, 1e-10), (1e-9, 1e-7)])
 @pytest.mark.parametrize("dow", [False, True])
 @pytest.mark.parametrize("vdt", [torch.complex64, torch.complex128])
-def test_dirty2ms_f64_matches_exact(eps, tol, dow, vdt):
+def test_dirty2ms_f64_matches_exact(eps, tol, dow, vdt, gridder):
     from ska_sdp_func_python_amd import kernels
     uvw, freq, _, wgt, cell = _problem(72)
     rng = np.random.default_rng(73)
@@ -77,6 +77,27 @@ def test_dirty2ms_f64_matches_exact(eps, tol, dow, vdt):
     assert info["fp64"] == 1
     # a c64 output rounds each visibility to fp32 (~3e-8 relative)
     assert e < max(tol, 1e-7 if vdt == torch.complex64 else 0.0)
+
+
+@pytest.mark.parametrize("dow", [False, True])
+def test_f64_dense_cells_match_exact(dow, gridder):
+    """Many records per cell (blocks of 16 records, several per cell; cells
+    split across work items): invert and predict against the exact sums."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(78, nrow=3000, nchan=4, frac=0.45)
+    rng = np.random.default_rng(79)
+    npx = npy = 16
+    ex = orc.ms2dirty_exact(uvw * FLIP_UW, freq, ms, wgt, npx, npy, cell, cell, dow)
+    out, info = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), npx, npy, cell, cell, 1e-12,
+                                 dow, flip_uw=True)
+    e = rel_rms(out.cpu().numpy(), ex)
+    img = rng.normal(size=(npx, npy))
+    exv = orc.dirty2ms_exact(uvw * FLIP_UW, freq, img, wgt, cell, cell, dow)
+    v, _ = kernels.dirty2ms(T(uvw), T(freq), T(img), T(wgt), cell, cell, 1e-12, dow,
+                            flip_uw=True, vis_dtype=torch.complex128)
+    ev = rel_rms(v.cpu().numpy(), exv)
+    print(f"\nfp64 dense cells ({gridder}, w {dow}): invert {e:.2e}, predict {ev:.2e}")
+    assert e < 1e-10 and ev < 1e-10
 
 
 def test_f64_adjointness_and_accumulate():
