@@ -211,16 +211,68 @@ def api_rates(args, obs, cell):
         return min(ts)
 
     t_dev = timed(make(d))
+    nvis = nrow * nchan
+    out = {"invert_ng_device_visibility_ms": round(t_dev * 1e3, 2)}
+
+    def both(bvis, mdl):
+        """(pipelined, serial) ms of one invert_ng: consecutive NUFFT calls
+        alternating two streams and scratch slots (the default), and
+        SDP_HIP_OVERLAP=0 (one stream; pols share one bucketing)."""
+        r = {}
+        for tag, val in (("pipelined", "1"), ("serial", "0")):
+            os.environ["SDP_HIP_OVERLAP"] = val
+            invert_ng(bvis, mdl, epsilon=EPS_REQUESTED)
+            ts = []
+            for _ in range(2):
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                invert_ng(bvis, mdl, epsilon=EPS_REQUESTED)
+                torch.cuda.synchronize(dev)
+                ts.append(time.perf_counter() - t0)
+            r[tag] = min(ts)
+        os.environ.pop("SDP_HIP_OVERLAP", None)
+        return r
+
+    # a 4-pol MFS image (linear vis -> stokesIQUV, 4 NUFFT calls of 123.6 Mvis)
+    s4 = (nt, nb, nchan, 4)
+    v4 = obs["vis"].to(torch.complex128).reshape(nt, nb, nchan, 1).expand(s4).contiguous()
+    d4 = {"uvw": d["uvw"], "vis": v4, "w": torch.ones(s4, dtype=torch.float64, device=dev),
+          "f": torch.zeros(s4, dtype=torch.int64, device=dev)}
+    b4 = dm.Visibility.constructor(
+        frequency=freq, channel_bandwidth=np.full(nchan, 1e6), phasecentre=pc, uvw=d4["uvw"],
+        time=np.arange(nt, dtype=float), vis=d4["vis"], weight=d4["w"], imaging_weight=d4["w"],
+        flags=d4["f"], baselines=np.stack(np.triu_indices(197, 1), 1),
+        polarisation_frame=dm.PolarisationFrame("linear"))
+    m4 = dm.create_image(args.npix, cell, pc, polarisation_frame=dm.PolarisationFrame("stokesIQUV"),
+                         frequency=float(freq.mean()),
+                         channel_bandwidth=float(2 * (freq.max() - freq.min()) + 1e6), nchan=1)
+    r4 = both(b4, m4)
+    del b4, d4, v4
+    torch.cuda.empty_cache()
+    # a 16-channel cube (stokesI; 64 NUFFT calls of one visibility channel)
+    dfc = float(freq[1] - freq[0])
+    mc = dm.create_image(args.npix, cell, pc, frequency=float(freq[:4].mean()),
+                         channel_bandwidth=4 * dfc, nchan=16)
+    rc = both(make(d), mc)
+    out.update({
+        "invert_ng_4pol_ms": round(r4["pipelined"] * 1e3, 2),
+        "invert_ng_4pol_serial_ms": round(r4["serial"] * 1e3, 2),
+        "invert_ng_4pol_Mvis_s": round(4 * nvis / r4["pipelined"] / 1e6, 1),
+        "invert_ng_cube16_ms": round(rc["pipelined"] * 1e3, 2),
+        "invert_ng_cube16_serial_ms": round(rc["serial"] * 1e3, 2),
+        "invert_ng_cube16_Mvis_s": round(nvis / rc["pipelined"] / 1e6, 1)})
     h = {k: v.cpu().numpy() for k, v in d.items()}
     del d
     torch.cuda.empty_cache()
     t_host = timed(make(h))
-    nvis = nrow * nchan
-    return {"invert_ng_device_visibility_ms": round(t_dev * 1e3, 2),
-            "invert_ng_host_visibility_ms": round(t_host * 1e3, 2),
-            "host_visibility_Mvis_s": round(nvis / t_host / 1e6, 1),
-            "note": "reference-shaped invert_ng on a c128/f64/int64 Visibility; the host "
-                    "figure includes the H2D copies of ~5 GB (PCIe-inclusive) and the image D2H"}
+    out.update({"invert_ng_host_visibility_ms": round(t_host * 1e3, 2),
+                "host_visibility_Mvis_s": round(nvis / t_host / 1e6, 1),
+                "note": "reference-shaped invert_ng on a c128/f64/int64 Visibility; the host "
+                        "figure includes the H2D copies of ~5 GB (PCIe-inclusive) and the image "
+                        "D2H; 4pol: a linear-frame Visibility imaged to stokesIQUV (4 NUFFT "
+                        "calls); cube16: 64 vis channels onto a 16-channel image (64 calls); "
+                        "'serial' = SDP_HIP_OVERLAP=0 (one stream, pols share one bucketing)"})
+    return out
 
 
 def _timed_calls(fn, steps, warmup, dev):
@@ -332,12 +384,27 @@ def c2_predict_and_fp64(args, obs, cell, dev, cpu):
         "stages_ms": {k: round(float(info[k]), 3) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": f"k_grid_f64<{W},true>", "kernel_ms": round(kms, 4),
+                     "kernel": f"k_grid_f64_mfma<{W},true>", "kernel_ms": round(kms, 4),
                      "alg_bytes_per_launch": int(alg / max(1, info["grid_launches"])),
                      "compute": {"achieved": round(tfl, 2), "peak": FP64_PEAK_TFLOPS,
                                  "unit": "TFLOP/s", "frac": round(tfl / FP64_PEAK_TFLOPS, 4),
                                  "note": "4 W^3 fp64 flops per visibility"}},
         "cpu_baseline": c64}
+    del out
+    # the fp64 predict (dirty2ms at 1e-12: k_degrid_f64_mfma), same model
+    vout = torch.empty((obs["nrow"], nchan), dtype=torch.complex128, device=dev)
+
+    def pred64():
+        return kernels.dirty2ms(obs["uvw"], obs["freq"], img, None, cell, cell, EPS_REFERENCE,
+                                True, flip_uw=True, out=vout)
+    el, info = _timed_calls(pred64, max(2, args.extra_steps), 1, dev)
+    kms = info["ms_grid"] / max(1, info["grid_launches"])
+    fp64["predict"] = {
+        "value": round(nvis / el / 1e6, 3), "unit": "Mvis/s", "ms_per_step": round(el * 1e3, 3),
+        "stages_ms": {k: round(float(info[k]), 3) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
+        "kernel": f"k_degrid_f64_mfma<{info['support']},true>", "kernel_ms": round(kms, 4),
+        "compute_TFLOP_s": round(nvis * 4 * info["support"] ** 3 / (info["ms_grid"] * 1e-3) / 1e12, 2)}
+    del vout
     return {"c2_predict": predict, "c2_fp64": fp64}
 
 
@@ -977,16 +1044,26 @@ def main():
                         "frac": round(nvis_rank * 4 * info["support"] ** 3 / (ms_grid * 1e-3) / 1e12
                                       / FP32_PEAK_TFLOPS, 4)}}
 
+    def guarded(fn, *a):
+        """an auxiliary object of the line: its failure is recorded in the
+        line instead of losing the headline measurement"""
+        try:
+            return fn(*a)
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: {fn.__name__} failed: {e!r}", file=sys.stderr, flush=True)
+            return {"error": repr(e)[:300]}
+
     api = None
     if rank == 0 and world == 1 and not args.no_api:
-        api = api_rates(args, obs, cell)
+        api = guarded(api_rates, args, obs, cell)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_chans > 0:
         cpu = cpu_baseline(args, obs["umax"], nchan_total)
 
     extra = {}
     if world == 1 and not args.no_extra:
-        extra.update(c2_predict_and_fp64(args, obs, cell, dev, cpu))
+        r = guarded(c2_predict_and_fp64, args, obs, cell, dev, cpu)
+        extra.update(r if "error" not in r else {"c2_predict": r})
         # the other configurations, each timed on its own (free the C2 inputs
         # first: the whole-band C4 needs ~250 GB of HBM)
         del obs
@@ -994,11 +1071,11 @@ def main():
         torch.cuda.synchronize(dev)
         kernels.release_workspace()
         torch.cuda.empty_cache()
-        extra["c4_n1"] = run_c4(args, 1, 0, local, dev, sub=True)
+        extra["c4_n1"] = guarded(run_c4, args, 1, 0, local, dev, False, True)
         kernels.release_workspace()
         torch.cuda.empty_cache()
-        extra["c3"] = run_c3(args, 1, 0, dev, sub=True)
-        extra["c5"] = run_c5(args, 1, 0, dev, sub=True)
+        extra["c3"] = guarded(run_c3, args, 1, 0, dev, True)
+        extra["c5"] = guarded(run_c5, args, 1, 0, dev, True)
         kernels.release_workspace()
         torch.cuda.empty_cache()
 
@@ -1015,6 +1092,8 @@ def main():
                                      "slots: step i+1's bucketing under step i's gridding + "
                                      "FFT" if pipe else False),
                        "ms_per_step_serial": round(elapsed_serial / args.steps * 1e3, 3),
+                       "value_serial": round(nvis_rank * world / (elapsed_serial / args.steps)
+                                             / 1e6, 3),
                        "nvis_per_gpu": nvis_rank, "nchan_total": nchan_total,
                        "npix": args.npix, "cell_rad": cell, "support": info["support"],
                        "nplanes": info["nplanes"], "epsilon_requested": EPS_REQUESTED,

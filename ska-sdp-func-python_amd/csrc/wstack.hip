@@ -3035,64 +3035,114 @@ __global__ __launch_bounds__(64) void k_grid_f64(Geo g, const VisRec64 *__restri
 // fp64 MFMA kernels (epsilon < 1e-7, W <= 16) on one-cell buckets.
 //
 // Taps.  The ES kernel's W taps of an offset f (s = f + W/2 in (0, 1]) are
-// evaluated as W polynomials of degree kPoly64 in t = 2 s - 1 (Horner, the
-// coefficients uniform across lanes: scalar loads of a per-W table fitted on
-// the host at Chebyshev nodes, es_poly64_table), interior taps within ~1e-14
-// of the kernel; the two edge taps, where the kernel's sqrt(1 - x^2) is not
-// analytic, are evaluated exactly.  One lane computes all taps of one
-// (record, axis) pair of a 16-record block: a few hundred FMAs where the
-// per-tap exp/sqrt cost ~3x more.
+// evaluated as W polynomials of degree kPoly64 in t = 2 s - 1 (Horner; the
+// coefficients, uniform across lanes, fitted on the host at Chebyshev nodes,
+// es_poly64_table, and copied to LDS per workgroup).  Interior taps are
+// within ~1e-14 of the kernel; the two edge taps, where sqrt(1 - x^2) is not
+// analytic, within ~0.15 e^-beta, i.e. a tenth of the epsilon W is chosen
+// for (W = 9: 1.5e-9, W = 13: 1.6e-13, W = 16: 7e-15; the fp64 exp they
+// replace kept a dozen constants live in registers across the kernel).  One
+// lane computes all taps of one (record, axis) pair of a 16-record block.
 constexpr int kPoly64 = 12;
 constexpr int kPolyStride = 16;  // table [kPoly64 + 1][kPolyStride]
 constexpr int kBlk64 = 16;       // records per tap block
 
-// taps j in [j0, j1) of the pair's offset f into dst[j]
-template <int W>
-__device__ __forceinline__ void es_taps_poly(double f, int j0, int j1, const double *__restrict__ pc,
-                                             double ihw, double beta, double *dst) {
+constexpr int kPolyN = (kPoly64 + 1) * kPolyStride;  // doubles of the table
+
+// taps J0 .. J1 - 1 of the pair's offset f into dst[j]: Horner over the
+// degrees (outer) for all the taps at once (inner), the coefficients read
+// from the workgroup's LDS copy of the table (uniform addresses: broadcast
+// reads; as scalar loads the whole table stayed live in SGPRs and spilled)
+template <int W, int J0, int J1>
+__device__ __forceinline__ void es_taps_poly(double f, const double *cl, double ihw, double beta,
+                                             double *dst) {
+    constexpr int NJ = J1 - J0;
     const double t = 2.0 * (f + 0.5 * W) - 1.0;
+    // one degree's coefficients in registers at a time: each row's reads
+    // take their offset through an empty asm statement, so the compiler can
+    // neither hoist the table out of the caller's loops (it did: 169 doubles
+    // live, scratch spills) nor batch every row up front; the next row's
+    // reads are issued before this row's FMAs
+    int zo = 0;
+    asm volatile("" : "+v"(zo));
+    double v[NJ], c[NJ];
 #pragma unroll
-    for (int j = 0; j < W; ++j) {
-        if (j < j0 || j >= j1) continue;
-        double v;
-        if (j == 0 || j == W - 1) {
-            v = es_tap64(f, j, ihw, beta);
-        } else {
-            v = pc[kPoly64 * kPolyStride + j];
+    for (int j = 0; j < NJ; ++j) v[j] = cl[zo + kPoly64 * kPolyStride + J0 + j];
 #pragma unroll
-            for (int d = kPoly64 - 1; d >= 0; --d) v = fma(v, t, pc[d * kPolyStride + j]);
+    for (int j = 0; j < NJ; ++j) c[j] = cl[zo + (kPoly64 - 1) * kPolyStride + J0 + j];
+#pragma unroll
+    for (int d = kPoly64 - 1; d >= 0; --d) {
+        // row d - 1's reads hang on an offset that the previous row's FMA
+        // results fed (one row of lookahead, never the whole table)
+        double cn[NJ];
+        if (d > 0) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) cn[j] = cl[zo + (d - 1) * kPolyStride + J0 + j];
         }
-        dst[j] = v;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) v[j] = fma(v[j], t, c[j]);
+        asm volatile("" : "+v"(zo) : "v"(v[0]));
+        if (d > 0) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) c[j] = cn[j];
+        }
     }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) dst[J0 + j] = v[j];
 }
 
 // The tap block of nb <= kBlk64 records (b0 ..): [record][tu | tv | tw |
-// cre, cim] rows of TR = 3 W + 2 doubles.  `part` / `nparts`: this wave's
-// share of each pair's taps (the gridder's two waves split them in halves).
-template <int W, bool WS>
-__device__ __forceinline__ void stage_block64(const VisRec64 *__restrict__ recs, uint32_t b0, int nb,
-                                              double *tap, const double *__restrict__ pc,
-                                              double ihw, double beta, int lane, int part,
-                                              int nparts) {
-    constexpr int TR = 3 * W + 2;
-    const int hw = (W + nparts - 1) / nparts, j0 = part * hw, j1 = min(W, j0 + hw);
+// cre, cim] rows of TR = 3 W + 2 doubles, in two phases so that a block's
+// record loads can be issued a block ahead: stage64_load (lane < 48: the
+// offset of pair (record lane / 3, axis lane % 3); lanes 48..63: the value of
+// record lane - 48; lane < 16: the output index of record lane) and
+// stage64_write (the taps: `part` / `nparts` is this wave's share of each
+// pair's taps -- the gridder's two waves split them in halves).
+struct Stage64 {
+    double a, b;   // pair offset, or (cre, cim)
+    uint32_t idx;  // output index (degridder)
+};
+
+__device__ __forceinline__ Stage64 stage64_load(const VisRec64 *__restrict__ recs, uint32_t b0,
+                                                int nb, int lane) {
+    Stage64 s;
+    s.a = s.b = 0.0;
+    s.idx = 0u;
+    if (nb <= 0) return s;
     if (lane < 3 * kBlk64) {
         const int r = lane / 3, ax = lane - 3 * r;
         if (r < nb) {
             const VisRec64 *R = recs + b0 + r;
+            s.a = ax == 0 ? R->du : (ax == 1 ? R->dv : R->dw);
+        }
+    } else if (lane - 3 * kBlk64 < nb) {
+        const VisRec64 *R = recs + b0 + (lane - 3 * kBlk64);
+        s.a = R->cre;
+        s.b = R->cim;
+    }
+    if (lane < nb) s.idx = recs[b0 + lane].idx;
+    return s;
+}
+
+template <int W, bool WS, int J0, int J1>
+__device__ __forceinline__ void stage64_write(const Stage64 &s, int nb, double *tap, const double *cl,
+                                              double ihw, double beta, int lane, bool vals) {
+    constexpr int TR = 3 * W + 2;
+    if (lane < 3 * kBlk64) {
+        const int r = lane / 3, ax = lane - 3 * r;
+        if (r < nb) {
             double *dst = tap + r * TR + ax * W;
             if (ax == 2 && !WS) {
-                for (int j = j0; j < j1; ++j) dst[j] = j == 0 ? 1.0 : 0.0;
+#pragma unroll
+                for (int j = J0; j < J1; ++j) dst[j] = j == 0 ? 1.0 : 0.0;
             } else {
-                const double f = ax == 0 ? R->du : (ax == 1 ? R->dv : R->dw);
-                es_taps_poly<W>(f, j0, j1, pc, ihw, beta, dst);
+                es_taps_poly<W, J0, J1>(s.a, cl, ihw, beta, dst);
             }
         }
-    } else if (part == 0 && lane - 3 * kBlk64 < nb) {
+    } else if (vals && lane - 3 * kBlk64 < nb) {
         const int r = lane - 3 * kBlk64;
-        const VisRec64 *R = recs + b0 + r;
-        tap[r * TR + 3 * W] = R->cre;
-        tap[r * TR + 3 * W + 1] = R->cim;
+        tap[r * TR + 3 * W] = s.a;
+        tap[r * TR + 3 * W + 1] = s.b;
     }
 }
 
@@ -3121,7 +3171,7 @@ constexpr int f64m_ry() {
 template <int W, bool WS>
 constexpr size_t grid_f64m_lds() {
     return (size_t)(W + 1) * f64m_ry<W, WS>() * 2 * (WS ? W : 1) * sizeof(double) +
-           (size_t)kBlk64 * (3 * W + 2) * sizeof(double);
+           (size_t)kBlk64 * (3 * W + 2) * sizeof(double) + kPolyN * sizeof(double);
 }
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
@@ -3129,7 +3179,7 @@ template <int W, bool WS>
 __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64_mfma(
     Geo g, const VisRec64 *__restrict__ recs, const FineItem *__restrict__ items,
     uint32_t n_items, double *__restrict__ grid, int p_lo, int p_hi,
-    const double *__restrict__ pc) {
+    const double *__restrict__ pc, int dbg) {
     static_assert(W <= 16, "one M-tile of 16 rows per kx");
     constexpr int NQ = WS ? W : 1, NC = 2 * NQ, NW = f64m_waves<W, WS>();
     constexpr int RX = W + 1, RY = f64m_ry<W, WS>(), RS = RX * RY * NC;
@@ -3137,8 +3187,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
     extern __shared__ __attribute__((aligned(16))) double smd[];
     double *const reg = smd;       // [RX][RY][NC]
     double *const tap = smd + RS;  // [kBlk64][TR]
+    double *const cl = tap + kBlk64 * TR;  // the tap polynomials
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const double ihw = 2.0 / W, beta = (double)g.beta;
+    for (int i = threadIdx.x; i < kPolyN; i += NTH) cl[i] = pc[i];
+    constexpr int HW = (W + NW - 1) / NW;  // taps per wave (NW <= 2)
+    static_assert(NW <= 2, "the taps are split over at most two waves");
     const int col = wv * 16 + (lane & 15);
     const bool colok = col < NC;
     // B operand: tw[q] c[re/im] of record (lane >> 4); A: tu[kx] tv[ky]
@@ -3179,12 +3233,25 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[kx][i] = s[kx * RY * NC + 4 * i * NC];
         };
+        Stage64 nxt = stage64_load(recs, it.b, (int)min((uint32_t)kBlk64, it.e - it.b), lane);
         for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlk64) {
             __syncthreads();  // the region zeroing / previous block's tap reads
             const int nb = (int)min((uint32_t)kBlk64, it.e - b0);  // (a multiple of 4)
-            stage_block64<W, WS>(recs, b0, nb, tap, pc, ihw, beta, lane, wv, NW);
+            if (!(dbg & 2)) {
+            if (NW == 1 || wv == 0)
+                stage64_write<W, WS, 0, HW>(nxt, nb, tap, cl, ihw, beta, lane, true);
+            else
+                stage64_write<W, WS, (NW > 1 ? HW : 0), W>(nxt, nb, tap, cl, ihw, beta, lane, false);
+            }
+            // the next block's records, in flight during this block's K-steps
+            if (b0 + kBlk64 < it.e)
+                nxt = stage64_load(recs, b0 + kBlk64, (int)min((uint32_t)kBlk64, it.e - b0 - kBlk64),
+                                   lane);
             __syncthreads();
-#pragma unroll
+            // (K-steps not unrolled: unrolled, the register allocator gave
+            // the accumulators two register sets and copied all 104 doubles
+            // on every K-step without a cell change, behind the MFMAs)
+#pragma unroll 1
             for (int kk = 0; kk < kBlk64 / 4; ++kk) {
                 if (4 * kk >= nb) break;
                 const uint32_t ri = b0 + 4u * (uint32_t)kk;
@@ -3202,9 +3269,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
                 double aop[W];
 #pragma unroll
                 for (int kx = 0; kx < W; ++kx) aop[kx] = T[kx] * tv;
+                if (!(dbg & 4)) {
 #pragma unroll
                 for (int kx = 0; kx < W; ++kx)
                     acc[kx] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[kx], bop, acc[kx], 0, 0, 0);
+                } else {
+#pragma unroll
+                for (int kx = 0; kx < W; ++kx) acc[kx][0] += aop[kx] * bop;
+                }
             }
         }
         if (cur >= 0) store_cell();
@@ -3219,7 +3291,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
             const int xl = cell / RYV, yl = cell - xl * RYV;
             const double v = reg[(xl * RY + yl) * NC + 2 * q + (f & 1)];
             const int p = (int)it.p0 + q;
-            if (v == 0.0 || p < p_lo || p >= p_hi) continue;
+            if (v == 0.0 || p < p_lo || p >= p_hi || (dbg & 1)) continue;
             int gx = ibase + xl;
             if (gx >= g.ngx) gx -= g.ngx;
             int gy = jbase + yl;
@@ -3243,7 +3315,7 @@ constexpr int kDeg64Waves = 8;
 template <int W, bool WS>
 constexpr size_t degrid_f64m_lds() {
     return (size_t)(W + 1) * 23 * 2 * (WS ? W : 1) * sizeof(double) +
-           (size_t)kDeg64Waves * kBlk64 * (3 * W + 2) * sizeof(double);
+           (size_t)kDeg64Waves * kBlk64 * (3 * W + 2) * sizeof(double) + kPolyN * sizeof(double);
 }
 
 template <int W, bool WS, class VT>
@@ -3255,10 +3327,17 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
     constexpr int NQ = WS ? W : 1, NC = 2 * NQ, MT = (NC + 15) / 16;
     constexpr int RX = W + 1, RY = 23, RS = RX * RY * NC, TR = 3 * W + 2;
     constexpr int NTH = 64 * kDeg64Waves;
+    constexpr int RYV = 8 + W - 1;                          // region rows footprints reach
+    constexpr int NLD = (NQ * RX * RYV + NTH - 1) / NTH;  // c128 loads per thread
     extern __shared__ __attribute__((aligned(16))) double smd[];
     double *const reg = smd;  // [RX][RY][NC]
+    // rows RYV .. RY - 1 are read by K-steps whose B is zero: they must hold
+    // finite values, so they are zeroed once (the item loads never write them)
+    for (int i = threadIdx.x; i < RS; i += NTH) reg[i] = 0.0;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     double *const tap = smd + RS + wv * kBlk64 * TR;  // this wave's tap block
+    double *const cl = smd + RS + kDeg64Waves * kBlk64 * TR;  // the tap polynomials
+    for (int i = threadIdx.x; i < kPolyN; i += NTH) cl[i] = pc[i];
     const double ihw = 2.0 / W, beta = (double)g.beta;
     const int rn = lane & 15, gk = lane >> 4;  // B column (record), K row
     const size_t plane_elems = (size_t)g.ngx * g.ngy;
@@ -3271,33 +3350,85 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
         if (it.b >= it.e) continue;
         int ibase, jbase;
         group_origin(g, (int)it.tile, ibase, jbase);
-        __syncthreads();  // the previous item's region reads
-        for (int i = threadIdx.x; i < RS; i += NTH) {
-            const int cell = i / NC, c = i - cell * NC, q = c >> 1;
-            const int xl = cell / RY, yl = cell - xl * RY;
+        // the region's planes: consecutive threads take consecutive y of one
+        // plane row (16-B c128 loads, coalesced), all loads issued before
+        // any LDS store; planes outside [p_lo, p_hi) are zeros
+        // (the thread index through an empty asm statement: the index math
+        // is redone per item instead of being hoisted and kept live -- it
+        // was, 8 x 5 registers spilled to scratch)
+        int tid = (int)threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        double2 gv[NLD];
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int i = tid + k * NTH;
+            const int q = i / (RX * RYV), rem = i - q * (RX * RYV);
+            const int xl = rem / RYV, yl = rem - xl * RYV;
             const int p = (int)it.p0 + q;
-            double v = 0.0;
-            if (yl < 8 + W - 1 && p >= p_lo && p < p_hi) {
-                int gx = ibase + xl;
-                if (gx >= g.ngx) gx -= g.ngx;
-                int gy = jbase + yl;
-                if (gy >= g.ngy) gy -= g.ngy;
-                const double *src = reinterpret_cast<const double *>(
-                    grid + (size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy);
-                v = src[c & 1];
+            const bool ok = i < NQ * RX * RYV && p >= p_lo && p < p_hi;
+            int gx = ibase + xl;
+            if (gx >= g.ngx) gx -= g.ngx;
+            int gy = jbase + yl;
+            if (gy >= g.ngy) gy -= g.ngy;
+            const double2 *src = grid + (size_t)(ok ? p - p_lo : 0) * plane_elems +
+                                 (ok ? (size_t)gx * g.ngy + gy : 0);
+            gv[k] = *src;
+            if (!ok) gv[k] = make_double2(0.0, 0.0);
+        }
+        __syncthreads();  // the previous item's region reads
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int i = tid + k * NTH;
+            if (i < NQ * RX * RYV) {
+                const int q = i / (RX * RYV), rem = i - q * (RX * RYV);
+                const int xl = rem / RYV, yl = rem - xl * RYV;
+                *reinterpret_cast<double2 *>(reg + (xl * RY + yl) * NC + 2 * q) = gv[k];
             }
-            reg[i] = v;
         }
         __syncthreads();
-        // the item's blocks: cell c's records [s_c, e_c) in blocks of 16
-        uint32_t cs = it.b;
-        int blk = 0;
-        for (int c = 0; c < kGroupCell; ++c) {
-            const uint32_t ce = max(cs, c < kGroupCell - 1 ? min(bnd[c], it.e) : it.e);
-            for (uint32_t b0 = cs; b0 < ce; b0 += kBlk64, ++blk) {
-                if (blk % kDeg64Waves != wv) continue;
-                const int nb = (int)min((uint32_t)kBlk64, ce - b0);
-                stage_block64<W, WS>(recs, b0, nb, tap, pc, ihw, beta, lane, 0, 1);
+        // the item's blocks: cell c's records [cs, ce) in blocks of 16; this
+        // wave takes every kDeg64Waves-th, its next block's records loaded
+        // while the current one runs
+        struct Blk {
+            int c;
+            uint32_t cs, ce, b0;
+        };
+        auto cell_end = [&](int c, uint32_t cs) -> uint32_t {
+            const uint32_t e = c < kGroupCell - 1 ? min((uint32_t)bnd[c], (uint32_t)it.e)
+                                                  : (uint32_t)it.e;
+            return max(cs, e);
+        };
+        auto step = [&](Blk &k, int n) {  // advance n blocks (k.c == kGroupCell: done)
+            while (k.c < kGroupCell) {
+                if (k.b0 < k.ce) {
+                    if (n == 0) return;
+                    --n;
+                    k.b0 += kBlk64;
+                    if (k.b0 < k.ce) continue;
+                }
+                ++k.c;
+                k.cs = k.ce;
+                if (k.c < kGroupCell) {
+                    k.ce = cell_end(k.c, k.cs);
+                    k.b0 = k.cs;
+                }
+            }
+        };
+        Blk kb{0, (uint32_t)it.b, cell_end(0, (uint32_t)it.b), (uint32_t)it.b};
+        step(kb, wv);
+        Stage64 nxt = kb.c < kGroupCell
+                          ? stage64_load(recs, kb.b0, (int)min((uint32_t)kBlk64, kb.ce - kb.b0), lane)
+                          : Stage64{};
+        while (kb.c < kGroupCell) {
+            {
+                const int c = kb.c;
+                const uint32_t b0 = kb.b0;
+                const int nb = (int)min((uint32_t)kBlk64, kb.ce - b0);
+                const Stage64 cur_s = nxt;
+                stage64_write<W, WS, 0, W>(cur_s, nb, tap, cl, ihw, beta, lane, true);
+                step(kb, kDeg64Waves);
+                if (kb.c < kGroupCell)
+                    nxt = stage64_load(recs, kb.b0, (int)min((uint32_t)kBlk64, kb.ce - kb.b0), lane);
                 wave_lds_sync();
                 const double *T = tap + rn * TR;  // this lane's record (B column)
                 const bool rok = rn < nb;
@@ -3305,7 +3436,9 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
                 doublex4 acc[MT];
 #pragma unroll
                 for (int m = 0; m < MT; ++m) acc[m] = doublex4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
+                // (kx not unrolled: unrolled, the compiler hoists every K-step's
+                // LDS reads to the top, 256 registers and scratch spills)
+#pragma unroll 1
                 for (int kx = 0; kx < W; ++kx) {
                     const double tu = rok ? T[kx] : 0.0;
 #pragma unroll
@@ -3337,7 +3470,7 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
                     const double sr = part, si = pim;
                     const double cr = T[3 * W], ci = T[3 * W + 1];
                     const double xr = cr * sr - ci * si, xi = cr * si + ci * sr;
-                    const uint32_t idx = recs[b0 + rn].idx;
+                    const uint32_t idx = cur_s.idx;  // (lane rn < 16: record rn)
                     const int64_t row = idx / (uint32_t)g.nchan;
                     const int chan = (int)(idx - row * g.nchan);
                     VT *pv_ = vis + row * vrs + chan * vcs;
@@ -3353,7 +3486,6 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
                 }
                 wave_lds_sync();  // the block's tap reads before the next staging
             }
-            cs = ce;
         }
     }
 }
@@ -4552,7 +4684,8 @@ static void launch_grid_f64_mfma(const Plan &P, int p_lo, int p_hi, hipStream_t 
     (void)attr;
     k_grid_f64_mfma<W, WS><<<n, 64 * f64m_waves<W, WS>(), grid_f64m_lds<W, WS>(), st>>>(
         P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
-        reinterpret_cast<double *>(P.grid), p_lo, p_hi, es_poly64_table(W, P.g.beta, st));
+        reinterpret_cast<double *>(P.grid), p_lo, p_hi, es_poly64_table(W, P.g.beta, st),
+        env_int("SDP_HIP_F64_DBG", 0));
 }
 
 template <int W, bool WS, class VT>
