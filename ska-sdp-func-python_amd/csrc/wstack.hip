@@ -3179,7 +3179,7 @@ template <int W, bool WS>
 __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64_mfma(
     Geo g, const VisRec64 *__restrict__ recs, const FineItem *__restrict__ items,
     uint32_t n_items, double *__restrict__ grid, int p_lo, int p_hi,
-    const double *__restrict__ pc, int dbg) {
+    const double *__restrict__ pc) {
     static_assert(W <= 16, "one M-tile of 16 rows per kx");
     constexpr int NQ = WS ? W : 1, NC = 2 * NQ, NW = f64m_waves<W, WS>();
     constexpr int RX = W + 1, RY = f64m_ry<W, WS>(), RS = RX * RY * NC;
@@ -3237,12 +3237,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
         for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlk64) {
             __syncthreads();  // the region zeroing / previous block's tap reads
             const int nb = (int)min((uint32_t)kBlk64, it.e - b0);  // (a multiple of 4)
-            if (!(dbg & 2)) {
             if (NW == 1 || wv == 0)
                 stage64_write<W, WS, 0, HW>(nxt, nb, tap, cl, ihw, beta, lane, true);
             else
                 stage64_write<W, WS, (NW > 1 ? HW : 0), W>(nxt, nb, tap, cl, ihw, beta, lane, false);
-            }
             // the next block's records, in flight during this block's K-steps
             if (b0 + kBlk64 < it.e)
                 nxt = stage64_load(recs, b0 + kBlk64, (int)min((uint32_t)kBlk64, it.e - b0 - kBlk64),
@@ -3269,14 +3267,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
                 double aop[W];
 #pragma unroll
                 for (int kx = 0; kx < W; ++kx) aop[kx] = T[kx] * tv;
-                if (!(dbg & 4)) {
 #pragma unroll
                 for (int kx = 0; kx < W; ++kx)
                     acc[kx] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[kx], bop, acc[kx], 0, 0, 0);
-                } else {
-#pragma unroll
-                for (int kx = 0; kx < W; ++kx) acc[kx][0] += aop[kx] * bop;
-                }
             }
         }
         if (cur >= 0) store_cell();
@@ -3291,7 +3284,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
             const int xl = cell / RYV, yl = cell - xl * RYV;
             const double v = reg[(xl * RY + yl) * NC + 2 * q + (f & 1)];
             const int p = (int)it.p0 + q;
-            if (v == 0.0 || p < p_lo || p >= p_hi || (dbg & 1)) continue;
+            if (v == 0.0 || p < p_lo || p >= p_hi) continue;
             int gx = ibase + xl;
             if (gx >= g.ngx) gx -= g.ngx;
             int gy = jbase + yl;
@@ -4684,8 +4677,7 @@ static void launch_grid_f64_mfma(const Plan &P, int p_lo, int p_hi, hipStream_t 
     (void)attr;
     k_grid_f64_mfma<W, WS><<<n, 64 * f64m_waves<W, WS>(), grid_f64m_lds<W, WS>(), st>>>(
         P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
-        reinterpret_cast<double *>(P.grid), p_lo, p_hi, es_poly64_table(W, P.g.beta, st),
-        env_int("SDP_HIP_F64_DBG", 0));
+        reinterpret_cast<double *>(P.grid), p_lo, p_hi, es_poly64_table(W, P.g.beta, st));
 }
 
 template <int W, bool WS, class VT>
