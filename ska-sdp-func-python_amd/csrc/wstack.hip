@@ -4185,7 +4185,12 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     g.tiled = 0;
     g.tlx = g.tly = g.nbins = 0;
     const int b2 = env_int("SDP_HIP_BUCKET2", 1);
+    // A kept bucketing (SDP_HIP_KEEP_BUCKETS, the pols of invert_ng) also
+    // stays single-level: its reuse calls then run only the value pass,
+    // where the two-level sort's would add the second move (C2 4 pols:
+    // 57.6 vs 50 ms).
     if (b2 != 0 && (grid_mode || P.f64 || b2 == 2) &&
+        (!(in.flags & SDP_HIP_KEEP_BUCKETS) || b2 == 2) &&
         env_int("SDP_HIP_BUCKET", 0) != kTileCoarse) {
         int x0, nx_, y0, ny_;
         window(amax, g.ngx, kTile, x0, nx_);

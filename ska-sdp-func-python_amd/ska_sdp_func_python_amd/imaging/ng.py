@@ -259,13 +259,16 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
         calls = [(pol, slice(vchan - lo, vchan - lo + 1), int(vis_to_im[vchan]))
                  for vchan in range(lo, hi) for pol in range(npol)]
     grid_calls = [c for c in calls if not (dopsf and c[0] != 0)]
-    # Two or more NUFFT calls are pipelined: consecutive calls alternate
-    # between two streams and the library's two scratch slots, so call k+1's
-    # bucketing runs under call k's gridding and FFT (SDP_HIP_OVERLAP=0: one
-    # stream).  Otherwise the image pols of one channel range share one
-    # bucketing: the first pol keeps it, the others re-run only the value pass
-    # (SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS).
-    overlap = len(grid_calls) > 1 and dev.type == "cuda" and \
+    # The image pols of an MFS image share one bucketing: the first pol keeps
+    # it, the others re-run only the value pass (SDP_HIP_KEEP_BUCKETS /
+    # SDP_HIP_REUSE_BUCKETS; C2 4 pols 54.0 ms against 59.7 pipelined, bench
+    # api object).  Otherwise two or more NUFFT calls -- a cube's channels --
+    # are pipelined: consecutive calls alternate between two streams and the
+    # library's two scratch slots, so call k+1's bucketing runs under call
+    # k's gridding and FFT (C2 as a 16-channel cube: 284.8 against 316.4 ms
+    # on one stream).  SDP_HIP_OVERLAP=0 keeps every call on one stream.
+    share_mfs = mfs and npol > 1 and not dopsf
+    overlap = len(grid_calls) > 1 and not share_mfs and dev.type == "cuda" and \
         os.environ.get("SDP_HIP_OVERLAP", "1") != "0"
     share = npol > 1 and not dopsf and not overlap
     main = torch.cuda.current_stream(dev) if overlap else None

@@ -409,14 +409,17 @@ def test_invert_ng_fused_prologue(pf, ipf, mfs, dopsf, device):
     np.testing.assert_allclose(sumwt, exp_sw, rtol=1e-6 if device else 1e-12)
 
 
-def test_shared_bucketing_across_pols():
+@pytest.mark.parametrize("bucket2", ["1", "2"])
+def test_shared_bucketing_across_pols(bucket2, monkeypatch):
     """SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS (invert_ng's image pols):
     pol 0 keeps its bucketing, pols 1-3 -- different weights and flags, pol 0
     zero where the others are not -- re-run only the value pass.  Each image
     and weight sum equals an independent call (1e-6 relative RMS: the order
     of the fp32 sums inside a cell differs; sumwt 1e-12); a reuse after
-    another wstack call, or with other uvw, is refused."""
+    another wstack call, or with other uvw, is refused.  A kept bucketing is
+    single-level by default; SDP_HIP_BUCKET2=2 keeps a two-level one."""
     from ska_sdp_func_python_amd import kernels
+    monkeypatch.setenv("SDP_HIP_BUCKET2", bucket2)
     rng = np.random.default_rng(71)
     nrow, nchan, npol, npix = 6000, 8, 4, 256
     freq = np.linspace(1.0e9, 1.2e9, nchan)
@@ -446,6 +449,7 @@ def test_shared_bucketing_across_pols():
         assert rel_rms(shared[p][0], ind[p][0]) < 1e-6, p
         assert abs(shared[p][1] - ind[p][1]) <= 1e-12 * abs(ind[p][1])
     assert shared[0][2]["nvis_used"] == nrow * nchan  # zero weights bucketed too
+    assert shared[0][2]["tiled"] == (1 if bucket2 == "2" else 0)
     # any other wstack call drops the kept bucketing
     kernels.dirty2ms(uvw, freq_t, torch.zeros((npix, npix), dtype=torch.float64, device=dev),
                      None, cell, cell, 1e-5, True, flip_uw=True)
