@@ -3161,8 +3161,12 @@ __device__ __forceinline__ void stage64_write(const Stage64 &s, int nb, double *
 // deep); columns >= 2 NQ are never stored.  The region is zeroed per item
 // and flushed once with fp64 global atomics (zeros skipped) in plane order.
 template <int W, bool WS>
-constexpr int f64m_waves() {
+constexpr int f64m_ntiles() {  // 16-column N-tiles of the 2 NQ (q, re/im) columns
     return (2 * (WS ? W : 1) + 15) / 16;
+}
+template <int W, bool WS>
+constexpr int f64m_waves() {  // one wave per (N-tile, half of the kx M-tiles)
+    return 2 * f64m_ntiles<W, WS>();
 }
 template <int W, bool WS>
 constexpr int f64m_ry() {
@@ -3175,15 +3179,38 @@ constexpr size_t grid_f64m_lds() {
 }
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
+// taps [J0, J1) of wave P of NP: the W taps in NP near-equal parts
+template <int W, bool WS, int NP>
+__device__ __forceinline__ void stage64_part(int part, const Stage64 &s, int nb, double *tap,
+                                             const double *cl, double ihw, double beta, int lane) {
+    static_assert(NP >= 1 && NP <= 4, "up to four parts");
+    switch (part) {
+        case 0: stage64_write<W, WS, 0, W / NP>(s, nb, tap, cl, ihw, beta, lane, true); break;
+        case 1:
+            if constexpr (NP > 1)
+                stage64_write<W, WS, W / NP, 2 * W / NP>(s, nb, tap, cl, ihw, beta, lane, false);
+            break;
+        case 2:
+            if constexpr (NP > 2)
+                stage64_write<W, WS, 2 * W / NP, 3 * W / NP>(s, nb, tap, cl, ihw, beta, lane, false);
+            break;
+        default:
+            if constexpr (NP > 3)
+                stage64_write<W, WS, 3 * W / NP, W>(s, nb, tap, cl, ihw, beta, lane, false);
+            break;
+    }
+}
+
 template <int W, bool WS>
-__global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64_mfma(
+__global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64_mfma(
     Geo g, const VisRec64 *__restrict__ recs, const FineItem *__restrict__ items,
     uint32_t n_items, double *__restrict__ grid, int p_lo, int p_hi,
     const double *__restrict__ pc) {
     static_assert(W <= 16, "one M-tile of 16 rows per kx");
-    constexpr int NQ = WS ? W : 1, NC = 2 * NQ, NW = f64m_waves<W, WS>();
+    constexpr int NQ = WS ? W : 1, NC = 2 * NQ, NT = f64m_ntiles<W, WS>(), NW = f64m_waves<W, WS>();
     constexpr int RX = W + 1, RY = f64m_ry<W, WS>(), RS = RX * RY * NC;
     constexpr int TR = 3 * W + 2, NTH = 64 * NW;
+    constexpr int KH = (W + 1) / 2;  // kx M-tiles per wave
     extern __shared__ __attribute__((aligned(16))) double smd[];
     double *const reg = smd;       // [RX][RY][NC]
     double *const tap = smd + RS;  // [kBlk64][TR]
@@ -3191,18 +3218,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const double ihw = 2.0 / W, beta = (double)g.beta;
     for (int i = threadIdx.x; i < kPolyN; i += NTH) cl[i] = pc[i];
-    constexpr int HW = (W + NW - 1) / NW;  // taps per wave (NW <= 2)
-    static_assert(NW <= 2, "the taps are split over at most two waves");
-    const int col = wv * 16 + (lane & 15);
+    // wave (N-tile wv % NT, kx half wv / NT): 4 waves for W > 8 with
+    // w-stacking, two per SIMD at two workgroups per CU
+    const int kx0 = (wv / NT) * KH, nkx = min(KH, W - kx0);
+    const int col = (wv % NT) * 16 + (lane & 15);
     const bool colok = col < NC;
     // B operand: tw[q] c[re/im] of record (lane >> 4); A: tu[kx] tv[ky]
     const int bq = 2 * W + (colok ? col >> 1 : 0), bc = 3 * W + (col & 1);
     const int ky = lane & 15;
     const bool kyok = ky < W;
     const int rk = lane >> 4;
-    // accumulator (kx, i) of a cell at region cell (cx, cy): element
-    // ((cx + kx) RY + cy + rk + 4 i) NC + col
-    const int lbase = rk * NC + col;
+    // accumulator (k, i) = tap row (kx0 + k, rk + 4 i) of a cell at region
+    // cell (cx, cy): element ((cx + kx0 + k) RY + cy + rk + 4 i) NC + col
+    const int lbase = kx0 * RY * NC + rk * NC + col;
     const size_t plane_elems = (size_t)g.ngx * g.ngy;
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
         uint32_t bnd[kGroupCell];
@@ -3212,35 +3240,36 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
         group_origin(g, (int)it.tile, ibase, jbase);
         __syncthreads();  // the previous item's flush reads of the region
         for (int i = threadIdx.x; i < RS; i += NTH) reg[i] = 0.0;
-        doublex4 acc[W];
+        doublex4 acc[KH];
 #pragma unroll
-        for (int kx = 0; kx < W; ++kx) acc[kx] = doublex4{0.0, 0.0, 0.0, 0.0};
+        for (int k = 0; k < KH; ++k) acc[k] = doublex4{0.0, 0.0, 0.0, 0.0};
         int cur = -1, cb = 0;
         auto store_cell = [&]() {
             if (colok) {
                 double *d = reg + cb + lbase;
 #pragma unroll
-                for (int kx = 0; kx < W; ++kx)
+                for (int k = 0; k < KH; ++k)
+                    if (k < nkx) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) d[kx * RY * NC + 4 * i * NC] = acc[kx][i];
+                        for (int i = 0; i < 4; ++i) d[k * RY * NC + 4 * i * NC] = acc[k][i];
+                    }
             }
         };
         auto load_cell = [&](int cell) {
             cb = ((cell & 1) * RY + (cell >> 1)) * NC;
             const double *s = reg + cb + lbase;
 #pragma unroll
-            for (int kx = 0; kx < W; ++kx)
+            for (int k = 0; k < KH; ++k)
+                if (k < nkx) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc[kx][i] = s[kx * RY * NC + 4 * i * NC];
+                    for (int i = 0; i < 4; ++i) acc[k][i] = s[k * RY * NC + 4 * i * NC];
+                }
         };
         Stage64 nxt = stage64_load(recs, it.b, (int)min((uint32_t)kBlk64, it.e - it.b), lane);
         for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlk64) {
             __syncthreads();  // the region zeroing / previous block's tap reads
             const int nb = (int)min((uint32_t)kBlk64, it.e - b0);  // (a multiple of 4)
-            if (NW == 1 || wv == 0)
-                stage64_write<W, WS, 0, HW>(nxt, nb, tap, cl, ihw, beta, lane, true);
-            else
-                stage64_write<W, WS, (NW > 1 ? HW : 0), W>(nxt, nb, tap, cl, ihw, beta, lane, false);
+            stage64_part<W, WS, NW>(wv, nxt, nb, tap, cl, ihw, beta, lane);
             // the next block's records, in flight during this block's K-steps
             if (b0 + kBlk64 < it.e)
                 nxt = stage64_load(recs, b0 + kBlk64, (int)min((uint32_t)kBlk64, it.e - b0 - kBlk64),
@@ -3256,20 +3285,25 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 128))) void k_grid_f64
                 int cell = 0;
 #pragma unroll
                 for (int c = 0; c < kGroupCell - 1; ++c) cell += ri >= bnd[c] ? 1 : 0;
-                if (cell != cur) {
+                if (cell != cur) {  // (workgroup-uniform)
                     if (cur >= 0) store_cell();
+                    // the two kx halves of one column tile touch the same
+                    // region cells from neighbouring cells' footprints: every
+                    // wave's stores land before any wave loads the next cell
+                    if (NW > NT) __syncthreads();
                     cur = cell;
                     load_cell(cur);
                 }
                 const double *T = tap + (4 * kk + rk) * TR;
                 const double bop = T[bq] * T[bc];
                 const double tv = kyok ? T[W + ky] : 0.0;
-                double aop[W];
+                double aop[KH];
 #pragma unroll
-                for (int kx = 0; kx < W; ++kx) aop[kx] = T[kx] * tv;
+                for (int k = 0; k < KH; ++k) aop[k] = T[kx0 + k] * tv;
 #pragma unroll
-                for (int kx = 0; kx < W; ++kx)
-                    acc[kx] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[kx], bop, acc[kx], 0, 0, 0);
+                for (int k = 0; k < KH; ++k)
+                    if (k < nkx)
+                        acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[k], bop, acc[k], 0, 0, 0);
             }
         }
         if (cur >= 0) store_cell();
