@@ -3452,7 +3452,9 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
                 const uint32_t b0 = kb.b0;
                 const int nb = (int)min((uint32_t)kBlk64, kb.ce - b0);
                 const Stage64 cur_s = nxt;
-                stage64_write<W, WS, 0, W>(cur_s, nb, tap, cl, ihw, beta, lane, true);
+                // (in two halves of the taps: half the Horner registers live)
+                stage64_write<W, WS, 0, W / 2>(cur_s, nb, tap, cl, ihw, beta, lane, true);
+                stage64_write<W, WS, W / 2, W>(cur_s, nb, tap, cl, ihw, beta, lane, false);
                 step(kb, kDeg64Waves);
                 if (kb.c < kGroupCell)
                     nxt = stage64_load(recs, kb.b0, (int)min((uint32_t)kBlk64, kb.ce - kb.b0), lane);
