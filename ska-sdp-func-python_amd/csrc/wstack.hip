@@ -3244,6 +3244,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
 #pragma unroll
         for (int k = 0; k < KH; ++k) acc[k] = doublex4{0.0, 0.0, 0.0, 0.0};
         int cur = -1, cb = 0;
+        uint32_t cend = 0;  // end of the current cell's records
         auto store_cell = [&]() {
             if (colok) {
                 double *d = reg + cb + lbase;
@@ -3282,10 +3283,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
             for (int kk = 0; kk < kBlk64 / 4; ++kk) {
                 if (4 * kk >= nb) break;
                 const uint32_t ri = b0 + 4u * (uint32_t)kk;
-                int cell = 0;
+                // one scalar compare per K-step against the current cell's
+                // end; the 15 compares of the cell search only at a change
+                // (the compare chain per K-step was ~45 of the kernel's
+                // ~340 SALU per block and wave)
+                if (ri >= cend) {  // (workgroup-uniform)
+                    int cell = 0;
+                    uint32_t e = bnd[kGroupCell - 1];
 #pragma unroll
-                for (int c = 0; c < kGroupCell - 1; ++c) cell += ri >= bnd[c] ? 1 : 0;
-                if (cell != cur) {  // (workgroup-uniform)
+                    for (int c = 0; c < kGroupCell - 1; ++c) {
+                        cell += ri >= bnd[c] ? 1 : 0;
+                        e = (ri < bnd[c] && bnd[c] < e) ? bnd[c] : e;
+                    }
+                    cend = e;
                     if (cur >= 0) store_cell();
                     // the two kx halves of one column tile touch the same
                     // region cells from neighbouring cells' footprints: every
