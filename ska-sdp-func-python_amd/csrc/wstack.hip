@@ -3349,10 +3349,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
 // shared read-only by the workgroup's waves, each of which takes every NW-th
 // 16-record block of the item's cells (no barriers between blocks).
 constexpr int kDeg64Waves = 8;
+// blocks of one item: chunk / 16 + one partial block per cell (plan_geometry
+// caps a k_degrid_f64_mfma plan's chunk to fit)
+constexpr int kMaxBlk64 = 1024;
 template <int W, bool WS>
 constexpr size_t degrid_f64m_lds() {
     return (size_t)(W + 1) * 23 * 2 * (WS ? W : 1) * sizeof(double) +
-           (size_t)kDeg64Waves * kBlk64 * (3 * W + 2) * sizeof(double) + kPolyN * sizeof(double);
+           (size_t)kDeg64Waves * kBlk64 * (3 * W + 2) * sizeof(double) + kPolyN * sizeof(double) +
+           (size_t)(2 * kMaxBlk64 + 1) * sizeof(uint32_t);
 }
 
 template <int W, bool WS, class VT>
@@ -3375,6 +3379,8 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
     double *const tap = smd + RS + wv * kBlk64 * TR;  // this wave's tap block
     double *const cl = smd + RS + kDeg64Waves * kBlk64 * TR;  // the tap polynomials
     for (int i = threadIdx.x; i < kPolyN; i += NTH) cl[i] = pc[i];
+    uint32_t *const bcel = reinterpret_cast<uint32_t *>(cl + kPolyN);  // block: cell | records << 8
+    uint32_t *const btab = bcel + kMaxBlk64;                            // block: first record (+ count)
     const double ihw = 2.0 / W, beta = (double)g.beta;
     const int rn = lane & 15, gk = lane >> 4;  // B column (record), K row
     const size_t plane_elems = (size_t)g.ngx * g.ngy;
@@ -3422,52 +3428,49 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
                 *reinterpret_cast<double2 *>(reg + (xl * RY + yl) * NC + 2 * q) = gv[k];
             }
         }
-        __syncthreads();
-        // the item's blocks: cell c's records [cs, ce) in blocks of 16; this
-        // wave takes every kDeg64Waves-th, its next block's records loaded
-        // while the current one runs
-        struct Blk {
-            int c;
-            uint32_t cs, ce, b0;
-        };
-        auto cell_end = [&](int c, uint32_t cs) -> uint32_t {
-            const uint32_t e = c < kGroupCell - 1 ? min((uint32_t)bnd[c], (uint32_t)it.e)
-                                                  : (uint32_t)it.e;
-            return max(cs, e);
-        };
-        auto step = [&](Blk &k, int n) {  // advance n blocks (k.c == kGroupCell: done)
-            while (k.c < kGroupCell) {
-                if (k.b0 < k.ce) {
-                    if (n == 0) return;
-                    --n;
-                    k.b0 += kBlk64;
-                    if (k.b0 < k.ce) continue;
-                }
-                ++k.c;
-                k.cs = k.ce;
-                if (k.c < kGroupCell) {
-                    k.ce = cell_end(k.c, k.cs);
-                    k.b0 = k.cs;
-                }
+        // the item's blocks (cell c's records [cs, ce) in blocks of 16) as a
+        // table in LDS: lane c of wave 0 counts its cell's blocks, a wave
+        // prefix sum places them (a scalar walk of the cells per block cost
+        // ~400 SALU per block and wave)
+        if (wv == 0) {
+            const int c = lane & 15;
+            const FineItem *F = items + item_index(w_it, n_items);  // (load_fine_item's)
+            const uint32_t o_prev = c == 0 ? (uint32_t)it.b : F->o[c - 1];
+            const uint32_t o_c = c == kGroupCell - 1 ? (uint32_t)it.e : F->o[c];
+            const uint32_t cs = min(max(o_prev, (uint32_t)it.b), (uint32_t)it.e);
+            const uint32_t ce = min(max(o_c, cs), (uint32_t)it.e);
+            const uint32_t nbk = lane < kGroupCell ? (ce - cs + kBlk64 - 1) / kBlk64 : 0u;
+            uint32_t x = nbk;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if ((lane & 15) >= o) x += y;
             }
-        };
-        Blk kb{0, (uint32_t)it.b, cell_end(0, (uint32_t)it.b), (uint32_t)it.b};
-        step(kb, wv);
-        Stage64 nxt = kb.c < kGroupCell
-                          ? stage64_load(recs, kb.b0, (int)min((uint32_t)kBlk64, kb.ce - kb.b0), lane)
-                          : Stage64{};
-        while (kb.c < kGroupCell) {
+            const uint32_t off = x - nbk;  // exclusive prefix
+            if (lane == 15) btab[kMaxBlk64] = x;  // the block count
+            if (lane < kGroupCell)
+                for (uint32_t j = 0; j < nbk && off + j < kMaxBlk64; ++j) {
+                    const uint32_t b0 = cs + j * kBlk64;
+                    btab[off + j] = b0;
+                    bcel[off + j] = (uint32_t)c | (min((uint32_t)kBlk64, ce - b0) << 8);
+                }
+        }
+        __syncthreads();
+        const uint32_t nblk = min(btab[kMaxBlk64], (uint32_t)kMaxBlk64);
+        uint32_t kb = (uint32_t)wv;
+        Stage64 nxt = kb < nblk ? stage64_load(recs, btab[kb], (int)(bcel[kb] >> 8), lane) : Stage64{};
+        for (; kb < nblk; kb += kDeg64Waves) {
             {
-                const int c = kb.c;
-                const uint32_t b0 = kb.b0;
-                const int nb = (int)min((uint32_t)kBlk64, kb.ce - b0);
+                const uint32_t b0 = btab[kb], cn = bcel[kb];
+                const int c = (int)(cn & 15u);
+                const int nb = (int)(cn >> 8);
                 const Stage64 cur_s = nxt;
                 // (in two halves of the taps: half the Horner registers live)
                 stage64_write<W, WS, 0, W / 2>(cur_s, nb, tap, cl, ihw, beta, lane, true);
                 stage64_write<W, WS, W / 2, W>(cur_s, nb, tap, cl, ihw, beta, lane, false);
-                step(kb, kDeg64Waves);
-                if (kb.c < kGroupCell)
-                    nxt = stage64_load(recs, kb.b0, (int)min((uint32_t)kBlk64, kb.ce - kb.b0), lane);
+                if (kb + kDeg64Waves < nblk)
+                    nxt = stage64_load(recs, btab[kb + kDeg64Waves], (int)(bcel[kb + kDeg64Waves] >> 8),
+                                       lane);
                 wave_lds_sync();
                 const double *T = tap + rn * TR;  // this lane's record (B column)
                 const bool rok = rn < nb;
@@ -4387,6 +4390,8 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // the MFMA gridder (SDP_HIP_F64_MFMA=0: the VALU gridder, unpadded)
     P.pad64 = grid_mode && g.tiled && P.f64 && env_int("SDP_HIP_F64_MFMA", 1) != 0;
     P.mfma64 = !grid_mode && g.sub == kTileCell && P.f64 && env_int("SDP_HIP_F64_MFMA", 1) != 0;
+    // (k_degrid_f64_mfma's per-item block table holds kMaxBlk64 blocks)
+    if (P.mfma64) P.chunk = std::min<unsigned>(P.chunk, (kMaxBlk64 - kGroupCell) * kBlk64);
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
     P.pt.nvis = nvis;
     if (g.tiled) return P;  // (records: bucket_tiled, once their padded count is known)
