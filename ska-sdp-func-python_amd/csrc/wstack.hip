@@ -3039,8 +3039,8 @@ __global__ __launch_bounds__(64) void k_grid_f64(Geo g, const VisRec64 *__restri
 // coefficients, uniform across lanes, fitted on the host at Chebyshev nodes,
 // es_poly64_table, and copied to LDS per workgroup).  Interior taps are
 // within ~1e-14 of the kernel; the two edge taps, where sqrt(1 - x^2) is not
-// analytic, within ~0.15 e^-beta, i.e. a tenth of the epsilon W is chosen
-// for (W = 9: 1.5e-9, W = 13: 1.6e-13, W = 16: 7e-15; the fp64 exp they
+// analytic, within ~1.5 e^-beta, about 0.15 of the epsilon W is chosen for
+// (W = 9: 1.5e-9, W = 13: 1.6e-13, W = 16: 7e-15; the fp64 exp they
 // replace kept a dozen constants live in registers across the kernel).  One
 // lane computes all taps of one (record, axis) pair of a 16-record block.
 constexpr int kPoly64 = 12;
