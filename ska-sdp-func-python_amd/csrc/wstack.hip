@@ -3489,10 +3489,11 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
                         const double tv = T[W + min(ky, W - 1)];
                         const double bop = ky < W ? tu * tv : 0.0;
 #pragma unroll
+                        // (rows (q, re/im) >= NC read the next region cell's
+                        // values: finite, and those rows of D are never used)
                         for (int m = 0; m < MT; ++m) {
                             const double gv = G[(kx * RY + 4 * s) * NC + 16 * m];
-                            const double aop = 16 * m + rn < NC ? gv : 0.0;
-                            acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop, acc[m], 0, 0, 0);
+                            acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv, bop, acc[m], 0, 0, 0);
                         }
                     }
                 }
