@@ -4376,8 +4376,11 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     if (grid_mode) P.spec_in = band_input(P, st);
 
     // records per item: large enough to amortise the tile flush over dense
-    // tiles, small enough to leave >= ~16k items for the 256 CUs
-    P.chunk = (unsigned)std::min<int64_t>(kChunkMax, std::max<int64_t>(kChunkMin, nvis / 16384));
+    // tiles, small enough that the uv core's heavy groups split into items
+    // the CUs share evenly (C2, round 4: chunk 2048 / 3072 against the
+    // former nvis / 16384 = 7488: gridding 3.97 / 3.94 vs 4.23 ms, the
+    // degridder 5.50 / 5.53 vs 5.77, the fp64 pair 1-2 % faster)
+    P.chunk = (unsigned)std::min<int64_t>(kChunkMax, std::max<int64_t>(kChunkMin, nvis / 40960));
     if (const char *e = std::getenv("SDP_HIP_CHUNK"))
         if (std::atoi(e) >= 64) P.chunk = (unsigned)std::atoi(e);
     // large grids: the 16x16-cell items are re-ordered by cell (k_subsort)
