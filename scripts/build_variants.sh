@@ -9,7 +9,7 @@ mkdir -p ../../exp build/var
 objs=$(ls build/*.o | grep -v wstack.o)
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -munsafe-fp-atomics -I../../include -I. $defs -c wstack.hip -o build/var/$name.o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form=true -I../../include -I. $defs -c wstack.hip -o build/var/$name.o &
 done
 wait
 for o in build/var/*.o; do

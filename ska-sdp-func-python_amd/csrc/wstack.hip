@@ -2140,6 +2140,10 @@ constexpr int kT1Threads = 512;     // count and value passes (VGPR-limited occu
 constexpr unsigned kTChunk = 131072;  // records per second-level chunk
 constexpr unsigned kTSeg = 16;       // chunks per segment of the cells' column prefix
 constexpr int kTU = 2;               // visibilities per lane in flight (count / value pass)
+#ifndef SDP_TUC
+#define SDP_TUC 2
+#endif
+constexpr int kTUc = SDP_TUC;        // the same for the count pass alone
 constexpr int kTU2 = 4;              // records per lane in flight (cell count / final move)
 
 struct TChunk {
@@ -2270,14 +2274,14 @@ __global__ __launch_bounds__(kT1Threads) void k_t_count(Geo g, int64_t nvis, int
     __syncthreads();
     const int64_t v0 = (int64_t)blockIdx.x * vpw, v1 = min(nvis, v0 + vpw);
     double ws = 0.0;
-    for (int64_t base = v0; base < v1; base += (int64_t)kT1Threads * kTU) {
-        TLoad L[kTU];
+    for (int64_t base = v0; base < v1; base += (int64_t)kT1Threads * kTUc) {
+        TLoad L[kTUc];
 #pragma unroll
-        for (int u = 0; u < kTU; ++u)
+        for (int u = 0; u < kTUc; ++u)
             L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, fsc, wgt, wrs, wcs,
                           x);
 #pragma unroll
-        for (int u = 0; u < kTU; ++u) {
+        for (int u = 0; u < kTUc; ++u) {
             const TPoint p = t_classify<true>(g, L[u], x, nbad);
             ws += p.wd;
             lds_run_add<false>(p.in ? tiled_key(g, p.c) >> 12 : 0u, p.in, hist);
@@ -2765,15 +2769,16 @@ __global__ __launch_bounds__(kTThreads) void k_t_final(const TChunk *__restrict_
         for (uint32_t i0 = t.b; i0 < t.e; i0 += kTThreads * kTU2) {
             uint4 r[kTU2][NW];
             unsigned k[kTU2];
+            // loads from a clamped index (the chunk is never empty): the
+            // records then stay in VGPRs; behind `if (i < t.e)` the compiler
+            // kept them in scratch between the two loops
 #pragma unroll
             for (int u = 0; u < kTU2; ++u) {
-                const uint32_t i = i0 + u * kTThreads + threadIdx.x;
-                k[u] = 0xffffu;
-                if (i < t.e) {
-                    k[u] = lkey[i];
+                const uint32_t i = i0 + u * kTThreads + threadIdx.x, ic = min(i, t.e - 1u);
+                k[u] = lkey[ic];
+                if (i >= t.e) k[u] = 0xffffu;
 #pragma unroll
-                    for (int q = 0; q < NW; ++q) r[u][q] = src[(size_t)i * NW + q];
-                }
+                for (int q = 0; q < NW; ++q) r[u][q] = src[(size_t)ic * NW + q];
             }
 #pragma unroll
             for (int u = 0; u < kTU2; ++u) {
@@ -2839,16 +2844,23 @@ __global__ __launch_bounds__(kTThreads) void k_t_final_s(const TChunk *__restric
         }
         __syncthreads();
         for (uint32_t i0 = t.b; i0 < t.e; i0 += NB) {
-            uint4 r[U][NW];
+            // the records as scalars: held as uint4 arrays the compiler kept
+            // them in scratch between the load and the staging loop
+            unsigned r[U][4 * NW];
             unsigned k[U], rk[U];
+            // clamped-index loads, as in k_t_final
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t i = i0 + u * kTThreads + threadIdx.x;
-                k[u] = 0xffffu;
-                if (i < t.e) {
-                    k[u] = lkey[i];
+                const uint32_t i = i0 + u * kTThreads + threadIdx.x, ic = min(i, t.e - 1u);
+                k[u] = lkey[ic];
+                if (i >= t.e) k[u] = 0xffffu;
 #pragma unroll
-                    for (int q = 0; q < NW; ++q) r[u][q] = src[(size_t)i * NW + q];
+                for (int q = 0; q < NW; ++q) {
+                    const uint4 v = src[(size_t)ic * NW + q];
+                    r[u][4 * q] = v.x;
+                    r[u][4 * q + 1] = v.y;
+                    r[u][4 * q + 2] = v.z;
+                    r[u][4 * q + 3] = v.w;
                 }
             }
             // rank of each record among the batch's records of its cell
@@ -2875,7 +2887,9 @@ __global__ __launch_bounds__(kTThreads) void k_t_final_s(const TChunk *__restric
                     const unsigned slot = cnt[k[u]] + rk[u];
                     sdst[slot] = cur[k[u]] + rk[u];
 #pragma unroll
-                    for (int q = 0; q < NW; ++q) stg[slot * NW + q] = r[u][q];
+                    for (int q = 0; q < NW; ++q)
+                        stg[slot * NW + q] =
+                            make_uint4(r[u][4 * q], r[u][4 * q + 1], r[u][4 * q + 2], r[u][4 * q + 3]);
                 }
             }
             __syncthreads();
@@ -5008,7 +5022,7 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     const int64_t nvis = pt.nvis;
     const size_t lds_bins = (size_t)nb * sizeof(unsigned);
     if (!values_only) {
-        pt.t_g1 = 4 * cu_count();
+        pt.t_g1 = env_int("SDP_HIP_TG1", 8) * cu_count();
         pt.t_vpw = std::max<int64_t>(kT1Threads, (nvis + pt.t_g1 - 1) / pt.t_g1);
         pt.t_vpw = (pt.t_vpw + 63) / 64 * 64;
         pt.t_g1 = (int)std::max<int64_t>(1, (nvis + pt.t_vpw - 1) / pt.t_vpw);
