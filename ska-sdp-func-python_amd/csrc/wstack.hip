@@ -5022,7 +5022,12 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     const int64_t nvis = pt.nvis;
     const size_t lds_bins = (size_t)nb * sizeof(unsigned);
     if (!values_only) {
-        pt.t_g1 = env_int("SDP_HIP_TG1", 8) * cu_count();
+        // 16 workgroups per CU (C2 prep: 4 -> 4.72, 8 -> 4.44, 16 -> 4.27 ms),
+        // fewer where the per-workgroup bin offsets (t_m1: t_g1 x nb words,
+        // written by the count pass, read by the value pass) would pass half
+        // a word per visibility
+        pt.t_g1 = env_int("SDP_HIP_TG1", 16) * cu_count();
+        while (pt.t_g1 > cu_count() && (int64_t)pt.t_g1 * nb > nvis / 2) pt.t_g1 /= 2;
         pt.t_vpw = std::max<int64_t>(kT1Threads, (nvis + pt.t_g1 - 1) / pt.t_g1);
         pt.t_vpw = (pt.t_vpw + 63) / 64 * 64;
         pt.t_g1 = (int)std::max<int64_t>(1, (nvis + pt.t_vpw - 1) / pt.t_vpw);
