@@ -436,7 +436,11 @@ def test_c4_largest_w_rank_of_the_8way_row_partition():
         gen.manual_seed(7919 * 7 + a)
         return torch.randn((n7, e - a), generator=gen, device=dev, dtype=torch.complex64)
 
-    _c4_streamed_checks(f"C4 wrow rank 7/8 ({n7} rows)", u7, freqs, batches, vis_of, 8192, cell)
+    # adjointness: the fp32 planes' atomic accumulation order varies from run
+    # to run (same build, same inputs: 3.1e-6 and 7.5e-6 measured), so the
+    # bound sits at 2e-5 -- still 5x below the full band's fp32 figure
+    _c4_streamed_checks(f"C4 wrow rank 7/8 ({n7} rows)", u7, freqs, batches, vis_of, 8192, cell,
+                        adj_tol=2e-5)
 
 
 # ---------------------------------------------------------------------------
