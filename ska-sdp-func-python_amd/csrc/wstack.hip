@@ -897,6 +897,23 @@ __global__ __launch_bounds__(256) void k_sub_count(const Item *__restrict__ item
     if (threadIdx.x == 0) pcnt[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// one workgroup: 64-bit sum of n 32-bit counts
+__global__ __launch_bounds__(1024) void k_sum_u32(const unsigned *__restrict__ c, unsigned n,
+                                                  unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long red[16];
+    unsigned long long s = 0;
+    for (unsigned i = threadIdx.x; i < n; i += 1024) s += c[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int i = 0; i < 16; ++i) t += red[i];
+        *out = t;
+    }
+}
+
 __global__ __launch_bounds__(kSubThreads) void k_subsort_pad(Geo g, const Item *__restrict__ items,
                                                              const RecC *__restrict__ in,
                                                              const uint8_t *__restrict__ cls,
@@ -4260,7 +4277,14 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
         window(amax, g.ngx, kTile, x0, nx_);
         window(bmax, g.ngy, kTile, y0, ny_);
         const int64_t nbins = (int64_t)(nx_ / kTile) * (ny_ / kTile) * g.nps;
-        if (nbins <= kMaxBins) {
+        // the padded record total and the cell bases are 32-bit: every
+        // non-empty cell may add up to 3 pad records, so the two-level sort
+        // needs nvis + 3 min(nvis, cells) < 2^32 (else the single-level or
+        // coarse bucketing below, whose totals are 64-bit)
+        const int64_t nv = in.nrow * (int64_t)in.nchan;
+        const int64_t cells = (int64_t)nx_ * ny_ * g.nps;
+        const bool fits32 = !grid_mode || nv + 3 * std::min(nv, cells) < (int64_t)0xffffffffll;
+        if (nbins <= kMaxBins && fits32) {
             g.tiled = 1;
             g.wx0 = x0;
             g.wnx = nx_;
@@ -4285,7 +4309,11 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // SDP_HIP_BUCKET=16 forces the latter (tests of the large-grid path)
     {
         const int64_t cell = (int64_t)g.wnx * g.wny * g.nps;
-        g.sub = (g.tiled || cell <= kMaxCellKeys) ? kTileCell : kTileCoarse;
+        // (the one-cell invert's 4-padded record total is 32-bit: see fits32
+        // above; the coarse path checks its padded total exactly)
+        const int64_t nv = in.nrow * (int64_t)in.nchan;
+        const bool fits32 = !grid_mode || nv + 3 * std::min(nv, cell) < (int64_t)0xffffffffll;
+        g.sub = (g.tiled || (cell <= kMaxCellKeys && fits32)) ? kTileCell : kTileCoarse;
         if (env_int("SDP_HIP_BUCKET", 0) == kTileCoarse) g.sub = kTileCoarse;
     }
     g.nty = g.wny / g.sub;
@@ -5225,9 +5253,15 @@ static void subsort_items(Plan &P, hipStream_t st) {
     SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, pcnt, pbase, (int)ni + 1, st));
     void *tmp = scratch<char>("scan_tmp", tb + 16);
     SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, pcnt, pbase, (int)ni + 1, st));
-    unsigned *htot = pinned_host<unsigned>(56, 1);
-    SDP_HIP_CHECK(hipMemcpyAsync(htot, pbase + ni, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    // the exact (64-bit) padded total beside the 32-bit scan: the record
+    // offsets are 32-bit, so a total past 2^32 is refused, not wrapped
+    unsigned long long *tot64 = scratch<unsigned long long>("sub_tot64", 1);
+    k_sum_u32<<<1, 1024, 0, st>>>(pcnt, ni, tot64);
+    unsigned long long *htot = pinned_host<unsigned long long>(56, 1);
+    SDP_HIP_CHECK(hipMemcpyAsync(htot, tot64, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     SDP_HIP_CHECK(hipStreamSynchronize(st));
+    SDP_REQUIRE(*htot < 0xffffffffull,
+                "more than 2^32 padded records in one invert call: split it into batches");
     P.recs_pad = scratch<RecC>("recs_pad", (size_t)*htot + 1);
     k_subsort_pad<<<ni, kSubThreads, 0, st>>>(P.g, pt.items, reinterpret_cast<const RecC *>(P.recs),
                                               P.cls, pbase, P.recs_pad, pt.fitems);

@@ -465,7 +465,7 @@ class Visibility(Dataset):
         drivers use it: (time, one-time-sample Visibility) pairs."""
         if coord != "time":
             raise ValueError(f"groupby: only 'time' is supported, not {coord}")
-        times = np.asarray(self._vars["time"])
+        times = np.unique(np.asarray(self._vars["time"], dtype=float))
         return list(zip(times.tolist(), visibility_time_slices(self)))
 
     @classmethod
@@ -835,11 +835,28 @@ _TIME_VARS = ("vis", "uvw", "weight", "imaging_weight", "flags", "time", "integr
 
 
 def visibility_time_slices(vis):
-    """One Visibility per time sample, as ``vis.groupby("time", squeeze=False)``
-    yields them (views of the parent's arrays)."""
-    nt = vis.vis.shape[0]
+    """One Visibility per distinct time value, in increasing time order, as
+    xarray's ``vis.groupby("time", squeeze=False)`` yields them: the rows
+    sharing a time value form one group (a view of the parent's arrays when
+    they are consecutive, a gathered copy otherwise)."""
+    times = np.asarray(vis._vars["time"], dtype=float)
     out = []
-    for t in range(nt):
-        rep = {k: vis._vars[k][t:t + 1] for k in _TIME_VARS if k in vis._vars}
+    for t in np.unique(times):
+        rows = np.flatnonzero(times == t)
+        if rows[-1] - rows[0] + 1 == rows.size:
+            sel = slice(int(rows[0]), int(rows[-1]) + 1)
+        else:
+            sel = rows
+        rep = {}
+        for k in _TIME_VARS:
+            if k not in vis._vars:
+                continue
+            a = vis._vars[k]
+            if isinstance(sel, slice):
+                rep[k] = a[sel]
+            elif torch is not None and isinstance(a, torch.Tensor):
+                rep[k] = a[torch.as_tensor(sel, device=a.device)]
+            else:
+                rep[k] = np.asarray(a)[sel]
         out.append(vis._copy_with(deep=False, replace=rep))
     return out

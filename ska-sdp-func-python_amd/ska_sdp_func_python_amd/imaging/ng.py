@@ -61,6 +61,19 @@ def _vis_to_im(model, freq):
     return np.round(model.image_acc.wcs.sub([4]).wcs_world2pix(np.asarray(freq), 0)[0]).astype(int)
 
 
+def _channel_runs(vis_to_im, lo, hi):
+    """(image channel, first, end) of each run of consecutive visibility
+    channels in [lo, hi) that map to the same image channel."""
+    runs = []
+    for v in range(lo, hi):
+        ichan = int(vis_to_im[v])
+        if runs and runs[-1][0] == ichan:
+            runs[-1][2] = v + 1
+        else:
+            runs.append([ichan, v, v + 1])
+    return [tuple(r) for r in runs]
+
+
 def _pixsize(model):
     return float(np.abs(np.radians(model.image_acc.wcs.wcs.cdelt[0])))
 
@@ -251,32 +264,40 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     vis_to_im = _vis_to_im(model, freq)
 
     # the (pol, channel) images the reference loops over (ng.py:236-289): all
-    # pols of the band for MFS, channel-major per visibility channel else
-    # (each image is independent, so the order does not matter)
+    # pols of the band for MFS; for a cube, one call per image pol and run of
+    # consecutive visibility channels that map to one image channel.  The
+    # reference adds one ducc0 call per visibility channel into im[ichan]
+    # (ng.py:259-289); the sum is linear in the visibilities, so a run's
+    # channels grid as one call into the same image and weight sum (C2 as a
+    # 16-channel cube: 16 calls of 4 channels instead of 64 of one).
     if mfs:
         calls = [(pol, slice(0, nloc), 0) for pol in range(npol if nloc > 0 else 0)]
     else:
-        calls = [(pol, slice(vchan - lo, vchan - lo + 1), int(vis_to_im[vchan]))
-                 for vchan in range(lo, hi) for pol in range(npol)]
+        calls = [(pol, slice(a - lo, b - lo), ichan)
+                 for ichan, a, b in _channel_runs(vis_to_im, lo, hi) for pol in range(npol)]
     grid_calls = [c for c in calls if not (dopsf and c[0] != 0)]
-    # The image pols of an MFS image share one bucketing: the first pol keeps
+    # The pols of one image channel share one bucketing: the first pol keeps
     # it, the others re-run only the value pass (SDP_HIP_KEEP_BUCKETS /
     # SDP_HIP_REUSE_BUCKETS; C2 4 pols 54.0 ms against 59.7 pipelined, bench
-    # api object).  Otherwise two or more NUFFT calls -- a cube's channels --
-    # are pipelined: consecutive calls alternate between two streams and the
-    # library's two scratch slots, so call k+1's bucketing runs under call
-    # k's gridding and FFT (C2 as a 16-channel cube: 284.8 against 316.4 ms
-    # on one stream).  SDP_HIP_OVERLAP=0 keeps every call on one stream.
-    share_mfs = mfs and npol > 1 and not dopsf
-    overlap = len(grid_calls) > 1 and not share_mfs and dev.type == "cuda" and \
+    # api object).  Otherwise two or more NUFFT calls -- a single-pol cube's
+    # channel runs -- are pipelined over two streams and the library's two
+    # scratch slots, so one call's bucketing runs under the other's gridding
+    # and FFT.  The stream is picked by the OUTPUT (image channel, pol), not
+    # by the call's position: the image and weight-sum accumulation is a
+    # plain read-modify-write, so every call into one target stays on one
+    # stream.  SDP_HIP_OVERLAP=0 keeps every call on one stream.
+    share = npol > 1 and not dopsf
+    overlap = len(grid_calls) > 1 and not share and dev.type == "cuda" and \
         os.environ.get("SDP_HIP_OVERLAP", "1") != "0"
-    share = npol > 1 and not dopsf and not overlap
     main = torch.cuda.current_stream(dev) if overlap else None
     side = _side_stream(dev) if overlap else None
     if overlap:
         side.wait_stream(main)
+    lane_of = {}
+    for pol, _, ichan in grid_calls:
+        lane_of.setdefault((ichan, pol), len(lane_of) % 2)
 
-    def grid_pol(pol, chans, ichan, k):
+    def grid_pol(pol, chans, ichan, first_pol):
         sw = sumwt_d[ichan, pol:pol + 1]
         if dopsf and pol != 0:
             # PSF: pol 0 holds unit visibilities, the others are zero and are
@@ -285,23 +306,20 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
             sw += (wgt[:, chans, pol].to(torch.float64) * m).sum()
             return
         coef = None if (dopsf or conv is None) else conv[pol]
-        ctx = torch.cuda.stream(side if k % 2 else main) if overlap else contextlib.nullcontext()
+        lane = lane_of[(ichan, pol)] if overlap else 0
+        ctx = torch.cuda.stream(side if lane else main) if overlap else contextlib.nullcontext()
         with ctx:
             _, info = kernels.ms2dirty_vis(
                 uvw, freq_t[chans], None if dopsf else ms[:, chans, :], pol, wgt[:, chans, pol],
                 flags[:, chans, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
                 do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
-                accumulate=True, sumwt=sw, shift_lmn=lmn, keep_buckets=share and pol == 0,
-                reuse_buckets=share and pol > 0, precision=precision,
-                slot=(k % 2) if overlap else 0)
+                accumulate=True, sumwt=sw, shift_lmn=lmn, keep_buckets=share and first_pol,
+                reuse_buckets=share and not first_pol, precision=precision, slot=lane)
         if verbosity:
             log.info("invert_ng: %s", info)
 
-    k = 0
     for pol, chans, ichan in calls:
-        grid_pol(pol, chans, ichan, k)
-        if not (dopsf and pol != 0):
-            k += 1
+        grid_pol(pol, chans, ichan, pol == 0)
     if overlap:
         main.wait_stream(side)
     if shard:

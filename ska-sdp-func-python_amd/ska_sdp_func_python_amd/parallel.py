@@ -51,31 +51,75 @@ def shard_info(kwargs=None):
     return dist.get_rank(), world, None
 
 
+_HASH_CHUNK = 1 << 24  # bytes hashed per step (bounds the temporaries)
+
+
+def _byte_hash(a):
+    """Two int64 sums over the array's bytes taken as 32-bit words: plain and
+    position-weighted (weight = word index mod 65521, plus 1), both modulo
+    2^64.  Computed in chunks of _HASH_CHUNK bytes on the array's own device,
+    so the temporaries stay small whatever the array's size; identical bytes
+    (NaNs included) hash identically."""
+    if isinstance(a, torch.Tensor):
+        flat = a.reshape(-1)
+        item = flat.element_size()
+        step = max(1, _HASH_CHUNK // item)
+        s0 = torch.zeros((), dtype=torch.int64, device=a.device)
+        s1 = torch.zeros((), dtype=torch.int64, device=a.device)
+        word0 = 0
+        for i in range(0, flat.numel(), step):
+            b = flat[i:i + step].contiguous().view(torch.uint8)
+            pad = (-b.numel()) % 4
+            if pad:
+                b = torch.cat([b, b.new_zeros(pad)])
+            w = b.view(torch.int32).to(torch.int64)
+            idx = (torch.arange(word0, word0 + w.numel(), device=a.device) % 65521) + 1
+            s0 += w.sum()
+            s1 += (w * idx).sum()
+            word0 += w.numel()
+        return [int(s0), int(s1)]
+    flat = np.asarray(a).reshape(-1)
+    step = max(1, _HASH_CHUNK // max(flat.itemsize, 1))
+    s0 = s1 = 0
+    word0 = 0
+    for i in range(0, flat.size, step):
+        b = np.ascontiguousarray(flat[i:i + step]).view(np.uint8)
+        if b.size % 4:
+            b = np.concatenate([b, np.zeros((-b.size) % 4, np.uint8)])
+        w = b.view(np.int32).astype(np.int64)
+        idx = (np.arange(word0, word0 + w.size, dtype=np.int64) % 65521) + 1
+        with np.errstate(over="ignore"):
+            s0 = (s0 + int(w.sum(dtype=np.int64))) & 0xFFFFFFFFFFFFFFFF
+            s1 = (s1 + int((w * idx).sum(dtype=np.int64))) & 0xFFFFFFFFFFFFFFFF
+        word0 += w.size
+    return [s0 - (1 << 64) if s0 >= 1 << 63 else s0, s1 - (1 << 64) if s1 >= 1 << 63 else s1]
+
+
 def _fingerprint(arrays):
-    """float64 vector: per array its shape, element count and (for numbers)
-    the sums of its values and of their magnitudes, in a fixed order."""
+    """int64 vector: per array its rank, shape and (for arrays) a hash of its
+    bytes (_byte_hash), in a fixed order."""
     out = []
     for a in arrays:
         if a is None:
-            out += [-1.0]
+            out += [-1]
             continue
-        t = a if isinstance(a, torch.Tensor) else torch.as_tensor(np.asarray(a))
-        out += [float(t.dim())] + [float(s) for s in t.shape]
-        if t.numel() == 0:
+        if isinstance(a, (tuple, list)) and all(isinstance(s, (int, np.integer)) for s in a):
+            out += [len(a)] + [int(s) for s in a]  # a shape
             continue
-        if t.is_complex():
-            t = torch.view_as_real(t)
-        t = t.to(torch.float64)
-        out += [float(t.sum()), float(t.abs().sum())]
-    return torch.tensor(out, dtype=torch.float64)
+        t = a if isinstance(a, torch.Tensor) else np.asarray(a)
+        out += [t.ndim] + [int(s) for s in t.shape]
+        if t.size == 0 if isinstance(t, np.ndarray) else t.numel() == 0:
+            continue
+        out += _byte_hash(t)
+    return torch.tensor(out, dtype=torch.int64)
 
 
 def check_replicated(shard, arrays, what):
     """Raise ValueError on EVERY rank unless every rank of ``shard`` passed
-    the same arrays (shapes, element sums and magnitude sums agree): a
-    sharded call splits one replicated problem, and ranks that pass their
-    own data would otherwise combine unrelated partial results (or hang in
-    a collective of mismatched shapes).  One small all-reduce pair."""
+    the same arrays (shapes and byte hashes agree): a sharded call splits
+    one replicated problem, and ranks that pass their own data would
+    otherwise combine unrelated partial results (or hang in a collective of
+    mismatched shapes).  One small all-reduce pair of int64 vectors."""
     if not shard:
         return
     fp = _fingerprint(arrays)
@@ -84,9 +128,9 @@ def check_replicated(shard, arrays, what):
         dev = torch.device("cuda", torch.cuda.current_device())
     fp = fp.to(dev)
     # the fingerprints' lengths first: a shape mismatch changes the length
-    n = torch.tensor([float(len(fp)), -float(len(fp))], dtype=torch.float64, device=dev)
+    n = torch.tensor([len(fp), -len(fp)], dtype=torch.int64, device=dev)
     dist.all_reduce(n, op=dist.ReduceOp.MAX, group=shard[2])
-    same = float(n[0]) == -float(n[1])
+    same = int(n[0]) == -int(n[1])
     if same:
         hi = fp.clone()
         lo = -fp

@@ -176,3 +176,64 @@ def test_default_is_per_rank_and_mismatched_shards_raise(monkeypatch):
     res = _spawn("invert_mfs", shard=True, own_data=True)
     for _, out, _, _ in res:
         assert out[0] == "ValueError" and "same inputs" in out[1]
+
+
+def _check_worker(rank, world, port, q, own):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ska_sdp_func_python_amd import parallel
+    try:
+        rng = np.random.default_rng(5 + (rank if own else 0))
+        vis = (rng.normal(size=(40, 3, 2)) + 1j * rng.normal(size=(40, 3, 2))).astype(np.complex64)
+        vis[::7, 1, 0] = np.nan  # flagged NaN samples, replicated on every rank
+        wgt = torch.as_tensor(rng.uniform(size=(40, 3)))
+        wgt[3, 2] = float("nan")
+        flags = np.zeros((40, 3, 2), np.int8)
+        try:
+            parallel.check_replicated((rank, world, None), [vis, wgt, flags, (4, 1, 32, 32)],
+                                      "invert_ng")
+            q.put((rank, "ok"))
+        except ValueError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("own", [False, True])
+def test_replication_check_is_bitwise_and_nan_safe(own):
+    """parallel.check_replicated hashes the inputs' bytes in chunks (no
+    float64 copy of the Visibility): replicated inputs holding NaNs pass on
+    every rank; ranks with different data raise ValueError on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + int(np.random.default_rng().integers(300, 600))
+    procs = [ctx.Process(target=_check_worker, args=(r, 2, port, q, own)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for _, msg in res:
+        if own:
+            assert "same inputs" in msg
+        else:
+            assert msg == "ok"
+
+
+def test_byte_hash_matches_between_host_and_torch():
+    """The hash of an array is the same whether a rank holds it as numpy or
+    as a torch tensor, and whatever the chunking."""
+    from ska_sdp_func_python_amd import parallel
+    rng = np.random.default_rng(3)
+    for a in (rng.normal(size=1001), (rng.normal(size=(17, 3)) + 1j).astype(np.complex64),
+              rng.integers(0, 2, (33, 5)).astype(np.int8), np.array([np.nan, 1.0, -0.0])):
+        h = parallel._byte_hash(a)
+        assert h == parallel._byte_hash(torch.as_tensor(a))
+        old = parallel._HASH_CHUNK
+        try:
+            parallel._HASH_CHUNK = 24
+            assert parallel._byte_hash(a) == h == parallel._byte_hash(torch.as_tensor(a))
+        finally:
+            parallel._HASH_CHUNK = old
+    assert parallel._byte_hash(np.array([1.0, 2.0])) != parallel._byte_hash(np.array([2.0, 1.0]))

@@ -409,6 +409,61 @@ def test_invert_ng_fused_prologue(pf, ipf, mfs, dopsf, device):
     np.testing.assert_allclose(sumwt, exp_sw, rtol=1e-6 if device else 1e-12)
 
 
+@pytest.mark.parametrize("pf,ipf,dopsf", [("stokesI", "stokesI", False),
+                                          ("linear", "stokesIQUV", True),
+                                          ("linear", "stokesIQUV", False)])
+@pytest.mark.parametrize("order", ["sorted", "interleaved"])
+def test_invert_ng_cube_channel_runs(pf, ipf, dopsf, order, monkeypatch):
+    """A cube whose image channels each collect several visibility channels
+    (8 -> 2, the reference's many-to-one vis_to_im, ng.py:259-289): invert_ng
+    grids each run of consecutive channels of one image channel as one call.
+    With interleaved frequencies the runs alternate image channels, so two
+    calls add into one image; the pipelined (two-stream) result must equal
+    the one-stream result (SDP_HIP_OVERLAP=0) and the exact sums per image
+    channel, and sumwt must count every channel once."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import invert_ng
+    rng = np.random.default_rng(23)
+    nt, nb, nchan = 6, 40, 8
+    npol = dm.PolarisationFrame(pf).npol
+    freq = 1.0e9 + 1.0e7 * np.arange(nchan)
+    if order == "interleaved":
+        freq = freq[[0, 4, 1, 5, 2, 6, 3, 7]]
+    umax = 1500.0
+    uvw = rng.uniform(-1, 1, (nt, nb, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw[..., 2] *= 0.5
+    shape = (nt, nb, nchan, npol)
+    v = rng.normal(size=shape) + 1j * rng.normal(size=shape)
+    fl = (rng.uniform(size=shape) < 0.1).astype(int)
+    vis = vis_from_arrays(uvw, freq, v, weight=rng.uniform(0.5, 2.0, shape), flags=fl, pf=pf,
+                          phasecentre=dm.SkyCoord(0.0, -0.6))
+    vis["imaging_weight"] = rng.uniform(0.5, 2.0, shape)
+    npix, cell = 128, 0.4 / umax
+    im = dm.create_image(npix, cell, dm.SkyCoord(0.0, -0.6),
+                         polarisation_frame=dm.PolarisationFrame(ipf), frequency=1.015e9,
+                         channel_bandwidth=4.0e7, nchan=2)
+    ichan = np.round((freq - 1.015e9) / 4.0e7).astype(int)
+    assert sorted(np.bincount(ichan)) == [4, 4]
+    ms, wgt, fuvw = _prologue_reference(vis, im, dopsf)
+    out = {}
+    for tag in ("1", "0"):
+        monkeypatch.setenv("SDP_HIP_OVERLAP", tag)
+        d, sw = invert_ng(vis, im, dopsf=dopsf, normalise=False)
+        out[tag] = (np.asarray(d["pixels"].data), sw)
+    np.testing.assert_allclose(out["1"][1], out["0"][1], rtol=1e-13)
+    assert rel_rms(out["1"][0], out["0"][0]) < 1e-6  # fp32 atomics' order only
+    for c in range(2):
+        chans = np.flatnonzero(ichan == c)
+        for pol in range(npol):
+            np.testing.assert_allclose(out["1"][1][c, pol], wgt[:, chans, pol].sum(), rtol=1e-12)
+            if dopsf and pol > 0:
+                assert not np.any(out["1"][0][c, pol])
+                continue
+            ref = orc.ms2dirty_exact(fuvw * FLIP_UW, freq[chans], ms[:, chans, pol],
+                                     wgt[:, chans, pol], npix, npix, cell, cell, True).T
+            assert rel_rms(out["1"][0][c, pol], ref) < TOL, (c, pol)
+
+
 @pytest.mark.parametrize("bucket2", ["1", "2"])
 def test_shared_bucketing_across_pols(bucket2, monkeypatch):
     """SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS (invert_ng's image pols):

@@ -262,3 +262,25 @@ def test_wrow_partition_covers_the_rows_and_balances():
                   for a, e in zip(cuts[:-1], cuts[1:])]
             mid = world // 2
             assert pl[mid] <= max(pl[0], pl[-1])
+
+
+def test_groupby_time_groups_distinct_sorted_times():
+    """Visibility.groupby("time") follows xarray: one group per distinct time
+    value, in increasing order, holding every row with that time (repeated
+    and unsorted time stamps included)."""
+    import numpy as np
+    from ska_sdp_func_python_amd import datamodels as dm
+    times = np.array([3.0, 1.0, 3.0, 2.0, 2.0])
+    nt, nb = len(times), 3
+    vis = dm.Visibility.constructor(
+        frequency=np.array([1e9]), channel_bandwidth=np.array([1e6]),
+        phasecentre=dm.SkyCoord(0.0, -0.5), uvw=np.arange(nt * nb * 3, dtype=float).reshape(nt, nb, 3),
+        time=times, vis=np.arange(nt * nb, dtype=complex).reshape(nt, nb, 1, 1),
+        baselines=np.stack(np.triu_indices(3, 1), 1))
+    groups = vis.groupby("time", squeeze=False)
+    assert [t for t, _ in groups] == [1.0, 2.0, 3.0]
+    rows = {1.0: [1], 2.0: [3, 4], 3.0: [0, 2]}
+    for t, g in groups:
+        np.testing.assert_array_equal(np.asarray(g.time.data), [t] * len(rows[t]))
+        np.testing.assert_array_equal(np.asarray(g.vis.data)[:, :, 0, 0],
+                                      np.arange(nt * nb).reshape(nt, nb)[rows[t]])
