@@ -1344,10 +1344,27 @@ constexpr size_t grid_mfma_pad_lds() {
            kTapBatch * sizeof(float2);
 }
 
+// The dense uv core's cells take 10^6-10^7 flushed additions per invert (C4's
+// whole band: 13.4 Gvis into 71 planes), whose fp32 rounding grows with the
+// count and varies with the atomics' order.  A work item whose whole region
+// lies in the core window [x0, x0 + nx) x [y0, y0 + ny) therefore flushes into
+// c128 companion planes with fp64 atomics; the companion is added to the fp32
+// planes once, before the FFT (k_core_merge).  C4 full band against exact
+// sums at 64 pixels: 1.9e-6 - 2.8e-6 -> 0.88e-6 - 0.94e-6 relative RMS, +0.6 %
+// time (scripts/c4_precision.py, profiles/r05_c4_precision.jsonl).  Capping
+// a cell's fp32 MFMA chain at 64 records (partial sums added to the region
+// per batch) changed nothing measurable there and cost C2 4 % of its
+// gridding, so the in-item accumulation stays one chain.  p == nullptr: no
+// companion.
+struct CoreAcc {
+    double *p;
+    int x0, nx, y0, ny;
+};
+
 template <int W, bool WS, int NG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma_pad(
     Geo g, const RecC *__restrict__ recs, const FineItem *__restrict__ items, uint32_t n_items,
-    float *__restrict__ grid, int p_lo, int p_hi) {
+    float *__restrict__ grid, int p_lo, int p_hi, CoreAcc core) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
     static_assert(NG == 1 || NG == 2 || NG == 4 || NG == 8 || NG == 16, "units of 1-16 groups");
     // (NG = 2, 8, 16 are valid but measured slower on C4; only 1 and 4 are launched)
@@ -1552,6 +1569,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         // buffer atomics off a per-plane descriptor (32-bit offsets); zero
         // floats are dropped by the range check
         constexpr int FPP = RX * RY * 2;
+        if (core.p != nullptr && ibase >= core.x0 && ibase + RX <= core.x0 + core.nx &&
+            jbase >= core.y0 && jbase + RY <= core.y0 + core.ny) {
+            // the whole region lies in the core window: fp64 atomics into the
+            // companion planes [p - p_lo][x - x0][y - y0] (c128)
+            for (int i0 = 0; i0 < FPP; i0 += 64) {
+                const int f = i0 + lane;
+                if (f >= FPP) break;
+                const int c = f >> 1, xl = c / RY, yl = c - xl * RY;
+                const size_t cell = (size_t)(ibase + xl - core.x0) * core.ny + (jbase + yl - core.y0);
+                const float *src = reg + (xl * kRegY + yl) * kRegCell + (f & 1);
+                float vals[NQ];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) vals[q] = src[4 * reg_chunk(q >> 1, yl) + 2 * (q & 1)];
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const int p = (int)p0 + q;
+                    if (vals[q] != 0.0f && p >= p_lo && p < p_hi)
+                        unsafeAtomicAdd(core.p + ((size_t)(p - p_lo) * core.nx * core.ny + cell) * 2 +
+                                            (f & 1),
+                                        (double)vals[q]);
+                }
+            }
+            continue;
+        }
         const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
         // one buffer descriptor per plane (scalar registers); a plane outside
         // [p_lo, p_hi) gets an empty range, and a zero float an offset past
@@ -3882,6 +3923,7 @@ struct Plan {
     float2 *grid = nullptr;
     float2 *spec = nullptr;     // T[q][iy][kx]: transposed y-spectra (pruned FFT)
     float2 *spec_in = nullptr;  // band-only input of the backward x-FFT (zeros elsewhere)
+    CoreAcc core{nullptr, 0, 0, 0, 0};  // fp32 invert: fp64 companion of the uv core
 };
 
 // the element size of the planes and spectra: c64, or c128 on the fp64 path
@@ -4652,11 +4694,12 @@ static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t 
         // ~120 records each, were bound by them) but hold more LDS per wave
         const unsigned nu = n * 4u;
         k_grid_mfma_pad<W, WS, 4><<<nu, 64, grid_mfma_pad_lds<4>(), st>>>(
-            P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo, p_hi);
+            P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo, p_hi,
+            P.core);
     } else
         k_grid_mfma_pad<W, WS, 1><<<n, 64, grid_mfma_pad_lds<1>(), st>>>(
             P.g, reinterpret_cast<const RecC *>(P.recs), P.pt.fitems + r.first, n, (float *)P.grid,
-            p_lo, p_hi);
+            p_lo, p_hi, P.core);
 }
 
 template <int W, bool WS>
@@ -4957,6 +5000,48 @@ static void zero_band(const Plan &P, int np, hipStream_t st) {
     const size_t width = (size_t)(P.row_hi - P.row_lo) * g.ngy * cbytes(P);
     for (int q = 0; q < np; ++q)
         SDP_HIP_CHECK(hipMemsetAsync(plane_ptr(P, q, (size_t)P.row_lo * g.ngy), 0, width, st));
+    if (P.core.p)
+        SDP_HIP_CHECK(hipMemsetAsync(P.core.p, 0,
+                                     (size_t)np * P.core.nx * P.core.ny * sizeof(double2), st));
+}
+
+// The fp64 companion of the uv core (CoreAcc): a central window of
+// SDP_HIP_CORE (default 512) cells square, clipped to the grid rows the
+// visibilities reach, one c128 plane per resident plane (C4: 71 x 4 MiB).
+// SDP_HIP_CORE=0: no companion (every flush in fp32).
+static void setup_core(Plan &P) {
+    P.core = CoreAcc{nullptr, 0, 0, 0, 0};
+    const int cw = env_int("SDP_HIP_CORE", 512);
+    if (P.f64 || cw <= 0) return;
+    const Geo &g = P.g;
+    const int x0 = std::max(P.row_lo, g.ngx / 2 - cw / 2), x1 = std::min(P.row_hi, g.ngx / 2 + cw / 2);
+    const int y0 = std::max(0, g.ngy / 2 - cw / 2), y1 = std::min(g.ngy, g.ngy / 2 + cw / 2);
+    if (x1 <= x0 || y1 <= y0) return;
+    P.core = CoreAcc{scratch<double>("core64", (size_t)P.chunk_planes * (x1 - x0) * (y1 - y0) * 2),
+                     x0, x1 - x0, y0, y1 - y0};
+}
+
+// planes q0 .. q0 + np - 1 of the chunk += their fp64 companion, rounded once
+__global__ __launch_bounds__(256) void k_core_merge(float2 *__restrict__ grid, int ngx, int ngy,
+                                                    CoreAcc c, int q0, int np) {
+    const int64_t per = (int64_t)c.nx * c.ny, n = per * np;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int q = (int)(i / per);
+        const int64_t e = i - q * per;
+        const int x = (int)(e / c.ny), y = (int)(e - (int64_t)x * c.ny);
+        const double2 v = reinterpret_cast<const double2 *>(c.p)[(int64_t)(q0 + q) * per + e];
+        float2 &o = grid[((int64_t)(q0 + q) * ngx + c.x0 + x) * ngy + c.y0 + y];
+        o = make_float2((float)((double)o.x + v.x), (float)((double)o.y + v.y));
+    }
+}
+
+static void core_merge(const Plan &P, int q0, int np, hipStream_t st) {
+    if (!P.core.p || np <= 0) return;
+    const int64_t n = (int64_t)P.core.nx * P.core.ny * np;
+    k_core_merge<<<(unsigned)std::min<int64_t>((n + 255) / 256, 8192), 256, 0, st>>>(
+        P.grid, P.g.ngx, P.g.ngy, P.core, q0, np);
+    SDP_HIP_CHECK(hipGetLastError());
 }
 
 static dim3 tr_grid(const Geo &g, int xrows, int np) {
@@ -5314,6 +5399,7 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     // pass re-derives the bin ranks from that classification)
     inx.x.all = keep || reuse;
     Plan P = reuse ? reuse_buckets(in) : plan_geometry(inx, true, st);
+    setup_core(P);
     const Geo &g = P.g;
     // batched invert: planes zeroed by the first batch, FFT + screens by the
     // last; in between they stay resident in the workspace
@@ -5375,6 +5461,7 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
             tg.mark();
             tgrid += tg.ms(0, 1);
         }
+        if (last) core_merge(P, 0, np, st);
         for (int sb = 0; last && sb < np; sb += P.fft_planes) {
             const int nb = std::min(P.fft_planes, np - sb);
             StageTimer t2(st);

@@ -520,7 +520,20 @@ def make_skymodel():
     out["invert_ng_sumwt"] = sw
     p = ng["predict_ng"](vis.copy(deep=True), sm.image)
     out["predict_ng_vis"] = p["vis"].data
+    # a 2-channel cube over the 3 visibility channels (vis_to_im = [0, 0, 1]):
+    # the reference's per-channel branches (ng.py:113-129, :259-289), two
+    # visibility channels summed into image channel 0
+    from skymodel_case import cube_case
+    cube, px = cube_case(sm.image, vis)
+    out["cube_pixels"] = px
+    d, sw = ng["invert_ng"](vis.copy(deep=True), cube)
+    out["invert_cube_dirty"] = d["pixels"].data
+    out["invert_cube_sumwt"] = sw
+    cube["pixels"].data = px
+    p = ng["predict_ng"](vis.copy(deep=True), cube)
+    out["predict_cube_vis"] = p["vis"].data
     save("skymodel.npz", cell=np.array(cell), **out)
+
 
 
 def make_awprojection():

@@ -51,3 +51,20 @@ def _pb(im):
     return beam
 
 
+def cube_case(image, vis):
+    """The 2-channel cube of the sky-model fixture: image channel 0 centred
+    between visibility channels 0 and 1, channel 1 on channel 2, and its
+    seeded model pixels (a few bright ones per channel)."""
+    f = np.asarray(vis.frequency.data, dtype=float)
+    npix = image["pixels"].data.shape[-1]
+    cell = abs(float(image.image_acc.wcs.wcs.cdelt[0]))
+    bw = 1.5 * float(f[1] - f[0])
+    from ska_sdp_func_python_amd import datamodels as dm
+    cube = dm.create_image(npix, math.radians(cell), image.image_acc.phasecentre,
+                           frequency=0.5 * float(f[0] + f[1]), channel_bandwidth=bw, nchan=2)
+    rng = np.random.default_rng(17)
+    px = np.zeros((2, 1, npix, npix))
+    for c in range(2):
+        for _ in range(5):
+            px[c, 0, rng.integers(40, 88), rng.integers(40, 88)] = rng.uniform(0.5, 2.0)
+    return cube, px
