@@ -106,6 +106,11 @@ def parse():
                          "every plane); 'wslab' -- every rank scans the band and grids its slab "
                          "of the band's w planes (parallel.wslab_partition; 2.6x at N = 8: the "
                          "w ~ 0 plane holds 38 %% of the visibilities) -- DESIGN.md §6")
+    ap.add_argument("--c4-api", action="store_true",
+                    help="C4 through the drop-in API: each rank builds a Visibility of its own "
+                         "block (resident c64 vis, unit weights) and calls invert_ng(..., "
+                         "shard='local'), which batches the block's channels and all-reduces "
+                         "the image and weights; needs --gpus >= 2 or --emulate")
     ap.add_argument("--emulate", default=None, metavar="RANK/WORLD",
                     help="c4 on one GPU: run only rank RANK's block of a WORLD-way partition "
                          "(no collective), to measure per-rank times")
@@ -524,6 +529,9 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
         gen.manual_seed(7919 * (0 if wslab else rank) + a)  # (w slabs: one band, every rank)
         return torch.randn((nrow, e - a), generator=gen, device=dev, dtype=torch.complex64)
 
+    if args.c4_api:
+        return run_c4_api(args, world, rank, local, dev, uvw, nrow, lo, hi, freqs, obs["umax"],
+                          batches, make_vis, emulated, sub)
     store = {(a, e): make_vis(a, e) for a, e in batches} if resident else {}
 
     def vis_of_block(a, e):
@@ -687,6 +695,91 @@ def run_c4(args, world, rank, local, dev, emulated=False, sub=False):
                                                4)}},
         "cpu_baseline": cpu,
     }
+    if sub:
+        return line
+    print(json.dumps(line), flush=True)
+    return None
+
+
+def run_c4_api(args, world, rank, local, dev, uvw, nrow, lo, hi, freqs, umax, batches, make_vis,
+               emulated, sub):
+    """C4 through the reference-shaped API: the rank's block (its rows by w,
+    or its channel block) as a Visibility of [1, nrow, nchan, 1] (resident c64
+    visibilities generated with run_c4's seeds; weights and flags are
+    zero-stride views: unit weights, no flags) and one
+    invert_ng(vis, model, shard="local", epsilon=1e-7) per step -- the call a
+    pipeline holding one observation in N blocks makes.  invert_ng grids the
+    block in channel batches (SDP_HIP_MAX_CALL_GVIS) through one set of
+    resident planes, all-reduces the image and sumwt (ng.py:288-292) and
+    normalises.  Step time: barrier + synchronize around each call, max over
+    ranks; the line's value = the band's visibilities / that time."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import invert_ng
+    if args.partition == "wslab":
+        raise SystemExit("--c4-api: a w-slab rank scans the whole band (no Visibility block)")
+    if world == 1 and not emulated:
+        raise SystemExit("--c4-api: the 107 GB band does not fit beside its 152 GB of planes on "
+                         "one GPU; use --gpus >= 2 or --emulate r/N")
+    nch = hi - lo
+    vis = torch.empty((1, nrow, nch, 1), dtype=torch.complex64, device=dev)
+    for a, e in batches:
+        vis[0, :, a - lo:e - lo, 0] = make_vis(a, e)
+    ones = torch.ones((1, 1, 1, 1), dtype=torch.float32, device=dev).expand(1, nrow, nch, 1)
+    noflag = torch.zeros((1, 1, 1, 1), dtype=torch.int8, device=dev).expand(1, nrow, nch, 1)
+    pc = dm.SkyCoord(0.0, -0.5)
+    f = freqs[lo:hi]
+    bv = dm.Visibility.constructor(frequency=f, channel_bandwidth=np.full(nch, 1.17e6),
+                                   phasecentre=pc, uvw=uvw.view(1, nrow, 3), time=np.zeros(1),
+                                   vis=vis, weight=ones, imaging_weight=ones, flags=noflag,
+                                   integration_time=np.ones(1))
+    cell = 0.25 / umax
+    model = dm.create_image(C4_NPIX, cell, pc, frequency=float(np.mean(freqs)),
+                            channel_bandwidth=float(2 * (freqs.max() - freqs.min()) + 1e6))
+    kw = {"shard": "local"} if world > 1 and not emulated else {}
+    dist_on = world > 1 and not emulated
+    steps = args.extra_steps if sub else args.steps
+    warmup = min(args.warmup, 1) if sub else args.warmup
+
+    def barrier():
+        if dist_on:
+            dist.barrier(device_ids=[local])
+        torch.cuda.synchronize(dev)
+
+    res = None
+    for _ in range(warmup):
+        res = invert_ng(bv, model, epsilon=EPS_REQUESTED, **kw)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = invert_ng(bv, model, epsilon=EPS_REQUESTED, **kw)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_step = elapsed / steps * 1e3
+    sumwt = float(np.sum(res[1]))
+    if emulated:
+        print(json.dumps({"emulated_rank": rank, "world": world, "api": "invert_ng",
+                          "block": (lo, hi), "rows": nrow, "ms_per_step": round(ms_step, 3),
+                          "nvis_rank": nrow * nch, "sumwt": sumwt,
+                          "note": "rank's block only; no all-reduce"}), flush=True)
+        return None
+    if rank != 0:
+        return None
+    nvis_total = int(round(sumwt))  # unit weights: the band's visibility count
+    line = {
+        "metric": METRIC, "value": round(nvis_total / (elapsed / steps) / 1e6, 3), "unit": "Mvis/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded SKA-LOW-like layout, N(0,1) c64 vis, unit weights, generated "
+                "on device, resident)",
+        "config": {"workload": "C4 through invert_ng(shard='local'): SKA-LOW 512 stations x 400 "
+                               "times x 256 chan = 13.4 Gvis, 8192^2 image, 16384^2 w-stack grid",
+                   "api": "invert_ng", "partition": args.partition, "nvis_total": nvis_total,
+                   "parallelism": f"{args.partition} x{world}, each rank's own Visibility block, "
+                                  "invert_ng channel batches, 1 all-reduce (image + sumwt)"}}
     if sub:
         return line
     print(json.dumps(line), flush=True)

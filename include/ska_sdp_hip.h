@@ -231,6 +231,32 @@ int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride,
                          size_t errbuf_len);
 
 /*
+ * sdp_hip_ms2dirty_vis_batch -- sdp_hip_ms2dirty_vis as one batch of a
+ * sequence (SDP_HIP_BATCH_FIRST / _LAST in `flags`, `bounds` as
+ * sdp_hip_ms2dirty_batch): invert_ng grids an MFS image's (or a cube
+ * channel's) visibilities in channel batches through one set of resident w
+ * planes when they are too many for one call (reference imaging/ng.py:
+ * 240-256, one ducc0 call over all channels).  sumwt accumulates over the
+ * batches.  Other arguments as sdp_hip_ms2dirty_vis.
+ */
+int sdp_hip_ms2dirty_vis_batch(const double *uvw, int64_t uvw_row_stride,
+                               const double *freq, int nchan, int64_t nrow,
+                               const void *vis, int vis_dtype, int64_t vis_row_stride,
+                               int64_t vis_chan_stride, int64_t vis_pol_stride,
+                               int npol_vis, const double *pol_coeff, const void *wgt,
+                               int wgt_dtype, int64_t wgt_row_stride,
+                               int64_t wgt_chan_stride, const void *vis_flags,
+                               int flag_bytes, int64_t flag_row_stride,
+                               int64_t flag_chan_stride, int64_t flag_pol_stride,
+                               int pol, int npix_x, int npix_y, double pixsize_x,
+                               double pixsize_y, double epsilon, int do_wstacking,
+                               unsigned flags, const double *bounds, double *dirty,
+                               int64_t dirty_stride_x, int64_t dirty_stride_y,
+                               double *sumwt, const double *shift_lmn, void *stream,
+                               sdp_hip_wgrid_info *info, char *errbuf,
+                               size_t errbuf_len);
+
+/*
  * sdp_hip_dirty2ms -- replaces ducc0.wgridder.dirty2ms as called by
  * predict_ng (reference src/ska_sdp_func_python/imaging/ng.py:99-112 MFS,
  * :117-129 per channel).  Exact adjoint of sdp_hip_ms2dirty:

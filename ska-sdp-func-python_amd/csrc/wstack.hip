@@ -1350,8 +1350,10 @@ constexpr size_t grid_mfma_pad_lds() {
 // lies in the core window [x0, x0 + nx) x [y0, y0 + ny) therefore flushes into
 // c128 companion planes with fp64 atomics; the companion is added to the fp32
 // planes once, before the FFT (k_core_merge).  C4 full band against exact
-// sums at 64 pixels: 1.9e-6 - 2.8e-6 -> 0.88e-6 - 0.94e-6 relative RMS, +0.6 %
-// time (scripts/c4_precision.py, profiles/r05_c4_precision.jsonl).  Capping
+// sums at 64 pixels: 1.9e-6 - 2.8e-6 -> 0.91e-6 - 0.96e-6 relative RMS with a
+// 128-cell window (time within 0.3 %; 256 cells: the same error, +0.4 %;
+// 512: the same error, +2 %: more items pay fp64 atomics) (scripts/
+// c4_precision.py, profiles/r05_c4_precision.jsonl).  Capping
 // a cell's fp32 MFMA chain at 64 records (partial sums added to the region
 // per batch) changed nothing measurable there and cost C2 4 % of its
 // gridding, so the in-item accumulation stays one chain.  p == nullptr: no
@@ -5006,12 +5008,12 @@ static void zero_band(const Plan &P, int np, hipStream_t st) {
 }
 
 // The fp64 companion of the uv core (CoreAcc): a central window of
-// SDP_HIP_CORE (default 512) cells square, clipped to the grid rows the
-// visibilities reach, one c128 plane per resident plane (C4: 71 x 4 MiB).
+// SDP_HIP_CORE (default 128) cells square, clipped to the grid rows the
+// visibilities reach, one c128 plane per resident plane (C4: 71 x 256 KiB).
 // SDP_HIP_CORE=0: no companion (every flush in fp32).
 static void setup_core(Plan &P) {
     P.core = CoreAcc{nullptr, 0, 0, 0, 0};
-    const int cw = env_int("SDP_HIP_CORE", 512);
+    const int cw = env_int("SDP_HIP_CORE", 128);
     if (P.f64 || cw <= 0) return;
     const Geo &g = P.g;
     const int x0 = std::max(P.row_lo, g.ngx / 2 - cw / 2), x1 = std::min(P.row_hi, g.ngx / 2 + cw / 2);
@@ -5627,6 +5629,66 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
 
 using namespace sdp;
 
+static int ms2dirty_vis_entry(const double *uvw, int64_t uvw_row_stride, const double *freq, int nchan,
+                         int64_t nrow, const void *vis, int vis_dtype, int64_t vis_row_stride,
+                         int64_t vis_chan_stride, int64_t vis_pol_stride, int npol_vis,
+                         const double *pol_coeff, const void *wgt, int wgt_dtype,
+                         int64_t wgt_row_stride, int64_t wgt_chan_stride, const void *vis_flags,
+                         int flag_bytes, int64_t flag_row_stride, int64_t flag_chan_stride,
+                         int64_t flag_pol_stride, int pol, int npix_x, int npix_y,
+                         double pixsize_x, double pixsize_y, double epsilon, int do_wstacking,
+                         unsigned flags, const double *bounds, double *dirty, int64_t dirty_stride_x,
+                         int64_t dirty_stride_y, double *sumwt, const double *shift_lmn,
+                         void *stream, sdp_hip_wgrid_info *info, char *errbuf,
+                         size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE((dirty != nullptr || (bounds && !(flags & SDP_HIP_BATCH_LAST))) &&
+                        freq != nullptr && (uvw != nullptr || nrow == 0),
+                    "null pointer argument");
+        SDP_REQUIRE(npol_vis >= 1 && npol_vis <= 4, "npol_vis must be 1..4");
+        SDP_REQUIRE(pol >= 0 && pol < npol_vis, "pol out of range");
+        SDP_REQUIRE(wgt_dtype == SDP_HIP_F32 || wgt_dtype == SDP_HIP_F64,
+                    "weights must be f32 or f64");
+        SDP_REQUIRE(vis_flags == nullptr || flag_bytes == 1 || flag_bytes == 4 || flag_bytes == 8,
+                    "flag element size must be 1, 4 or 8 bytes");
+        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                          nrow,        vis,             vis_dtype,      vis_row_stride,
+                          vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
+                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                          epsilon,     do_wstacking,    flags};
+        in.bounds = bounds;
+        wstack::VisExtra &x = in.x;
+        x.vps = vis_pol_stride;
+        x.npv = npol_vis;
+        x.wgt_f64 = wgt_dtype == SDP_HIP_F64;
+        x.flags = vis_flags;
+        x.fbytes = vis_flags ? flag_bytes : 0;
+        x.frs = flag_row_stride;
+        x.fcs = flag_chan_stride;
+        x.fps = flag_pol_stride;
+        x.fpol = pol;
+        x.sumwt = sumwt;
+        if (shift_lmn) {
+            x.shift = true;
+            x.sl = shift_lmn[0];
+            x.sm = shift_lmn[1];
+            x.sn = shift_lmn[2];
+        }
+        if (pol_coeff) {
+            x.conv = true;
+            for (int k = 0; k < npol_vis; ++k) {
+                x.cre[k] = pol_coeff[2 * k];
+                x.cim[k] = pol_coeff[2 * k + 1];
+            }
+        } else if (vis) {
+            // no conversion: the image pol is the vis pol `pol`
+            in.vis = static_cast<const char *>(vis) +
+                     pol * vis_pol_stride * (vis_dtype == SDP_HIP_C128 ? 16 : 8);
+        }
+        wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
+    });
+}
+
 extern "C" {
 
 int sdp_hip_version(void) { return 1; }
@@ -5748,50 +5810,40 @@ int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride, const double
                          int64_t dirty_stride_y, double *sumwt, const double *shift_lmn,
                          void *stream, sdp_hip_wgrid_info *info, char *errbuf,
                          size_t errbuf_len) {
-    return guarded(errbuf, errbuf_len, [&] {
-        SDP_REQUIRE(dirty != nullptr && freq != nullptr && (uvw != nullptr || nrow == 0),
-                    "null pointer argument");
-        SDP_REQUIRE(npol_vis >= 1 && npol_vis <= 4, "npol_vis must be 1..4");
-        SDP_REQUIRE(pol >= 0 && pol < npol_vis, "pol out of range");
-        SDP_REQUIRE(wgt_dtype == SDP_HIP_F32 || wgt_dtype == SDP_HIP_F64,
-                    "weights must be f32 or f64");
-        SDP_REQUIRE(vis_flags == nullptr || flag_bytes == 1 || flag_bytes == 4 || flag_bytes == 8,
-                    "flag element size must be 1, 4 or 8 bytes");
-        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
-                          nrow,        vis,             vis_dtype,      vis_row_stride,
-                          vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
-                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
-                          epsilon,     do_wstacking,    flags};
-        wstack::VisExtra &x = in.x;
-        x.vps = vis_pol_stride;
-        x.npv = npol_vis;
-        x.wgt_f64 = wgt_dtype == SDP_HIP_F64;
-        x.flags = vis_flags;
-        x.fbytes = vis_flags ? flag_bytes : 0;
-        x.frs = flag_row_stride;
-        x.fcs = flag_chan_stride;
-        x.fps = flag_pol_stride;
-        x.fpol = pol;
-        x.sumwt = sumwt;
-        if (shift_lmn) {
-            x.shift = true;
-            x.sl = shift_lmn[0];
-            x.sm = shift_lmn[1];
-            x.sn = shift_lmn[2];
-        }
-        if (pol_coeff) {
-            x.conv = true;
-            for (int k = 0; k < npol_vis; ++k) {
-                x.cre[k] = pol_coeff[2 * k];
-                x.cim[k] = pol_coeff[2 * k + 1];
-            }
-        } else if (vis) {
-            // no conversion: the image pol is the vis pol `pol`
-            in.vis = static_cast<const char *>(vis) +
-                     pol * vis_pol_stride * (vis_dtype == SDP_HIP_C128 ? 16 : 8);
-        }
-        wstack::ms2dirty(in, dirty, dirty_stride_x, dirty_stride_y, info, as_stream(stream));
-    });
+    return ms2dirty_vis_entry(uvw, uvw_row_stride, freq, nchan, nrow, vis, vis_dtype,
+                              vis_row_stride, vis_chan_stride, vis_pol_stride, npol_vis, pol_coeff,
+                              wgt, wgt_dtype, wgt_row_stride, wgt_chan_stride, vis_flags,
+                              flag_bytes, flag_row_stride, flag_chan_stride, flag_pol_stride, pol,
+                              npix_x, npix_y, pixsize_x, pixsize_y, epsilon, do_wstacking,
+                              flags & ~(SDP_HIP_BATCH_FIRST | SDP_HIP_BATCH_LAST), nullptr, dirty,
+                              dirty_stride_x, dirty_stride_y, sumwt, shift_lmn, stream, info,
+                              errbuf, errbuf_len);
+}
+
+int sdp_hip_ms2dirty_vis_batch(const double *uvw, int64_t uvw_row_stride, const double *freq,
+                               int nchan, int64_t nrow, const void *vis, int vis_dtype,
+                               int64_t vis_row_stride, int64_t vis_chan_stride,
+                               int64_t vis_pol_stride, int npol_vis, const double *pol_coeff,
+                               const void *wgt, int wgt_dtype, int64_t wgt_row_stride,
+                               int64_t wgt_chan_stride, const void *vis_flags, int flag_bytes,
+                               int64_t flag_row_stride, int64_t flag_chan_stride,
+                               int64_t flag_pol_stride, int pol, int npix_x, int npix_y,
+                               double pixsize_x, double pixsize_y, double epsilon,
+                               int do_wstacking, unsigned flags, const double *bounds,
+                               double *dirty, int64_t dirty_stride_x, int64_t dirty_stride_y,
+                               double *sumwt, const double *shift_lmn, void *stream,
+                               sdp_hip_wgrid_info *info, char *errbuf, size_t errbuf_len) {
+    if (bounds == nullptr) {
+        if (errbuf && errbuf_len) std::snprintf(errbuf, errbuf_len, "null pointer argument");
+        return SDP_HIP_ERR_INVALID_ARG;
+    }
+    return ms2dirty_vis_entry(uvw, uvw_row_stride, freq, nchan, nrow, vis, vis_dtype,
+                              vis_row_stride, vis_chan_stride, vis_pol_stride, npol_vis, pol_coeff,
+                              wgt, wgt_dtype, wgt_row_stride, wgt_chan_stride, vis_flags,
+                              flag_bytes, flag_row_stride, flag_chan_stride, flag_pol_stride, pol,
+                              npix_x, npix_y, pixsize_x, pixsize_y, epsilon, do_wstacking, flags,
+                              bounds, dirty, dirty_stride_x, dirty_stride_y, sumwt, shift_lmn,
+                              stream, info, errbuf, errbuf_len);
 }
 
 int sdp_hip_dirty2ms(const double *uvw, int64_t uvw_row_stride, const double *freq, int nchan,

@@ -106,6 +106,17 @@ SIGNATURES = {
         c_vp, c_i64, c_i64, c_vp,                 # dirty, strides, sumwt
         c_vp,                                     # shift_lmn (host doubles) or NULL
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
+    "sdp_hip_ms2dirty_vis_batch": [
+        c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
+        c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # vis, dtype, row/chan/pol strides, npol_vis
+        c_vp,                                     # pol_coeff (host doubles) or NULL
+        c_vp, c_int, c_i64, c_i64,                # wgt, dtype, strides
+        c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # flags, bytes, strides, pol
+        c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,
+        c_vp,                                     # bounds (host, 6 doubles)
+        c_vp, c_i64, c_i64, c_vp,                 # dirty, strides, sumwt
+        c_vp,                                     # shift_lmn (host doubles) or NULL
+        c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_dirty2ms": [
         c_vp, c_i64, c_vp, c_int, c_i64,
         c_vp, c_i64, c_i64, c_int, c_int, c_dbl, c_dbl,

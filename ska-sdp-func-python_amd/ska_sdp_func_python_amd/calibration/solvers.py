@@ -24,8 +24,11 @@ the reference's) or SDP_HIP_SHARD=1: with torch.distributed initialised
 checked first) each rank forms the sums and solves a contiguous block of the
 gain rows, with no collective in the solve; one all-gather assembles the
 table on every rank, and the mean/median normalisation (:135-143) then runs
-over the whole table as in the reference.  By default every rank solves its
-own call.
+over the whole table as in the reference.  With ``shard="local"`` every rank
+passes its own visibilities (its times) and gets its own rows of the table;
+the normalisation is taken over all the ranks' rows (one all-reduce for the
+mean, an all-gather of |g| for the median).  By default every rank solves
+its own call.
 """
 
 import logging
@@ -97,6 +100,10 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
     parallel.check_replicated(sh, [v, m, w, np.asarray(vis.time.data, dtype=float),
                                   tuple(gain_table["gain"].data.shape)],
                               "solve_gaintable")
+    # shard="local": each rank solves the gain table of its OWN visibilities
+    # (its time rows); only the mean / median normalisation spans the ranks
+    loc = parallel.local_info({"shard": shard})
+    parallel.check_replicated(loc, [(nants, nchan, npol)], "solve_gaintable(shard='local')")
     rblocks = [(0, nrow_g)]
     r0, r1 = 0, nrow_g
     if sh:
@@ -175,7 +182,11 @@ def solve_gaintable(vis, modelvis=None, gain_table=None, phase_only=True, niter=
         gwt = parallel.gather_blocks(gwt, rblocks, sh[0], dim=0, group=sh[2])
         residual = parallel.gather_blocks(residual, rblocks, sh[0], dim=0, group=sh[2])
 
-    if normalise_gains in ["median", "mean"] and not phase_only:
+    if normalise_gains in ["median", "mean"] and not phase_only and loc:
+        # the reference normalises over its whole table (solvers.py:135-143):
+        # here the table is every rank's rows
+        gain = parallel.normalise_gains_global(gain, normalise_gains, loc[2])
+    elif normalise_gains in ["median", "mean"] and not phase_only:
         ga = gain.abs().flatten()
         if normalise_gains == "median":
             # numpy median (mean of the two middle values for even counts),

@@ -36,6 +36,17 @@ a channel block at the top of a wide band holds them all; SDP_HIP_SHARD=chan
 keeps channel blocks); predict_ng predicts its block and all-gathers the
 channel blocks.  Every rank returns
 the reference's full result.
+
+Pre-sharded mode, ``shard="local"`` (or SDP_HIP_SHARD=local): every rank
+passes its OWN block of one observation -- its channels, or its rows (e.g.
+an interval of w from parallel.wrow_partition) -- and only the image
+geometry is checked to agree.  invert_ng grids the rank's block and
+all-reduces the partial image and weight sums before normalise_sumwt
+(ng.py:288-292), so every rank returns the whole observation's image;
+predict_ng predicts the rank's block with no exchange.  A block larger than
+one NUFFT call holds (SDP_HIP_MAX_CALL_GVIS, default 1.8 Gvis) is gridded in
+channel batches through one set of resident w planes
+(sdp_hip_ms2dirty_vis_batch).
 Kwargs ``epsilon`` (default 1e-12), ``do_wstacking`` (True), ``threads``
 and ``verbosity`` are accepted as in the reference; ``threads`` is ignored
 (one GPU per process).  epsilon < 1e-7 runs the fp64 NUFFT (as ducc0 with
@@ -72,6 +83,14 @@ def _channel_runs(vis_to_im, lo, hi):
         else:
             runs.append([ichan, v, v + 1])
     return [tuple(r) for r in runs]
+
+
+def _image_geometry(model):
+    """What every rank of a shard="local" call must agree on: the image shape
+    and its WCS (reference pixels, increments, values)."""
+    w = model.image_acc.wcs.wcs
+    return [tuple(model["pixels"].data.shape), np.asarray(w.crpix, dtype=float),
+            np.asarray(w.cdelt, dtype=float), np.asarray(w.crval, dtype=float)]
 
 
 def _pixsize(model):
@@ -121,6 +140,11 @@ def predict_ng(bvis, model, **kwargs):
     uvw = torch.nan_to_num(uvw).contiguous()
     shard = parallel.shard_info(kwargs)
     parallel.check_replicated(shard, [uvw, freq, model["pixels"].data], "predict_ng")
+    # shard="local": each rank predicts its own block, no exchange; the model
+    # must be the same on every rank
+    loc = parallel.local_info(kwargs)
+    parallel.check_replicated(loc, _image_geometry(model) + [model["pixels"].data],
+                              "predict_ng(shard='local')")
     blocks = [(0, vnchan)]
     lo, hi = 0, vnchan
     if shard:
@@ -202,6 +226,7 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     nchan, npol, ny, nx = model["pixels"].data.shape
     image = torch.zeros((nchan, npol, ny, nx), dtype=torch.float64, device=dev)
     shard = parallel.shard_info(kwargs)
+    loc = parallel.local_info(kwargs)
     # the reference's deep copy + zero fill (ng.py:173, :218) without
     # copying the model's pixels
     im = model.copy(deep=True, data=image)
@@ -219,6 +244,9 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     parallel.check_replicated(
         shard, [uvw, freq, sbvis.imaging_weight.data, None if dopsf else sbvis.vis.data,
                 model["pixels"].data.shape], "invert_ng")
+    # shard="local": each rank passes its own block; only the image geometry
+    # must agree across the ranks
+    parallel.check_replicated(loc, _image_geometry(model), "invert_ng(shard='local')")
     rows = None
     if shard and mfs and do_wstacking and parallel.shard_mode() != "chan":
         rows = _rank_rows(uvw, freq, nx, _pixsize(im), epsilon, precision, shard)
@@ -270,12 +298,29 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     # (ng.py:259-289); the sum is linear in the visibilities, so a run's
     # channels grid as one call into the same image and weight sum (C2 as a
     # 16-channel cube: 16 calls of 4 channels instead of 64 of one).
+    nrow_loc = uvw.shape[0]
     if mfs:
         calls = [(pol, slice(0, nloc), 0) for pol in range(npol if nloc > 0 else 0)]
     else:
         calls = [(pol, slice(a - lo, b - lo), ichan)
                  for ichan, a, b in _channel_runs(vis_to_im, lo, hi) for pol in range(npol)]
+    if nrow_loc == 0:
+        calls = []  # (a rank with no rows: its share of the exchange is zeros)
     grid_calls = [c for c in calls if not (dopsf and c[0] != 0)]
+    # A call over more visibilities than one NUFFT call holds (records,
+    # 2^32 limit: SDP_HIP_MAX_CALL_GVIS, default 1.8 Gvis -- a C4 rank's
+    # block) grids its channels in batches through one set of resident w
+    # planes (sdp_hip_ms2dirty_vis_batch); the reference makes one ducc0 call
+    # over all channels (ng.py:240-256).
+    max_call = max(1, int(float(os.environ.get("SDP_HIP_MAX_CALL_GVIS", "1.8")) * 1e9))
+
+    def batches(chans):
+        n = chans.stop - chans.start
+        nb = min(n, max(1, -(-nrow_loc * n // max_call)))
+        cuts = [chans.start + n * i // nb for i in range(nb + 1)]
+        return [slice(a, e) for a, e in zip(cuts[:-1], cuts[1:])]
+
+    batched = any(len(batches(c[1])) > 1 for c in grid_calls)
     # The pols of one image channel share one bucketing: the first pol keeps
     # it, the others re-run only the value pass (SDP_HIP_KEEP_BUCKETS /
     # SDP_HIP_REUSE_BUCKETS; C2 4 pols 54.0 ms against 59.7 pipelined, bench
@@ -286,8 +331,8 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     # by the call's position: the image and weight-sum accumulation is a
     # plain read-modify-write, so every call into one target stays on one
     # stream.  SDP_HIP_OVERLAP=0 keeps every call on one stream.
-    share = npol > 1 and not dopsf
-    overlap = len(grid_calls) > 1 and not share and dev.type == "cuda" and \
+    share = npol > 1 and not dopsf and not batched
+    overlap = len(grid_calls) > 1 and not share and not batched and dev.type == "cuda" and \
         os.environ.get("SDP_HIP_OVERLAP", "1") != "0"
     main = torch.cuda.current_stream(dev) if overlap else None
     side = _side_stream(dev) if overlap else None
@@ -308,25 +353,33 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
         coef = None if (dopsf or conv is None) else conv[pol]
         lane = lane_of[(ichan, pol)] if overlap else 0
         ctx = torch.cuda.stream(side if lane else main) if overlap else contextlib.nullcontext()
+        parts = batches(chans)
+        seq = {}
+        if len(parts) > 1:
+            seq = {"bounds": kernels.uvw_bounds(uvw, freq_t[chans])}
         with ctx:
-            _, info = kernels.ms2dirty_vis(
-                uvw, freq_t[chans], None if dopsf else ms[:, chans, :], pol, wgt[:, chans, pol],
-                flags[:, chans, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
-                do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
-                accumulate=True, sumwt=sw, shift_lmn=lmn, keep_buckets=share and first_pol,
-                reuse_buckets=share and not first_pol, precision=precision, slot=lane)
-        if verbosity:
-            log.info("invert_ng: %s", info)
+            for i, part in enumerate(parts):
+                if seq:
+                    seq.update(first=i == 0, last=i == len(parts) - 1)
+                _, info = kernels.ms2dirty_vis(
+                    uvw, freq_t[part], None if dopsf else ms[:, part, :], pol, wgt[:, part, pol],
+                    flags[:, part, :], coef, npixdirty, npixdirty, pixsize, pixsize, epsilon,
+                    do_wstacking, flip_uw=True, out=image[ichan, pol], out_strides=(1, nx),
+                    accumulate=True, sumwt=sw, shift_lmn=lmn, keep_buckets=share and first_pol,
+                    reuse_buckets=share and not first_pol, precision=precision, slot=lane, **seq)
+                if verbosity:
+                    log.info("invert_ng: %s", info)
 
     for pol, chans, ichan in calls:
         grid_pol(pol, chans, ichan, pol == 0)
     if overlap:
         main.wait_stream(side)
-    if shard:
+    if shard or loc:
         # the one exchange: partial images and weight sums of the ranks'
-        # channel blocks (before normalise_sumwt, ng.py:292)
-        parallel.all_reduce_sum(image, shard[2])
-        parallel.all_reduce_sum(sumwt_d, shard[2])
+        # blocks (before normalise_sumwt, ng.py:292)
+        grp = (shard or loc)[2]
+        parallel.all_reduce_sum(image, grp)
+        parallel.all_reduce_sum(sumwt_d, grp)
     sumwt = sumwt_d.cpu().numpy()
 
     im["pixels"].data = image

@@ -266,7 +266,8 @@ _FLAG_DT = {torch.int64: 8, torch.int32: 4, torch.int8: 1, torch.uint8: 1, torch
 def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_x, pixsize_y,
                  epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None, out_strides=None,
                  accumulate=False, sumwt=None, shift_lmn=None, keep_buckets=False,
-                 reuse_buckets=False, precision=None, slot=0):
+                 reuse_buckets=False, precision=None, slot=0, bounds=None, first=False,
+                 last=False):
     """ms2dirty with invert_ng's visibility prologue fused in
     (sdp_hip_ms2dirty_vis): ``vis`` [nrow, nchan, npol_vis] complex (any
     strides, read in place; None = unit visibilities), ``flags`` the same
@@ -280,7 +281,12 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
     freq and geometry (another image pol) runs only the value pass, gridding
     and FFT (SDP_HIP_KEEP_BUCKETS / SDP_HIP_REUSE_BUCKETS).  ``slot=1`` uses
     the library's second scratch set (SDP_HIP_SLOT1; not with kept / reused
-    buckets): calls alternated between two streams and slots overlap."""
+    buckets): calls alternated between two streams and slots overlap.
+
+    ``bounds`` (uvw_bounds / merge_bounds of the whole sequence) makes the
+    call one batch of a sequence sharing one set of resident w planes
+    (sdp_hip_ms2dirty_vis_batch, as ms2dirty_batch): ``first`` zeroes them,
+    ``last`` transforms them into ``out``."""
     pbits = _prec_bits(epsilon, precision)
     _check_uvw(uvw)
     dev = uvw.device
@@ -325,8 +331,17 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
     bits |= (_lib.SDP_HIP_KEEP_BUCKETS if keep_buckets else 0) | \
         (_lib.SDP_HIP_REUSE_BUCKETS if reuse_buckets else 0) | (_lib.SDP_HIP_SLOT1 if slot else 0)
     info = _lib.WGridInfo()
+    batch = ()
+    name = "sdp_hip_ms2dirty_vis"
+    if bounds is not None:
+        if len(bounds) != 6:
+            raise ValueError("bounds: {wmin, wmax, umax, vmax, fmin, fmax}")
+        bits |= (_lib.SDP_HIP_BATCH_FIRST if first else 0) | (_lib.SDP_HIP_BATCH_LAST if last else 0)
+        bbuf = (ctypes.c_double * 6)(*[float(x) for x in bounds])
+        batch = (ctypes.cast(bbuf, ctypes.c_void_p),)
+        name = "sdp_hip_ms2dirty_vis_batch"
     _lib.call(
-        "sdp_hip_ms2dirty_vis",
+        name,
         _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
         _ptr(vis), _DT_CODE[vis.dtype] if vis is not None else _lib.SDP_HIP_C64,
         *(vis.stride() if vis is not None else (0, 0, 0)), npv,
@@ -336,7 +351,7 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
         _ptr(flags), _FLAG_DT[flags.dtype] if flags is not None else 0,
         *(flags.stride() if flags is not None else (0, 0, 0)), int(pol),
         int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
-        int(bool(do_wstacking)), bits,
+        int(bool(do_wstacking)), bits, *batch,
         _ptr(out), int(out_strides[0]), int(out_strides[1]), _ptr(sumwt), _host3(shift_lmn),
         _stream(dev), ctypes.byref(info))
     return out, info.as_dict()

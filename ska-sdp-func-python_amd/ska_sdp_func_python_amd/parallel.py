@@ -40,15 +40,41 @@ def shard_info(kwargs=None):
     import os
     want = None if kwargs is None else kwargs.get("shard")
     if want is None:
-        want = os.environ.get("SDP_HIP_SHARD", "0") not in ("", "0")
-    if not want:
+        env = os.environ.get("SDP_HIP_SHARD", "0")
+        want = env not in ("", "0", "local")
+    if not want or want == "local":
         return None
+    return _group_info()
+
+
+def _group_info():
     if not (dist.is_available() and dist.is_initialized()):
         return None
     world = dist.get_world_size()
     if world <= 1:
         return None
     return dist.get_rank(), world, None
+
+
+def local_info(kwargs=None):
+    """(rank, world, group) for the PRE-SHARDED mode, ``shard="local"`` (or
+    SDP_HIP_SHARD=local), with torch.distributed initialised over more than
+    one rank: every rank passes its OWN block of one observation (its
+    channels, or its rows -- e.g. an interval of w, wrow_partition) and the
+    calls combine the blocks at the reference's exchange points: invert_ng
+    all-reduces the partial images and weight sums before normalise_sumwt
+    (ng.py:288-292); predict_ng predicts each block with no exchange;
+    solve_gaintable solves each rank's gain rows and normalises the gains
+    over the whole table (solvers.py:135-143).  Nothing is replicated, so the
+    visibilities of a band too large for one GPU (C4: 13.4 Gvis) never sit on
+    one device.  None otherwise."""
+    import os
+    want = None if kwargs is None else kwargs.get("shard")
+    if want is None:
+        want = os.environ.get("SDP_HIP_SHARD", "0")
+    if want != "local":
+        return None
+    return _group_info()
 
 
 _HASH_CHUNK = 1 << 24  # bytes hashed per step (bounds the temporaries)
@@ -138,9 +164,9 @@ def check_replicated(shard, arrays, what):
         dist.all_reduce(lo, op=dist.ReduceOp.MAX, group=shard[2])
         same = bool(torch.equal(hi, -lo))
     if not same:
-        raise ValueError(f"{what}: shard=True needs the same inputs on every rank (the ranks "
-                         "passed different visibilities, models or tables); call without "
-                         "sharding to process each rank's own data")
+        raise ValueError(f"{what}: sharding needs the same inputs on every rank (the ranks "
+                         "passed different visibilities, models, tables or image geometries); "
+                         "call without sharding to process each rank's own data")
 
 
 def _host_staged(group, t):

@@ -28,11 +28,17 @@ SEEN = set()  # visibility channels (frequencies) this process computed
 ROWS = set()  # rows (their u) this process gridded
 
 
+BATCHES = []  # (first, last) of every batched call this process made
+
+
 def _oracle_ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, px, py,
                          epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None,
                          out_strides=None, accumulate=False, sumwt=None, shift_lmn=None,
-                         keep_buckets=False, reuse_buckets=False, precision=None, slot=0):
+                         keep_buckets=False, reuse_buckets=False, precision=None, slot=0,
+                         bounds=None, first=False, last=False):
     assert shift_lmn is None
+    if bounds is not None:
+        BATCHES.append((first, last))
     SEEN.update(freq.numpy().tolist())
     ROWS.update(np.round(uvw.numpy()[:, 0], 6).tolist())
     m = 1.0 - flags.numpy().astype(float)
@@ -69,11 +75,17 @@ def _oracle_dirty2ms_vis(uvw, freq, dirty, out, coef, px, py, epsilon=1e-7, do_w
     return out, {}
 
 
+def _host_bounds(uvw, freq):
+    return [float(uvw[:, 2].min()), float(uvw[:, 2].max()), float(uvw[:, 0].abs().max()),
+            float(uvw[:, 1].abs().max()), float(freq.min()), float(freq.max())]
+
+
 def _patch():
     from ska_sdp_func_python_amd import _device, kernels
     _device.device = lambda: torch.device("cpu")
     kernels.ms2dirty_vis = _oracle_ms2dirty_vis
     kernels.dirty2ms_vis = _oracle_dirty2ms_vis
+    kernels.uvw_bounds = _host_bounds
 
 
 def _case(kind, seed=51):
@@ -237,3 +249,76 @@ def test_byte_hash_matches_between_host_and_torch():
         finally:
             parallel._HASH_CHUNK = old
     assert parallel._byte_hash(np.array([1.0, 2.0])) != parallel._byte_hash(np.array([2.0, 1.0]))
+
+
+def _local_worker(rank, world, port, kind, q, max_call=None):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if max_call:
+        os.environ["SDP_HIP_MAX_CALL_GVIS"] = max_call
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _patch()
+    try:
+        q.put((rank, _run_local(kind, rank, world), sorted(SEEN), sorted(ROWS), list(BATCHES)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _block(vis, rank, world, by):
+    """This rank's own Visibility: its time rows or its channels."""
+    from gpu_helpers import vis_from_arrays
+    nt, _, nchan, _ = vis.vis.data.shape
+    t = slice(rank * nt // world, (rank + 1) * nt // world) if by == "rows" else slice(0, nt)
+    c = slice(rank * nchan // world, (rank + 1) * nchan // world) if by == "chans" else slice(0, nchan)
+    b = vis_from_arrays(np.asarray(vis.uvw.data)[t], np.asarray(vis.frequency.data)[c],
+                        np.asarray(vis.vis.data)[t, :, c], weight=np.asarray(vis.weight.data)[t, :, c],
+                        flags=np.asarray(vis.flags.data)[t, :, c], phasecentre=vis.phasecentre)
+    b["imaging_weight"] = np.asarray(vis.imaging_weight.data)[t, :, c]
+    return b, t, c
+
+
+def _run_local(kind, rank, world):
+    from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng
+    base = {"invert_rows": "invert_mfs", "invert_chans": "invert_cube", "predict_chans": "predict"}
+    vis, im = _case(base[kind])
+    mine, t, c = _block(vis, rank, world, kind.split("_")[1])
+    if kind == "predict_chans":
+        return np.asarray(predict_ng(mine, im, shard="local").vis.data), (t.start, t.stop, c.start, c.stop)
+    d, sw = invert_ng(mine, im, normalise=True, shard="local")
+    return np.asarray(d["pixels"].data), np.asarray(sw)
+
+
+@pytest.mark.parametrize("kind", ["invert_rows", "invert_chans", "predict_chans"])
+@pytest.mark.parametrize("max_call", [None, "1e-8"])
+def test_presharded_local_mode(kind, max_call, monkeypatch):
+    """shard="local": each rank passes its OWN block of the observation (its
+    time rows, or its channels); invert_ng all-reduces the partial images
+    and weight sums, so both ranks return the whole observation's image;
+    predict_ng predicts each block with no exchange.  With
+    SDP_HIP_MAX_CALL_GVIS tiny, the rank's calls run as channel-batch
+    sequences (first ... last) through sdp_hip_ms2dirty_vis_batch."""
+    from ska_sdp_func_python_amd import _device, kernels
+    monkeypatch.setattr(_device, "device", lambda: torch.device("cpu"))
+    monkeypatch.setattr(kernels, "ms2dirty_vis", _oracle_ms2dirty_vis)
+    monkeypatch.setattr(kernels, "dirty2ms_vis", _oracle_dirty2ms_vis)
+    ref = _run({"invert_rows": "invert_mfs", "invert_chans": "invert_cube",
+                "predict_chans": "predict"}[kind])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + int(np.random.default_rng().integers(600, 900))
+    procs = [ctx.Process(target=_local_worker, args=(r, 2, port, kind, q, max_call))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, out, seen, rows, batches in res:
+        if max_call and kind == "invert_rows":  # (the cube: one channel per call)
+            assert batches and batches[0] == (True, False) and batches[-1] == (False, True)
+        if kind == "predict_chans":
+            t0, t1, c0, c1 = out[1]
+            np.testing.assert_allclose(out[0], ref[0][t0:t1, :, c0:c1], rtol=1e-10, atol=1e-12)
+        else:
+            for a, b in zip(out, ref):
+                np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)

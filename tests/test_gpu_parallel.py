@@ -130,11 +130,37 @@ def _api_worker(rank, world, port, q):
         gt0 = solve_gaintable(copy_vis(cv), phase_only=False, normalise_gains="mean",
                               jones_type="B", shard=False)
         e_gain = float(np.max(np.abs(np.asarray(gt1["gain"].data) - np.asarray(gt0["gain"].data))))
-        q.put((rank, e_inv, e_sw, e_pred, e_gain, None))
+        # shard="local": each rank passes its OWN time block; invert_ng's
+        # calls split into channel batches (sdp_hip_ms2dirty_vis_batch) by a
+        # tiny per-call limit; predict_ng needs no exchange; the gains are
+        # normalised over both ranks' rows
+        t0, t1 = rank * 3, rank * 3 + 3
+        os.environ["SDP_HIP_MAX_CALL_GVIS"] = "2e-6"
+        try:
+            dl, sl = invert_ng(_time_block(vis, t0, t1), im, shard="local", verbosity=1)
+        finally:
+            os.environ.pop("SDP_HIP_MAX_CALL_GVIS")
+        e_linv = rel_rms(dl["pixels"].data, d0["pixels"].data)
+        e_lsw = float(np.max(np.abs(np.asarray(sl) - np.asarray(s0)) / np.abs(np.asarray(s0))))
+        pl = predict_ng(_time_block(vis, t0, t1), model, shard="local").vis.data
+        e_lpred = rel_rms(pl, np.asarray(p0)[t0:t1])
+        g0, g1 = (0, 3) if rank == 0 else (3, 5)
+        gl = solve_gaintable(_time_block(cv, g0, g1), phase_only=False, normalise_gains="mean",
+                             jones_type="B", shard="local")
+        e_lgain = float(np.max(np.abs(np.asarray(gl["gain"].data)
+                                      - np.asarray(gt0["gain"].data)[g0:g1])))
+        q.put((rank, e_inv, e_sw, e_pred, e_gain, (e_linv, e_lsw, e_lpred, e_lgain), None))
     except Exception as exc:  # report, do not hang the parent
-        q.put((rank, None, None, None, None, repr(exc)))
+        q.put((rank, None, None, None, None, None, repr(exc)))
     finally:
         dist.destroy_process_group()
+
+
+def _time_block(vis, t0, t1):
+    """Times [t0, t1) of a Visibility as its own Visibility (a rank's block)."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    rep = {k: vis._vars[k][t0:t1] for k in dm._TIME_VARS if k in vis._vars}
+    return vis._copy_with(deep=True, replace=rep)
 
 
 def copy_vis(v):
@@ -159,8 +185,10 @@ def test_api_sharding_two_ranks_one_gpu():
     res = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    for rank, e_inv, e_sw, e_pred, e_gain, err in res:
+    for rank, e_inv, e_sw, e_pred, e_gain, loc, err in res:
         assert err is None, err
         print(f"\nrank {rank}: invert {e_inv:.2e}, sumwt {e_sw:.1e}, predict {e_pred:.2e}, "
-              f"gains {e_gain:.1e}")
+              f"gains {e_gain:.1e}; shard='local' (own time block): invert {loc[0]:.2e}, "
+              f"sumwt {loc[1]:.1e}, predict {loc[2]:.2e}, gains {loc[3]:.1e}")
         assert e_inv < 1e-5 and e_sw < 1e-12 and e_pred < 1e-5 and e_gain < 1e-9
+        assert loc[0] < 1e-8 and loc[1] < 1e-12 and loc[2] < 1e-8 and loc[3] < 1e-9
