@@ -255,7 +255,8 @@ def api_rates(args, obs, cell):
     r4 = both(b4, m4)
     del b4, d4, v4
     torch.cuda.empty_cache()
-    # a 16-channel cube (stokesI; 64 NUFFT calls of one visibility channel)
+    # a 16-channel cube (stokesI; 4 visibility channels per image channel, one
+    # NUFFT call per image channel)
     dfc = float(freq[1] - freq[0])
     mc = dm.create_image(args.npix, cell, pc, frequency=float(freq[:4].mean()),
                          channel_bandwidth=4 * dfc, nchan=16)
@@ -277,7 +278,8 @@ def api_rates(args, obs, cell):
                         "figure includes the H2D copies of ~5 GB (PCIe-inclusive) and the image "
                         "D2H; 4pol: a linear-frame Visibility imaged to stokesIQUV (4 NUFFT "
                         "calls sharing one bucketing); cube16: 64 vis channels onto a 16-channel "
-                        "image (64 calls, pipelined over two streams); 'serial' = "
+                        "image (one call per image channel's run of 4 vis channels, 16 calls "
+                        "pipelined over two streams); 'serial' = "
                         "SDP_HIP_OVERLAP=0 (one stream)"})
     return out
 
