@@ -3246,9 +3246,16 @@ template <int W, bool WS>
 constexpr int f64m_ry() {
     return 8 + 15;
 }
+// region rows: each kx half of the waves owns a slab of the region, rows
+// x + kx of its own tiles (lower half KH + 1 rows, upper W - KH + 1; the row
+// where they meet is held twice and flushed from both)
+template <int W>
+constexpr int f64m_rows() {
+    return ((W + 1) / 2 + 1) + (W - (W + 1) / 2 + 1);
+}
 template <int W, bool WS>
 constexpr size_t grid_f64m_lds() {
-    return (size_t)(W + 1) * f64m_ry<W, WS>() * 2 * (WS ? W : 1) * sizeof(double) +
+    return (size_t)f64m_rows<W>() * f64m_ry<W, WS>() * 2 * (WS ? W : 1) * sizeof(double) +
            (size_t)kBlk64 * (3 * W + 2) * sizeof(double) + kPolyN * sizeof(double);
 }
 typedef double doublex4 __attribute__((ext_vector_type(4)));
@@ -3282,135 +3289,157 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
     const double *__restrict__ pc) {
     static_assert(W <= 16, "one M-tile of 16 rows per kx");
     constexpr int NQ = WS ? W : 1, NC = 2 * NQ, NT = f64m_ntiles<W, WS>(), NW = f64m_waves<W, WS>();
-    constexpr int RX = W + 1, RY = f64m_ry<W, WS>(), RS = RX * RY * NC;
+    constexpr int RX = f64m_rows<W>(), RY = f64m_ry<W, WS>(), RS = RX * RY * NC;
     constexpr int TR = 3 * W + 2, NTH = 64 * NW;
     constexpr int KH = (W + 1) / 2;  // kx M-tiles per wave
     extern __shared__ __attribute__((aligned(16))) double smd[];
-    double *const reg = smd;       // [RX][RY][NC]
+    double *const reg = smd;       // [RX][RY][NC]: the lower slab's rows, then the upper's
     double *const tap = smd + RS;  // [kBlk64][TR]
     double *const cl = tap + kBlk64 * TR;  // the tap polynomials
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const double ihw = 2.0 / W, beta = (double)g.beta;
     for (int i = threadIdx.x; i < kPolyN; i += NTH) cl[i] = pc[i];
     // wave (N-tile wv % NT, kx half wv / NT): 4 waves for W > 8 with
     // w-stacking, two per SIMD at two workgroups per CU
-    const int kx0 = (wv / NT) * KH, nkx = min(KH, W - kx0);
+    const int kx0 = (wv / NT) * KH;
     const int col = (wv % NT) * 16 + (lane & 15);
     const bool colok = col < NC;
     // B operand: tw[q] c[re/im] of record (lane >> 4); A: tu[kx] tv[ky]
     const int bq = 2 * W + (colok ? col >> 1 : 0), bc = 3 * W + (col & 1);
     const int ky = lane & 15;
-    const bool kyok = ky < W;
+    // rows ky >= W take A = 0: a clamped read times a 0 / 1 factor (no exec
+    // masking in the K-step)
+    const int kyc = min(ky, W - 1);
+    const double kym = ky < W ? 1.0 : 0.0;
     const int rk = lane >> 4;
+    const bool lower = kx0 == 0;  // this wave's kx tiles: KH (lower half) or W - KH
     // accumulator (k, i) = tap row (kx0 + k, rk + 4 i) of a cell at region
     // cell (cx, cy): element ((cx + kx0 + k) RY + cy + rk + 4 i) NC + col
-    const int lbase = kx0 * RY * NC + rk * NC + col;
+    // (the upper half's slab starts at row KH + 1 of reg: its row x + k is
+    // region row KH + x + k)
+    const int lbase = (kx0 == 0 ? 0 : (KH + 1) * RY * NC) + rk * NC + col;
     const size_t plane_elems = (size_t)g.ngx * g.ngy;
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        uint32_t bnd[kGroupCell];
-        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
-        if (it.b >= it.e) continue;
-        int ibase, jbase;
-        group_origin(g, (int)it.tile, ibase, jbase);
-        __syncthreads();  // the previous item's flush reads of the region
-        for (int i = threadIdx.x; i < RS; i += NTH) reg[i] = 0.0;
-        doublex4 acc[KH];
+    // the item loop on two code paths, the wave's kx tile count NK a
+    // compile-time constant on each (KH for the lower half, W - KH for the
+    // upper): a runtime guard `k < nkx` became an exec-mask branch around
+    // every MFMA, and a per-K-step branch between two tile counts gave the
+    // accumulators two register sets (24 v_mov_b64 per K-step); both paths
+    // meet the same barriers in the same order
+    auto run = [&](auto nk_tag) {
+        for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+            uint32_t bnd[kGroupCell];
+            const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
+            if (it.b >= it.e) continue;
+            int ibase, jbase;
+            group_origin(g, (int)it.tile, ibase, jbase);
+            __syncthreads();  // the previous item's flush reads of the region
+            for (int i = threadIdx.x; i < RS; i += NTH) reg[i] = 0.0;
+            doublex4 acc[KH];
 #pragma unroll
-        for (int k = 0; k < KH; ++k) acc[k] = doublex4{0.0, 0.0, 0.0, 0.0};
-        int cur = -1, cb = 0;
-        uint32_t cend = 0;  // end of the current cell's records
-        auto store_cell = [&]() {
-            if (colok) {
-                double *d = reg + cb + lbase;
+            for (int k = 0; k < KH; ++k) acc[k] = doublex4{0.0, 0.0, 0.0, 0.0};
+            int cur = -1, cb = 0;
+            uint32_t cend = 0;  // end of the current cell's records
+            auto store_n = [&](auto nt) {
+                constexpr int NK = decltype(nt)::value;
+                if (colok) {
+                    double *d = reg + cb + lbase;
 #pragma unroll
-                for (int k = 0; k < KH; ++k)
-                    if (k < nkx) {
+                    for (int k = 0; k < NK; ++k)
 #pragma unroll
                         for (int i = 0; i < 4; ++i) d[k * RY * NC + 4 * i * NC] = acc[k][i];
-                    }
-            }
-        };
-        auto load_cell = [&](int cell) {
-            cb = ((cell & 1) * RY + (cell >> 1)) * NC;
-            const double *s = reg + cb + lbase;
+                }
+            };
+            auto load_n = [&](auto nt) {
+                constexpr int NK = decltype(nt)::value;
+                const double *s = reg + cb + lbase;
 #pragma unroll
-            for (int k = 0; k < KH; ++k)
-                if (k < nkx) {
+                for (int k = 0; k < NK; ++k)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) acc[k][i] = s[k * RY * NC + 4 * i * NC];
-                }
-        };
-        Stage64 nxt = stage64_load(recs, it.b, (int)min((uint32_t)kBlk64, it.e - it.b), lane);
-        for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlk64) {
-            __syncthreads();  // the region zeroing / previous block's tap reads
-            const int nb = (int)min((uint32_t)kBlk64, it.e - b0);  // (a multiple of 4)
-            stage64_part<W, WS, NW>(wv, nxt, nb, tap, cl, ihw, beta, lane);
-            // the next block's records, in flight during this block's K-steps
-            if (b0 + kBlk64 < it.e)
-                nxt = stage64_load(recs, b0 + kBlk64, (int)min((uint32_t)kBlk64, it.e - b0 - kBlk64),
-                                   lane);
-            __syncthreads();
-            // (K-steps not unrolled: unrolled, the register allocator gave
-            // the accumulators two register sets and copied all 104 doubles
-            // on every K-step without a cell change, behind the MFMAs)
-#pragma unroll 1
-            for (int kk = 0; kk < kBlk64 / 4; ++kk) {
-                if (4 * kk >= nb) break;
-                const uint32_t ri = b0 + 4u * (uint32_t)kk;
-                // one scalar compare per K-step against the current cell's
-                // end; the 15 compares of the cell search only at a change
-                // (the compare chain per K-step was ~45 of the kernel's
-                // ~340 SALU per block and wave)
-                if (ri >= cend) {  // (workgroup-uniform)
-                    int cell = 0;
-                    uint32_t e = bnd[kGroupCell - 1];
-#pragma unroll
-                    for (int c = 0; c < kGroupCell - 1; ++c) {
-                        cell += ri >= bnd[c] ? 1 : 0;
-                        e = (ri < bnd[c] && bnd[c] < e) ? bnd[c] : e;
-                    }
-                    cend = e;
-                    if (cur >= 0) store_cell();
-                    // the two kx halves of one column tile touch the same
-                    // region cells from neighbouring cells' footprints: every
-                    // wave's stores land before any wave loads the next cell
-                    if (NW > NT) __syncthreads();
-                    cur = cell;
-                    load_cell(cur);
-                }
-                const double *T = tap + (4 * kk + rk) * TR;
+            };
+            auto store_cell = [&]() { store_n(nk_tag); };
+            auto load_cell = [&](int cell) {
+                cb = ((cell & 1) * RY + (cell >> 1)) * NC;
+                load_n(nk_tag);
+            };
+            auto kstep = [&](auto nt, const double *T) {
+                constexpr int NK = decltype(nt)::value;
                 const double bop = T[bq] * T[bc];
-                const double tv = kyok ? T[W + ky] : 0.0;
-                double aop[KH];
+                const double tv = T[W + kyc] * kym;
+                double aop[NK];
 #pragma unroll
-                for (int k = 0; k < KH; ++k) aop[k] = T[kx0 + k] * tv;
+                for (int k = 0; k < NK; ++k) aop[k] = T[kx0 + k] * tv;
 #pragma unroll
-                for (int k = 0; k < KH; ++k)
-                    if (k < nkx)
-                        acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[k], bop, acc[k], 0, 0, 0);
+                for (int k = 0; k < NK; ++k)
+                    acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[k], bop, acc[k], 0, 0, 0);
+            };
+            Stage64 nxt = stage64_load(recs, it.b, (int)min((uint32_t)kBlk64, it.e - it.b), lane);
+            for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlk64) {
+                __syncthreads();  // the region zeroing / previous block's tap reads
+                const int nb = (int)min((uint32_t)kBlk64, it.e - b0);  // (a multiple of 4)
+                stage64_part<W, WS, NW>(wv, nxt, nb, tap, cl, ihw, beta, lane);
+                // the next block's records, in flight during this block's K-steps
+                if (b0 + kBlk64 < it.e)
+                    nxt = stage64_load(recs, b0 + kBlk64, (int)min((uint32_t)kBlk64, it.e - b0 - kBlk64),
+                                       lane);
+                __syncthreads();
+                // (K-steps not unrolled: unrolled, the register allocator gave
+                // the accumulators two register sets and copied all 104 doubles
+                // on every K-step without a cell change, behind the MFMAs)
+#pragma unroll 1
+                for (int kk = 0; kk < kBlk64 / 4; ++kk) {
+                    if (4 * kk >= nb) break;
+                    const uint32_t ri = b0 + 4u * (uint32_t)kk;
+                    // one scalar compare per K-step against the current cell's
+                    // end; the 15 compares of the cell search only at a change
+                    // (the compare chain per K-step was ~45 of the kernel's
+                    // ~340 SALU per block and wave)
+                    if (ri >= cend) {  // (workgroup-uniform)
+                        int cell = 0;
+                        uint32_t e = bnd[kGroupCell - 1];
+#pragma unroll
+                        for (int c = 0; c < kGroupCell - 1; ++c) {
+                            cell += ri >= bnd[c] ? 1 : 0;
+                            e = (ri < bnd[c] && bnd[c] < e) ? bnd[c] : e;
+                        }
+                        cend = e;
+                        if (cur >= 0) store_cell();
+                        // (no barrier: the two kx halves accumulate into slabs of
+                        // their own, and the two column tiles of a half touch
+                        // disjoint columns; a barrier here with the shared region
+                        // stopped all four waves at every cell change)
+                        cur = cell;
+                        load_cell(cur);
+                    }
+                    const double *T = tap + (4 * kk + rk) * TR;
+                    kstep(nk_tag, T);
+                }
+            }
+            if (cur >= 0) store_cell();
+            __syncthreads();
+            // flush in the planes' own order: consecutive lanes take consecutive
+            // doubles of one plane's region rows (re/im interleaved), so a wave's
+            // atomics cover a few contiguous segments
+            constexpr int RYV = 8 + W - 1;  // rows a footprint reaches
+            constexpr int FPP = RX * RYV * 2;  // doubles per plane of the region
+            for (int i = threadIdx.x; i < NQ * FPP; i += NTH) {
+                const int q = i / FPP, f = i - q * FPP, cell = f >> 1;
+                const int xl = cell / RYV, yl = cell - xl * RYV;
+                const double v = reg[(xl * RY + yl) * NC + 2 * q + (f & 1)];
+                const int p = (int)it.p0 + q;
+                if (v == 0.0 || p < p_lo || p >= p_hi) continue;
+                // slab row -> region row (the upper slab starts at KH)
+                int gx = ibase + (xl <= KH ? xl : xl - 1);
+                if (gx >= g.ngx) gx -= g.ngx;
+                int gy = jbase + yl;
+                if (gy >= g.ngy) gy -= g.ngy;
+                atomicAdd(grid + 2 * ((size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy) + (f & 1),
+                          v);
             }
         }
-        if (cur >= 0) store_cell();
-        __syncthreads();
-        // flush in the planes' own order: consecutive lanes take consecutive
-        // doubles of one plane's region rows (re/im interleaved), so a wave's
-        // atomics cover a few contiguous segments
-        constexpr int RYV = 8 + W - 1;  // rows a footprint reaches
-        constexpr int FPP = RX * RYV * 2;  // doubles per plane of the region
-        for (int i = threadIdx.x; i < NQ * FPP; i += NTH) {
-            const int q = i / FPP, f = i - q * FPP, cell = f >> 1;
-            const int xl = cell / RYV, yl = cell - xl * RYV;
-            const double v = reg[(xl * RY + yl) * NC + 2 * q + (f & 1)];
-            const int p = (int)it.p0 + q;
-            if (v == 0.0 || p < p_lo || p >= p_hi) continue;
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            atomicAdd(grid + 2 * ((size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy) + (f & 1),
-                      v);
-        }
-    }
+    };
+    if (lower) run(std::integral_constant<int, KH>{});
+    else run(std::integral_constant<int, W - KH>{});
 }
 
 // fp64 MFMA degridder (predict), the adjoint GEMM per block of <= 16
@@ -3453,6 +3482,9 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
     double *const tap = smd + RS + wv * kBlk64 * TR;  // this wave's tap block
     double *const cl = smd + RS + kDeg64Waves * kBlk64 * TR;  // the tap polynomials
     for (int i = threadIdx.x; i < kPolyN; i += NTH) cl[i] = pc[i];
+    // tap rows past a block's records are read (times 0) by its K-steps: they
+    // start finite
+    for (int i = threadIdx.x; i < kDeg64Waves * kBlk64 * TR; i += NTH) smd[RS + i] = 0.0;
     uint32_t *const bcel = reinterpret_cast<uint32_t *>(cl + kPolyN);  // block: cell | records << 8
     uint32_t *const btab = bcel + kMaxBlk64;                            // block: first record (+ count)
     const double ihw = 2.0 / W, beta = (double)g.beta;
@@ -3552,24 +3584,42 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
                 doublex4 acc[MT];
 #pragma unroll
                 for (int m = 0; m < MT; ++m) acc[m] = doublex4{0.0, 0.0, 0.0, 0.0};
+                // the four tv taps of this lane's K rows (the same for every
+                // kx), zero for rows ky >= W; lanes past the block's records
+                // take tu = 0 by a factor, not an exec-masked read
+                double tvk[4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int ky = 4 * s + gk;
+                    tvk[s] = ky < W ? T[W + min(ky, W - 1)] : 0.0;
+                }
+                const double rokf = rok ? 1.0 : 0.0;
                 // (kx not unrolled: unrolled, the compiler hoists every K-step's
-                // LDS reads to the top, 256 registers and scratch spills)
+                // LDS reads to the top, 256 registers and scratch spills); one
+                // kx's 4 MT A operands are all read before its MFMAs
 #pragma unroll 1
                 for (int kx = 0; kx < W; ++kx) {
-                    const double tu = rok ? T[kx] : 0.0;
+                    const double tu = T[kx] * rokf;
+                    double gvs[4][MT];
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const int ky = 4 * s + gk;
-                        const double tv = T[W + min(ky, W - 1)];
-                        const double bop = ky < W ? tu * tv : 0.0;
+                    for (int s = 0; s < 4; ++s)
 #pragma unroll
                         // (rows (q, re/im) >= NC read the next region cell's
                         // values: finite, and those rows of D are never used)
-                        for (int m = 0; m < MT; ++m) {
-                            const double gv = G[(kx * RY + 4 * s) * NC + 16 * m];
-                            acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv, bop, acc[m], 0, 0, 0);
-                        }
+                        for (int m = 0; m < MT; ++m) gvs[s][m] = G[(kx * RY + 4 * s) * NC + 16 * m];
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        const double bop = tu * tvk[s];
+#pragma unroll
+                        for (int m = 0; m < MT; ++m)
+                            acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(gvs[s][m], bop, acc[m], 0, 0, 0);
                     }
+                    // the LDS reads first, then the products, then the MFMAs
+                    // (left to itself the scheduler waited on each read right
+                    // before its MFMA)
+                    __builtin_amdgcn_sched_group_barrier(0x0100, 4 * MT + 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x0002, 5, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x0008, 4 * MT, 0);
                 }
                 // lane holds rows 16 m + gk + 4 i of column rn: (q, re/im) =
                 // ((16 m + gk + 4 i) >> 1, gk & 1)
