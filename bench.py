@@ -794,6 +794,33 @@ def run_c4_api(args, world, rank, local, dev, uvw, nrow, lo, hi, freqs, umax, ba
 C3_NCOMP, C3_NTIMES = 1000, 518   # 19,306 SKA-MID baselines x 518 times = 10.0 Mvis
 
 
+# k_dft's component loop (npol 1, c64 output; gfx950 ISA of csrc/dft.hip): per
+# component and wave64 one v_sin_f32 + one v_cos_f32 (8 issue cycles each,
+# MI355X_MICROARCH.md "vector-instruction ISSUE cost"), five fp64 VALU ops
+# (the phase u l + v m + w (n - 1): mul + 2 fma; rndne; add) and one cvt at 4
+# cycles, the complex multiply-accumulate as 4 packed-f32 ops (counted at 8)
+# and a v_mov (4): 76 issue cycles per 64 component-visibilities per SIMD.
+DFT_TRANS_CYC = 2 * 8
+DFT_ISSUE_CYC = DFT_TRANS_CYC + 5 * 4 + 4 + 4 * 8 + 4
+MI355X_SIMDS, MI355X_GHZ = 256 * 4, 2.4
+
+
+def _dft_issue_roofline(compvis, k_ms):
+    """The DFT against its binding pipe: the transcendental issue rate (two
+    per component-visibility) and the whole per-component issue count."""
+    rate = compvis / (k_ms * 1e-3)
+    lanes = MI355X_SIMDS * MI355X_GHZ * 1e9 * 64
+    trans_peak = lanes / DFT_TRANS_CYC  # component-visibilities / s if only sincos issued
+    issue_peak = lanes / DFT_ISSUE_CYC
+    return {"achieved": round(rate / 1e12, 3), "unit": "T comp*vis/s",
+            "sincos_peak": round(trans_peak / 1e12, 3),
+            "sincos_frac": round(rate / trans_peak, 4),
+            "issue_peak": round(issue_peak / 1e12, 3), "issue_frac": round(rate / issue_peak, 4),
+            "note": f"sincos: 2 transcendentals x 8 issue cycles per 64 comp*vis per SIMD; issue: "
+                    f"{DFT_ISSUE_CYC} cycles per component per wave64 from the k_dft ISA "
+                    f"(bench.py DFT_ISSUE_CYC), {MI355X_SIMDS} SIMDs at {MI355X_GHZ} GHz"}
+
+
 def run_c3(args, world, rank, dev, sub=False):
     """configs[2]: the point-component DFT (reference imaging/dft.py:135-183,
     dft_cpu_looped) of 1000 components onto 10.0 Mvis (one channel, stokesI,
@@ -881,7 +908,8 @@ def run_c3(args, world, rank, dev, sub=False):
                      "frac": round(flops / (k_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
                      "traffic": None, "kernel": "k_dft", "kernel_ms": round(k_ms, 4),
                      "note": "N_vis N_comp (6 + 8 npol) flops (SURVEY.md 8(d)), sincos excluded; "
-                             "MFMA does not apply (the contraction's N is npol = 1, DESIGN.md 3)"},
+                             "MFMA does not apply (the contraction's N is npol = 1, DESIGN.md 3)",
+                     "transcendental": _dft_issue_roofline(nvis_total * C3_NCOMP, k_ms)},
         "cpu_baseline": cpu,
     }
     if sub:
