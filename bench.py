@@ -304,6 +304,16 @@ def _timed_calls(fn, steps, warmup, dev):
     return el, infos[-1]
 
 
+def _traffic(name):
+    """PMC bytes per launch of a kernel from profiles/<name> (scripts/
+    pmc_traffic.sh), or None when no such measurement is committed."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("bytes_per_launch")
+
+
 def c2_predict_and_fp64(args, obs, cell, dev, cpu):
     """Two more C2 objects (SURVEY.md §8 a2 and the reference's default
     precision), each with its own roofline and CPU baseline:
@@ -360,7 +370,8 @@ def c2_predict_and_fp64(args, obs, cell, dev, cpu):
                                "w-stack grid, epsilon 1e-7 (W = 8)", "nplanes": info["nplanes"]},
         "stages_ms": {k: round(float(info[k]), 3) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": _traffic("traffic_k_degrid.json"),
                      "kernel": f"k_degrid_mfma<{info['support']},true>", "kernel_ms": round(kms, 4),
                      "alg_bytes_per_launch": int(alg / max(1, info["grid_launches"]))},
         "cpu_baseline": pcpu}
@@ -392,7 +403,8 @@ def c2_predict_and_fp64(args, obs, cell, dev, cpu):
                    "epsilon_requested": EPS_REFERENCE, "fp64": info["fp64"]},
         "stages_ms": {k: round(float(info[k]), 3) for k in ("ms_prep", "ms_grid", "ms_fft", "ms_screen")},
         "roofline": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": _traffic("traffic_k_grid_f64.json"),
                      "kernel": f"k_grid_f64_mfma<{W},true>", "kernel_ms": round(kms, 4),
                      "alg_bytes_per_launch": int(alg / max(1, info["grid_launches"])),
                      "compute": {"achieved": round(tfl, 2), "peak": FP64_PEAK_TFLOPS,
