@@ -1036,10 +1036,14 @@ __device__ __forceinline__ Item load_item(const Item *items, uint32_t w, uint32_
     return it;
 }
 
+// natural: item w itself -- the degridders only read the grid, so they visit
+// items in order and neighbouring items' overlapping regions are L2 hits (C2
+// k_degrid_mfma 5.55 -> 5.09 ms); the gridders keep the transposed order for
+// their atomics
 template <int NO>
 __device__ __forceinline__ Item load_fine_item(const FineItem *items, uint32_t w, uint32_t n,
-                                               uint32_t (&fo)[NO]) {
-    const FineItem raw = items[item_index(w, n)];
+                                               uint32_t (&fo)[NO], bool natural = false) {
+    const FineItem raw = items[natural ? w : item_index(w, n)];
     Item it;
     it.b = __builtin_amdgcn_readfirstlane(raw.b);
     it.e = __builtin_amdgcn_readfirstlane(raw.e);
@@ -1641,16 +1645,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 // 4 (s & 1) + k), k = lane >> 4.  The w taps then weight the rows:
 // V_r = sum_q tw_r[q] D[(q, .), r], a 4-lane-group reduction.  The 24 taps
 // of a record are evaluated once, 6 by each of its 4 lanes (lane group k:
-// tu 2k, 2k+1; tv k, k+4; tw 2k, 2k+1), the tu taps shared by ds_bpermute.
+// tu 2k, 2k+1; tv k, k+4; tw 2k, 2k+1), the tu taps shared by ds_bpermute
+// (each lane evaluating its group's 4 x 4 tap block itself, with no
+// broadcast, measured 5.40 vs 4.69 ms on C2: the transcendentals cost more).
 // One wave per work item (a chunk of a group of 16 cells, a 2 x 8-cell
-// region whose W planes are staged in LDS once).  The record factor
-// wgt * exp(-2 pi i w s0) is applied and the visibility written in place
-// (VD: out = the visibilities), or the raw sum added to out[record] for
-// k_finalize.  Every lane stores, without a branch: lanes past the batch's
-// records write to a per-block slot of `sink` (a skipped store left the
-// loop-top wait for the prefetched records at vmcnt(0), i.e. behind the
+// region), items in their natural order (the grid is only read, so
+// neighbouring items' overlapping regions hit L2).  The region's W planes
+// are copied into LDS by LDS-DMA, 16-byte cell pairs in rows of 16 cells:
+// no staging registers, one round trip per item.  The item's batches (16
+// records of one cell; a cell's last batch may be short) run in one flat
+// loop: a batch's cell and end come from a ballot over the 16 cell ends (lane
+// j holds cell j's), the next batch's records are loaded while this one is
+// computed, and the A operands are reloaded only when the cell changes (the
+// per-cell loop nest this replaced waited for the prefetched records at every
+// cell change: C2 5.05 -> 4.69 ms).  The record factor wgt * exp(-2 pi i w s0)
+// is applied and the visibility written in place (VD: out = the
+// visibilities), or the raw sum added to out[record] for k_finalize.  Every
+// lane stores, without a branch: lanes past the batch's records write to a
+// per-block slot of `sink` (a skipped store left the record wait behind the
 // previous batch's store), and the 4 lanes of a record write the same value.
 constexpr int kDegridSinkBlocks = 4096;  // sink slots (x 64 lanes)
+__device__ float4 g_zero16[1];            // 16 zero bytes (never written)
+template <int W, bool WS>
+constexpr int degrid_lds_bytes() {  // 16-byte pieces of the region, whole waves of them
+    return (((WS ? W : 1) * (W + 1) * 8 + 63) / 64) * 64 * 16;
+}
+struct DgBatch {
+    uint32_t b, ce;  // start, end of its cell's records (clipped to the item)
+    int c;           // cell
+};
 template <int W, bool WS, bool VD>
 __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restrict__ recs,
                                                     uint32_t n_items,
@@ -1660,7 +1683,7 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
                                                     float2 *__restrict__ sink) {
     static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
+    constexpr int RX = 2 + W - 1, RY = 16;  // LDS rows of 16 cells (8 + W - 1 used)
     constexpr int NQ = WS ? W : 1;
     const int lane = threadIdx.x;
     const int r16 = lane & 15, kg = lane >> 4;
@@ -1670,124 +1693,130 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
     const float tv0 = (float)kg * ihw, tv1 = (float)(kg + 4) * ihw;
     const float *const ftile = reinterpret_cast<const float *>(tile);
     const int64_t plane_elems = (int64_t)g.ngx * g.ngy;
+    float2 *const dump = sink + (blockIdx.x & (kDegridSinkBlocks - 1)) * 64 + lane;
 
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
         uint32_t fo[kGroupCell];
-        Item it;
-        it = load_fine_item<kGroupCell>(fitems, w_it, n_items, fo);
+        const Item it = load_fine_item<kGroupCell>(fitems, w_it, n_items, fo, true);
         if (it.b >= it.e) continue;
+        const uint32_t ie = it.e;
+        const uint32_t fol = fitems[w_it].o[r16];  // lane j < 16: end of cell j's records
+        // the batch starting at record x: the first cell whose end exceeds x
+        auto locate = [&](uint32_t x) {
+            DgBatch s;
+            s.b = x;
+            const uint64_t m = __ballot(fol > x) & 0xffffull;
+            s.c = m ? (int)__builtin_ctzll(m) : kGroupCell;
+            s.ce = min(m ? (uint32_t)__builtin_amdgcn_readlane((int)fol, s.c) : ie, ie);
+            return s;
+        };
+        // the next batch: the rest of this cell, else the next non-empty cell
+        auto advance = [&](const DgBatch &s) {
+            const uint32_t nb = min(s.b + 16u, s.ce);
+            if (nb < s.ce || nb >= ie) {
+                DgBatch t = s;
+                t.b = nb;
+                return t;
+            }
+            return locate(nb);
+        };
         int ibase, jbase;
         group_origin(g, (int)it.tile, ibase, jbase);
 
-        // the item's first 16 records are requested before the region is
-        // staged (both depend only on the item descriptor)
-        uint32_t pf = it.b;
-        VisRec nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
-        // the region's W planes: every load of the lane issued before the
-        // first LDS store (one memory round trip per item, not one per 64
-        // cells -- the load / wait / store loop cost ~17 serial round trips)
-        // (three rounds of up to 6 loads per lane: the registers of a single
-        // batch of 17 would cost the kernel a wave per SIMD)
-        constexpr int NSTG = (NQ * PS + 63) / 64, NH = (NSTG + 2) / 3;
+        DgBatch s0 = locate(it.b);
+        DgBatch s1 = advance(s0);
+        // the first batch's records are requested before the region
+        VisRec nxt = recs[min(s0.b + (uint32_t)r16, ie - 1)];
         wave_lds_sync();  // previous item's reads of the region
+        {
+            // piece i: plane q, row xl, cell pair m (jbase and ngy are even, so
+            // a pair never straddles the y wrap); planes outside the call's
+            // range (and the pieces past the region) read 16 zero bytes
+            constexpr int NPC = RX * 8, NGL = degrid_lds_bytes<W, WS>() / 1024;
 #pragma unroll
-        for (int k0 = 0; k0 < NSTG; k0 += NH) {
-            float2 stg[NH];
-#pragma unroll
-            for (int k = 0; k < NH; ++k) {
-                const int i = lane + 64 * (k0 + k);
-                const int q = i / PS;
+            for (int k = 0; k < NGL; ++k) {
+                const int i = lane + 64 * k;
+                const int q = i / NPC, rem = i - q * NPC, xl = rem >> 3, m = rem & 7;
                 const int p = (int)it.p0 + q;
-                const int rem = i - q * PS;
-                const int xl = rem / RY, yl = rem - (rem / RY) * RY;
                 int gx = ibase + xl;
                 if (gx >= g.ngx) gx -= g.ngx;
-                int gy = jbase + yl;
+                int gy = jbase + 2 * m;
                 if (gy >= g.ngy) gy -= g.ngy;
-                stg[k] = (k0 + k < NSTG && i < NQ * PS && p >= p_lo && p < p_hi)
-                             ? grid[(int64_t)(p - p_lo) * plane_elems + (int64_t)gx * g.ngy + gy]
-                             : make_float2(0.0f, 0.0f);
+                const void *src = (q < NQ && p >= p_lo && p < p_hi)
+                                      ? (const void *)(grid + (int64_t)(p - p_lo) * plane_elems +
+                                                       (int64_t)gx * g.ngy + gy)
+                                      : (const void *)g_zero16;
+                __builtin_amdgcn_global_load_lds(
+                    src,
+                    (__attribute__((address_space(3))) void *)(
+                        (__attribute__((address_space(3))) char *)tile + 1024 * k),
+                    16, 0, 0);
             }
-#pragma unroll
-            for (int k = 0; k < NH; ++k)
-                if (k0 + k < NSTG && lane + 64 * (k0 + k) < NQ * PS) tile[lane + 64 * (k0 + k)] = stg[k];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        wave_lds_sync();
 
-        // the item's cells are consecutive, so the batch after [b0, b0 + 16)
-        // starts at min(b0 + 16, re) -- in the next cell when this one ends;
-        // its records are loaded one batch ahead (pf = the prefetched start)
-        uint32_t cb = it.b;  // start of cell c's records (clipped to the item)
-        for (int c = 0; c < kGroupCell; ++c) {
-            const uint32_t rb = max(cb, it.b), re = min(fo[c], it.e);
-            cb = fo[c];
-            if (rb >= re) continue;
-            const int xo = c & 1, yo = c >> 1;
-            float a[16];
+        int acell = -1;
+        float a[16];
+        while (s0.b < ie) {
+            if (s0.c != acell) {
+                acell = s0.c;
+                const int xo = acell & 1, yo = acell >> 1;
 #pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const int kx = s >> 1, ky = 4 * (s & 1) + kg;
-                a[s] = (aq < NQ && kx < W && ky < W)
-                           ? ftile[((aq * RX + xo + kx) * RY + yo + ky) * 2 + aim]
-                           : 0.0f;
-            }
-            for (uint32_t b0 = rb; b0 < re; b0 += 16) {
-                // pf == b0 always: a cell's batches end at its last record and
-                // the next non-empty cell starts there (an empty cell has
-                // b == e), so the prefetched batch is this one (a reload path
-                // here left the loop's record wait at vmcnt(0))
-                const uint32_t ri = b0 + (uint32_t)r16;
-                const VisRec rec = nxt;
-                pf = min(b0 + 16, re);
-                nxt = recs[min(pf + (uint32_t)r16, it.e - 1)];
-                // the next batch's loads issue here, a whole batch before the
-                // loop-carried copy that waits for them (scheduled freely they
-                // sank under the MFMAs, ~50 instructions from that wait)
-                __builtin_amdgcn_sched_barrier(0);
-                const float u0 = es_tap<W>(rec.fu, tu0, ihw, bl);
-                const float u1 = es_tap<W>(rec.fu, tu1, ihw, bl);
-                float tu[8];
-#pragma unroll
-                for (int h = 0; h < 4; ++h) {
-                    tu[2 * h] = __shfl(u0, r16 + 16 * h);
-                    tu[2 * h + 1] = __shfl(u1, r16 + 16 * h);
-                }
-                // all 8 tap broadcasts in flight before the v / w taps are
-                // evaluated under them (interleaved with the MFMAs each
-                // waited for its own round trip)
-                __builtin_amdgcn_sched_barrier(0);
-                const float v0 = es_tap<W>(rec.fv, tv0, ihw, bl);
-                const float v1 = es_tap<W>(rec.fv, tv1, ihw, bl);
-                const float w0 = WS ? es_tap<W>(rec.fw, tu0, ihw, bl) : (kg == 0 ? 1.0f : 0.0f);
-                const float w1 = WS ? es_tap<W>(rec.fw, tu1, ihw, bl) : 0.0f;
-                floatx4 d0 = floatx4{0.0f, 0.0f, 0.0f, 0.0f}, d1 = d0;
-#pragma unroll
-                for (int s = 0; s < 16; s += 2) {
-                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], tu[s >> 1] * v0, d0, 0, 0, 0);
-                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s + 1], tu[s >> 1] * v1, d1, 0, 0, 0);
-                }
-                // (the loop-carried copy of the prefetched records, and its
-                // wait, stay below the MFMAs)
-                __builtin_amdgcn_sched_barrier(0);
-                // row 4 kg + i of D = (q = 2 kg + (i >> 1), re/im = i & 1)
-                float sr = w0 * (d0[0] + d1[0]) + w1 * (d0[2] + d1[2]);
-                float si = w0 * (d0[1] + d1[1]) + w1 * (d0[3] + d1[3]);
-                sr += __shfl_xor(sr, 16);
-                si += __shfl_xor(si, 16);
-                sr += __shfl_xor(sr, 32);
-                si += __shfl_xor(si, 32);
-                float2 *const dump = sink + (blockIdx.x & (kDegridSinkBlocks - 1)) * 64 + lane;
-                if constexpr (VD) {
-                    float2 *const dst = ri < re ? out + rec.idx : dump;
-                    *dst = make_float2(rec.cre * sr - rec.cim * si, rec.cre * si + rec.cim * sr);
-                } else {
-                    float2 *const dst = ri < re ? out + ri : dump;
-                    float2 v = *dst;
-                    v.x += sr;
-                    v.y += si;
-                    *dst = v;
+                for (int s = 0; s < 16; ++s) {
+                    const int kx = s >> 1, ky = 4 * (s & 1) + kg;
+                    a[s] = (aq < NQ && kx < W && ky < W)
+                               ? ftile[((aq * RX + xo + kx) * RY + yo + ky) * 2 + aim]
+                               : 0.0f;
                 }
             }
+            const float fu = nxt.fu, fv = nxt.fv, fw = nxt.fw, cre = nxt.cre, cim = nxt.cim;
+            const uint32_t idx = nxt.idx;
+            const uint32_t ri = s0.b + (uint32_t)r16;
+            const bool valid = ri < s0.ce;
+            nxt = recs[min(s1.b + (uint32_t)r16, ie - 1)];
+            // (the next batch's loads issue first, a whole batch ahead of use)
+            __builtin_amdgcn_sched_barrier(0);
+            const float u0 = es_tap<W>(fu, tu0, ihw, bl);
+            const float u1 = es_tap<W>(fu, tu1, ihw, bl);
+            float tu[8];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                tu[2 * h] = __shfl(u0, r16 + 16 * h);
+                tu[2 * h + 1] = __shfl(u1, r16 + 16 * h);
+            }
+            // all 8 tap broadcasts in flight before the v / w taps are
+            // evaluated under them
+            __builtin_amdgcn_sched_barrier(0);
+            const float v0 = es_tap<W>(fv, tv0, ihw, bl);
+            const float v1 = es_tap<W>(fv, tv1, ihw, bl);
+            const float w0 = WS ? es_tap<W>(fw, tu0, ihw, bl) : (kg == 0 ? 1.0f : 0.0f);
+            const float w1 = WS ? es_tap<W>(fw, tu1, ihw, bl) : 0.0f;
+            floatx4 d0 = floatx4{0.0f, 0.0f, 0.0f, 0.0f}, d1 = d0;
+#pragma unroll
+            for (int s = 0; s < 16; s += 2) {
+                d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], tu[s >> 1] * v0, d0, 0, 0, 0);
+                d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s + 1], tu[s >> 1] * v1, d1, 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // row 4 kg + i of D = (q = 2 kg + (i >> 1), re/im = i & 1)
+            float sr = w0 * (d0[0] + d1[0]) + w1 * (d0[2] + d1[2]);
+            float si = w0 * (d0[1] + d1[1]) + w1 * (d0[3] + d1[3]);
+            sr += __shfl_xor(sr, 16);
+            si += __shfl_xor(si, 16);
+            sr += __shfl_xor(sr, 32);
+            si += __shfl_xor(si, 32);
+            if constexpr (VD) {
+                float2 *const dst = valid ? out + idx : dump;
+                *dst = make_float2(cre * sr - cim * si, cre * si + cim * sr);
+            } else {
+                float2 *const dst = valid ? out + ri : dump;
+                float2 v = *dst;
+                v.x += sr;
+                v.y += si;
+                *dst = v;
+            }
+            s0 = s1;
+            s1 = advance(s1);
         }
     }
 }
@@ -3497,7 +3526,7 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
     // (kx RY + cy + 4 s + gk) NC + 16 m + rn of the cell's origin (cx, cy)
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
         uint32_t bnd[kGroupCell];
-        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
+        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd, true);
         if (it.b >= it.e) continue;
         int ibase, jbase;
         group_origin(g, (int)it.tile, ibase, jbase);
@@ -3542,7 +3571,7 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
         // ~400 SALU per block and wave)
         if (wv == 0) {
             const int c = lane & 15;
-            const FineItem *F = items + item_index(w_it, n_items);  // (load_fine_item's)
+            const FineItem *F = items + w_it;  // (load_fine_item's, natural order)
             const uint32_t o_prev = c == 0 ? (uint32_t)it.b : F->o[c - 1];
             const uint32_t o_c = c == kGroupCell - 1 ? (uint32_t)it.e : F->o[c];
             const uint32_t cs = min(max(o_prev, (uint32_t)it.b), (uint32_t)it.e);
@@ -3692,7 +3721,7 @@ __global__ __launch_bounds__(64) void k_degrid_f64(Geo g, const VisRec64 *__rest
     const bool plain = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
     for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
         uint32_t bnd[kGroupCell];
-        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd);
+        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd, true);
         if (it.b >= it.e) continue;
         int ibase, jbase;
         group_origin(g, (int)it.tile, ibase, jbase);
@@ -4954,7 +4983,7 @@ static float2 *degrid_sink() {
 
 template <int W, bool WS>
 static void launch_degrid_mfma(const Plan &P, int p_lo, int p_hi, float2 *acc, hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) * (2 + W - 1) * (8 + W - 1) * sizeof(float2);
+    const size_t lds = degrid_lds_bytes<W, WS>();
     // one-cell plans: one FineItem per item; sub-sorted coarse plans: 16
     const auto r = chunk_items(P, p_lo, p_hi);
     const unsigned per = P.subsort ? 16u : 1u;
