@@ -1,8 +1,8 @@
 #!/bin/bash
-# GPU suite + C2 timings on the current build
+# A/B: HEAD lib vs in-tree, C2 fp64 (eps 1e-12); then the fp64 NUFFT tests
 cd "$(dirname "$0")/.." || exit 1
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=5 > gpurun_out/gpu_suite.log 2>&1; rc=$?
-tail -12 gpurun_out/gpu_suite.log
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python3 scripts/time_c2.py --reps 7 || exit 1
-timeout -k 10 200 python3 scripts/time_c2.py --reps 3 --eps 1e-12 || exit 1
+for L in abtmp/lib_head.so "" abtmp/lib_head.so ""; do
+  echo "== lib ${L:-in-tree}"
+  SDP_HIP_LIB_OVERRIDE=$L timeout -k 10 200 python3 scripts/time_c2.py --reps 3 --eps 1e-12 || exit 1
+done
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_nufft_f64.py > gpurun_out/f64_tests.log 2>&1; rc=$?; tail -3 gpurun_out/f64_tests.log; exit $rc

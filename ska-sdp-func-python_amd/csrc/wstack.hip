@@ -3272,9 +3272,10 @@ constexpr int f64m_waves() {  // one wave per (N-tile, half of the kx M-tiles)
     return 2 * f64m_ntiles<W, WS>();
 }
 template <int W, bool WS>
-constexpr int f64m_ry() {
-    return 8 + 15;
+constexpr int f64m_ry() {  // rows a cell's footprint reaches (rows ky >= W are never stored)
+    return 8 + W - 1;
 }
+constexpr int kBlkG64 = 32;  // records per tap block of k_grid_f64_mfma (two 16-record halves)
 // region rows: each kx half of the waves owns a slab of the region, rows
 // x + kx of its own tiles (lower half KH + 1 rows, upper W - KH + 1; the row
 // where they meet is held twice and flushed from both)
@@ -3285,7 +3286,7 @@ constexpr int f64m_rows() {
 template <int W, bool WS>
 constexpr size_t grid_f64m_lds() {
     return (size_t)f64m_rows<W>() * f64m_ry<W, WS>() * 2 * (WS ? W : 1) * sizeof(double) +
-           (size_t)kBlk64 * (3 * W + 2) * sizeof(double) + kPolyN * sizeof(double);
+           (size_t)kBlkG64 * (3 * W + 2) * sizeof(double) + kPolyN * sizeof(double);
 }
 typedef double doublex4 __attribute__((ext_vector_type(4)));
 
@@ -3323,8 +3324,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
     constexpr int KH = (W + 1) / 2;  // kx M-tiles per wave
     extern __shared__ __attribute__((aligned(16))) double smd[];
     double *const reg = smd;       // [RX][RY][NC]: the lower slab's rows, then the upper's
-    double *const tap = smd + RS;  // [kBlk64][TR]
-    double *const cl = tap + kBlk64 * TR;  // the tap polynomials
+    double *const tap = smd + RS;  // [kBlkG64][TR]
+    double *const cl = tap + kBlkG64 * TR;  // the tap polynomials
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const double ihw = 2.0 / W, beta = (double)g.beta;
     for (int i = threadIdx.x; i < kPolyN; i += NTH) cl[i] = pc[i];
@@ -3368,6 +3369,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
             for (int k = 0; k < KH; ++k) acc[k] = doublex4{0.0, 0.0, 0.0, 0.0};
             int cur = -1, cb = 0;
             uint32_t cend = 0;  // end of the current cell's records
+            // rows ky = rk + 4 i >= W hold exact zeros (A = 0 there): never
+            // stored or loaded, so the region is only 8 + W - 1 rows deep
             auto store_n = [&](auto nt) {
                 constexpr int NK = decltype(nt)::value;
                 if (colok) {
@@ -3375,7 +3378,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
 #pragma unroll
                     for (int k = 0; k < NK; ++k)
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) d[k * RY * NC + 4 * i * NC] = acc[k][i];
+                        for (int i = 0; i < 4; ++i)
+                            if (4 * i + 3 < W || rk + 4 * i < W) d[k * RY * NC + 4 * i * NC] = acc[k][i];
                 }
             };
             auto load_n = [&](auto nt) {
@@ -3384,7 +3388,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
 #pragma unroll
                 for (int k = 0; k < NK; ++k)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[k][i] = s[k * RY * NC + 4 * i * NC];
+                    for (int i = 0; i < 4; ++i)
+                        acc[k][i] = (4 * i + 3 < W || rk + 4 * i < W) ? s[k * RY * NC + 4 * i * NC] : 0.0;
             };
             auto store_cell = [&]() { store_n(nk_tag); };
             auto load_cell = [&](int cell) {
@@ -3402,23 +3407,31 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
                 for (int k = 0; k < NK; ++k)
                     acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[k], bop, acc[k], 0, 0, 0);
             };
-            Stage64 nxt = stage64_load(recs, it.b, (int)min((uint32_t)kBlk64, it.e - it.b), lane);
-            for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlk64) {
+            // a block = two 16-record halves (stage64_* handle 16 records)
+            auto half_n = [&](uint32_t b, int h) {
+                return (int)min((uint32_t)kBlk64, b + h * kBlk64 < it.e ? it.e - b - h * kBlk64 : 0u);
+            };
+            Stage64 nxa = stage64_load(recs, it.b, half_n(it.b, 0), lane);
+            Stage64 nxb = stage64_load(recs, it.b + kBlk64, half_n(it.b, 1), lane);
+            for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlkG64) {
                 __syncthreads();  // the region zeroing / previous block's tap reads
-                const int nb = (int)min((uint32_t)kBlk64, it.e - b0);  // (a multiple of 4)
-                stage64_part<W, WS, NW>(wv, nxt, nb, tap, cl, ihw, beta, lane);
+                const int nb = (int)min((uint32_t)kBlkG64, it.e - b0);  // (a multiple of 4)
+                stage64_part<W, WS, NW>(wv, nxa, min(nb, kBlk64), tap, cl, ihw, beta, lane);
+                if (nb > kBlk64)
+                    stage64_part<W, WS, NW>(wv, nxb, nb - kBlk64, tap + kBlk64 * TR, cl, ihw, beta, lane);
                 // the next block's records, in flight during this block's K-steps
-                // (three blocks ahead, in three unrolled register sets, measured
-                // the same: 61.3 ms)
-                if (b0 + kBlk64 < it.e)
-                    nxt = stage64_load(recs, b0 + kBlk64, (int)min((uint32_t)kBlk64, it.e - b0 - kBlk64),
-                                       lane);
+                // (three blocks of 16 ahead, in three unrolled register sets,
+                // measured the same: 61.3 ms)
+                if (b0 + kBlkG64 < it.e) {
+                    nxa = stage64_load(recs, b0 + kBlkG64, half_n(b0 + kBlkG64, 0), lane);
+                    nxb = stage64_load(recs, b0 + kBlkG64 + kBlk64, half_n(b0 + kBlkG64, 1), lane);
+                }
                 __syncthreads();
                 // (K-steps not unrolled: unrolled, the register allocator gave
                 // the accumulators two register sets and copied all 104 doubles
                 // on every K-step without a cell change, behind the MFMAs)
 #pragma unroll 1
-                for (int kk = 0; kk < kBlk64 / 4; ++kk) {
+                for (int kk = 0; kk < kBlkG64 / 4; ++kk) {
                     if (4 * kk >= nb) break;
                     const uint32_t ri = b0 + 4u * (uint32_t)kk;
                     // one scalar compare per K-step against the current cell's
