@@ -84,6 +84,11 @@ def parse():
                     help="c4: max Gvis per batch -- the 4-padded record copy of the "
                          "large-grid invert (~38 B per visibility with the 16-B records "
                          "and ranks) must fit beside the 71 resident 16384^2 planes")
+    ap.add_argument("--cu-split", default=os.environ.get("SDP_BENCH_CU_SPLIT", "alt"),
+                    help="c2 pipelined: the two streams on disjoint CU masks ('alt', default: "
+                         "alternate CUs, hipExtStreamCreateWithCUMask; 'half': the low / high "
+                         "halves; '' = both streams on every CU).  C2: alt 11,717 vs 11,461 "
+                         "Mvis/s unmasked, half 11,213 (profiles/r05_cu_split.txt)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="c2: run the steps back to back on one stream (default: two streams "
                          "and two library scratch slots, consecutive inverts overlapping)")
@@ -1056,6 +1061,29 @@ def run_c5(args, world, rank, dev, sub=False):
     print(json.dumps(line), flush=True)
 
 
+def _cu_split_streams(dev, mode):
+    """Two HIP streams on disjoint CU masks (hipExtStreamCreateWithCUMask),
+    wrapped as torch ExternalStreams."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ncu + 31) // 32
+    out = []
+    for which in (0, 1):
+        bits = [0] * words
+        for c in range(ncu):
+            take = (c % 2 == which) if mode == "alt" else ((c < ncu // 2) == (which == 0))
+            if take:
+                bits[c // 32] |= 1 << (c % 32)
+        arr = (ctypes.c_uint32 * words)(*bits)
+        st = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), arr)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+        out.append(torch.cuda.ExternalStream(st.value, device=dev))
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1098,8 +1126,14 @@ def main():
     # stream i % 2, so step i+1's bucketing (memory-side atomics) overlaps
     # step i's gridding and FFTs; every step is still a complete invert with
     # its own image
+    # (--cu-split, default 'alt': the two streams on disjoint halves of the CUs,
+    # so one step's latency-bound bucketing and the other's gridding / FFT
+    # share the chip by CU instead of by workgroup dispatch order; the serial
+    # pass below runs on the default stream, every CU)
     pipe = args.pipeline
     streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)] if pipe else [None]
+    if pipe and args.cu_split:
+        streams = _cu_split_streams(dev, args.cu_split)
     outs = [out] + ([torch.empty_like(out)] if pipe else [])
 
     def grid_fn_slot(slot):
@@ -1109,14 +1143,14 @@ def main():
             return r
         return fn
 
-    def step(i=0):
-        j = i % len(streams)
+    def step(i=0, pipelined=True):
+        j = i % len(streams) if pipelined else 0
 
         def run():
             parallel.invert_sharded(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], args.npix,
                                     cell, EPS_REQUESTED, True, flip_uw=True, normalise=True,
                                     grid_fn=grid_fn_slot(j), out=outs[j])
-        if streams[j] is None:
+        if streams[j] is None or not pipelined:  # (serial: the whole GPU, default stream)
             run()
         else:
             with torch.cuda.stream(streams[j]):
@@ -1136,7 +1170,7 @@ def main():
         barrier()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(i if pipelined else 0)
+            step(i, pipelined)
         barrier()
         el = time.perf_counter() - t0
         if world > 1:
@@ -1227,7 +1261,8 @@ def main():
                                    f"{args.npix}^2 image, {info['ngrid_x']}^2 w-stack grid",
                        "pipelined": ("consecutive inverts on two streams / library scratch "
                                      "slots: step i+1's bucketing under step i's gridding + "
-                                     "FFT" if pipe else False),
+                                     "FFT" + (f"; streams on disjoint CU masks ({args.cu_split})"
+                                              if args.cu_split else "") if pipe else False),
                        "ms_per_step_serial": round(elapsed_serial / args.steps * 1e3, 3),
                        "value_serial": round(nvis_rank * world / (elapsed_serial / args.steps)
                                              / 1e6, 3),

@@ -1,8 +1,3 @@
 #!/bin/bash
-# A/B: HEAD lib vs in-tree, C2 fp64 (eps 1e-12); then the fp64 NUFFT tests
 cd "$(dirname "$0")/.." || exit 1
-for L in abtmp/lib_head.so "" abtmp/lib_head.so ""; do
-  echo "== lib ${L:-in-tree}"
-  SDP_HIP_LIB_OVERRIDE=$L timeout -k 10 200 python3 scripts/time_c2.py --reps 3 --eps 1e-12 || exit 1
-done
-timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_nufft_f64.py > gpurun_out/f64_tests.log 2>&1; rc=$?; tail -3 gpurun_out/f64_tests.log; exit $rc
+timeout -k 10 400 python3 bench.py --no-extra --steps 10 > gpurun_out/bench_cusplit.json 2> gpurun_out/bench_cusplit.err || { tail -20 gpurun_out/bench_cusplit.err; exit 1; }
