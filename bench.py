@@ -1072,7 +1072,12 @@ def _cu_split_streams(dev, mode):
     for which in (0, 1):
         bits = [0] * words
         for c in range(ncu):
-            take = (c % 2 == which) if mode == "alt" else ((c < ncu // 2) == (which == 0))
+            if mode == "alt":
+                take = c % 2 == which
+            elif mode == "ovl":  # 3/4 of the CUs each, half of them shared
+                take = c % 4 != (3 if which == 0 else 1)
+            else:
+                take = (c < ncu // 2) == (which == 0)
             if take:
                 bits[c // 32] |= 1 << (c % 32)
         arr = (ctypes.c_uint32 * words)(*bits)

@@ -1,3 +1,7 @@
 #!/bin/bash
+# C2 headline pipelined with stream CU-mask variants
 cd "$(dirname "$0")/.." || exit 1
-timeout -k 10 400 python3 bench.py --no-extra --steps 10 > gpurun_out/bench_cusplit.json 2> gpurun_out/bench_cusplit.err || { tail -20 gpurun_out/bench_cusplit.err; exit 1; }
+for m in alt ovl "" alt ovl ""; do
+  echo "== cu-split '$m'"
+  timeout -k 10 300 python3 bench.py --no-extra --no-api --cpu-chans 0 --steps 10 --cu-split "$m" || exit 1
+done
