@@ -3275,7 +3275,9 @@ template <int W, bool WS>
 constexpr int f64m_ry() {  // rows a cell's footprint reaches (rows ky >= W are never stored)
     return 8 + W - 1;
 }
-constexpr int kBlkG64 = 32;  // records per tap block of k_grid_f64_mfma (two 16-record halves)
+// records per tap block of k_grid_f64_mfma, in 16-record parts (C2 eps 1e-12 gridding: 16 -> 60.8,
+// 32 -> 59.4, 48 -> 58.7 ms; 48 is the most whose LDS still fits two workgroups per CU)
+constexpr int kBlkG64 = 48;
 // region rows: each kx half of the waves owns a slab of the region, rows
 // x + kx of its own tiles (lower half KH + 1 rows, upper W - KH + 1; the row
 // where they meet is held twice and flushed from both)
@@ -3407,24 +3409,29 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
                 for (int k = 0; k < NK; ++k)
                     acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(aop[k], bop, acc[k], 0, 0, 0);
             };
-            // a block = two 16-record halves (stage64_* handle 16 records)
+            // a block = 16-record parts (stage64_* handle 16 records)
             auto half_n = [&](uint32_t b, int h) {
                 return (int)min((uint32_t)kBlk64, b + h * kBlk64 < it.e ? it.e - b - h * kBlk64 : 0u);
             };
-            Stage64 nxa = stage64_load(recs, it.b, half_n(it.b, 0), lane);
-            Stage64 nxb = stage64_load(recs, it.b + kBlk64, half_n(it.b, 1), lane);
+            constexpr int NH = kBlkG64 / kBlk64;
+            Stage64 nx[NH];
+#pragma unroll
+            for (int h = 0; h < NH; ++h) nx[h] = stage64_load(recs, it.b + h * kBlk64, half_n(it.b, h), lane);
             for (uint32_t b0 = it.b; b0 < it.e; b0 += kBlkG64) {
                 __syncthreads();  // the region zeroing / previous block's tap reads
                 const int nb = (int)min((uint32_t)kBlkG64, it.e - b0);  // (a multiple of 4)
-                stage64_part<W, WS, NW>(wv, nxa, min(nb, kBlk64), tap, cl, ihw, beta, lane);
-                if (nb > kBlk64)
-                    stage64_part<W, WS, NW>(wv, nxb, nb - kBlk64, tap + kBlk64 * TR, cl, ihw, beta, lane);
+#pragma unroll
+                for (int h = 0; h < NH; ++h)
+                    if (nb > h * kBlk64)
+                        stage64_part<W, WS, NW>(wv, nx[h], min(nb - h * kBlk64, kBlk64), tap + h * kBlk64 * TR,
+                                                cl, ihw, beta, lane);
                 // the next block's records, in flight during this block's K-steps
                 // (three blocks of 16 ahead, in three unrolled register sets,
                 // measured the same: 61.3 ms)
                 if (b0 + kBlkG64 < it.e) {
-                    nxa = stage64_load(recs, b0 + kBlkG64, half_n(b0 + kBlkG64, 0), lane);
-                    nxb = stage64_load(recs, b0 + kBlkG64 + kBlk64, half_n(b0 + kBlkG64, 1), lane);
+#pragma unroll
+                    for (int h = 0; h < NH; ++h)
+                        nx[h] = stage64_load(recs, b0 + kBlkG64 + h * kBlk64, half_n(b0 + kBlkG64, h), lane);
                 }
                 __syncthreads();
                 // (K-steps not unrolled: unrolled, the register allocator gave
