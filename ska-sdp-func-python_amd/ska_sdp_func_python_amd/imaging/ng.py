@@ -57,6 +57,7 @@ serves such requests with the fp32 NUFFT at its floor (W = 8, ~1e-6).
 import contextlib
 import logging
 import os
+import threading
 
 import numpy as np
 import torch
@@ -106,6 +107,36 @@ def _side_stream(dev):
     if s is None:
         s = _SIDE[dev.index] = torch.cuda.Stream(dev)
     return s
+
+
+_COPY = {}
+
+
+def _copy_stream(dev):
+    """The host-to-device copy stream of a streamed host-resident invert."""
+    s = _COPY.get(dev.index)
+    if s is None:
+        s = _COPY[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
+def _host_row_blocks(sbvis, dev, single_call, dopsf, lo, hi, vnchan, nvis, max_call):
+    """Time blocks for streaming a host-resident Visibility through one NUFFT
+    call, or None.  A host Visibility's vis / weight / flag arrays cross PCIe
+    before any compute (~4 GB for C2); cut by time (contiguous slices), block
+    k + 1 is copied on a copy stream while block k grids, as one batch
+    sequence through one set of w planes.  SDP_HIP_HOST_BLOCKS (default 4;
+    0 or 1 = copy everything first)."""
+    nb = int(os.environ.get("SDP_HIP_HOST_BLOCKS", "4"))
+    ntimes = sbvis.vis.shape[0]
+    arrs = (sbvis.vis.data, sbvis.imaging_weight.data, sbvis.flags.data)
+    if (dev.type != "cuda" or not single_call or dopsf or nb <= 1 or (lo, hi) != (0, vnchan)
+            or not all(isinstance(a, np.ndarray) for a in arrs)):
+        return None
+    nb = min(ntimes, max(nb, -(-nvis // max_call)))
+    if nb <= 1:
+        return None
+    return [ntimes * i // nb for i in range(nb + 1)]
 
 
 def _rank_rows(uvw, freq, npix, pixsize, epsilon, precision, shard):
@@ -265,21 +296,30 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
             return _device.to_dev(a[rows.cpu().numpy()], dtype, dev)
         return _device.to_dev(a, dtype, dev)[rows]
 
+    max_call = max(1, int(float(os.environ.get("SDP_HIP_MAX_CALL_GVIS", "1.8")) * 1e9))
+    tcuts = None
+    if rows is None and uvw.shape[0] > 0:
+        tcuts = _host_row_blocks(sbvis, dev, mfs and npol == 1, dopsf, lo, hi, vnchan,
+                                 nrow * vnchan, max_call)
+
+    def typed(flags, wgt, ms):
+        if flags.dtype not in kernels._FLAG_DT:
+            flags = flags.to(torch.int64)
+        if wgt.dtype not in (torch.float32, torch.float64):
+            wgt = wgt.to(torch.float64)
+        if ms is not None and ms.dtype not in (torch.complex64, torch.complex128):
+            ms = ms.to(torch.complex128)
+        return flags, wgt, ms
+
     # The Visibility's own arrays, read in place by the fused prologue of
     # sdp_hip_ms2dirty_vis: flag masking (ng.py:191, :202), the pol-frame
     # conversion (ng.py:193-198) as one matrix row per image pol, f64 weights
     # and the weight sums (ng.py:258, :289) -- no O(Nvis) passes here.
-    flags = local(sbvis.flags.data)
-    if flags.dtype not in kernels._FLAG_DT:
-        flags = flags.to(torch.int64)
-    wgt = local(sbvis.imaging_weight.data)
-    if wgt.dtype not in (torch.float32, torch.float64):
-        wgt = wgt.to(torch.float64)
-    ms = None
-    if not dopsf:
-        ms = local(sbvis.vis.data)
-        if ms.dtype not in (torch.complex64, torch.complex128):
-            ms = ms.to(torch.complex128)
+    # (A streamed host Visibility copies them block by block below.)
+    flags = wgt = ms = None
+    if tcuts is None:
+        flags, wgt, ms = typed(local(sbvis.flags.data), local(sbvis.imaging_weight.data),
+                               None if dopsf else local(sbvis.vis.data))
     conv = pol_conversion_matrix(bvis.visibility_acc.polarisation_frame,
                                  im.image_acc.polarisation_frame)
     if rows is not None:
@@ -312,15 +352,13 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     # block) grids its channels in batches through one set of resident w
     # planes (sdp_hip_ms2dirty_vis_batch); the reference makes one ducc0 call
     # over all channels (ng.py:240-256).
-    max_call = max(1, int(float(os.environ.get("SDP_HIP_MAX_CALL_GVIS", "1.8")) * 1e9))
-
     def batches(chans):
         n = chans.stop - chans.start
         nb = min(n, max(1, -(-nrow_loc * n // max_call)))
         cuts = [chans.start + n * i // nb for i in range(nb + 1)]
         return [slice(a, e) for a, e in zip(cuts[:-1], cuts[1:])]
 
-    batched = any(len(batches(c[1])) > 1 for c in grid_calls)
+    batched = tcuts is not None or any(len(batches(c[1])) > 1 for c in grid_calls)
     # The pols of one image channel share one bucketing: the first pol keeps
     # it, the others re-run only the value pass (SDP_HIP_KEEP_BUCKETS /
     # SDP_HIP_REUSE_BUCKETS; C2 4 pols 54.0 ms against 59.7 pipelined, bench
@@ -342,7 +380,67 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     for pol, _, ichan in grid_calls:
         lane_of.setdefault((ichan, pol), len(lane_of) % 2)
 
+    def grid_streamed(pol, chans, ichan):
+        """One call over time blocks of a host Visibility: a copy thread moves
+        the blocks to the device on the copy stream (a pageable copy blocks
+        its host thread, not the GPU) while this thread grids the blocks
+        already there, one batch sequence through one set of resident w
+        planes (sdp_hip_ms2dirty_vis_batch)."""
+        sw = sumwt_d[ichan, pol:pol + 1]
+        coef = None if conv is None else conv[pol]
+        main_s, cs = torch.cuda.current_stream(dev), _copy_stream(dev)
+        nbl = sbvis.vis.shape[1]
+        bounds = kernels.uvw_bounds(uvw, freq_t)
+        cs.wait_stream(main_s)
+        nblk = len(tcuts) - 1
+        got = [None] * nblk
+        ready = [threading.Event() for _ in range(nblk)]
+
+        def copier():
+            try:
+                with torch.cuda.device(dev), torch.cuda.stream(cs):
+                    for i in range(nblk):
+                        t0, t1 = tcuts[i], tcuts[i + 1]
+                        n = (t1 - t0) * nbl
+                        ts = typed(*(_device.to_dev(a[t0:t1], None, dev).reshape(n, vnchan, vnpol)
+                                     for a in (sbvis.flags.data, sbvis.imaging_weight.data,
+                                               sbvis.vis.data)))
+                        ev = torch.cuda.Event()
+                        ev.record(cs)
+                        got[i] = (ts, ev)
+                        ready[i].set()
+            except BaseException as e:  # noqa: BLE001 -- re-raised by the gridding thread
+                for i in range(nblk):
+                    if got[i] is None:
+                        got[i] = e
+                    ready[i].set()
+
+        th = threading.Thread(target=copier, daemon=True)
+        th.start()
+        for i in range(nblk):
+            ready[i].wait()
+            if isinstance(got[i], BaseException):
+                th.join()
+                raise got[i]
+            (fl, wg, vs), ev = got[i]
+            got[i] = None
+            main_s.wait_event(ev)
+            for t in (fl, wg, vs):
+                t.record_stream(main_s)
+            r0, r1 = tcuts[i] * nbl, tcuts[i + 1] * nbl
+            _, info = kernels.ms2dirty_vis(
+                uvw[r0:r1], freq_t, vs, pol, wg[:, :, pol], fl, coef, npixdirty, npixdirty,
+                pixsize, pixsize, epsilon, do_wstacking, flip_uw=True, out=image[ichan, pol],
+                out_strides=(1, nx), accumulate=True, sumwt=sw, shift_lmn=lmn,
+                precision=precision, bounds=bounds, first=i == 0, last=i == nblk - 1)
+            if verbosity:
+                log.info("invert_ng: %s", info)
+            del fl, wg, vs
+        th.join()
+
     def grid_pol(pol, chans, ichan, first_pol):
+        if tcuts is not None:
+            return grid_streamed(pol, chans, ichan)
         sw = sumwt_d[ichan, pol:pol + 1]
         if dopsf and pol != 0:
             # PSF: pol 0 holds unit visibilities, the others are zero and are

@@ -409,6 +409,43 @@ def test_invert_ng_fused_prologue(pf, ipf, mfs, dopsf, device):
     np.testing.assert_allclose(sumwt, exp_sw, rtol=1e-6 if device else 1e-12)
 
 
+@pytest.mark.parametrize("eps,tol", [(1e-7, 1e-6), (1e-12, 1e-10)])
+def test_invert_ng_host_visibility_streamed(eps, tol, monkeypatch):
+    """A host-resident Visibility (numpy c128 / f64 / int64) is copied in time
+    blocks, block k + 1 on a copy stream while block k grids, as one batch
+    sequence through one set of w planes (SDP_HIP_HOST_BLOCKS, ragged blocks
+    of 7 times): the same image as copying everything first (fp32 atomics'
+    order only, or fp64) and the same sumwt, and the exact sums."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import invert_ng
+    rng = np.random.default_rng(29)
+    nt, nb, nchan = 7, 60, 4
+    freq = np.linspace(1.0e9, 1.2e9, nchan)
+    umax = 1500.0
+    uvw = rng.uniform(-1, 1, (nt, nb, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw[..., 2] *= 0.5
+    shape = (nt, nb, nchan, 1)
+    v = rng.normal(size=shape) + 1j * rng.normal(size=shape)
+    fl = (rng.uniform(size=shape) < 0.1).astype(np.int64)
+    vis = vis_from_arrays(uvw, freq, v, weight=rng.uniform(0.5, 2.0, shape), flags=fl,
+                          pf="stokesI", phasecentre=dm.SkyCoord(0.0, -0.6))
+    vis["imaging_weight"] = rng.uniform(0.5, 2.0, shape)
+    npix, cell = 128, 0.4 / umax
+    im = dm.create_image(npix, cell, dm.SkyCoord(0.0, -0.6), frequency=float(freq.mean()),
+                         channel_bandwidth=1e9, nchan=1)
+    out = {}
+    for nblk in ("4", "1"):
+        monkeypatch.setenv("SDP_HIP_HOST_BLOCKS", nblk)
+        d, sw = invert_ng(vis, im, normalise=False, epsilon=eps)
+        out[nblk] = (np.asarray(d["pixels"].data)[0, 0], sw)
+    np.testing.assert_allclose(out["4"][1], out["1"][1], rtol=1e-13)
+    assert rel_rms(out["4"][0], out["1"][0]) < tol
+    ms, wgt, fuvw = _prologue_reference(vis, im, False)
+    ref = orc.ms2dirty_exact(fuvw * FLIP_UW, freq, ms[..., 0], wgt[..., 0], npix, npix, cell,
+                             cell, True).T
+    assert rel_rms(out["4"][0], ref) < (TOL if eps > 1e-8 else 1e-9)
+
+
 @pytest.mark.parametrize("pf,ipf,dopsf", [("stokesI", "stokesI", False),
                                           ("linear", "stokesIQUV", True),
                                           ("linear", "stokesIQUV", False)])
