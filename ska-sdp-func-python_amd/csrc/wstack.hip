@@ -2093,6 +2093,20 @@ struct __attribute__((aligned(16))) VisRec64 {
 };
 static_assert(sizeof(VisRec64) == 64, "record layout");
 
+// The 48-byte fp64 record of the two-level bucketing for the MFMA kernels:
+// VisRec64 without the cell / first plane (the bucket's) -- the value pass
+// writes, the final move moves and the kernels read 48 instead of 64 bytes.
+// A 32-byte record with 42-bit fixed-point offsets halved the moves (C2 eps
+// 1e-12 invert prep 11.1 -> 7.6 ms) but its decode cost the gridder +1.9 ms
+// and the degridder +1.0 ms (each of a gridder workgroup's four waves decodes
+// every record of a block).
+struct __attribute__((aligned(16))) Rec64 {
+    double cre, cim;
+    double du, dv, dw;
+    uint32_t idx, pad;
+};
+static_assert(sizeof(Rec64) == 48, "record layout");
+
 // tap t of offset f: exp(beta (sqrt(1 - x^2) - 1)), x = (f + t) 2 / W
 __device__ __forceinline__ double es_tap64(double f, int t, double ihw, double beta) {
     const double x = (f + (double)t) * ihw;
@@ -2459,14 +2473,14 @@ __global__ __launch_bounds__(kTThreads) void k_t_bins(int nb, const unsigned *__
 // the visibility's value (phase 1 of the value pass: loads only)
 template <class VT, int KIND, bool kGrid>
 struct TVal {
-    using type = typename std::conditional<KIND == 2, double2, float2>::type;
+    using type = typename std::conditional<KIND >= 2, double2, float2>::type;
     __device__ static __forceinline__ type load(const VT *vis, int64_t vrs, int64_t vcs,
                                                 const VisExtra &x, const TLoad &L) {
         type xv;
         xv.x = 1;
         xv.y = 0;
         if constexpr (kGrid) {
-            if constexpr (KIND == 2) {
+            if constexpr (KIND >= 2) {
                 if (vis && L.live && L.wd != 0.0) xv = eff_vis_d(vis, vrs, vcs, x, L.row, L.chan);
             } else {
                 if (vis && L.live && (float)L.wd != 0.0f) xv = eff_vis(vis, vrs, vcs, x, L.row, L.chan);
@@ -2476,7 +2490,8 @@ struct TVal {
     }
 };
 
-// KIND 0: RecC (4-padded invert), 1: VisRec (fp32 predict), 2: VisRec64
+// KIND 0: RecC (4-padded invert), 1: VisRec (fp32 predict), 2: VisRec64,
+// 3: Rec64 (the fp64 MFMA kernels)
 template <int KIND>
 struct TRec;
 template <>
@@ -2491,6 +2506,10 @@ template <>
 struct TRec<2> {
     using type = VisRec64;
 };
+template <>
+struct TRec<3> {
+    using type = Rec64;
+};
 
 // Record writers of the value pass: the fields bucket_one / k_bucket_f64
 // write for the single-level path, computed the same way.
@@ -2504,7 +2523,7 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x, const T
         if (x.shift) ph += (L.um * x.sl + L.vm * x.sm + L.wm * x.sn) * L.s;
         ph -= rint(ph);
     }
-    if constexpr (KIND == 2) {
+    if constexpr (KIND >= 2) {
         double cr = p.wd, ci = 0.0;
         if (kGrid) {
             cr = p.wd != 0.0 ? xv.x * p.wd : 0.0;
@@ -2518,6 +2537,18 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x, const T
             cr = r_;
             ci = i_;
         }
+        if constexpr (KIND == 3) {
+            Rec64 rec;
+            rec.cre = cr;
+            rec.cim = ci;
+            rec.du = p.c.du;
+            rec.dv = p.c.dv;
+            rec.dw = p.c.dw;
+            rec.idx = (uint32_t)(L.row * (uint32_t)g.nchan + L.chan);
+            rec.pad = 0u;
+            static_cast<Rec64 *>(out)[pos] = rec;
+            return;
+        } else {
         VisRec64 rec;
         rec.cre = cr;
         rec.cim = ci;
@@ -2529,6 +2560,7 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x, const T
         rec.idx = (uint32_t)(L.row * (uint32_t)g.nchan + L.chan);
         rec.pad = 0u;
         static_cast<VisRec64 *>(out)[pos] = rec;
+        }
     } else {
         const float wt = (float)p.wd;
         float cr = wt, ci = 0.0f;
@@ -2805,6 +2837,12 @@ __global__ __launch_bounds__(256) void k_t_cellfin(const Geo g, const unsigned *
                     z.du = z.dv = z.dw = 1.0 - 0.5 * g.W;
                     z.ij = z.p0 = z.idx = z.pad = 0u;
                     for (unsigned i = run + n[j]; i < run + r; ++i) static_cast<VisRec64 *>(recs)[i] = z;
+                } else if constexpr (KIND == 3) {
+                    Rec64 z;
+                    z.cre = z.cim = 0.0;
+                    z.du = z.dv = z.dw = 1.0 - 0.5 * g.W;
+                    z.idx = z.pad = 0u;
+                    for (unsigned i = run + n[j]; i < run + r; ++i) static_cast<Rec64 *>(recs)[i] = z;
                 } else {
                     RecC z;
                     z.cre = z.cim = 0.0f;
@@ -3206,8 +3244,9 @@ struct Stage64 {
     uint32_t idx;  // output index (degridder)
 };
 
-__device__ __forceinline__ Stage64 stage64_load(const VisRec64 *__restrict__ recs, uint32_t b0,
-                                                int nb, int lane) {
+template <class RT>  // VisRec64 or Rec64
+__device__ __forceinline__ Stage64 stage64_load(const RT *__restrict__ recs, uint32_t b0, int nb,
+                                                int lane) {
     Stage64 s;
     s.a = s.b = 0.0;
     s.idx = 0u;
@@ -3215,11 +3254,11 @@ __device__ __forceinline__ Stage64 stage64_load(const VisRec64 *__restrict__ rec
     if (lane < 3 * kBlk64) {
         const int r = lane / 3, ax = lane - 3 * r;
         if (r < nb) {
-            const VisRec64 *R = recs + b0 + r;
+            const RT *R = recs + b0 + r;
             s.a = ax == 0 ? R->du : (ax == 1 ? R->dv : R->dw);
         }
     } else if (lane - 3 * kBlk64 < nb) {
-        const VisRec64 *R = recs + b0 + (lane - 3 * kBlk64);
+        const RT *R = recs + b0 + (lane - 3 * kBlk64);
         s.a = R->cre;
         s.b = R->cim;
     }
@@ -3316,7 +3355,7 @@ __device__ __forceinline__ void stage64_part(int part, const Stage64 &s, int nb,
 
 template <int W, bool WS>
 __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64_mfma(
-    Geo g, const VisRec64 *__restrict__ recs, const FineItem *__restrict__ items,
+    Geo g, const Rec64 *__restrict__ recs, const FineItem *__restrict__ items,
     uint32_t n_items, double *__restrict__ grid, int p_lo, int p_hi,
     const double *__restrict__ pc) {
     static_assert(W <= 16, "one M-tile of 16 rows per kx");
@@ -3431,7 +3470,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64, 256))) void k_grid_f64
                 if (b0 + kBlkG64 < it.e) {
 #pragma unroll
                     for (int h = 0; h < NH; ++h)
-                        nx[h] = stage64_load(recs, b0 + kBlkG64 + h * kBlk64, half_n(b0 + kBlkG64, h), lane);
+                        nx[h] = stage64_load(recs, b0 + kBlkG64 + h * kBlk64, half_n(b0 + kBlkG64, h),
+                                             lane);
                 }
                 __syncthreads();
                 // (K-steps not unrolled: unrolled, the register allocator gave
@@ -3513,9 +3553,9 @@ constexpr size_t degrid_f64m_lds() {
            (size_t)(2 * kMaxBlk64 + 1) * sizeof(uint32_t);
 }
 
-template <int W, bool WS, class VT>
+template <int W, bool WS, class VT, class R>
 __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
-    Geo g, const VisRec64 *__restrict__ recs, const FineItem *__restrict__ items,
+    Geo g, const R *__restrict__ recs, const FineItem *__restrict__ items,
     uint32_t n_items, const double2 *__restrict__ grid, int p_lo, int p_hi, VT *vis, int64_t vrs,
     int64_t vcs, int accumulate, OutConv oc, const double *__restrict__ pc) {
     static_assert(W <= 16, "K-steps of 4 rows ky < 16");
@@ -3615,7 +3655,8 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
         __syncthreads();
         const uint32_t nblk = min(btab[kMaxBlk64], (uint32_t)kMaxBlk64);
         uint32_t kb = (uint32_t)wv;
-        Stage64 nxt = kb < nblk ? stage64_load(recs, btab[kb], (int)(bcel[kb] >> 8), lane) : Stage64{};
+        Stage64 nxt =
+            kb < nblk ? stage64_load(recs, btab[kb], (int)(bcel[kb] >> 8), lane) : Stage64{};
         for (; kb < nblk; kb += kDeg64Waves) {
             {
                 const uint32_t b0 = btab[kb], cn = bcel[kb];
@@ -3626,8 +3667,8 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
                 stage64_write<W, WS, 0, W / 2>(cur_s, nb, tap, cl, ihw, beta, lane, true);
                 stage64_write<W, WS, W / 2, W>(cur_s, nb, tap, cl, ihw, beta, lane, false);
                 if (kb + kDeg64Waves < nblk)
-                    nxt = stage64_load(recs, btab[kb + kDeg64Waves], (int)(bcel[kb + kDeg64Waves] >> 8),
-                                       lane);
+                    nxt = stage64_load(recs, btab[kb + kDeg64Waves],
+                                       (int)(bcel[kb + kDeg64Waves] >> 8), lane);
                 wave_lds_sync();
                 const double *T = tap + rn * TR;  // this lane's record (B column)
                 const bool rok = rn < nb;
@@ -4924,7 +4965,7 @@ static void launch_grid_f64_mfma(const Plan &P, int p_lo, int p_hi, hipStream_t 
     }();
     (void)attr;
     k_grid_f64_mfma<W, WS><<<n, 64 * f64m_waves<W, WS>(), grid_f64m_lds<W, WS>(), st>>>(
-        P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
+        P.g, reinterpret_cast<const Rec64 *>(P.recs), P.pt.fitems + r.first, n,
         reinterpret_cast<double *>(P.grid), p_lo, p_hi, es_poly64_table(W, P.g.beta, st));
 }
 
@@ -4935,17 +4976,24 @@ static void launch_degrid_f64_mfma(const Plan &P, int p_lo, int p_hi, VT *vis, i
     const auto r = chunk_items(P, p_lo, p_hi);
     const unsigned n = r.second - r.first;
     if (n == 0) return;
-    static const bool attr = [] {  // dynamic LDS above 64 KiB
-        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_degrid_f64_mfma<W, WS, VT>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)degrid_f64m_lds<W, WS>()));
-        return true;
-    }();
-    (void)attr;
-    k_degrid_f64_mfma<W, WS, VT><<<n, 64 * kDeg64Waves, degrid_f64m_lds<W, WS>(), st>>>(
-        P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
-        reinterpret_cast<const double2 *>(P.grid), p_lo, p_hi, vis, vrs, vcs, accumulate, oc,
-        es_poly64_table(W, P.g.beta, st));
+    // records: Rec64 from the two-level bucketing, VisRec64 from the
+    // single-level one (SDP_HIP_BUCKET2=0, or windows past the LDS histogram)
+    auto go = [&](auto rec_tag) {
+        using R = typename decltype(rec_tag)::type;
+        static const bool attr = [] {  // dynamic LDS above 64 KiB
+            SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_degrid_f64_mfma<W, WS, VT, R>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)degrid_f64m_lds<W, WS>()));
+            return true;
+        }();
+        (void)attr;
+        k_degrid_f64_mfma<W, WS, VT, R><<<n, 64 * kDeg64Waves, degrid_f64m_lds<W, WS>(), st>>>(
+            P.g, reinterpret_cast<const R *>(P.recs), P.pt.fitems + r.first, n,
+            reinterpret_cast<const double2 *>(P.grid), p_lo, p_hi, vis, vrs, vcs, accumulate, oc,
+            es_poly64_table(W, P.g.beta, st));
+    };
+    if (P.g.tiled) go(TypeTag<Rec64>{});
+    else go(TypeTag<VisRec64>{});
 }
 
 static void grid_f64(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
@@ -5233,8 +5281,13 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     const Geo &g = P.g;
     Part &pt = P.pt;
     const int nb = g.nbins;
-    const int kind = P.f64 ? 2 : (grid_mode ? 0 : 1);
-    const size_t rsz = kind == 2 ? sizeof(VisRec64) : kind == 0 ? sizeof(RecC) : sizeof(VisRec);
+    // fp64: 48-byte Rec64 for the MFMA kernels, VisRec64 for the VALU ones
+    // (SDP_HIP_F64_MFMA=0)
+    const int kind = P.f64 ? ((P.pad64 || P.mfma64) ? 3 : 2) : (grid_mode ? 0 : 1);
+    const size_t rsz = kind == 2   ? sizeof(VisRec64)
+                       : kind == 3 ? sizeof(Rec64)
+                       : kind == 0 ? sizeof(RecC)
+                                   : sizeof(VisRec);
     const int64_t nvis = pt.nvis;
     const size_t lds_bins = (size_t)nb * sizeof(unsigned);
     if (!values_only) {
@@ -5291,6 +5344,9 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
             if (kind == 2) {
                 if (grid_mode) go(vt_tag, std::integral_constant<int, 2>{}, std::true_type{});
                 else go(vt_tag, std::integral_constant<int, 2>{}, std::false_type{});
+            } else if (kind == 3) {
+                if (grid_mode) go(vt_tag, std::integral_constant<int, 3>{}, std::true_type{});
+                else go(vt_tag, std::integral_constant<int, 3>{}, std::false_type{});
             } else if (kind == 0) {
                 go(vt_tag, std::integral_constant<int, 0>{}, std::true_type{});
             } else {
@@ -5319,7 +5375,9 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     };
     auto final_move = [&] {
         using I = std::integral_constant<int, 0>;
-        if (tfinal == 0) {
+        if (kind == 3) {
+            staged(std::integral_constant<int, 3>{}, std::integral_constant<int, 2048>{});
+        } else if (tfinal == 0) {
             if (kind == 2)
                 k_t_final<2><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
                                                          pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
@@ -5394,7 +5452,7 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         k_t_cellfin<true, 0><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
                                                    pt.t_cbase, P.recs, pt.fitems);
     else if (P.pad64)
-        k_t_cellfin<true, 2><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
+        k_t_cellfin<true, 3><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
                                                    pt.t_cbase, P.recs, pt.fitems);
     else
         k_t_cellfin<false, 1><<<gfin, 256, 0, st>>>(g, pt.t_nbl, pt.t_tot, pt.t_bofs, P.chunk,
