@@ -369,7 +369,10 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     # by the call's position: the image and weight-sum accumulation is a
     # plain read-modify-write, so every call into one target stays on one
     # stream.  SDP_HIP_OVERLAP=0 keeps every call on one stream.
-    share = npol > 1 and not dopsf and not batched
+    # (not at fp64: a kept bucketing is single-level, whose unpadded
+    # records only the VALU fp64 gridder reads -- the pols then run the
+    # two-level sort and the MFMA gridder each, pipelined over two streams)
+    share = npol > 1 and not dopsf and not batched and not kernels.is_fp64(epsilon, precision)
     overlap = len(grid_calls) > 1 and not share and not batched and dev.type == "cuda" and \
         os.environ.get("SDP_HIP_OVERLAP", "1") != "0"
     main = torch.cuda.current_stream(dev) if overlap else None

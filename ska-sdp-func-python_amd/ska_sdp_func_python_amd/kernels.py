@@ -39,6 +39,12 @@ def set_precision(mode):
     _PRECISION = mode
 
 
+def is_fp64(epsilon, precision=None):
+    """True when a NUFFT call at `epsilon` runs the fp64 path."""
+    mode = precision or _PRECISION
+    return float(epsilon) < EPS_FLOOR and mode == "auto"
+
+
 def _prec_bits(epsilon, precision=None):
     """Flag bits of a NUFFT call for `epsilon` under `precision`."""
     global _eps_warned
