@@ -1147,7 +1147,11 @@ def main():
     pipe = args.pipeline
     streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)] if pipe else [None]
     if pipe and args.cu_split:
-        streams = _cu_split_streams(dev, args.cu_split)
+        try:
+            streams = _cu_split_streams(dev, args.cu_split)
+        except (OSError, AttributeError, RuntimeError) as e:  # (no CU-mask API: unmasked)
+            print(f"bench: CU-masked streams unavailable ({e!r}); unmasked", file=sys.stderr)
+            args.cu_split = ""
     outs = [out] + ([torch.empty_like(out)] if pipe else [])
 
     def grid_fn_slot(slot):
