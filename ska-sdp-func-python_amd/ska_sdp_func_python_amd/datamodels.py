@@ -465,7 +465,8 @@ class Visibility(Dataset):
         drivers use it: (time, one-time-sample Visibility) pairs."""
         if coord != "time":
             raise ValueError(f"groupby: only 'time' is supported, not {coord}")
-        times = np.unique(np.asarray(self._vars["time"], dtype=float))
+        times = np.asarray(self._vars["time"], dtype=float)
+        times = np.unique(times[np.isfinite(times)])
         return list(zip(times.tolist(), visibility_time_slices(self)))
 
     @classmethod
@@ -838,11 +839,17 @@ def visibility_time_slices(vis):
     """One Visibility per distinct time value, in increasing time order, as
     xarray's ``vis.groupby("time", squeeze=False)`` yields them: the rows
     sharing a time value form one group (a view of the parent's arrays when
-    they are consecutive, a gathered copy otherwise)."""
+    they are consecutive, a gathered copy otherwise).  Rows whose time is not
+    finite belong to no group, as xarray's groupby drops NaN labels."""
     times = np.asarray(vis._vars["time"], dtype=float)
+    finite = np.isfinite(times)
+    keys, inv = np.unique(times[finite], return_inverse=True)
+    idx = np.flatnonzero(finite)
+    order = np.argsort(inv, kind="stable")
+    bounds = np.searchsorted(inv[order], np.arange(keys.size + 1))
     out = []
-    for t in np.unique(times):
-        rows = np.flatnonzero(times == t)
+    for g in range(keys.size):
+        rows = idx[order[bounds[g]:bounds[g + 1]]]
         if rows[-1] - rows[0] + 1 == rows.size:
             sel = slice(int(rows[0]), int(rows[-1]) + 1)
         else:

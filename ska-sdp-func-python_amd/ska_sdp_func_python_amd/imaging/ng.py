@@ -86,12 +86,17 @@ def _channel_runs(vis_to_im, lo, hi):
     return [tuple(r) for r in runs]
 
 
-def _image_geometry(model):
-    """What every rank of a shard="local" call must agree on: the image shape
-    and its WCS (reference pixels, increments, values)."""
+def _image_geometry(model, **scalars):
+    """What every rank of a shard="local" call must agree on: the image shape,
+    its WCS (reference pixels, increments, values) and polarisation frame,
+    and the call's scalar options (epsilon, do_wstacking, dopsf, ...): ranks
+    that pass different ones would all-reduce images that do not match."""
     w = model.image_acc.wcs.wcs
+    frame = model.image_acc.polarisation_frame
+    text = repr((str(getattr(frame, "type", frame)), sorted(scalars.items()))).encode()
     return [tuple(model["pixels"].data.shape), np.asarray(w.crpix, dtype=float),
-            np.asarray(w.cdelt, dtype=float), np.asarray(w.crval, dtype=float)]
+            np.asarray(w.cdelt, dtype=float), np.asarray(w.crval, dtype=float),
+            np.frombuffer(text, dtype=np.uint8)]
 
 
 def _pixsize(model):
@@ -110,6 +115,7 @@ def _side_stream(dev):
 
 
 _COPY = {}
+_HOST_LOOKAHEAD = 2  # time blocks a streamed host invert copies ahead of its gridding
 
 
 def _copy_stream(dev):
@@ -174,8 +180,10 @@ def predict_ng(bvis, model, **kwargs):
     # shard="local": each rank predicts its own block, no exchange; the model
     # must be the same on every rank
     loc = parallel.local_info(kwargs)
-    parallel.check_replicated(loc, _image_geometry(model) + [model["pixels"].data],
-                              "predict_ng(shard='local')")
+    parallel.check_replicated(
+        loc, _image_geometry(model, epsilon=float(epsilon), do_wstacking=bool(do_wstacking),
+                             precision=precision) + [model["pixels"].data],
+        "predict_ng(shard='local')")
     blocks = [(0, vnchan)]
     lo, hi = 0, vnchan
     if shard:
@@ -270,14 +278,20 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     # this rank's visibility channels [lo, hi) (all of them unsharded), or
     # for an MFS w-stacked invert its rows (an interval of w, all channels)
     lo, hi = 0, vnchan
-    mfs = nchan == 1 and vnchan > 1
+    # MFS: one image channel collecting several visibility channels.  In the
+    # pre-sharded mode a rank's block may hold a single channel of a
+    # many-channel observation, so there an MFS image alone decides it
+    mfs = nchan == 1 and (vnchan > 1 or loc is not None)
     uvw = _device.to_dev(sbvis.uvw.data, torch.float64, dev).reshape(nrow, 3).contiguous()
     parallel.check_replicated(
         shard, [uvw, freq, sbvis.imaging_weight.data, None if dopsf else sbvis.vis.data,
                 model["pixels"].data.shape], "invert_ng")
-    # shard="local": each rank passes its own block; only the image geometry
-    # must agree across the ranks
-    parallel.check_replicated(loc, _image_geometry(model), "invert_ng(shard='local')")
+    # shard="local": each rank passes its own block; the image geometry and
+    # the call's options must agree across the ranks
+    parallel.check_replicated(
+        loc, _image_geometry(model, epsilon=float(epsilon), do_wstacking=bool(do_wstacking),
+                             dopsf=bool(dopsf), normalise=bool(normalise), precision=precision),
+        "invert_ng(shard='local')")
     rows = None
     if shard and mfs and do_wstacking and parallel.shard_mode() != "chan":
         rows = _rank_rows(uvw, freq, nx, _pixsize(im), epsilon, precision, shard)
@@ -317,9 +331,14 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
     # and the weight sums (ng.py:258, :289) -- no O(Nvis) passes here.
     # (A streamed host Visibility copies them block by block below.)
     flags = wgt = ms = None
-    if tcuts is None:
+
+    def whole_arrays():
+        nonlocal flags, wgt, ms
         flags, wgt, ms = typed(local(sbvis.flags.data), local(sbvis.imaging_weight.data),
                                None if dopsf else local(sbvis.vis.data))
+
+    if tcuts is None:
+        whole_arrays()
     conv = pol_conversion_matrix(bvis.visibility_acc.polarisation_frame,
                                  im.image_acc.polarisation_frame)
     if rows is not None:
@@ -388,7 +407,13 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
         the blocks to the device on the copy stream (a pageable copy blocks
         its host thread, not the GPU) while this thread grids the blocks
         already there, one batch sequence through one set of resident w
-        planes (sdp_hip_ms2dirty_vis_batch)."""
+        planes (sdp_hip_ms2dirty_vis_batch).  The copier runs at most
+        _HOST_LOOKAHEAD blocks ahead of the gridding (so the device holds at
+        most that many blocks beyond the one gridding) and stops when the
+        gridding ends or fails.  Returns False, with nothing gridded, when the
+        w planes do not all fit in device memory at once (a batch sequence
+        needs them resident): the caller then copies everything first and
+        grids in one call, whose planes are chunked."""
         sw = sumwt_d[ichan, pol:pol + 1]
         coef = None if conv is None else conv[pol]
         main_s, cs = torch.cuda.current_stream(dev), _copy_stream(dev)
@@ -398,11 +423,16 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
         nblk = len(tcuts) - 1
         got = [None] * nblk
         ready = [threading.Event() for _ in range(nblk)]
+        slots = threading.Semaphore(_HOST_LOOKAHEAD)
+        stop = threading.Event()
 
         def copier():
             try:
                 with torch.cuda.device(dev), torch.cuda.stream(cs):
                     for i in range(nblk):
+                        slots.acquire()
+                        if stop.is_set():
+                            return
                         t0, t1 = tcuts[i], tcuts[i + 1]
                         n = (t1 - t0) * nbl
                         ts = typed(*(_device.to_dev(a[t0:t1], None, dev).reshape(n, vnchan, vnpol)
@@ -420,30 +450,50 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
 
         th = threading.Thread(target=copier, daemon=True)
         th.start()
-        for i in range(nblk):
-            ready[i].wait()
-            if isinstance(got[i], BaseException):
-                th.join()
-                raise got[i]
-            (fl, wg, vs), ev = got[i]
-            got[i] = None
-            main_s.wait_event(ev)
-            for t in (fl, wg, vs):
-                t.record_stream(main_s)
-            r0, r1 = tcuts[i] * nbl, tcuts[i + 1] * nbl
-            _, info = kernels.ms2dirty_vis(
-                uvw[r0:r1], freq_t, vs, pol, wg[:, :, pol], fl, coef, npixdirty, npixdirty,
-                pixsize, pixsize, epsilon, do_wstacking, flip_uw=True, out=image[ichan, pol],
-                out_strides=(1, nx), accumulate=True, sumwt=sw, shift_lmn=lmn,
-                precision=precision, bounds=bounds, first=i == 0, last=i == nblk - 1)
-            if verbosity:
-                log.info("invert_ng: %s", info)
-            del fl, wg, vs
-        th.join()
+        try:
+            for i in range(nblk):
+                ready[i].wait()
+                if isinstance(got[i], BaseException):
+                    raise got[i]
+                (fl, wg, vs), ev = got[i]
+                got[i] = None
+                main_s.wait_event(ev)
+                for t in (fl, wg, vs):
+                    t.record_stream(main_s)
+                r0, r1 = tcuts[i] * nbl, tcuts[i + 1] * nbl
+                try:
+                    _, info = kernels.ms2dirty_vis(
+                        uvw[r0:r1], freq_t, vs, pol, wg[:, :, pol], fl, coef, npixdirty,
+                        npixdirty, pixsize, pixsize, epsilon, do_wstacking, flip_uw=True,
+                        out=image[ichan, pol], out_strides=(1, nx), accumulate=True, sumwt=sw,
+                        shift_lmn=lmn, precision=precision, bounds=bounds, first=i == 0,
+                        last=i == nblk - 1)
+                except ValueError as e:
+                    # (raised by the first batch's plan, before any gridding
+                    # or weight sum)
+                    if i == 0 and "do not all fit" in str(e):
+                        log.info("invert_ng: w planes exceed device memory, host Visibility "
+                                 "copied whole instead of streamed")
+                        return False
+                    raise
+                if verbosity:
+                    log.info("invert_ng: %s", info)
+                del fl, wg, vs
+                slots.release()
+        finally:
+            stop.set()
+            slots.release()  # (wakes a copier waiting for a slot)
+            th.join()
+            got.clear()
+        return True
 
     def grid_pol(pol, chans, ichan, first_pol):
+        nonlocal tcuts
         if tcuts is not None:
-            return grid_streamed(pol, chans, ichan)
+            if grid_streamed(pol, chans, ichan):
+                return
+            tcuts = None
+            whole_arrays()
         sw = sumwt_d[ichan, pol:pol + 1]
         if dopsf and pol != 0:
             # PSF: pol 0 holds unit visibilities, the others are zero and are

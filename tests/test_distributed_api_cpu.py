@@ -103,6 +103,8 @@ def _case(kind, seed=51):
     vis["imaging_weight"] = rng.uniform(0.5, 2.0, shape)
     cube = kind == "invert_cube"
     fc, bw = (float(freq[0]), float(freq[1] - freq[0])) if cube else (float(freq.mean()), 1e9)
+    if kind == "invert_mfsnarrow":  # an MFS image whose WCS maps no vis channel to 0
+        bw = 1e6
     im = dm.create_image(32, 0.4 / umax, dm.SkyCoord(0.0, -0.6), frequency=fc,
                          channel_bandwidth=bw, nchan=nchan if cube else 1)
     if kind == "predict":
@@ -270,6 +272,8 @@ def _block(vis, rank, world, by):
     nt, _, nchan, _ = vis.vis.data.shape
     t = slice(rank * nt // world, (rank + 1) * nt // world) if by == "rows" else slice(0, nt)
     c = slice(rank * nchan // world, (rank + 1) * nchan // world) if by == "chans" else slice(0, nchan)
+    if by == "chans1":  # rank 0 holds a single channel of the band
+        c = slice(0, 1) if rank == 0 else slice(1, nchan)
     b = vis_from_arrays(np.asarray(vis.uvw.data)[t], np.asarray(vis.frequency.data)[c],
                         np.asarray(vis.vis.data)[t, :, c], weight=np.asarray(vis.weight.data)[t, :, c],
                         flags=np.asarray(vis.flags.data)[t, :, c], phasecentre=vis.phasecentre)
@@ -279,16 +283,43 @@ def _block(vis, rank, world, by):
 
 def _run_local(kind, rank, world):
     from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng
-    base = {"invert_rows": "invert_mfs", "invert_chans": "invert_cube", "predict_chans": "predict"}
+    base = {"invert_rows": "invert_mfs", "invert_chans": "invert_cube", "predict_chans": "predict",
+            "invert_chans1": "invert_mfsnarrow", "invert_rowseps": "invert_mfs"}
     vis, im = _case(base[kind])
-    mine, t, c = _block(vis, rank, world, kind.split("_")[1])
+    mine, t, c = _block(vis, rank, world, kind.split("_")[1].replace("rowseps", "rows"))
     if kind == "predict_chans":
         return np.asarray(predict_ng(mine, im, shard="local").vis.data), (t.start, t.stop, c.start, c.stop)
+    kw = {}
+    if kind == "invert_rowseps":  # the ranks disagree on epsilon: refused on both
+        kw["epsilon"] = 1e-12 if rank == 0 else 1e-6
+        try:
+            invert_ng(mine, im, normalise=True, shard="local", **kw)
+        except ValueError as e:
+            return ("ValueError", str(e))
+        return ("no error",)
     d, sw = invert_ng(mine, im, normalise=True, shard="local")
     return np.asarray(d["pixels"].data), np.asarray(sw)
 
 
-@pytest.mark.parametrize("kind", ["invert_rows", "invert_chans", "predict_chans"])
+def test_presharded_local_mode_refuses_mismatched_options():
+    """shard="local" checks the call's scalar options across the ranks as
+    well as the image geometry: ranks passing different epsilon would
+    otherwise all-reduce images of different precision."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + int(np.random.default_rng().integers(300, 590))
+    procs = [ctx.Process(target=_local_worker, args=(r, 2, port, "invert_rowseps", q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for _, out, *_ in res:
+        assert out[0] == "ValueError" and "same inputs" in out[1]
+
+
+@pytest.mark.parametrize("kind", ["invert_rows", "invert_chans", "invert_chans1", "predict_chans"])
 @pytest.mark.parametrize("max_call", [None, "1e-8"])
 def test_presharded_local_mode(kind, max_call, monkeypatch):
     """shard="local": each rank passes its OWN block of the observation (its
@@ -302,7 +333,7 @@ def test_presharded_local_mode(kind, max_call, monkeypatch):
     monkeypatch.setattr(kernels, "ms2dirty_vis", _oracle_ms2dirty_vis)
     monkeypatch.setattr(kernels, "dirty2ms_vis", _oracle_dirty2ms_vis)
     ref = _run({"invert_rows": "invert_mfs", "invert_chans": "invert_cube",
-                "predict_chans": "predict"}[kind])
+                "invert_chans1": "invert_mfsnarrow", "predict_chans": "predict"}[kind])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29600 + int(np.random.default_rng().integers(600, 900))

@@ -446,6 +446,42 @@ def test_invert_ng_host_visibility_streamed(eps, tol, monkeypatch):
     assert rel_rms(out["4"][0], ref) < (TOL if eps > 1e-8 else 1e-9)
 
 
+@pytest.mark.parametrize("eps", [1e-6, 1e-12])
+def test_invert_ng_host_visibility_planes_chunked(eps, monkeypatch):
+    """When the w planes cannot all stay resident (a grid budget of one plane,
+    SDP_HIP_GRID_BUDGET_GB), a batch sequence cannot hold them, so the
+    streamed host invert falls back to copying the Visibility whole and one
+    call with chunked planes: the same image and sumwt as the resident
+    call, and the exact sums."""
+    from ska_sdp_func_python_amd import datamodels as dm
+    from ska_sdp_func_python_amd.imaging import invert_ng
+    rng = np.random.default_rng(31)
+    nt, nb, nchan = 6, 50, 3
+    freq = np.linspace(1.0e9, 1.2e9, nchan)
+    umax = 1500.0
+    uvw = rng.uniform(-1, 1, (nt, nb, 3)) * umax * orc.C_LIGHT / freq.max()
+    shape = (nt, nb, nchan, 1)
+    v = rng.normal(size=shape) + 1j * rng.normal(size=shape)
+    vis = vis_from_arrays(uvw, freq, v, weight=rng.uniform(0.5, 2.0, shape),
+                          pf="stokesI", phasecentre=dm.SkyCoord(0.0, -0.6))
+    vis["imaging_weight"] = rng.uniform(0.5, 2.0, shape)
+    npix, cell = 128, 0.4 / umax
+    im = dm.create_image(npix, cell, dm.SkyCoord(0.0, -0.6), frequency=float(freq.mean()),
+                         channel_bandwidth=1e9, nchan=1)
+    monkeypatch.setenv("SDP_HIP_HOST_BLOCKS", "3")
+    d0, sw0 = invert_ng(vis, im, normalise=False, epsilon=eps)
+    monkeypatch.setenv("SDP_HIP_GRID_BUDGET_GB", "0.000001")
+    d1, sw1 = invert_ng(vis, im, normalise=False, epsilon=eps)
+    monkeypatch.delenv("SDP_HIP_GRID_BUDGET_GB")
+    a0, a1 = np.asarray(d0["pixels"].data)[0, 0], np.asarray(d1["pixels"].data)[0, 0]
+    np.testing.assert_allclose(sw1, sw0, rtol=1e-13)
+    assert rel_rms(a1, a0) < (1e-6 if eps > 1e-8 else 1e-12)
+    ms, wgt, fuvw = _prologue_reference(vis, im, False)
+    ref = orc.ms2dirty_exact(fuvw * FLIP_UW, freq, ms[..., 0], wgt[..., 0], npix, npix, cell,
+                             cell, True).T
+    assert rel_rms(a1, ref) < (TOL if eps > 1e-8 else 1e-9)
+
+
 @pytest.mark.parametrize("pf,ipf,dopsf", [("stokesI", "stokesI", False),
                                           ("linear", "stokesIQUV", True),
                                           ("linear", "stokesIQUV", False)])

@@ -284,3 +284,23 @@ def test_groupby_time_groups_distinct_sorted_times():
         np.testing.assert_array_equal(np.asarray(g.time.data), [t] * len(rows[t]))
         np.testing.assert_array_equal(np.asarray(g.vis.data)[:, :, 0, 0],
                                       np.arange(nt * nb).reshape(nt, nb)[rows[t]])
+
+
+def test_groupby_time_skips_non_finite_times():
+    """A row with a NaN (or infinite) time belongs to no group, as xarray's
+    groupby drops NaN labels; the finite times still group as usual."""
+    import numpy as np
+    from ska_sdp_func_python_amd import datamodels as dm
+    times = np.array([3.0, np.nan, 1.0, 3.0, np.inf, 2.0])
+    nt, nb = len(times), 3
+    vis = dm.Visibility.constructor(
+        frequency=np.array([1e9]), channel_bandwidth=np.array([1e6]),
+        phasecentre=dm.SkyCoord(0.0, -0.5), uvw=np.zeros((nt, nb, 3)),
+        time=times, vis=np.arange(nt * nb, dtype=complex).reshape(nt, nb, 1, 1),
+        baselines=np.stack(np.triu_indices(3, 1), 1))
+    groups = vis.groupby("time", squeeze=False)
+    assert [t for t, _ in groups] == [1.0, 2.0, 3.0]
+    rows = {1.0: [2], 2.0: [5], 3.0: [0, 3]}
+    for t, g in groups:
+        np.testing.assert_array_equal(np.asarray(g.vis.data)[:, :, 0, 0],
+                                      np.arange(nt * nb).reshape(nt, nb)[rows[t]])
