@@ -1,0 +1,34 @@
+"""C3's sky-component DFT (1000 point components x 10 Mvis, stokesI, c64
+output) run --reps times: the driver for rocprofv3 PMC passes on k_dft."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func-python_amd"))
+
+import torch  # noqa: E402
+
+from ska_sdp_func_python_amd import kernels  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--ncomp", type=int, default=1000)
+ap.add_argument("--nvis", type=int, default=10_000_000)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev)
+g.manual_seed(3)
+nchan = 10
+nrow = a.nvis // nchan
+uvw = (torch.rand((nrow, 3), dtype=torch.float64, device=dev, generator=g) - 0.5) * 2e4
+uvw[:, 2] *= 0.2
+freq = torch.linspace(1.0e9, 1.2e9, nchan, dtype=torch.float64, device=dev)
+lmn = (torch.rand((a.ncomp, 3), dtype=torch.float64, device=dev, generator=g) - 0.5) * 0.05
+lmn[:, 2] = torch.sqrt(1 - lmn[:, 0] ** 2 - lmn[:, 1] ** 2) - 1
+flux = torch.rand((a.ncomp, 1, 1), dtype=torch.float64, device=dev, generator=g).to(torch.complex128)
+out = torch.empty((nrow, nchan, 1), dtype=torch.complex64, device=dev)
+for _ in range(a.reps):
+    kernels.dft_point(lmn, flux, uvw, freq, out)
+torch.cuda.synchronize()
+print("done", float(out.abs().sum()))
