@@ -1055,34 +1055,8 @@ __device__ __forceinline__ Item load_fine_item(const FineItem *items, uint32_t w
 }
 
 
-// MFMA gridder (invert): one wave per work item = a chunk of the records of
-// a 2 x 8-cell region (16 one-cell buckets, same first plane p0; records
-// ordered by cell).  All records of a cell share their footprint origin, so
-// a cell's contribution to its W x W x W footprint is one GEMM
-//     C[(kx, ky), (q, re/im)] += sum_r  tu_r[kx] tv_r[ky] * tw_r[q] c_r
-// with A = the separable (u, v) taps (64 rows) and B = the w taps x value
-// (8 planes x re/im = 16 columns), K = records: v_mfma_f32_16x16x4_f32
-// (exact fp32 multiply-adds), 4 M-tiles of 16 taps, 4 records per K-step.
-//
-// Records stream through the wave 64 at a time (one per lane, one coalesced
-// 2 KiB load, the next batch prefetched while this one is consumed).  Inside
-// a batch the cell runs are found with ballots; a run is consumed in K-steps
-// of 4 records (lanes k0..k0+3; the tail K-step of a run carries zero
-// values).  In a K-step, lane l gathers the fields of record k0 + (l >> 4)
-// (ds_bpermute) and evaluates its 1-D taps (l & 7) for u, v and w; the MFMA
-// operands are those taps permuted inside the 16-lane record group:
-// A[row][k] = tu[2t + (row >> 3)] tv[row & 7], B[k][col] = tw[col >> 1] x
-// (re | im of c).  When the cell changes, the four 16 x 16 accumulators are
-// added into the region's (2+W-1) x (8+W-1) x W LDS tile, which is flushed
-// once per item with global float atomics (zero cells skipped), exactly as
-// k_grid_reg.  Per record: one MFMA, ~8 VALU, 2.5 ds_bpermute -- versus 24
-// VALU, 7.6 SALU and 4 LDS instructions in k_grid_reg.
+// MFMA kernels' operand types and wave-level helpers
 typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ float bperm(int byte_addr, float v) {
-    return __builtin_bit_cast(float,
-                              __builtin_amdgcn_ds_bpermute(byte_addr, __builtin_bit_cast(int, v)));
-}
 
 // One-wave workgroups: the LDS operations of one wavefront execute in
 // program order, so a hand-off between the wave's own lanes through LDS needs
@@ -1108,184 +1082,6 @@ __device__ __forceinline__ float es_tap(float f, float tihw, float ihw, float bl
     const float e = __builtin_amdgcn_exp2f(
         fmaf(bl, __builtin_amdgcn_sqrtf(W == 8 ? y : fmaxf(y, 0.0f)), -bl));
     return W == 8 ? e : (y > 0.0f ? e : 0.0f);
-}
-
-template <int W, bool WS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma(
-    Geo g, const VisRec *__restrict__ recs, uint32_t n_items, const FineItem *__restrict__ fitems,
-    float *__restrict__ grid, int p_lo, int p_hi) {
-    static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
-    // LDS: the region tile (W planes x RX x RY complex) + the staged batch
-    // (64 records: fu fv fw - | cre cim - - as two float4 rows per record)
-    extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int RX = 2 + W - 1, RY = 8 + W - 1, PS = RX * RY;
-    constexpr int NQ = WS ? W : 1;
-    float4 *const stage = reinterpret_cast<float4 *>(tile + NQ * PS);  // [64][2]
-    const int lane = threadIdx.x;
-    const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const float tihw = (float)(lane & 7) * ihw;
-    const int grp16 = lane & ~15;
-    const int srcA = (grp16 | ((lane >> 3) & 1)) << 2;  // + 8 t bytes: tu tap 2t + (row >> 3)
-    const int srcB = (grp16 | ((lane & 15) >> 1)) << 2;   // tw tap q = col >> 1
-    const bool col_im = lane & 1;
-    // accumulator element i of M-tile t: tap (2t + (lane >> 5), 4 ((lane >> 4) & 1) + i),
-    // column (q, re/im) = ((lane & 15) >> 1, lane & 1)
-    const int cq = (lane & 15) >> 1;
-    const int ckx = lane >> 5, cky = 4 * ((lane >> 4) & 1);
-    float *const ftile = reinterpret_cast<float *>(tile);
-
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        uint32_t fo[1];
-        const Item it = load_fine_item<1>(fitems, w_it, n_items, fo);
-        if (it.b >= it.e) continue;
-        const int ntg = g.wny / 8;  // groups per x pair
-        const int sx = (int)it.tile / ntg, sg = (int)it.tile - sx * ntg;
-        const int ibase = g.wx0 + sx * 2, jbase = g.wy0 + sg * 8;
-
-        wave_lds_sync();
-        for (int i = lane; i < NQ * PS; i += 64) tile[i] = make_float2(0.0f, 0.0f);
-
-        floatx4 acc[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-        int cur = -1;  // cell of the accumulators (wave-uniform)
-        auto flush_cell = [&]() {
-            const int xo = cur & 1, yo = cur >> 1;
-            if (cq < NQ) {
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int kx = 2 * t + ckx;
-                    if (kx >= W) continue;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int ky = cky + i;
-                        if (ky >= W) continue;
-                        float *d = ftile + ((cq * RX + xo + kx) * RY + yo + ky) * 2 + (col_im ? 1 : 0);
-                        *d += acc[t][i];
-                    }
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-        };
-        // one K-step: records k0 .. k0+3 of the staged batch (lane >> 4 picks
-        // the record), valid below `rend`.  Phase 1 (taps): the three 1-D
-        // taps (lane & 7) of the record and its value; phase 2 (gather): the
-        // 5 operand values from the record group's lanes; phase 3: A, B.
-        // Two K-steps are interleaved phase by phase (sched_barrier keeps
-        // every ds_bpermute of both in flight before the first use).
-        struct Taps {
-            float tu, tv, tw, cv;
-        };
-        auto taps = [&](int k0, int rend) {
-            const int kl = k0 + (lane >> 4);
-            const float4 h = stage[2 * min(kl, 63)];      // fu fv fw -
-            const float4 c = stage[2 * min(kl, 63) + 1];  // cre cim - -
-            Taps r;
-            r.tu = es_tap<W>(h.x, tihw, ihw, bl);
-            r.tv = es_tap<W>(h.y, tihw, ihw, bl);
-            r.tw = WS ? es_tap<W>(h.z, tihw, ihw, bl) : ((lane & 7) == 0 ? 1.0f : 0.0f);
-            r.cv = (col_im ? c.y : c.x) * (kl < rend ? 1.0f : 0.0f);
-            return r;
-        };
-        struct Ops {
-            float u[4], w;
-        };
-        auto gather = [&](const Taps &r) {
-            Ops o;
-            o.w = bperm(srcB, r.tw);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) o.u[t] = bperm(srcA + 8 * t, r.tu);
-            return o;
-        };
-        auto mfma4 = [&](const Taps &r, const Ops &o) {
-            const float bop = o.w * r.cv;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(o.u[t] * r.tv, bop, acc[t], 0, 0, 0);
-        };
-
-        // batch = 64 records, lane l holds record b0 + l (staged in LDS); the
-        // next batch is loaded before this one is consumed
-        VisRec nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
-        for (uint32_t b0 = it.b; b0 < it.e; b0 += 64) {
-            const VisRec my = nx;
-            if (b0 + 64 < it.e) nx = recs[min(b0 + 64 + (uint32_t)lane, it.e - 1)];
-            const int nb = (int)min(64u, it.e - b0);
-            const bool live = lane < nb;
-            const int cj = live ? ((int)(my.ij >> 16) - jbase) * 2 + ((int)(my.ij & 0xffffu) - ibase)
-                                : 16;
-            wave_lds_sync();  // previous batch's stage reads
-            stage[2 * lane] = make_float4(my.fu, my.fv, my.fw, 0.0f);
-            stage[2 * lane + 1] = make_float4(live ? my.cre : 0.0f, live ? my.cim : 0.0f, 0.0f, 0.0f);
-            wave_lds_sync();
-            // run starts: lane 0, and every lane whose cell differs from the previous lane's
-            const int prev = __shfl_up(cj, 1);
-            uint64_t starts = __ballot(live && (lane == 0 || prev != cj));
-            while (starts) {
-                const int pos = __builtin_ctzll(starts);
-                starts &= starts - 1;
-                const int rend = starts ? __builtin_ctzll(starts) : nb;
-                const int cell = __builtin_amdgcn_readlane(cj, pos);
-                if (cell != cur) {
-                    if (cur >= 0) flush_cell();
-                    cur = cell;
-                }
-                int k0 = pos;
-                for (; k0 + 4 < rend; k0 += 8) {  // two K-steps
-                    const Taps r0 = taps(k0, rend), r1 = taps(k0 + 4, rend);
-                    __builtin_amdgcn_sched_barrier(0);
-                    const Ops o0 = gather(r0), o1 = gather(r1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    mfma4(r0, o0);
-                    mfma4(r1, o1);
-                }
-                if (k0 < rend) {  // last K-step of the run
-                    const Taps r0 = taps(k0, rend);
-                    __builtin_amdgcn_sched_barrier(0);
-                    const Ops o0 = gather(r0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    mfma4(r0, o0);
-                }
-            }
-        }
-        if (cur >= 0) flush_cell();
-        wave_lds_sync();
-
-        // flush: float f = i0 + lane of each plane's RX x RY complex cells,
-        // buffer atomics off a per-plane descriptor (32-bit offsets), the
-        // cell index advanced incrementally; zero floats are skipped
-        constexpr int FPP = RX * RY * 2;
-        const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
-        int xl = (lane >> 1) / RY, yl = (lane >> 1) - xl * RY;
-#pragma unroll
-        for (int i0 = 0; i0 < FPP; i0 += 64) {
-            const int f = i0 + lane;
-            if (f >= FPP) break;
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            const int voff = ((gx * g.ngy + gy) * 2 + (f & 1)) * (int)sizeof(float);
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int p = (int)it.p0 + q;
-                const float val = ftile[q * PS * 2 + f];
-                if (p >= p_lo && p < p_hi && val != 0.0f) {
-                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                        grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)), 0,
-                        (int)plane_bytes, 0x00020000);
-                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, rs, voff, 0, 0);
-                }
-            }
-            yl += 32 % RY;
-            xl += 32 / RY;
-            if (yl >= RY) {
-                yl -= RY;
-                ++xl;
-            }
-        }
-    }
 }
 
 // MFMA gridder on 4-padded cells (invert, one-cell buckets).  The bucketing
@@ -1366,6 +1162,82 @@ struct CoreAcc {
     double *p;
     int x0, nx, y0, ny;
 };
+
+// Flush of a k_grid_mfma_pad / k_grid_mfma_pc region tile into the planes:
+// the waves of the workgroup (wave wv of nwv) take every nwv-th 64-float
+// slice of each plane.
+template <int W, bool WS, int NG>
+__device__ __forceinline__ void region_flush(const Geo &g, const float *reg, int ibase, int jbase,
+                                             uint32_t p0, int p_lo, int p_hi, const CoreAcc &core,
+                                             float *__restrict__ grid, int lane, int wv, int nwv) {
+    constexpr int NQ = WS ? W : 1;
+    constexpr int kRegY = PadUnit<NG>::RGY;
+    constexpr int RX = PadUnit<NG>::TX + W - 1, RY = PadUnit<NG>::TY + W - 1;
+    // flush: lane l takes float f = i0 + l of a plane's RX x RY cells in
+    // the grid's order (x rows of RY cells, re/im interleaved), i.e.
+    // region float (x * kRegY + y) * 16 + 4 reg_chunk(q >> 1, y) +
+    // 2 (q & 1) + (f & 1); the NQ planes' values are read before any
+    // atomic is issued (one LDS wait per 64 floats, not one per plane);
+    // buffer atomics off a per-plane descriptor (32-bit offsets); zero
+    // floats are dropped by the range check
+    constexpr int FPP = RX * RY * 2;
+    if (core.p != nullptr && ibase >= core.x0 && ibase + RX <= core.x0 + core.nx &&
+        jbase >= core.y0 && jbase + RY <= core.y0 + core.ny) {
+        // the whole region lies in the core window: fp64 atomics into the
+        // companion planes [p - p_lo][x - x0][y - y0] (c128)
+        for (int i0 = 64 * wv; i0 < FPP; i0 += 64 * nwv) {
+            const int f = i0 + lane;
+            if (f >= FPP) break;
+            const int c = f >> 1, xl = c / RY, yl = c - xl * RY;
+            const size_t cell = (size_t)(ibase + xl - core.x0) * core.ny + (jbase + yl - core.y0);
+            const float *src = reg + (xl * kRegY + yl) * kRegCell + (f & 1);
+            float vals[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) vals[q] = src[4 * reg_chunk(q >> 1, yl) + 2 * (q & 1)];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int p = (int)p0 + q;
+                if (vals[q] != 0.0f && p >= p_lo && p < p_hi)
+                    unsafeAtomicAdd(core.p + ((size_t)(p - p_lo) * core.nx * core.ny + cell) * 2 +
+                                        (f & 1),
+                                    (double)vals[q]);
+            }
+        }
+        return;
+    }
+    const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
+    // one buffer descriptor per plane (scalar registers); a plane outside
+    // [p_lo, p_hi) gets an empty range, and a zero float an offset past
+    // the plane, so the buffer range check drops those atomics: no branch
+    __amdgpu_buffer_rsrc_t prs[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int p = (int)p0 + q;
+        const bool in = p >= p_lo && p < p_hi;
+        prs[q] = __builtin_amdgcn_make_buffer_rsrc(
+            in ? grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)) : grid, 0,
+            in ? (int)plane_bytes : 0, 0x00020000);
+    }
+#pragma unroll
+    for (int i0 = 64 * wv; i0 < FPP; i0 += 64 * nwv) {
+        const int f = i0 + lane;
+        if (f >= FPP) break;
+        const int c = f >> 1, xl = c / RY, yl = c - xl * RY;
+        int gx = ibase + xl;
+        if (gx >= g.ngx) gx -= g.ngx;
+        int gy = jbase + yl;
+        if (gy >= g.ngy) gy -= g.ngy;
+        const int voff = ((gx * g.ngy + gy) * 2 + (f & 1)) * (int)sizeof(float);
+        const float *src = reg + (xl * kRegY + yl) * kRegCell + (f & 1);
+        float vals[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) vals[q] = src[4 * reg_chunk(q >> 1, yl) + 2 * (q & 1)];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+                vals[q], prs[q], vals[q] != 0.0f ? voff : kDropOff, 0, 0);
+    }
+}
 
 template <int W, bool WS, int NG>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void k_grid_mfma_pad(
@@ -1567,70 +1439,221 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
         }
         wave_lds_sync();
 
-        // flush: lane l takes float f = i0 + l of a plane's RX x RY cells in
-        // the grid's order (x rows of RY cells, re/im interleaved), i.e.
-        // region float (x * kRegY + y) * 16 + 4 reg_chunk(q >> 1, y) +
-        // 2 (q & 1) + (f & 1); the NQ planes' values are read before any
-        // atomic is issued (one LDS wait per 64 floats, not one per plane);
-        // buffer atomics off a per-plane descriptor (32-bit offsets); zero
-        // floats are dropped by the range check
-        constexpr int FPP = RX * RY * 2;
-        if (core.p != nullptr && ibase >= core.x0 && ibase + RX <= core.x0 + core.nx &&
-            jbase >= core.y0 && jbase + RY <= core.y0 + core.ny) {
-            // the whole region lies in the core window: fp64 atomics into the
-            // companion planes [p - p_lo][x - x0][y - y0] (c128)
-            for (int i0 = 0; i0 < FPP; i0 += 64) {
-                const int f = i0 + lane;
-                if (f >= FPP) break;
-                const int c = f >> 1, xl = c / RY, yl = c - xl * RY;
-                const size_t cell = (size_t)(ibase + xl - core.x0) * core.ny + (jbase + yl - core.y0);
-                const float *src = reg + (xl * kRegY + yl) * kRegCell + (f & 1);
-                float vals[NQ];
+        region_flush<W, WS, NG>(g, reg, ibase, jbase, p0, p_lo, p_hi, core, grid, lane, 0, 1);
+    }
+}
+
+// Producer / consumer form of k_grid_mfma_pad: two waves per work item.
+// Wave 0 (producer) streams the item's records, decodes them and evaluates
+// each 16-record block's taps into one of two LDS tap buffers; wave 1
+// (consumer) runs the block's K-steps from the other buffer -- the operand
+// reads, 4 MFMAs per K-step and the accumulators' cell changes in the region
+// tile, exactly as k_grid_mfma_pad.  One workgroup barrier per block hands
+// the buffers over:
+//   iteration i:  the producer fills buffer i & 1 with block i,
+//                 the consumer runs block i - 1 from buffer (i - 1) & 1;  barrier
+// so a block's tap evaluation (VALU and transcendental) runs on one wave
+// while the previous block's MFMAs run on the other, instead of one wave
+// issuing both in order.  With each block the producer passes the number of
+// its K-steps and each K-step's region cell (x | y << 8).  Both waves zero
+// and flush the region.
+template <int NG>
+constexpr int pc_buf_floats() {  // taps, values, meta (K-steps, 4 cell keys, pad)
+    return kTapBatch * kTapRec + kTapBatch * 2 + 8;
+}
+template <int NG>
+constexpr size_t grid_pc_lds() {
+    return (size_t)PadUnit<NG>::RGX * PadUnit<NG>::RGY * kRegCell * sizeof(float) +
+           kTapBatch * sizeof(float4) + 2 * (size_t)pc_buf_floats<NG>() * sizeof(float);
+}
+
+template <int W, bool WS, int NG>
+__global__ __launch_bounds__(128) void k_grid_mfma_pc(Geo g, const RecC *__restrict__ recs,
+                                                      const FineItem *__restrict__ items,
+                                                      uint32_t n_items, float *__restrict__ grid,
+                                                      int p_lo, int p_hi, CoreAcc core) {
+    static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    constexpr int kRegX = PadUnit<NG>::RGX, kRegY = PadUnit<NG>::RGY;
+    constexpr int kBuf = pc_buf_floats<NG>();
+    float *const reg = reinterpret_cast<float *>(tile);  // [kRegX][kRegY][16]
+    float4 *const stage = reinterpret_cast<float4 *>(reg + kRegX * kRegY * kRegCell);
+    float *const bufs = reinterpret_cast<float *>(stage + kTapBatch);  // 2 x kBuf
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float ihw = g.inv_half_w, bl = g.beta_l2e;
+    const float fbase = 1.0f - 0.5f * (float)W;  // RecC offset origin
+    // producer: tap t = lane & 7 of records 8m + (lane >> 3)
+    const int tt = lane & 7;
+    const float tihw = (float)tt * ihw;
+    const int wu = (tt & 1) * 4 + (tt >> 1), wv_ = 8 + tt, ww = 16 + tt;
+    // consumer: operand and accumulator addressing of k_grid_mfma_pad
+    const int kBo = (lane >> 4) * kTapRec + ((lane >> 3) & 1) * 4;
+    const int kVo = (lane >> 4) * kTapRec + 8 + (lane & 7);
+    const int kWo = (lane >> 4) * kTapRec + 16 + ((lane & 15) >> 1);
+    const int kCo = kTapBatch * kTapRec + (lane >> 4) * 2 + (lane & 1);
+    const int acc_lane = (((lane & 15) >> 3) * kRegY) * kRegCell;
+    const int acc_y = lane & 7, acc_k = lane >> 4;
+    constexpr int acc_t = 2 * kRegY * kRegCell;
+
+    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
+        const uint32_t u = NG == 1 ? w_it : item_index(w_it, n_items);
+        uint32_t bnd[kGroupCell];
+        Item it = NG == 1 ? load_fine_item<kGroupCell>(items, w_it, n_items, bnd)
+                          : load_fine_item<kGroupCell>(items + (size_t)u * NG, 0, 1, bnd);
+        if (NG == 1 && it.b >= it.e) continue;
+        int ibase, jbase;
+        group_origin(g, (int)it.tile, ibase, jbase);
+        const uint32_t p0 = it.p0;
+        // blocks of the unit: its groups' padded records in 16-record blocks
+        uint32_t nblk = 0;
+        if (NG == 1) {
+            nblk = (it.e - it.b + kTapBatch - 1) / kTapBatch;
+        } else {
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) vals[q] = src[4 * reg_chunk(q >> 1, yl) + 2 * (q & 1)];
+            for (int gi = 0; gi < NG; ++gi) {
+                const FineItem *fi = items + (size_t)u * NG + gi;
+                const uint32_t b = __builtin_amdgcn_readfirstlane(fi->b),
+                               e = __builtin_amdgcn_readfirstlane(fi->e);
+                nblk += (e - b + kTapBatch - 1) / kTapBatch;
+            }
+        }
+        RecC nx;
+        if (wv == 0 && it.b < it.e) nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
+
+        __syncthreads();  // the previous item's flush reads of the region
+        {
+            constexpr int kZ = kRegX * kRegY * kRegCell / 4;  // float4s
+            float4 *r4 = reinterpret_cast<float4 *>(reg);
+            for (int i = threadIdx.x; i < kZ; i += 128) r4[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+        __syncthreads();
+
+        if (wv == 0) {
+            // ---- producer ----
+            uint32_t blk = 0;
+            for (int gi = 0; gi < NG; ++gi) {
+                if (NG > 1 && gi > 0) it = load_fine_item<kGroupCell>(items + (size_t)u * NG + gi, 0, 1, bnd);
+                const uint32_t rb = it.b, re = it.e;
+                if (rb >= re) continue;
+                const int gxo = NG == 1 ? 0 : 2 * (gi >> 1), gyo = NG == 1 ? 0 : 8 * (gi & 1);
+                if (gi > 0) nx = recs[min(rb + (uint32_t)lane, re - 1)];
+                for (uint32_t b0 = rb; b0 < re; b0 += 64) {
+                    const RecC my = nx;
+                    if (b0 + 64 < re) nx = recs[min(b0 + 64 + (uint32_t)lane, re - 1)];
+                    const int nb = (int)min(64u, re - b0);  // a multiple of 4
+                    const uint32_t ri = b0 + (uint32_t)lane;
+                    int cj = 0;
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const int p = (int)p0 + q;
-                    if (vals[q] != 0.0f && p >= p_lo && p < p_hi)
-                        unsafeAtomicAdd(core.p + ((size_t)(p - p_lo) * core.nx * core.ny + cell) * 2 +
-                                            (f & 1),
-                                        (double)vals[q]);
+                    for (int c = 0; c < kGroupCell - 1; ++c) cj += ri >= bnd[c] ? 1 : 0;
+                    const int key = (gxo + (cj & 1)) | ((gyo + (cj >> 1)) << 8);
+                    const float fu = fbase - (float)(my.lo & 0x1fffffu) * 0x1p-21f;
+                    const float fv =
+                        fbase - (float)((my.lo >> 21) | ((my.hi & 0x3ffu) << 11)) * 0x1p-21f;
+                    const float fw = fbase - (float)(my.hi >> 10) * 0x1p-22f;
+                    for (int h = 0; h < 64 / kTapBatch; ++h) {
+                        const int nbh = min(kTapBatch, nb - kTapBatch * h);
+                        if (nbh <= 0) break;
+                        float *const B = bufs + (blk & 1) * kBuf;
+                        wave_lds_sync();  // the previous block's stage reads
+                        if (lane / kTapBatch == h) {
+                            const int r = lane % kTapBatch;
+                            stage[r] = make_float4(fu, fv, fw, 0.0f);
+                            reinterpret_cast<float2 *>(B + kTapBatch * kTapRec)[r] =
+                                make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
+                        }
+                        // the block's K-step count and each K-step's cell
+                        int *const meta = reinterpret_cast<int *>(B + kTapBatch * kTapRec + kTapBatch * 2);
+                        const int kj = (lane - kTapBatch * h) >> 2;
+                        if (lane >= kTapBatch * h && lane < kTapBatch * h + nbh && (lane & 3) == 0)
+                            meta[1 + kj] = key;
+                        if (lane == 0) meta[0] = nbh >> 2;
+                        wave_lds_sync();
+                        float4 f[kTapBatch / 8];
+#pragma unroll
+                        for (int m = 0; m < kTapBatch / 8; ++m) f[m] = stage[8 * m + (lane >> 3)];
+                        float tv_[kTapBatch / 8][3];
+#pragma unroll
+                        for (int m = 0; m < kTapBatch / 8; ++m) {
+                            tv_[m][0] = es_tap<W>(f[m].x, tihw, ihw, bl);
+                            tv_[m][1] = es_tap<W>(f[m].y, tihw, ihw, bl);
+                            tv_[m][2] = WS ? es_tap<W>(f[m].z, tihw, ihw, bl) : (tt == 0 ? 1.0f : 0.0f);
+                        }
+#pragma unroll
+                        for (int m = 0; m < kTapBatch / 8; ++m) {
+                            float *d = B + ((lane >> 3) + 8 * m) * kTapRec;
+                            d[wu] = tv_[m][0];
+                            d[wv_] = tv_[m][1];
+                            d[ww] = tv_[m][2];
+                        }
+                        __syncthreads();  // block blk ready; the consumer is done with block blk - 1
+                        ++blk;
+                    }
                 }
             }
-            continue;
+            __syncthreads();  // (the consumer's last block)
+        } else {
+            // ---- consumer ----
+            floatx4 acc[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+            // zeros bound to a (zero) region slot: the store before the first
+            // cell's load needs no test
+            int cbase = acc_y * kRegCell + acc_lane + 4 * reg_chunk(acc_k, acc_y);
+            int cur = -1;
+            __syncthreads();  // block 0 ready
+            for (uint32_t blk = 0; blk < nblk; ++blk) {
+                const float *const B = bufs + (blk & 1) * kBuf;
+                const int *const meta = reinterpret_cast<const int *>(B + kTapBatch * kTapRec + kTapBatch * 2);
+                const int nk = __builtin_amdgcn_readfirstlane(meta[0]);
+                int keys[kTapBatch / 4];
+#pragma unroll
+                for (int jj = 0; jj < kTapBatch / 4; ++jj)
+                    keys[jj] = __builtin_amdgcn_readfirstlane(meta[1 + jj]);
+                struct Ops {
+                    floatx4 b;
+                    float v, w, c;
+                };
+                Ops o[kTapBatch / 4];
+#pragma unroll
+                for (int jj = 0; jj < kTapBatch / 4; ++jj) {
+                    o[jj].b = *reinterpret_cast<const floatx4 *>(B + kBo + 4 * jj * kTapRec);
+                    o[jj].v = B[kVo + 4 * jj * kTapRec];
+                    o[jj].w = B[kWo + 4 * jj * kTapRec];
+                    o[jj].c = B[kCo + 8 * jj];
+                }
+#pragma unroll
+                for (int jj = 0; jj < kTapBatch / 4; ++jj) {
+                    if (jj < nk) {
+                        if (keys[jj] != cur) {
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                *reinterpret_cast<floatx4 *>(reg + cbase + t * acc_t) = acc[t];
+                            cur = keys[jj];
+                            const int xo = cur & 255, y = (cur >> 8) + acc_y;
+                            cbase = (xo * kRegY + y) * kRegCell + acc_lane + 4 * reg_chunk(acc_k, y);
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                acc[t] = *reinterpret_cast<const floatx4 *>(reg + cbase + t * acc_t);
+                        }
+                        const float a = o[jj].w * o[jj].c;
+                        float bt[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) bt[t] = o[jj].b[t] * o[jj].v;
+#pragma unroll
+                        for (int t = 0; t < 4; ++t)
+                            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bt[t], acc[t], 0, 0, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x0002, 5, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x0008, 4, 0);
+                    }
+                }
+                __syncthreads();  // block blk consumed; block blk + 1 ready
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) *reinterpret_cast<floatx4 *>(reg + cbase + t * acc_t) = acc[t];
         }
-        const size_t plane_bytes = (size_t)g.ngx * g.ngy * sizeof(float2);
-        // one buffer descriptor per plane (scalar registers); a plane outside
-        // [p_lo, p_hi) gets an empty range, and a zero float an offset past
-        // the plane, so the buffer range check drops those atomics: no branch
-        __amdgpu_buffer_rsrc_t prs[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int p = (int)p0 + q;
-            const bool in = p >= p_lo && p < p_hi;
-            prs[q] = __builtin_amdgcn_make_buffer_rsrc(
-                in ? grid + (size_t)(p - p_lo) * (plane_bytes / sizeof(float)) : grid, 0,
-                in ? (int)plane_bytes : 0, 0x00020000);
-        }
-#pragma unroll
-        for (int i0 = 0; i0 < FPP; i0 += 64) {
-            const int f = i0 + lane;
-            if (f >= FPP) break;
-            const int c = f >> 1, xl = c / RY, yl = c - xl * RY;
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            const int voff = ((gx * g.ngy + gy) * 2 + (f & 1)) * (int)sizeof(float);
-            const float *src = reg + (xl * kRegY + yl) * kRegCell + (f & 1);
-            float vals[NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) vals[q] = src[4 * reg_chunk(q >> 1, yl) + 2 * (q & 1)];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q)
-                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
-                    vals[q], prs[q], vals[q] != 0.0f ? voff : kDropOff, 0, 0);
-        }
+        __syncthreads();  // the region complete
+        region_flush<W, WS, NG>(g, reg, ibase, jbase, p0, p_lo, p_hi, core, grid, lane, wv, 2);
     }
 }
 
@@ -1664,6 +1687,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
 // lane stores, without a branch: lanes past the batch's records write to a
 // per-block slot of `sink` (a skipped store left the record wait behind the
 // previous batch's store), and the 4 lanes of a record write the same value.
+#ifndef SDP_DG_STORE
+#define SDP_DG_STORE 0  // (A/B builds: 1 = one lane per record, 2 = masked store)
+#endif
 constexpr int kDegridSinkBlocks = 4096;  // sink slots (x 64 lanes)
 __device__ float4 g_zero16[1];            // 16 zero bytes (never written)
 template <int W, bool WS>
@@ -1806,8 +1832,15 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
             sr += __shfl_xor(sr, 32);
             si += __shfl_xor(si, 32);
             if constexpr (VD) {
+#if SDP_DG_STORE == 1
+                float2 *const dst = (valid && kg == 0) ? out + idx : dump;
+                *dst = make_float2(cre * sr - cim * si, cre * si + cim * sr);
+#elif SDP_DG_STORE == 2
+                if (valid && kg == 0) out[idx] = make_float2(cre * sr - cim * si, cre * si + cim * sr);
+#else
                 float2 *const dst = valid ? out + idx : dump;
                 *dst = make_float2(cre * sr - cim * si, cre * si + cim * sr);
+#endif
             } else {
                 float2 *const dst = valid ? out + ri : dump;
                 float2 v = *dst;
@@ -2233,7 +2266,7 @@ __global__ void k_bucket_f64(Geo g, int64_t nvis, const double *__restrict__ uvw
 //   k_t_binscan   one workgroup: record and item bases of the bins, the
 //                 metadata the host reads (the only host sync)
 //   k_t_cellfin   per bin: cell bases, pad records, FineItem work items
-//   k_t_final     per chunk: records moved to their cell (LDS cursors
+//   k_t_final_s   per chunk: records moved to their cell (LDS cursors
 //                 seeded with the cell base + the chunk's prefix)
 // The writes of the two scatter passes land in runs inside the few bins /
 // cells a workgroup touches at a time, not at random addresses.
@@ -2242,7 +2275,10 @@ constexpr int kTThreads = 1024;     // second-level kernels, bin scans
 constexpr int kT1Threads = 512;     // count and value passes (VGPR-limited occupancy)
 constexpr unsigned kTChunk = 131072;  // records per second-level chunk
 constexpr unsigned kTSeg = 16;       // chunks per segment of the cells' column prefix
-constexpr int kTU = 2;               // visibilities per lane in flight (count / value pass)
+#ifndef SDP_TU
+#define SDP_TU 2
+#endif
+constexpr int kTU = SDP_TU;          // visibilities per lane in flight (value pass)
 #ifndef SDP_TUC
 #define SDP_TUC 2
 #endif
@@ -2284,9 +2320,22 @@ __device__ __forceinline__ unsigned lds_run_add(unsigned key, bool valid, unsign
 struct TLoad {
     uint32_t row, chan;
     double um, vm, wm, s, wd;  // s = frequency / c (fsc[chan]: the same division as vis_coord)
+    double keep;               // 1 - flag of the weight's pol (1 without flags)
     bool live;
 };
 
+// The weight and flag element types are compile-time in the two-level
+// passes -- WT: 4 = f32, 8 = f64 (no weights: a device 1.0f with zero
+// strides); FB: 0 = no flags, 1 = int8, 8 = int64 flags (int32 flags are
+// widened to int64 first, k_widen_flags) -- and a lane's visibilities load
+// from clamped, in-bounds
+// indices with no branch before their first use: all of a lane's kTU
+// visibilities' loads (uvw, frequency scale, weight, flag, and in the value
+// pass the visibility) are in flight together.  A runtime switch on the
+// types, with each load behind its own branch and a `live` test, had put a
+// wait for every load before the next one issued (C2 count pass: ~200
+// instructions and four serialised memory round trips per visibility).
+template <int WT, int FB>
 __device__ __forceinline__ TLoad t_load(const Geo &g, int64_t v, int64_t vend,
                                         const double *__restrict__ uvw, int64_t rs,
                                         const double *__restrict__ fsc,
@@ -2294,7 +2343,7 @@ __device__ __forceinline__ TLoad t_load(const Geo &g, int64_t v, int64_t vend,
                                         const VisExtra &x) {
     TLoad L;
     L.live = v < vend;
-    const uint32_t v32 = L.live ? (uint32_t)v : 0u, nc = (uint32_t)g.nchan;
+    const uint32_t v32 = (uint32_t)(L.live ? v : vend - 1), nc = (uint32_t)g.nchan;
     // row = v / nchan through the fp64 reciprocal (exact to one step, then
     // corrected), not an integer division
     uint32_t r32 = (uint32_t)((double)v32 * g.inv_nchan);
@@ -2302,18 +2351,41 @@ __device__ __forceinline__ TLoad t_load(const Geo &g, int64_t v, int64_t vend,
     else if ((uint64_t)(r32 + 1u) * nc <= v32) ++r32;
     L.row = r32;
     L.chan = v32 - r32 * nc;
-    L.um = L.vm = L.wm = 0.0;
-    L.s = 1.0;
-    L.wd = 0.0;
-    if (L.live) {
-        const double *p = uvw + (int64_t)L.row * rs;
-        L.um = p[0];
-        L.vm = p[1];
-        L.wm = p[2];
-        L.s = fsc[L.chan];
-        L.wd = eff_weight(wgt, wrs, wcs, x, L.row, L.chan);
+    const double *p = uvw + (int64_t)L.row * rs;
+    L.um = p[0];
+    L.vm = p[1];
+    L.wm = p[2];
+    L.s = fsc[L.chan];
+    double w;
+    const int64_t wi = (int64_t)L.row * wrs + (int64_t)L.chan * wcs;
+    if constexpr (WT == 8) w = static_cast<const double *>(wgt)[wi];
+    else w = (double)static_cast<const float *>(wgt)[wi];
+    L.keep = 1.0;
+    if constexpr (FB != 0) {
+        using FT = typename std::conditional<FB == 8, int64_t, int8_t>::type;
+        L.keep = 1.0 - (double)static_cast<const FT *>(
+                           x.flags)[(int64_t)L.row * x.frs + (int64_t)L.chan * x.fcs + x.fpol * x.fps];
+        // select, not multiply: a flagged sample's weight is an exact zero
+        // even when the stored weight is NaN or Inf
+        w = L.keep == 0.0 ? 0.0 : w * L.keep;
     }
+    L.wd = L.live ? w : 0.0;
     return L;
+}
+
+// int32 flags of a two-level pass as int64 (FB = 8): a contiguous
+// [nrow, nchan, npol] copy (one element for a zero-stride broadcast)
+__device__ float g_unit_weight = 1.0f;  // the weights of a call without weights
+template <class FT>
+__global__ void k_widen_flags(const FT *__restrict__ src, int64_t frs, int64_t fcs, int64_t fps,
+                              int64_t nrow, int nchan, int npol, int64_t *__restrict__ dst) {
+    const int64_t n = nrow * nchan * (int64_t)npol;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t rc = i / npol, row = rc / nchan;
+        const int pol = (int)(i - rc * npol), chan = (int)(rc - row * nchan);
+        dst[i] = (int64_t)src[row * frs + chan * fcs + pol * fps];
+    }
 }
 
 // frequency / c per channel (the division vis_coord performs per visibility)
@@ -2363,6 +2435,7 @@ __device__ __forceinline__ void t_weight_sum(double ws, double *sw_slots) {
                   ws);
 }
 
+template <int WT, int FB>
 __global__ __launch_bounds__(kT1Threads) void k_t_count(Geo g, int64_t nvis, int64_t vpw,
                                                        const double *__restrict__ uvw, int64_t rs,
                                                        const double *__restrict__ fsc,
@@ -2381,8 +2454,8 @@ __global__ __launch_bounds__(kT1Threads) void k_t_count(Geo g, int64_t nvis, int
         TLoad L[kTUc];
 #pragma unroll
         for (int u = 0; u < kTUc; ++u)
-            L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, fsc, wgt, wrs, wcs,
-                          x);
+            L[u] = t_load<WT, FB>(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, fsc, wgt,
+                                  wrs, wcs, x);
 #pragma unroll
         for (int u = 0; u < kTUc; ++u) {
             const TPoint p = t_classify<true>(g, L[u], x, nbad);
@@ -2470,28 +2543,50 @@ __global__ __launch_bounds__(kTThreads) void k_t_bins(int nb, const unsigned *__
     }
 }
 
-// the visibility's value (phase 1 of the value pass: loads only)
-template <class VT, int KIND, bool kGrid>
+// the visibility's value in two phases: `load` issues the loads (the
+// visibility from clamped indices, beside the lane's other loads), `value`
+// combines them after every load is in flight.  Without a pol conversion the
+// weight pol's flag (TLoad::keep) masks it; a pol conversion (x.conv, the
+// 4-pol frames) reads its pols and flags in `value`.
+template <class VT, int KIND, bool kGrid, int FB>
 struct TVal {
     using type = typename std::conditional<KIND >= 2, double2, float2>::type;
-    __device__ static __forceinline__ type load(const VT *vis, int64_t vrs, int64_t vcs,
-                                                const VisExtra &x, const TLoad &L) {
+    __device__ static __forceinline__ VT load(const VT *vis, int64_t vrs, int64_t vcs,
+                                              const VisExtra &x, const TLoad &L) {
+        VT raw{};
+        if constexpr (kGrid)
+            if (vis && !x.conv) raw = vis[(int64_t)L.row * vrs + (int64_t)L.chan * vcs];
+        return raw;
+    }
+    __device__ static __forceinline__ type value(const VT *vis, int64_t vrs, int64_t vcs,
+                                                 const VisExtra &x, const TLoad &L, VT raw) {
         type xv;
         xv.x = 1;
         xv.y = 0;
         if constexpr (kGrid) {
-            if constexpr (KIND >= 2) {
-                if (vis && L.live && L.wd != 0.0) xv = eff_vis_d(vis, vrs, vcs, x, L.row, L.chan);
+            if (!vis) return xv;  // (unit visibilities: the PSF)
+            if (x.conv) {
+                if constexpr (KIND >= 2) return eff_vis_d(vis, vrs, vcs, x, L.row, L.chan);
+                else return eff_vis(vis, vrs, vcs, x, L.row, L.chan);
+            }
+            const double2 v = make_double2((double)raw.x, (double)raw.y);
+            if constexpr (FB == 0) {
+                xv.x = v.x;
+                xv.y = v.y;
             } else {
-                if (vis && L.live && (float)L.wd != 0.0f) xv = eff_vis(vis, vrs, vcs, x, L.row, L.chan);
+                // select, not multiply: a NaN in a flagged visibility must not
+                // reach the image
+                const double m = L.keep;
+                xv.x = m == 0.0 ? 0.0 : v.x * m;
+                xv.y = m == 0.0 ? 0.0 : v.y * m;
             }
         }
         return xv;
     }
 };
 
-// KIND 0: RecC (4-padded invert), 1: VisRec (fp32 predict), 2: VisRec64,
-// 3: Rec64 (the fp64 MFMA kernels)
+// KIND 0: RecC (4-padded invert), 1: VisRec (fp32 predict), 3: Rec64 (the
+// fp64 MFMA kernels)
 template <int KIND>
 struct TRec;
 template <>
@@ -2501,10 +2596,6 @@ struct TRec<0> {
 template <>
 struct TRec<1> {
     using type = VisRec;
-};
-template <>
-struct TRec<2> {
-    using type = VisRec64;
 };
 template <>
 struct TRec<3> {
@@ -2537,30 +2628,15 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x, const T
             cr = r_;
             ci = i_;
         }
-        if constexpr (KIND == 3) {
-            Rec64 rec;
-            rec.cre = cr;
-            rec.cim = ci;
-            rec.du = p.c.du;
-            rec.dv = p.c.dv;
-            rec.dw = p.c.dw;
-            rec.idx = (uint32_t)(L.row * (uint32_t)g.nchan + L.chan);
-            rec.pad = 0u;
-            static_cast<Rec64 *>(out)[pos] = rec;
-            return;
-        } else {
-        VisRec64 rec;
+        Rec64 rec;
         rec.cre = cr;
         rec.cim = ci;
         rec.du = p.c.du;
         rec.dv = p.c.dv;
         rec.dw = p.c.dw;
-        rec.ij = (uint32_t)p.c.ic0 | ((uint32_t)p.c.jc0 << 16);
-        rec.p0 = (uint32_t)p.c.p0;
         rec.idx = (uint32_t)(L.row * (uint32_t)g.nchan + L.chan);
         rec.pad = 0u;
-        static_cast<VisRec64 *>(out)[pos] = rec;
-        }
+        static_cast<Rec64 *>(out)[pos] = rec;
     } else {
         const float wt = (float)p.wd;
         float cr = wt, ci = 0.0f;
@@ -2601,14 +2677,14 @@ __device__ __forceinline__ void t_write(const Geo &g, const VisExtra &x, const T
     }
 }
 
-template <class VT, int KIND, bool kGrid>
+template <class VT, int KIND, bool kGrid, int WT, int FB>
 __global__ __launch_bounds__(kT1Threads) void k_t_scatter(
     Geo g, int64_t nvis, int64_t vpw, const double *__restrict__ uvw, int64_t rs,
     const double *__restrict__ fsc, const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
     const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x, double *sw_slots,
     const unsigned *__restrict__ binbase, const unsigned *__restrict__ m1, void *__restrict__ out,
     uint16_t *__restrict__ lkey) {
-    using V = TVal<VT, KIND, kGrid>;
+    using V = TVal<VT, KIND, kGrid, FB>;
     extern __shared__ unsigned cur[];
     const int nb = g.nbins;
     const unsigned *row = m1 + (size_t)blockIdx.x * nb;
@@ -2618,21 +2694,22 @@ __global__ __launch_bounds__(kT1Threads) void k_t_scatter(
     double ws = 0.0;
     for (int64_t base = v0; base < v1; base += (int64_t)kT1Threads * kTU) {
         TLoad L[kTU];
-        typename V::type xv[kTU];
+        VT raw[kTU];
 #pragma unroll
         for (int u = 0; u < kTU; ++u) {
-            L[u] = t_load(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, fsc, wgt, wrs, wcs,
-                          x);
-            xv[u] = V::load(vis, vrs, vcs, x, L[u]);
+            L[u] = t_load<WT, FB>(g, base + u * kT1Threads + threadIdx.x, v1, uvw, rs, fsc, wgt,
+                                  wrs, wcs, x);
+            raw[u] = V::load(vis, vrs, vcs, x, L[u]);
         }
 #pragma unroll
         for (int u = 0; u < kTU; ++u) {
+            const typename V::type xv = V::value(vis, vrs, vcs, x, L[u], raw[u]);
             const TPoint p = t_classify<false>(g, L[u], x, nullptr);
             ws += p.wd;
             const unsigned key = p.in ? tiled_key(g, p.c) : 0u;
             const unsigned pos = lds_run_add<true>(key >> 12, p.in, cur);
             if (p.in) {
-                t_write<KIND, kGrid>(g, x, L[u], p, xv[u], out, pos);
+                t_write<KIND, kGrid>(g, x, L[u], p, xv, out, pos);
                 lkey[pos] = (uint16_t)(key & (kBinCells - 1));
             }
         }
@@ -2831,13 +2908,7 @@ __global__ __launch_bounds__(256) void k_t_cellfin(const Geo g, const unsigned *
             if (PAD && r != n[j]) {
                 // zero-valued pads with in-range offsets (finite taps): RecC
                 // fractions 0 (offset 1 - W/2), or VisRec64 offsets 1 - W/2
-                if constexpr (KIND == 2) {
-                    VisRec64 z;
-                    z.cre = z.cim = 0.0;
-                    z.du = z.dv = z.dw = 1.0 - 0.5 * g.W;
-                    z.ij = z.p0 = z.idx = z.pad = 0u;
-                    for (unsigned i = run + n[j]; i < run + r; ++i) static_cast<VisRec64 *>(recs)[i] = z;
-                } else if constexpr (KIND == 3) {
+                if constexpr (KIND == 3) {
                     Rec64 z;
                     z.cre = z.cim = 0.0;
                     z.du = z.dv = z.dw = 1.0 - 0.5 * g.W;
@@ -2868,60 +2939,7 @@ __global__ __launch_bounds__(256) void k_t_cellfin(const Geo g, const unsigned *
     }
 }
 
-// per chunk: each record to its cell, at the cell base + the segment's
-// prefix + the chunk's prefix inside its segment + its rank among the
-// chunk's records of that cell (LDS cursors)
-template <int KIND>
-__global__ __launch_bounds__(kTThreads) void k_t_final(const TChunk *__restrict__ chunks,
-                                                       const unsigned *__restrict__ meta_ch,
-                                                       const uint16_t *__restrict__ lkey,
-                                                       const unsigned *__restrict__ m2,
-                                                       const unsigned *__restrict__ stot,
-                                                       const unsigned *__restrict__ cbase,
-                                                       const void *__restrict__ in,
-                                                       void *__restrict__ out) {
-    using R = typename TRec<KIND>::type;
-    constexpr int NW = (int)(sizeof(R) / sizeof(uint4));
-    __shared__ unsigned cur[kBinCells];
-    const unsigned n = meta_ch[0];
-    const uint4 *src = reinterpret_cast<const uint4 *>(in);
-    uint4 *dst = reinterpret_cast<uint4 *>(out);
-    for (unsigned c = blockIdx.x; c < n; c += gridDim.x) {
-        const TChunk t = chunks[c];
-        const unsigned *pre = m2 + (size_t)c * kBinCells;
-        const unsigned *sp = stot + (size_t)t.seg * kBinCells;
-        const unsigned *cb = cbase + (size_t)t.bin * kBinCells;
-        for (int i = threadIdx.x; i < kBinCells; i += kTThreads) cur[i] = cb[i] + sp[i] + pre[i];
-        __syncthreads();
-        for (uint32_t i0 = t.b; i0 < t.e; i0 += kTThreads * kTU2) {
-            uint4 r[kTU2][NW];
-            unsigned k[kTU2];
-            // loads from a clamped index (the chunk is never empty): the
-            // records then stay in VGPRs; behind `if (i < t.e)` the compiler
-            // kept them in scratch between the two loops
-#pragma unroll
-            for (int u = 0; u < kTU2; ++u) {
-                const uint32_t i = i0 + u * kTThreads + threadIdx.x, ic = min(i, t.e - 1u);
-                k[u] = lkey[ic];
-                if (i >= t.e) k[u] = 0xffffu;
-#pragma unroll
-                for (int q = 0; q < NW; ++q) r[u][q] = src[(size_t)ic * NW + q];
-            }
-#pragma unroll
-            for (int u = 0; u < kTU2; ++u) {
-                const bool ok = k[u] != 0xffffu;
-                const unsigned pos = lds_run_add<true>(k[u], ok, cur);
-                if (ok) {
-#pragma unroll
-                    for (int q = 0; q < NW; ++q) dst[(size_t)pos * NW + q] = r[u][q];
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// k_t_final with the batch's writes coalesced: each batch of NB records is
+// k_t_final_s, the final move of the two-level sort: each batch of NB records is
 // counting-sorted by cell in LDS (batch histogram, block scan, staging), then
 // written out in that order, so a cell's records of the batch leave as one
 // contiguous run instead of lane-scattered 16-byte stores.  LDS: cursors and
@@ -2975,7 +2993,8 @@ __global__ __launch_bounds__(kTThreads) void k_t_final_s(const TChunk *__restric
             // them in scratch between the load and the staging loop
             unsigned r[U][4 * NW];
             unsigned k[U], rk[U];
-            // clamped-index loads, as in k_t_final
+            // clamped-index loads: behind `if (i < t.e)` the compiler kept the
+            // records in scratch between the two loops
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t i = i0 + u * kTThreads + threadIdx.x, ic = min(i, t.e - 1u);
@@ -3749,119 +3768,6 @@ __global__ __launch_bounds__(64 * kDeg64Waves) void k_degrid_f64_mfma(
     }
 }
 
-// fp64 degridder (predict), the adjoint: the item's region of the W planes
-// staged in LDS; per cell each lane holds its footprint taps' values of every
-// plane in registers; per record V = sum over the lane's taps of
-// tu tv sum_q G[q] tw[q], reduced over the wave, times the record factor,
-// written to the visibility (through the pol conversion of OutConv).
-template <int W, bool WS, class VT>
-__global__ __launch_bounds__(64) void k_degrid_f64(Geo g, const VisRec64 *__restrict__ recs,
-                                                   const FineItem *__restrict__ items,
-                                                   uint32_t n_items,
-                                                   const double2 *__restrict__ grid, int p_lo,
-                                                   int p_hi, VT *vis, int64_t vrs, int64_t vcs,
-                                                   int accumulate, OutConv oc) {
-    constexpr int NQ = WS ? W : 1;
-    constexpr int RX = W + 1, RY = W + 7, NP = (W * W + 63) / 64, TR = 3 * W;
-    extern __shared__ __attribute__((aligned(16))) double2 sm64[];
-    double2 *const reg = sm64;  // [NQ][RX][RY]
-    double *const tap = reinterpret_cast<double *>(reg + NQ * RX * RY);
-    double2 *const cv = reinterpret_cast<double2 *>(tap + kTap64 * TR);
-    const int lane = threadIdx.x;
-    const double ihw = 2.0 / W, beta = (double)g.beta;
-    int px[NP], py[NP];
-    bool pv[NP];
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-        const int pp = lane + 64 * i;
-        pv[i] = pp < W * W;
-        px[i] = pv[i] ? pp / W : 0;
-        py[i] = pv[i] ? pp % W : 0;
-    }
-    const size_t plane_elems = (size_t)g.ngx * g.ngy;
-    const bool plain = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        uint32_t bnd[kGroupCell];
-        const Item it = load_fine_item<kGroupCell>(items, w_it, n_items, bnd, true);
-        if (it.b >= it.e) continue;
-        int ibase, jbase;
-        group_origin(g, (int)it.tile, ibase, jbase);
-        wave_lds_sync();  // the previous item's reads of the region
-        for (int i = lane; i < NQ * RX * RY; i += 64) {
-            const int q = i / (RX * RY), rem = i - q * (RX * RY);
-            const int p = (int)it.p0 + q;
-            const int xl = rem / RY, yl = rem - xl * RY;
-            int gx = ibase + xl;
-            if (gx >= g.ngx) gx -= g.ngx;
-            int gy = jbase + yl;
-            if (gy >= g.ngy) gy -= g.ngy;
-            reg[i] = (p >= p_lo && p < p_hi)
-                         ? grid[(size_t)(p - p_lo) * plane_elems + (size_t)gx * g.ngy + gy]
-                         : make_double2(0.0, 0.0);
-        }
-        double2 gq[NP][NQ];
-        int cur = -1;
-        for (uint32_t b0 = it.b; b0 < it.e; b0 += kTap64) {
-            wave_lds_sync();  // the region staging / previous block's tap reads
-            const int nb = stage_taps64<W, WS>(recs, b0, it.e, tap, cv, ihw, beta);
-            wave_lds_sync();
-            for (int r = 0; r < nb; ++r) {
-                const uint32_t ri = b0 + (uint32_t)r;
-                int cell = 0;
-#pragma unroll
-                for (int c = 0; c < kGroupCell - 1; ++c) cell += ri >= bnd[c] ? 1 : 0;
-                if (cell != cur) {
-                    cur = cell;
-                    const int xo = cur & 1, yo = cur >> 1;
-#pragma unroll
-                    for (int i = 0; i < NP; ++i)
-#pragma unroll
-                        for (int q = 0; q < NQ; ++q)
-                            gq[i][q] = pv[i] ? reg[(q * RX + xo + px[i]) * RY + yo + py[i]]
-                                             : make_double2(0.0, 0.0);
-                }
-                const double *T = tap + r * TR;
-                double sr = 0.0, si = 0.0;
-#pragma unroll
-                for (int i = 0; i < NP; ++i) {
-                    double ar = 0.0, ai = 0.0;
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const double tw = T[2 * W + q];
-                        ar = fma(gq[i][q].x, tw, ar);
-                        ai = fma(gq[i][q].y, tw, ai);
-                    }
-                    const double t = T[px[i]] * T[W + py[i]];
-                    sr = fma(t, ar, sr);
-                    si = fma(t, ai, si);
-                }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    sr += __shfl_xor(sr, o, 64);
-                    si += __shfl_xor(si, o, 64);
-                }
-                if (lane == 0) {
-                    const double2 c = cv[r];
-                    const double xr = c.x * sr - c.y * si, xi = c.x * si + c.y * sr;
-                    const uint32_t idx = recs[ri].idx;
-                    const int64_t row = idx / (uint32_t)g.nchan;
-                    const int chan = (int)(idx - row * g.nchan);
-                    VT *pv_ = vis + row * vrs + chan * vcs;
-                    if (plain) {
-                        store_vis_d(pv_, xr, xi, accumulate);
-                    } else {
-                        for (int k = 0; k < oc.npv; ++k) {
-                            if (oc.cre[k] == 0.0 && oc.cim[k] == 0.0) continue;
-                            store_vis_d(pv_ + k * oc.vps, oc.cre[k] * xr - oc.cim[k] * xi,
-                                        oc.cre[k] * xi + oc.cim[k] * xr, accumulate);
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
 // ------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------
@@ -4031,7 +3937,7 @@ struct Part {
     // host copies (read_part_meta)
     int64_t nrec = 0, nitems = 0;
     std::vector<unsigned> p0_items;
-    // two-level (tiled) plans: see k_t_count .. k_t_final
+    // two-level (tiled) plans: see k_t_count .. k_t_final_s
     int t_g1 = 0;          // workgroups of the count / value passes
     int64_t t_vpw = 0;     // visibilities per such workgroup
     unsigned t_maxch = 0;  // bound on the second-level chunks
@@ -4561,7 +4467,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // large-grid invert: RecC records + cell bytes, then the 4-padded copy
     // (k_subsort_pad; budgeted at 1.35x -- C4's top channels pad to <= 1.5x
     // one channel at a time, less over a batch of channels)
-    P.subpad = grid_mode && g.sub == kTileCoarse && env_int("SDP_HIP_SUBSORT_PAD", 1) != 0;
+    P.subpad = grid_mode && g.sub == kTileCoarse;
     // two-level plans: the bin-ordered records + their cell keys, then the
     // final (for the invert 4-padded, ~1.05x) copy
     const double tiled_rec = P.f64 ? sizeof(VisRec64) : grid_mode ? sizeof(RecC) : sizeof(VisRec);
@@ -4618,10 +4524,12 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     // (k_grid_mfma_pad); the padded record count is read back before the
     // scatter (one host sync)
     P.pad4 = grid_mode && g.sub == kTileCell && !P.f64;
-    // fp64 invert on the two-level bucketing: VisRec64 cells padded to 4 for
-    // the MFMA gridder (SDP_HIP_F64_MFMA=0: the VALU gridder, unpadded)
-    P.pad64 = grid_mode && g.tiled && P.f64 && env_int("SDP_HIP_F64_MFMA", 1) != 0;
-    P.mfma64 = !grid_mode && g.sub == kTileCell && P.f64 && env_int("SDP_HIP_F64_MFMA", 1) != 0;
+    // fp64 invert on the two-level bucketing: Rec64 cells padded to 4 for the
+    // MFMA gridder (a single-level plan -- windows past the LDS histogram, or
+    // SDP_HIP_BUCKET2=0 -- keeps unpadded VisRec64 records and the VALU
+    // gridder k_grid_f64); the fp64 predict always degrids on MFMA
+    P.pad64 = grid_mode && g.tiled && P.f64;
+    P.mfma64 = !grid_mode && g.sub == kTileCell && P.f64;
     // (k_degrid_f64_mfma's per-item block table holds kMaxBlk64 blocks)
     if (P.mfma64) P.chunk = std::min<unsigned>(P.chunk, (kMaxBlk64 - kGroupCell) * kBlk64);
     P.chunk &= ~63u;  // items start on 64-record batches (and 4-record K-steps)
@@ -4813,23 +4721,13 @@ static std::pair<unsigned, unsigned> chunk_items(const Plan &P, int p_lo, int p_
 }
 
 template <int W, bool WS>
-static void launch_grid_mfma_fi(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
-    const size_t lds = (size_t)(WS ? W : 1) * (2 + W - 1) * (8 + W - 1) * sizeof(float2) +
-                       128 * sizeof(float4);
-    const auto r = chunk_items(P, p_lo, p_hi);
-    const unsigned n = 16u * (r.second - r.first);
-    if (n == 0) return;
-    k_grid_mfma<W, WS><<<n, 64, lds, st>>>(P.g, P.recs, n, P.pt.fitems + 16 * (size_t)r.first,
-                                           (float *)P.grid, p_lo, p_hi);
-}
-
-template <int W, bool WS>
 static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
     // one-cell plans: one FineItem per work unit; padded sub-sorted coarse
     // plans: a coarse item's 16 FineItems per unit
     const auto r = chunk_items(P, p_lo, p_hi);
     const unsigned n = r.second - r.first;
     if (n == 0) return;
+    static const bool pc = env_int("SDP_HIP_GRID_PC", 0) != 0;
     if (P.subpad) {
         // units of 4 of a coarse item's 16 groups (2 x pairs x 2 y halves,
         // 4 x 16 cells, an 11 x 23-cell region).  C4 N = 1 gridding: 1 group
@@ -4837,9 +4735,18 @@ static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t 
         // units flush fewer atomics (the small groups of C4's sparse cells,
         // ~120 records each, were bound by them) but hold more LDS per wave
         const unsigned nu = n * 4u;
-        k_grid_mfma_pad<W, WS, 4><<<nu, 64, grid_mfma_pad_lds<4>(), st>>>(
-            P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo, p_hi,
-            P.core);
+        if (pc)
+            k_grid_mfma_pc<W, WS, 4><<<nu, 128, grid_pc_lds<4>(), st>>>(
+                P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo,
+                p_hi, P.core);
+        else
+            k_grid_mfma_pad<W, WS, 4><<<nu, 64, grid_mfma_pad_lds<4>(), st>>>(
+                P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo,
+                p_hi, P.core);
+    } else if (pc) {
+        k_grid_mfma_pc<W, WS, 1><<<n, 128, grid_pc_lds<1>(), st>>>(
+            P.g, reinterpret_cast<const RecC *>(P.recs), P.pt.fitems + r.first, n, (float *)P.grid,
+            p_lo, p_hi, P.core);
     } else
         k_grid_mfma_pad<W, WS, 1><<<n, 64, grid_mfma_pad_lds<1>(), st>>>(
             P.g, reinterpret_cast<const RecC *>(P.recs), P.pt.fitems + r.first, n, (float *)P.grid,
@@ -4861,24 +4768,6 @@ static void launch_grid_f64(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
     k_grid_f64<W, WS><<<n, 64, grid_f64_lds<W, WS>(), st>>>(
         P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
         reinterpret_cast<double *>(P.grid), p_lo, p_hi);
-}
-
-template <int W, bool WS, class VT>
-static void launch_degrid_f64(const Plan &P, int p_lo, int p_hi, VT *vis, int64_t vrs,
-                              int64_t vcs, int accumulate, const OutConv &oc, hipStream_t st) {
-    const auto r = chunk_items(P, p_lo, p_hi);
-    const unsigned n = r.second - r.first;
-    if (n == 0) return;
-    static const bool attr = [] {
-        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_degrid_f64<W, WS, VT>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)grid_f64_lds<W, WS>()));
-        return true;
-    }();
-    (void)attr;
-    k_degrid_f64<W, WS, VT><<<n, 64, grid_f64_lds<W, WS>(), st>>>(
-        P.g, reinterpret_cast<const VisRec64 *>(P.recs), P.pt.fitems + r.first, n,
-        reinterpret_cast<const double2 *>(P.grid), p_lo, p_hi, vis, vrs, vcs, accumulate, oc);
 }
 
 #define SDP_W64_DISPATCH(W, CALL) \
@@ -5009,30 +4898,22 @@ static void grid_f64(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
 template <class VT>
 static void degrid_f64(const Plan &P, int p_lo, int p_hi, VT *vis, int64_t vrs, int64_t vcs,
                        int accumulate, const OutConv &oc, hipStream_t st) {
-#define SDP_D64(WW)                                                                        \
-    (P.mfma64                                                                              \
-         ? (P.g.do_w                                                                       \
-                ? launch_degrid_f64_mfma<WW, true, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, \
-                                                       oc, st)                             \
-                : launch_degrid_f64_mfma<WW, false, VT>(P, p_lo, p_hi, vis, vrs, vcs,       \
-                                                        accumulate, oc, st))               \
-         : (P.g.do_w                                                                       \
-                ? launch_degrid_f64<WW, true, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, \
-                                                  st)                                      \
-                : launch_degrid_f64<WW, false, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, \
-                                                   st)))
+    SDP_REQUIRE(P.mfma64, "the fp64 predict needs one-cell buckets");
+#define SDP_D64(WW)                                                                             \
+    (P.g.do_w ? launch_degrid_f64_mfma<WW, true, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, oc, \
+                                                     st)                                        \
+              : launch_degrid_f64_mfma<WW, false, VT>(P, p_lo, p_hi, vis, vrs, vcs, accumulate, \
+                                                      oc, st))
     SDP_W64_DISPATCH(P.g.W, SDP_D64);
 #undef SDP_D64
 }
 
 template <int W>
 static void launch_grid(const Plan &P, int p_lo, int p_hi, hipStream_t st) {
-    if (P.pad4 || P.subpad) {
-        if (P.g.do_w) return launch_grid_mfma_pad<W, true>(P, p_lo, p_hi, st);
-        return launch_grid_mfma_pad<W, false>(P, p_lo, p_hi, st);
-    }
-    if (P.g.do_w) return launch_grid_mfma_fi<W, true>(P, p_lo, p_hi, st);
-    return launch_grid_mfma_fi<W, false>(P, p_lo, p_hi, st);
+    // (fp32 inverts are always 4-padded: one-cell plans by the bucketing,
+    // large grids by the sub-sort)
+    if (P.g.do_w) return launch_grid_mfma_pad<W, true>(P, p_lo, p_hi, st);
+    return launch_grid_mfma_pad<W, false>(P, p_lo, p_hi, st);
 }
 
 // the degridder's store sink (kDegridSinkBlocks x 64 float2 per device,
@@ -5268,7 +5149,7 @@ static int cu_count() {
     return cus[dev];
 }
 
-// Two-level bucketing of a tiled one-cell plan (k_t_count .. k_t_final):
+// Two-level bucketing of a tiled one-cell plan (k_t_count .. k_t_final_s):
 // the count pass, bins, value pass, cell counts and bases, then (one host
 // sync: the metadata, which sizes the final record array) the cell bases,
 // pads, work items and the move of every record to its cell.  The weight
@@ -5281,13 +5162,10 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
     const Geo &g = P.g;
     Part &pt = P.pt;
     const int nb = g.nbins;
-    // fp64: 48-byte Rec64 for the MFMA kernels, VisRec64 for the VALU ones
-    // (SDP_HIP_F64_MFMA=0)
-    const int kind = P.f64 ? ((P.pad64 || P.mfma64) ? 3 : 2) : (grid_mode ? 0 : 1);
-    const size_t rsz = kind == 2   ? sizeof(VisRec64)
-                       : kind == 3 ? sizeof(Rec64)
-                       : kind == 0 ? sizeof(RecC)
-                                   : sizeof(VisRec);
+    // records: 16-byte RecC (fp32 invert), 32-byte VisRec (fp32 predict,
+    // SDP_HIP_BUCKET2=2 only), 48-byte Rec64 (fp64, the MFMA kernels)
+    const int kind = P.f64 ? 3 : (grid_mode ? 0 : 1);
+    const size_t rsz = kind == 3 ? sizeof(Rec64) : kind == 0 ? sizeof(RecC) : sizeof(VisRec);
     const int64_t nvis = pt.nvis;
     const size_t lds_bins = (size_t)nb * sizeof(unsigned);
     if (!values_only) {
@@ -5328,6 +5206,54 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         if (after_clear) after_clear();
     }
     k_fscale<<<grid1d(g.nchan, 256), 256, 0, st>>>(in.freq, g.nchan, pt.t_fsc);
+    // the passes' weight and flag types (t_load): 1- and 4-byte flags are
+    // widened to a contiguous int64 copy first
+    VisExtra x = in.x;
+    const void *wgt = in.wgt;
+    int64_t wrs = in.wrs, wcs = in.wcs;
+    if (!wgt) {
+        void *one = nullptr;
+        SDP_HIP_CHECK(hipGetSymbolAddress(&one, HIP_SYMBOL(g_unit_weight)));
+        wgt = one;
+        wrs = wcs = 0;
+        x.wgt_f64 = 0;
+    }
+    const int wt = x.wgt_f64 ? 8 : 4;
+    if (x.fbytes == 4) {
+        // (a zero-stride broadcast flag widens to one element)
+        const bool bc = x.frs == 0 && x.fcs == 0 && x.fps == 0;
+        const int np = bc ? 1 : x.npv;
+        const int64_t nr = bc ? 1 : g.nrow, nc = bc ? 1 : g.nchan;
+        int64_t *f64 = scratch<int64_t>("flags64", (size_t)std::max<int64_t>(nr * nc * np, 1));
+        const unsigned gw = (unsigned)std::max<int64_t>(
+            1, std::min<int64_t>(grid1d(nr * nc * np, 256), 65536));
+        if (nvis > 0)
+            k_widen_flags<int32_t><<<gw, 256, 0, st>>>(static_cast<const int32_t *>(x.flags), x.frs,
+                                                      x.fcs, x.fps, nr, (int)nc, np, f64);
+        x.flags = f64;
+        x.fbytes = 8;
+        x.frs = bc ? 0 : nc * np;
+        x.fcs = bc ? 0 : np;
+        x.fps = bc ? 0 : 1;
+    }
+    const int fb = x.fbytes;
+    // calls the kernel template `launch` with the (WT, FB) of this call
+    auto with_types = [&](auto launch) {
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I4 = std::integral_constant<int, 4>;
+        using I8 = std::integral_constant<int, 8>;
+        if (fb == 0) {
+            if (wt == 4) launch(I4{}, I0{});
+            else launch(I8{}, I0{});
+        } else if (fb == 1) {
+            if (wt == 4) launch(I4{}, I1{});
+            else launch(I8{}, I1{});
+        } else {
+            if (wt == 4) launch(I4{}, I8{});
+            else launch(I8{}, I8{});
+        }
+    };
     const int cus = cu_count();
     const unsigned gch = std::min<unsigned>(pt.t_maxch, 4u * (unsigned)cus);
     auto scatter = [&](double *sl) {
@@ -5335,30 +5261,27 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
             using VT = typename decltype(vt_tag)::type;
             constexpr int K = decltype(kind_tag)::value;
             constexpr bool G = decltype(grid_tag)::value;
-            k_t_scatter<VT, K, G><<<pt.t_g1, kT1Threads, lds_bins, st>>>(
-                g, nvis, pt.t_vpw, in.uvw, in.uvw_rs, pt.t_fsc,
-                G ? static_cast<const VT *>(in.vis) : nullptr, in.vrs, in.vcs, in.wgt, in.wrs,
-                in.wcs, in.x, sl, pt.t_binbase, pt.t_m1, pt.t_a, pt.t_lkey);
+            with_types([&](auto wt_tag, auto fb_tag) {
+                k_t_scatter<VT, K, G, decltype(wt_tag)::value, decltype(fb_tag)::value>
+                    <<<pt.t_g1, kT1Threads, lds_bins, st>>>(
+                        g, nvis, pt.t_vpw, in.uvw, in.uvw_rs, pt.t_fsc,
+                        G ? static_cast<const VT *>(in.vis) : nullptr, in.vrs, in.vcs, wgt, wrs,
+                        wcs, x, sl, pt.t_binbase, pt.t_m1, pt.t_a, pt.t_lkey);
+            });
         };
-        auto by_kind = [&](auto vt_tag) {
-            if (kind == 2) {
-                if (grid_mode) go(vt_tag, std::integral_constant<int, 2>{}, std::true_type{});
-                else go(vt_tag, std::integral_constant<int, 2>{}, std::false_type{});
-            } else if (kind == 3) {
-                if (grid_mode) go(vt_tag, std::integral_constant<int, 3>{}, std::true_type{});
-                else go(vt_tag, std::integral_constant<int, 3>{}, std::false_type{});
-            } else if (kind == 0) {
-                go(vt_tag, std::integral_constant<int, 0>{}, std::true_type{});
-            } else {
-                go(vt_tag, std::integral_constant<int, 1>{}, std::false_type{});
-            }
+        auto grid_kind = [&](auto vt_tag) {
+            if (kind == 3) go(vt_tag, std::integral_constant<int, 3>{}, std::true_type{});
+            else go(vt_tag, std::integral_constant<int, 0>{}, std::true_type{});
         };
-        if (in.vis_dtype == SDP_HIP_C128) by_kind(TypeTag<double2>{});
-        else by_kind(TypeTag<float2>{});
+        if (grid_mode) {
+            if (in.vis_dtype == SDP_HIP_C128) grid_kind(TypeTag<double2>{});
+            else grid_kind(TypeTag<float2>{});
+        } else {
+            // (a predict reads no visibilities: one instantiation for both dtypes)
+            if (kind == 3) go(TypeTag<float2>{}, std::integral_constant<int, 3>{}, std::false_type{});
+            else go(TypeTag<float2>{}, std::integral_constant<int, 1>{}, std::false_type{});
+        }
     };
-    // SDP_HIP_TFINAL: 1 (default) batches staged through 64 KiB of LDS, 2
-    // through 32 KiB (two workgroups per CU), 0 the unstaged move
-    static const int tfinal = env_int("SDP_HIP_TFINAL", 1);
     auto staged = [&](auto kind_tag, auto nb_tag) {
         constexpr int K = decltype(kind_tag)::value, NB = decltype(nb_tag)::value;
         constexpr size_t lds = t_final_lds<K, NB>();
@@ -5374,31 +5297,10 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
                                                          P.recs);
     };
     auto final_move = [&] {
-        using I = std::integral_constant<int, 0>;
-        if (kind == 3) {
-            staged(std::integral_constant<int, 3>{}, std::integral_constant<int, 2048>{});
-        } else if (tfinal == 0) {
-            if (kind == 2)
-                k_t_final<2><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
-                                                         pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
-                                                         P.recs);
-            else if (kind == 0)
-                k_t_final<0><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
-                                                         pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
-                                                         P.recs);
-            else
-                k_t_final<1><<<gch, kTThreads, 0, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
-                                                         pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
-                                                         P.recs);
-        } else if (tfinal == 2) {
-            if (kind == 2) staged(std::integral_constant<int, 2>{}, std::integral_constant<int, 1024>{});
-            else if (kind == 0) staged(I{}, std::integral_constant<int, 2048>{});
-            else staged(std::integral_constant<int, 1>{}, std::integral_constant<int, 1024>{});
-        } else {
-            if (kind == 2) staged(std::integral_constant<int, 2>{}, std::integral_constant<int, 1024>{});
-            else if (kind == 0) staged(I{}, std::integral_constant<int, 4096>{});
-            else staged(std::integral_constant<int, 1>{}, std::integral_constant<int, 2048>{});
-        }
+        // batches of 4096 (RecC), 2048 (VisRec, Rec64) records staged in LDS
+        if (kind == 3) staged(std::integral_constant<int, 3>{}, std::integral_constant<int, 2048>{});
+        else if (kind == 0) staged(std::integral_constant<int, 0>{}, std::integral_constant<int, 4096>{});
+        else staged(std::integral_constant<int, 1>{}, std::integral_constant<int, 2048>{});
         SDP_HIP_CHECK(hipGetLastError());
     };
     if (values_only) {
@@ -5409,9 +5311,12 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         return;
     }
     if (nvis > 0)
-        k_t_count<<<pt.t_g1, kT1Threads, lds_bins, st>>>(g, nvis, pt.t_vpw, in.uvw, in.uvw_rs,
-                                                        pt.t_fsc, in.wgt, in.wrs, in.wcs, in.x,
-                                                        slots, pt.t_binc, pt.t_m1, pt.nbad);
+        with_types([&](auto wt_tag, auto fb_tag) {
+            k_t_count<decltype(wt_tag)::value, decltype(fb_tag)::value>
+                <<<pt.t_g1, kT1Threads, lds_bins, st>>>(g, nvis, pt.t_vpw, in.uvw, in.uvw_rs,
+                                                        pt.t_fsc, wgt, wrs, wcs, x, slots, pt.t_binc,
+                                                        pt.t_m1, pt.nbad);
+        });
     k_t_bins<<<1, kTThreads, 0, st>>>(nb, pt.t_binc, pt.t_binbase, pt.t_segb, pt.t_nsegb,
                                       pt.t_nbl, pt.t_chunks, pt.t_segs, pt.t_meta_ch);
     if (nvis > 0) scatter(nullptr);

@@ -31,15 +31,13 @@ def _problem(seed, nrow=400, nchan=3, umax=2000.0, frac=0.45):
     return uvw, freq, ms, wgt, frac / umax
 
 
-@pytest.fixture(params=["mfma", "valu", "single"])
+@pytest.fixture(params=["mfma", "single"])
 def gridder(request, monkeypatch):
-    """Both fp64 gridders: k_grid_f64_mfma on 4-padded cells of the two-level
-    sort's 48-byte records (default) and the VALU k_grid_f64 on unpadded
-    cells (SDP_HIP_F64_MFMA=0); "single": the single-level bucketing
-    (SDP_HIP_BUCKET2=0) -- VisRec64 records, the VALU gridder and the MFMA
-    degridder on them."""
-    if request.param == "valu":
-        monkeypatch.setenv("SDP_HIP_F64_MFMA", "0")
+    """Both fp64 record paths: k_grid_f64_mfma on 4-padded cells of the
+    two-level sort's 48-byte records (default), and "single": the
+    single-level bucketing (windows past the LDS histogram; forced by
+    SDP_HIP_BUCKET2=0) -- VisRec64 records, the VALU gridder k_grid_f64 on
+    unpadded cells and the MFMA degridder on them."""
     if request.param == "single":
         monkeypatch.setenv("SDP_HIP_BUCKET2", "0")
     return request.param
