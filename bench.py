@@ -789,7 +789,8 @@ def run_c4_api(args, world, rank, local, dev, uvw, nrow, lo, hi, freqs, umax, ba
     ms_step = elapsed / steps * 1e3
     sumwt = float(np.sum(res[1]))
     if emulated:
-        print(json.dumps({"emulated_rank": rank, "world": world, "api": "invert_ng",
+        print(json.dumps({"emulated_rank": rank, "world": world, "partition": args.partition,
+                          "api": "invert_ng",
                           "block": (lo, hi), "rows": nrow, "ms_per_step": round(ms_step, 3),
                           "nvis_rank": nrow * nch, "sumwt": sumwt,
                           "note": "rank's block only; no all-reduce"}), flush=True)
@@ -820,31 +821,43 @@ def run_c4_api(args, world, rank, local, dev, uvw, nrow, lo, hi, freqs, umax, ba
 C3_NCOMP, C3_NTIMES = 1000, 518   # 19,306 SKA-MID baselines x 518 times = 10.0 Mvis
 
 
-# k_dft's component loop (npol 1, c64 output; gfx950 ISA of csrc/dft.hip): per
-# component and wave64 one v_sin_f32 + one v_cos_f32 (8 issue cycles each,
-# MI355X_MICROARCH.md "vector-instruction ISSUE cost"), five fp64 VALU ops
-# (the phase u l + v m + w (n - 1): mul + 2 fma; rndne; add) and one cvt at 4
-# cycles, the complex multiply-accumulate as 4 packed-f32 ops (counted at 8)
-# and a v_mov (4): 76 issue cycles per 64 component-visibilities per SIMD.
+# k_dft_mfma's binding pipe, from a PMC pass of the same C3 launch
+# (scripts/pmc_sets.sh dft6 ... -- scripts/dft_once.py, summarised into
+# profiles/r06_dft_pmc.json): the SIMDs' VALU-active fraction
+# (SQ_ACTIVE_INST_VALU, quad-cycles, over SIMDs x GRBM_GUI_ACTIVE cycles), the
+# MFMA-busy fraction (they never overlap: SQ_VALU_MFMA_COEXEC_CYCLES = 0) and
+# the instruction mix per 64 component-visibilities.  The per-component work
+# is two transcendentals (v_sin_f32, v_cos_f32) plus v_fract_f64, one
+# conversion and two packed-f32 FMAs on the VALU; the phase product is a
+# quarter of a v_mfma_f64_16x16x4_f64 per 64.  The transcendental bound is
+# the sincos issue alone (8 cycles each per wave64, MI355X_MICROARCH.md
+# "vector-instruction ISSUE cost").
 DFT_TRANS_CYC = 2 * 8
-DFT_ISSUE_CYC = DFT_TRANS_CYC + 5 * 4 + 4 + 4 * 8 + 4
 MI355X_SIMDS, MI355X_GHZ = 256 * 4, 2.4
+DFT_PMC = os.path.join(ROOT, "profiles", "r06_dft_pmc.json")
 
 
 def _dft_issue_roofline(compvis, k_ms):
-    """The DFT against its binding pipe: the transcendental issue rate (two
-    per component-visibility) and the whole per-component issue count."""
+    """The DFT against its binding pipe: the VALU issue (measured active
+    fraction from the committed PMC pass) and the transcendental rate."""
     rate = compvis / (k_ms * 1e-3)
     lanes = MI355X_SIMDS * MI355X_GHZ * 1e9 * 64
     trans_peak = lanes / DFT_TRANS_CYC  # component-visibilities / s if only sincos issued
-    issue_peak = lanes / DFT_ISSUE_CYC
-    return {"achieved": round(rate / 1e12, 3), "unit": "T comp*vis/s",
-            "sincos_peak": round(trans_peak / 1e12, 3),
-            "sincos_frac": round(rate / trans_peak, 4),
-            "issue_peak": round(issue_peak / 1e12, 3), "issue_frac": round(rate / issue_peak, 4),
-            "note": f"sincos: 2 transcendentals x 8 issue cycles per 64 comp*vis per SIMD; issue: "
-                    f"{DFT_ISSUE_CYC} cycles per component per wave64 from the k_dft ISA "
-                    f"(bench.py DFT_ISSUE_CYC), {MI355X_SIMDS} SIMDs at {MI355X_GHZ} GHz"}
+    out = {"achieved": round(rate / 1e12, 3), "unit": "T comp*vis/s",
+           "sincos_peak": round(trans_peak / 1e12, 3), "sincos_frac": round(rate / trans_peak, 4)}
+    try:
+        pmc = json.load(open(DFT_PMC))
+        for k in ("valu_active_frac", "mfma_busy_frac", "simd_busy_frac", "insts_per_64_compvis"):
+            out[k] = pmc[k]
+        out["pmc_kernel_ms"] = pmc["kernel_ms"]
+        out["source"] = os.path.relpath(DFT_PMC, ROOT)
+    except (OSError, KeyError, ValueError):
+        pass
+    out["note"] = ("binding pipe: the SIMDs' issue (measured on the same launch: VALU active "
+                   "plus MFMA busy, which never overlap on gfx950, = simd_busy_frac); sincos: "
+                   "2 transcendentals x 8 issue cycles per 64 comp*vis per SIMD, "
+                   f"{MI355X_SIMDS} SIMDs at {MI355X_GHZ} GHz")
+    return out
 
 
 def run_c3(args, world, rank, dev, sub=False):
@@ -932,10 +945,11 @@ def run_c3(args, world, rank, dev, sub=False):
         "roofline": {"bound": "valu", "achieved": round(flops / (k_ms * 1e-3) / 1e12, 2),
                      "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(flops / (k_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
-                     "traffic": None, "kernel": "k_dft", "kernel_ms": round(k_ms, 4),
+                     "traffic": None, "kernel": "k_dft_mfma", "kernel_ms": round(k_ms, 4),
                      "note": "N_vis N_comp (6 + 8 npol) flops (SURVEY.md 8(d)), sincos excluded; "
-                             "MFMA does not apply (the contraction's N is npol = 1, DESIGN.md 3)",
-                     "transcendental": _dft_issue_roofline(nvis_total * C3_NCOMP, k_ms)},
+                             "the fp64 phase product runs on v_mfma_f64_16x16x4_f64, the "
+                             "VALU keeps sincos and the flux multiply-add (DESIGN.md 2)",
+                     "issue": _dft_issue_roofline(nvis_total * C3_NCOMP, k_ms)},
         "cpu_baseline": cpu,
     }
     if sub:

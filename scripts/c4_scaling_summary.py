@@ -12,7 +12,12 @@ IMG = 8192 * 8192 * 8
 by = {}
 for r in rows:
     if "emulated_rank" in r:
-        by.setdefault((r["world"], r.get("partition", "chan")), []).append(r)
+        # (the --c4-api lines before round 6's "partition" key: a rank holding
+        # every channel is a rows-by-w rank)
+        part = r.get("partition") or ("wrow" if r.get("block") == [0, 256] else "chan")
+        if r.get("api"):
+            part += "+api"
+        by.setdefault((r["world"], part), []).append(r)
 print(f"N=1: {base} ms")
 for (w, part), rs in sorted(by.items()):
     mx = max(r["ms_per_step"] for r in rs)

@@ -1,5 +1,6 @@
 """C3's sky-component DFT (1000 point components x 10 Mvis, stokesI, c64
-output) run --reps times: the driver for rocprofv3 PMC passes on k_dft."""
+output, one channel as bench.py --config c3) run --reps times: the driver
+for rocprofv3 PMC passes on k_dft_mfma."""
 import argparse
 import os
 import sys
@@ -15,11 +16,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--ncomp", type=int, default=1000)
 ap.add_argument("--nvis", type=int, default=10_000_000)
+ap.add_argument("--nchan", type=int, default=1)
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev)
 g.manual_seed(3)
-nchan = 10
+nchan = a.nchan
 nrow = a.nvis // nchan
 uvw = (torch.rand((nrow, 3), dtype=torch.float64, device=dev, generator=g) - 0.5) * 2e4
 uvw[:, 2] *= 0.2

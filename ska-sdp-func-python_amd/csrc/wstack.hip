@@ -503,150 +503,272 @@ struct TypeTag {
     using type = T;
 };
 
-// One visibility of k_bucket.
-template <class VT, bool kScatter, bool kGrid, bool kCompact>
+template <class VT>
+__device__ __forceinline__ double2 eff_vis_d(const VT *vis, int64_t vrs, int64_t vcs,
+                                             const VisExtra &x, int64_t row, int chan) {
+    const VT *p = vis + row * vrs + chan * vcs;
+    if (!x.conv) {
+        if (!x.fbytes) return load_vis_d(p);
+        const double m = flag_mask(x, row, chan, x.fpol);
+        if (m == 0.0) return make_double2(0.0, 0.0);
+        const double2 v = load_vis_d(p);
+        return make_double2(v.x * m, v.y * m);
+    }
+    double re = 0.0, im = 0.0;
+    for (int k = 0; k < x.npv; ++k) {
+        if (x.cre[k] == 0.0 && x.cim[k] == 0.0) continue;
+        double m = 1.0;
+        if (x.fbytes) {
+            m = flag_mask(x, row, chan, k);
+            if (m == 0.0) continue;
+        }
+        double2 v = load_vis_d(p + k * x.vps);
+        v.x *= m;
+        v.y *= m;
+        re += x.cre[k] * v.x - x.cim[k] * v.y;
+        im += x.cre[k] * v.y + x.cim[k] * v.x;
+    }
+    return make_double2(re, im);
+}
+
+struct TLoad {
+    uint32_t row, chan;
+    double um, vm, wm, s, wd;  // s = frequency / c (fsc[chan]: the same division as vis_coord)
+    double keep;               // 1 - flag of the weight's pol (1 without flags)
+    bool live;
+};
+
+// The weight and flag element types are compile-time in the bucketing
+// passes -- WT: 4 = f32, 8 = f64 (no weights: a device 1.0f with zero
+// strides); FB: 0 = no flags, 1 = int8, 8 = int64 flags (int32 flags are
+// widened to int64 first, k_widen_flags) -- and a lane's visibilities load
+// from clamped, in-bounds indices with no branch before their first use:
+// all of a lane's visibilities' loads (uvw, frequency scale, weight, flag,
+// and in the value pass the visibility) are in flight together.  A runtime switch on the
+// types, with each load behind its own branch and a `live` test, had put a
+// wait for every load before the next one issued (C2 count pass: ~200
+// instructions and four serialised memory round trips per visibility).
+template <int WT, int FB>
+__device__ __forceinline__ TLoad t_load(const Geo &g, int64_t v, int64_t vend,
+                                        const double *__restrict__ uvw, int64_t rs,
+                                        const double *__restrict__ fsc,
+                                        const void *__restrict__ wgt, int64_t wrs, int64_t wcs,
+                                        const VisExtra &x) {
+    TLoad L;
+    L.live = v < vend;
+    const uint32_t v32 = (uint32_t)(L.live ? v : vend - 1), nc = (uint32_t)g.nchan;
+    // row = v / nchan through the fp64 reciprocal (exact to one step, then
+    // corrected), not an integer division
+    uint32_t r32 = (uint32_t)((double)v32 * g.inv_nchan);
+    if ((uint64_t)r32 * nc > v32) --r32;
+    else if ((uint64_t)(r32 + 1u) * nc <= v32) ++r32;
+    L.row = r32;
+    L.chan = v32 - r32 * nc;
+    const double *p = uvw + (int64_t)L.row * rs;
+    L.um = p[0];
+    L.vm = p[1];
+    L.wm = p[2];
+    L.s = fsc[L.chan];
+    double w;
+    const int64_t wi = (int64_t)L.row * wrs + (int64_t)L.chan * wcs;
+    if constexpr (WT == 8) w = static_cast<const double *>(wgt)[wi];
+    else w = (double)static_cast<const float *>(wgt)[wi];
+    L.keep = 1.0;
+    if constexpr (FB != 0) {
+        using FT = typename std::conditional<FB == 8, int64_t, int8_t>::type;
+        L.keep = 1.0 - (double)static_cast<const FT *>(
+                           x.flags)[(int64_t)L.row * x.frs + (int64_t)L.chan * x.fcs + x.fpol * x.fps];
+        // select, not multiply: a flagged sample's weight is an exact zero
+        // even when the stored weight is NaN or Inf
+        w = L.keep == 0.0 ? 0.0 : w * L.keep;
+    }
+    L.wd = L.live ? w : 0.0;
+    return L;
+}
+
+// int32 flags of a two-level pass as int64 (FB = 8): a contiguous
+// [nrow, nchan, npol] copy (one element for a zero-stride broadcast)
+__device__ float g_unit_weight = 1.0f;  // the weights of a call without weights
+template <class FT>
+__global__ void k_widen_flags(const FT *__restrict__ src, int64_t frs, int64_t fcs, int64_t fps,
+                              int64_t nrow, int nchan, int npol, int64_t *__restrict__ dst) {
+    const int64_t n = nrow * nchan * (int64_t)npol;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t rc = i / npol, row = rc / nchan;
+        const int pol = (int)(i - rc * npol), chan = (int)(rc - row * nchan);
+        dst[i] = (int64_t)src[row * frs + chan * fcs + pol * fps];
+    }
+}
+
+// the visibility's value in two phases: `load` issues the loads (the
+// visibility from clamped indices, beside the lane's other loads), `value`
+// combines them after every load is in flight.  Without a pol conversion the
+// weight pol's flag (TLoad::keep) masks it; a pol conversion (x.conv, the
+// 4-pol frames) reads its pols and flags in `value`.
+template <class VT, int KIND, bool kGrid, int FB>
+struct TVal {
+    using type = typename std::conditional<KIND >= 2, double2, float2>::type;
+    __device__ static __forceinline__ VT load(const VT *vis, int64_t vrs, int64_t vcs,
+                                              const VisExtra &x, const TLoad &L) {
+        VT raw{};
+        if constexpr (kGrid)
+            if (vis && !x.conv) raw = vis[(int64_t)L.row * vrs + (int64_t)L.chan * vcs];
+        return raw;
+    }
+    __device__ static __forceinline__ type value(const VT *vis, int64_t vrs, int64_t vcs,
+                                                 const VisExtra &x, const TLoad &L, VT raw) {
+        type xv;
+        xv.x = 1;
+        xv.y = 0;
+        if constexpr (kGrid) {
+            if (!vis) return xv;  // (unit visibilities: the PSF)
+            if (x.conv) {
+                if constexpr (KIND >= 2) return eff_vis_d(vis, vrs, vcs, x, L.row, L.chan);
+                else return eff_vis(vis, vrs, vcs, x, L.row, L.chan);
+            }
+            const double2 v = make_double2((double)raw.x, (double)raw.y);
+            if constexpr (FB == 0) {
+                xv.x = v.x;
+                xv.y = v.y;
+            } else {
+                // select, not multiply: a NaN in a flagged visibility must not
+                // reach the image
+                const double m = L.keep;
+                xv.x = m == 0.0 ? 0.0 : v.x * m;
+                xv.y = m == 0.0 ? 0.0 : v.y * m;
+            }
+        }
+        return xv;
+    }
+};
+
+// One visibility of k_bucket (single-level bucketing: the fp32 predict, kept
+// buckets, large grids).  Its loads -- uvw, frequency scale, weight, flag,
+// and in the value pass its rank and visibility -- are issued together from
+// clamped indices (t_load<WT, FB>, TVal), before any of them is used.
+template <class VT, bool kScatter, bool kGrid, bool kCompact, int WT, int FB>
 __device__ __forceinline__ void bucket_one(const Geo &g, int64_t v, int64_t nvis,
                                            const double *__restrict__ uvw, int64_t uvw_rs,
-                                           const double *__restrict__ freq,
+                                           const double *__restrict__ fsc,
                                            const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
                                            const void *__restrict__ wgt, int64_t wrs,
                                            int64_t wcs, const VisExtra &x, double *sw_slots,
                                            unsigned *counter, unsigned *__restrict__ rk,
                                            VisRec *__restrict__ recs, unsigned long long *nbad,
-                                           uint8_t *__restrict__ cls) {
-    bool valid = v < nvis;
-    int64_t row = 0;
-    int chan = 0;
-    int64_t vg = v;  // row * nchan + chan
-    float wt = 1.0f;
-    Coord c;
-    c.ok = false;
-    unsigned mine = 0xffffffffu;  // rank in the bucket (0xffffffff: not gridded)
+                                           uint8_t *__restrict__ cls, float2 *__restrict__ zout) {
+    using V = TVal<VT, kCompact ? 0 : 1, kGrid, FB>;
+    const TLoad L = t_load<WT, FB>(g, v, nvis, uvw, uvw_rs, fsc, wgt, wrs, wcs, x);
+    const int64_t vg = (int64_t)L.row * g.nchan + L.chan;  // row * nchan + chan
+    // (a w-slab call's outsiders: no rank stored, no weight summed)
+    const bool outside = L.live && g.slab && slab_out_v(g, L.wm, L.s);
+    const double wd = outside ? 0.0 : L.wd;
+    const float wt = (float)wd;
     if (kScatter) {
-        double wd = 0.0;
-        if (valid) {
-            row = vg / g.nchan;
-            chan = (int)(vg - row * g.nchan);
-            // (a w-slab call's count pass left no rank for the slab's outsiders)
-            if (g.slab && slab_out(g, uvw, uvw_rs, row, freq[chan])) valid = false;
-        }
-        if (valid) {
-            wd = eff_weight(wgt, wrs, wcs, x, row, chan);
-            wt = (float)wd;
-        }
+        const unsigned mine = rk[vg];
+        const VT raw = V::load(vis, vrs, vcs, x, L);
         if (sw_slots) {
             // weight sum of a reused bucketing (SDP_HIP_REUSE_BUCKETS): the
             // count pass did not run, so the value pass sums the weights
+            double ws = wd;
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) wd += __shfl_xor(wd, o, 64);
-            if ((threadIdx.x & 63) == 0 && wd != 0.0)
+            for (int o = 32; o > 0; o >>= 1) ws += __shfl_xor(ws, o, 64);
+            if ((threadIdx.x & 63) == 0 && ws != 0.0)
                 atomicAdd(&sw_slots[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) &
                                     (kSumSlots - 1)],
-                          wd);
+                          ws);
         }
-        if (!valid) return;
-        mine = rk[v];
-        if (mine == 0xffffffffu) return;
-        c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
-    } else {
-        double wd = 0.0;
-        bool outside = false;  // w slab: another call's visibility (no rank stored)
-        if (valid) {
-            row = vg / g.nchan;
-            chan = (int)(vg - row * g.nchan);
-            outside = g.slab && slab_out(g, uvw, uvw_rs, row, freq[chan]);
-            valid = !outside;
+        if (!L.live || outside || mine == 0xffffffffu) return;
+        const Coord c = vis_coord_v(g, L.um, L.vm, L.wm, L.s);
+        const unsigned pos = counter[coord_key(g, c, L.row)] + mine;
+        float cr = wt, ci = 0.0f;
+        if (kGrid) {
+            // a zero-weight sample (bucketed only by a SDP_HIP_KEEP_BUCKETS
+            // plan, for the other pols) is an exact zero whatever its
+            // visibility holds
+            const float2 xv = V::value(vis, vrs, vcs, x, L, raw);
+            cr = wt != 0.0f ? xv.x * wt : 0.0f;
+            ci = wt != 0.0f ? xv.y * wt : 0.0f;
         }
-        if (valid) {
-            wd = eff_weight(wgt, wrs, wcs, x, row, chan);
-            wt = (float)wd;
-            valid = x.all || (wt != 0.0f);
-            if (valid) {
-                c = vis_coord(g, uvw, uvw_rs, row, freq[chan]);
-                if (!c.ok) {
-                    valid = false;
-                    if (!c.skip) atomicAdd(nbad, 1ull);
-                }
-            }
+        if (g.do_w || x.shift) {
+            double ph = g.do_w ? c.w * g.s0 : 0.0;
+            if (x.shift) ph += (L.um * x.sl + L.vm * x.sm + L.wm * x.sn) * L.s;
+            ph -= rint(ph);
+            float sn, cs;
+            sincospif((float)(2.0 * ph), &sn, &cs);
+            if (!kGrid) sn = -sn;
+            const float r_ = cr * cs - ci * sn, i_ = cr * sn + ci * cs;
+            cr = r_;
+            ci = i_;
         }
-        const unsigned key = valid ? coord_key(g, c, row) : 0xffffffffu;
-        const unsigned rank = run_reserve<true>(key, valid, counter);
-        // only the rank is kept: the scatter pass recomputes the key
-        if (v < nvis && !outside) rk[v] = valid ? rank : 0xffffffffu;
-        if (sw_slots) {
-            // weight sum: wave reduction, one atomic per wave into a slot
+        if (kCompact) {
+            // RecC: offsets as fractions of (1 - W/2) - offset (do_w off: w = 0)
+            const double base = 1.0 - 0.5 * g.W;
+            const uint32_t qu = fix_frac(base - c.du, 21), qv = fix_frac(base - c.dv, 21);
+            const uint32_t qw = g.do_w ? fix_frac(base - c.dw, 22) : 0u;
+            RecC rc;
+            rc.cre = cr;
+            rc.cim = ci;
+            rc.lo = qu | (qv << 21);
+            rc.hi = (qv >> 11) | (qw << 10);
+            reinterpret_cast<RecC *>(recs)[pos] = rc;
+            // large grids (16x16-cell buckets): the record's cell in its
+            // bucket, for the padded sub-sort (k_subsort_pad)
+            if (cls) cls[pos] = (uint8_t)(((c.ic0 & 15) >> 1) * 32 + (c.jc0 & 15) * 2 + (c.ic0 & 1));
+            return;
+        }
+        VisRec rec;
+        rec.cre = cr;
+        rec.cim = ci;
+        rec.fu = c.fu;
+        rec.fv = c.fv;
+        rec.fw = c.fw;
+        rec.ij = (uint32_t)c.ic0 | ((uint32_t)c.jc0 << 16);
+        rec.p0 = (uint32_t)c.p0;
+        rec.idx = (uint32_t)vg;
+        recs[pos] = rec;
+        return;
+    }
+    // rank pass
+    bool valid = L.live && !outside && (x.all || wt != 0.0f);
+    Coord c;
+    c.ok = false;
+    if (valid) {
+        c = vis_coord_v(g, L.um, L.vm, L.wm, L.s);
+        if (!c.ok) {
+            valid = false;
+            if (!c.skip) atomicAdd(nbad, 1ull);
+        }
+    }
+    const unsigned key = valid ? coord_key(g, c, L.row) : 0xffffffffu;
+    const unsigned rank = run_reserve<true>(key, valid, counter);
+    // only the rank is kept: the scatter pass recomputes the key
+    if (L.live && !outside) rk[vg] = valid ? rank : 0xffffffffu;
+    // a predict writing its visibilities in place zeroes the ones no record
+    // reaches here (the degridder writes every other one)
+    if (zout && L.live && !valid) zout[vg] = make_float2(0.0f, 0.0f);
+    if (sw_slots) {
+        // weight sum: wave reduction, one atomic per wave into a slot
+        double ws = wd;
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) wd += __shfl_xor(wd, o, 64);
-            if ((threadIdx.x & 63) == 0 && wd != 0.0)
-                atomicAdd(&sw_slots[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) &
-                                    (kSumSlots - 1)],
-                          wd);
-        }
-        return;
+        for (int o = 32; o > 0; o >>= 1) ws += __shfl_xor(ws, o, 64);
+        if ((threadIdx.x & 63) == 0 && ws != 0.0)
+            atomicAdd(&sw_slots[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) &
+                                (kSumSlots - 1)],
+                      ws);
     }
-    const unsigned pos = counter[coord_key(g, c, row)] + mine;
-    float cr = wt, ci = 0.0f;
-    if (kGrid) {
-        // a zero-weight sample (bucketed only by a SDP_HIP_KEEP_BUCKETS plan,
-        // for the other pols) is an exact zero whatever its visibility holds
-        const float2 xv = (vis && wt != 0.0f) ? eff_vis(vis, vrs, vcs, x, row, chan)
-                                              : make_float2(1.0f, 0.0f);
-        cr = wt != 0.0f ? xv.x * wt : 0.0f;
-        ci = wt != 0.0f ? xv.y * wt : 0.0f;
-    }
-    if (g.do_w || x.shift) {
-        double ph = g.do_w ? c.w * g.s0 : 0.0;
-        if (x.shift) {
-            const double *u = uvw + row * uvw_rs;
-            ph += (u[0] * x.sl + u[1] * x.sm + u[2] * x.sn) * (freq[chan] / kCLight);
-        }
-        ph -= rint(ph);
-        float sn, cs;
-        sincospif((float)(2.0 * ph), &sn, &cs);
-        if (!kGrid) sn = -sn;
-        const float r_ = cr * cs - ci * sn, i_ = cr * sn + ci * cs;
-        cr = r_;
-        ci = i_;
-    }
-    if (kCompact) {
-        // RecC: offsets as fractions of (1 - W/2) - offset (do_w off: w = 0)
-        const double base = 1.0 - 0.5 * g.W;
-        const uint32_t qu = fix_frac(base - c.du, 21), qv = fix_frac(base - c.dv, 21);
-        const uint32_t qw = g.do_w ? fix_frac(base - c.dw, 22) : 0u;
-        RecC rc;
-        rc.cre = cr;
-        rc.cim = ci;
-        rc.lo = qu | (qv << 21);
-        rc.hi = (qv >> 11) | (qw << 10);
-        reinterpret_cast<RecC *>(recs)[pos] = rc;
-        // large grids (16x16-cell buckets): the record's cell in its bucket,
-        // for the padded sub-sort (k_subsort_pad)
-        if (cls) cls[pos] = (uint8_t)(((c.ic0 & 15) >> 1) * 32 + (c.jc0 & 15) * 2 + (c.ic0 & 1));
-        return;
-    }
-    VisRec rec;
-    rec.cre = cr;
-    rec.cim = ci;
-    rec.fu = c.fu;
-    rec.fv = c.fv;
-    rec.fw = c.fw;
-    rec.ij = (uint32_t)c.ic0 | ((uint32_t)c.jc0 << 16);
-    rec.p0 = (uint32_t)c.p0;
-    rec.idx = (uint32_t)vg;
-    recs[pos] = rec;
 }
 
-template <class VT, bool kScatter, bool kGrid, bool kCompact = false>
-__global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw,
-                         int64_t uvw_rs, const double *__restrict__ freq,
-                         const VT *__restrict__ vis, int64_t vrs, int64_t vcs,
-                         const void *__restrict__ wgt, int64_t wrs, int64_t wcs, VisExtra x,
-                         double *sw_slots, unsigned *counter, unsigned *__restrict__ rk,
+template <class VT, bool kScatter, bool kGrid, bool kCompact, int WT, int FB>
+__global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw, int64_t uvw_rs,
+                         const double *__restrict__ fsc, const VT *__restrict__ vis, int64_t vrs,
+                         int64_t vcs, const void *__restrict__ wgt, int64_t wrs, int64_t wcs,
+                         VisExtra x, double *sw_slots, unsigned *counter, unsigned *__restrict__ rk,
                          VisRec *__restrict__ recs, unsigned long long *nbad,
-                         uint8_t *__restrict__ cls = nullptr) {
-    bucket_one<VT, kScatter, kGrid, kCompact>(g, blockIdx.x * (int64_t)blockDim.x + threadIdx.x,
-                                              nvis, uvw, uvw_rs, freq, vis, vrs, vcs, wgt, wrs,
-                                              wcs, x, sw_slots, counter, rk, recs, nbad, cls);
+                         uint8_t *__restrict__ cls, float2 *__restrict__ zout) {
+    bucket_one<VT, kScatter, kGrid, kCompact, WT, FB>(
+        g, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, nvis, uvw, uvw_rs, fsc, vis, vrs, vcs,
+        wgt, wrs, wcs, x, sw_slots, counter, rk, recs, nbad, cls, zout);
 }
 
 __global__ __launch_bounds__(64) void k_sum_slots(const double *__restrict__ slots, double *out) {
@@ -1163,9 +1285,8 @@ struct CoreAcc {
     int x0, nx, y0, ny;
 };
 
-// Flush of a k_grid_mfma_pad / k_grid_mfma_pc region tile into the planes:
-// the waves of the workgroup (wave wv of nwv) take every nwv-th 64-float
-// slice of each plane.
+// Flush of a k_grid_mfma_pad region tile into the planes: the waves of the
+// workgroup (wave wv of nwv) take every nwv-th 64-float slice of each plane.
 template <int W, bool WS, int NG>
 __device__ __forceinline__ void region_flush(const Geo &g, const float *reg, int ibase, int jbase,
                                              uint32_t p0, int p_lo, int p_hi, const CoreAcc &core,
@@ -1443,220 +1564,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 4))) void
     }
 }
 
-// Producer / consumer form of k_grid_mfma_pad: two waves per work item.
-// Wave 0 (producer) streams the item's records, decodes them and evaluates
-// each 16-record block's taps into one of two LDS tap buffers; wave 1
-// (consumer) runs the block's K-steps from the other buffer -- the operand
-// reads, 4 MFMAs per K-step and the accumulators' cell changes in the region
-// tile, exactly as k_grid_mfma_pad.  One workgroup barrier per block hands
-// the buffers over:
-//   iteration i:  the producer fills buffer i & 1 with block i,
-//                 the consumer runs block i - 1 from buffer (i - 1) & 1;  barrier
-// so a block's tap evaluation (VALU and transcendental) runs on one wave
-// while the previous block's MFMAs run on the other, instead of one wave
-// issuing both in order.  With each block the producer passes the number of
-// its K-steps and each K-step's region cell (x | y << 8).  Both waves zero
-// and flush the region.
-template <int NG>
-constexpr int pc_buf_floats() {  // taps, values, meta (K-steps, 4 cell keys, pad)
-    return kTapBatch * kTapRec + kTapBatch * 2 + 8;
-}
-template <int NG>
-constexpr size_t grid_pc_lds() {
-    return (size_t)PadUnit<NG>::RGX * PadUnit<NG>::RGY * kRegCell * sizeof(float) +
-           kTapBatch * sizeof(float4) + 2 * (size_t)pc_buf_floats<NG>() * sizeof(float);
-}
-
-template <int W, bool WS, int NG>
-__global__ __launch_bounds__(128) void k_grid_mfma_pc(Geo g, const RecC *__restrict__ recs,
-                                                      const FineItem *__restrict__ items,
-                                                      uint32_t n_items, float *__restrict__ grid,
-                                                      int p_lo, int p_hi, CoreAcc core) {
-    static_assert(W <= 8, "the MFMA tiles hold 8 taps per axis");
-    extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    constexpr int kRegX = PadUnit<NG>::RGX, kRegY = PadUnit<NG>::RGY;
-    constexpr int kBuf = pc_buf_floats<NG>();
-    float *const reg = reinterpret_cast<float *>(tile);  // [kRegX][kRegY][16]
-    float4 *const stage = reinterpret_cast<float4 *>(reg + kRegX * kRegY * kRegCell);
-    float *const bufs = reinterpret_cast<float *>(stage + kTapBatch);  // 2 x kBuf
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const float ihw = g.inv_half_w, bl = g.beta_l2e;
-    const float fbase = 1.0f - 0.5f * (float)W;  // RecC offset origin
-    // producer: tap t = lane & 7 of records 8m + (lane >> 3)
-    const int tt = lane & 7;
-    const float tihw = (float)tt * ihw;
-    const int wu = (tt & 1) * 4 + (tt >> 1), wv_ = 8 + tt, ww = 16 + tt;
-    // consumer: operand and accumulator addressing of k_grid_mfma_pad
-    const int kBo = (lane >> 4) * kTapRec + ((lane >> 3) & 1) * 4;
-    const int kVo = (lane >> 4) * kTapRec + 8 + (lane & 7);
-    const int kWo = (lane >> 4) * kTapRec + 16 + ((lane & 15) >> 1);
-    const int kCo = kTapBatch * kTapRec + (lane >> 4) * 2 + (lane & 1);
-    const int acc_lane = (((lane & 15) >> 3) * kRegY) * kRegCell;
-    const int acc_y = lane & 7, acc_k = lane >> 4;
-    constexpr int acc_t = 2 * kRegY * kRegCell;
-
-    for (uint32_t w_it = blockIdx.x; w_it < n_items; w_it += gridDim.x) {
-        const uint32_t u = NG == 1 ? w_it : item_index(w_it, n_items);
-        uint32_t bnd[kGroupCell];
-        Item it = NG == 1 ? load_fine_item<kGroupCell>(items, w_it, n_items, bnd)
-                          : load_fine_item<kGroupCell>(items + (size_t)u * NG, 0, 1, bnd);
-        if (NG == 1 && it.b >= it.e) continue;
-        int ibase, jbase;
-        group_origin(g, (int)it.tile, ibase, jbase);
-        const uint32_t p0 = it.p0;
-        // blocks of the unit: its groups' padded records in 16-record blocks
-        uint32_t nblk = 0;
-        if (NG == 1) {
-            nblk = (it.e - it.b + kTapBatch - 1) / kTapBatch;
-        } else {
-#pragma unroll
-            for (int gi = 0; gi < NG; ++gi) {
-                const FineItem *fi = items + (size_t)u * NG + gi;
-                const uint32_t b = __builtin_amdgcn_readfirstlane(fi->b),
-                               e = __builtin_amdgcn_readfirstlane(fi->e);
-                nblk += (e - b + kTapBatch - 1) / kTapBatch;
-            }
-        }
-        RecC nx;
-        if (wv == 0 && it.b < it.e) nx = recs[min(it.b + (uint32_t)lane, it.e - 1)];
-
-        __syncthreads();  // the previous item's flush reads of the region
-        {
-            constexpr int kZ = kRegX * kRegY * kRegCell / 4;  // float4s
-            float4 *r4 = reinterpret_cast<float4 *>(reg);
-            for (int i = threadIdx.x; i < kZ; i += 128) r4[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        }
-        __syncthreads();
-
-        if (wv == 0) {
-            // ---- producer ----
-            uint32_t blk = 0;
-            for (int gi = 0; gi < NG; ++gi) {
-                if (NG > 1 && gi > 0) it = load_fine_item<kGroupCell>(items + (size_t)u * NG + gi, 0, 1, bnd);
-                const uint32_t rb = it.b, re = it.e;
-                if (rb >= re) continue;
-                const int gxo = NG == 1 ? 0 : 2 * (gi >> 1), gyo = NG == 1 ? 0 : 8 * (gi & 1);
-                if (gi > 0) nx = recs[min(rb + (uint32_t)lane, re - 1)];
-                for (uint32_t b0 = rb; b0 < re; b0 += 64) {
-                    const RecC my = nx;
-                    if (b0 + 64 < re) nx = recs[min(b0 + 64 + (uint32_t)lane, re - 1)];
-                    const int nb = (int)min(64u, re - b0);  // a multiple of 4
-                    const uint32_t ri = b0 + (uint32_t)lane;
-                    int cj = 0;
-#pragma unroll
-                    for (int c = 0; c < kGroupCell - 1; ++c) cj += ri >= bnd[c] ? 1 : 0;
-                    const int key = (gxo + (cj & 1)) | ((gyo + (cj >> 1)) << 8);
-                    const float fu = fbase - (float)(my.lo & 0x1fffffu) * 0x1p-21f;
-                    const float fv =
-                        fbase - (float)((my.lo >> 21) | ((my.hi & 0x3ffu) << 11)) * 0x1p-21f;
-                    const float fw = fbase - (float)(my.hi >> 10) * 0x1p-22f;
-                    for (int h = 0; h < 64 / kTapBatch; ++h) {
-                        const int nbh = min(kTapBatch, nb - kTapBatch * h);
-                        if (nbh <= 0) break;
-                        float *const B = bufs + (blk & 1) * kBuf;
-                        wave_lds_sync();  // the previous block's stage reads
-                        if (lane / kTapBatch == h) {
-                            const int r = lane % kTapBatch;
-                            stage[r] = make_float4(fu, fv, fw, 0.0f);
-                            reinterpret_cast<float2 *>(B + kTapBatch * kTapRec)[r] =
-                                make_float2(lane < nb ? my.cre : 0.0f, lane < nb ? my.cim : 0.0f);
-                        }
-                        // the block's K-step count and each K-step's cell
-                        int *const meta = reinterpret_cast<int *>(B + kTapBatch * kTapRec + kTapBatch * 2);
-                        const int kj = (lane - kTapBatch * h) >> 2;
-                        if (lane >= kTapBatch * h && lane < kTapBatch * h + nbh && (lane & 3) == 0)
-                            meta[1 + kj] = key;
-                        if (lane == 0) meta[0] = nbh >> 2;
-                        wave_lds_sync();
-                        float4 f[kTapBatch / 8];
-#pragma unroll
-                        for (int m = 0; m < kTapBatch / 8; ++m) f[m] = stage[8 * m + (lane >> 3)];
-                        float tv_[kTapBatch / 8][3];
-#pragma unroll
-                        for (int m = 0; m < kTapBatch / 8; ++m) {
-                            tv_[m][0] = es_tap<W>(f[m].x, tihw, ihw, bl);
-                            tv_[m][1] = es_tap<W>(f[m].y, tihw, ihw, bl);
-                            tv_[m][2] = WS ? es_tap<W>(f[m].z, tihw, ihw, bl) : (tt == 0 ? 1.0f : 0.0f);
-                        }
-#pragma unroll
-                        for (int m = 0; m < kTapBatch / 8; ++m) {
-                            float *d = B + ((lane >> 3) + 8 * m) * kTapRec;
-                            d[wu] = tv_[m][0];
-                            d[wv_] = tv_[m][1];
-                            d[ww] = tv_[m][2];
-                        }
-                        __syncthreads();  // block blk ready; the consumer is done with block blk - 1
-                        ++blk;
-                    }
-                }
-            }
-            __syncthreads();  // (the consumer's last block)
-        } else {
-            // ---- consumer ----
-            floatx4 acc[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-            // zeros bound to a (zero) region slot: the store before the first
-            // cell's load needs no test
-            int cbase = acc_y * kRegCell + acc_lane + 4 * reg_chunk(acc_k, acc_y);
-            int cur = -1;
-            __syncthreads();  // block 0 ready
-            for (uint32_t blk = 0; blk < nblk; ++blk) {
-                const float *const B = bufs + (blk & 1) * kBuf;
-                const int *const meta = reinterpret_cast<const int *>(B + kTapBatch * kTapRec + kTapBatch * 2);
-                const int nk = __builtin_amdgcn_readfirstlane(meta[0]);
-                int keys[kTapBatch / 4];
-#pragma unroll
-                for (int jj = 0; jj < kTapBatch / 4; ++jj)
-                    keys[jj] = __builtin_amdgcn_readfirstlane(meta[1 + jj]);
-                struct Ops {
-                    floatx4 b;
-                    float v, w, c;
-                };
-                Ops o[kTapBatch / 4];
-#pragma unroll
-                for (int jj = 0; jj < kTapBatch / 4; ++jj) {
-                    o[jj].b = *reinterpret_cast<const floatx4 *>(B + kBo + 4 * jj * kTapRec);
-                    o[jj].v = B[kVo + 4 * jj * kTapRec];
-                    o[jj].w = B[kWo + 4 * jj * kTapRec];
-                    o[jj].c = B[kCo + 8 * jj];
-                }
-#pragma unroll
-                for (int jj = 0; jj < kTapBatch / 4; ++jj) {
-                    if (jj < nk) {
-                        if (keys[jj] != cur) {
-#pragma unroll
-                            for (int t = 0; t < 4; ++t)
-                                *reinterpret_cast<floatx4 *>(reg + cbase + t * acc_t) = acc[t];
-                            cur = keys[jj];
-                            const int xo = cur & 255, y = (cur >> 8) + acc_y;
-                            cbase = (xo * kRegY + y) * kRegCell + acc_lane + 4 * reg_chunk(acc_k, y);
-#pragma unroll
-                            for (int t = 0; t < 4; ++t)
-                                acc[t] = *reinterpret_cast<const floatx4 *>(reg + cbase + t * acc_t);
-                        }
-                        const float a = o[jj].w * o[jj].c;
-                        float bt[4];
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) bt[t] = o[jj].b[t] * o[jj].v;
-#pragma unroll
-                        for (int t = 0; t < 4; ++t)
-                            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bt[t], acc[t], 0, 0, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x0002, 5, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x0008, 4, 0);
-                    }
-                }
-                __syncthreads();  // block blk consumed; block blk + 1 ready
-            }
-#pragma unroll
-            for (int t = 0; t < 4; ++t) *reinterpret_cast<floatx4 *>(reg + cbase + t * acc_t) = acc[t];
-        }
-        __syncthreads();  // the region complete
-        region_flush<W, WS, NG>(g, reg, ibase, jbase, p0, p_lo, p_hi, core, grid, lane, wv, 2);
-    }
-}
-
 // MFMA degridder (predict) on one-cell buckets: the adjoint of
 // k_grid_mfma_pad's GEMM.  All records of a cell share their footprint
 // origin, so for 16 records of one cell
@@ -1687,9 +1594,11 @@ __global__ __launch_bounds__(128) void k_grid_mfma_pc(Geo g, const RecC *__restr
 // lane stores, without a branch: lanes past the batch's records write to a
 // per-block slot of `sink` (a skipped store left the record wait behind the
 // previous batch's store), and the 4 lanes of a record write the same value.
-#ifndef SDP_DG_STORE
-#define SDP_DG_STORE 0  // (A/B builds: 1 = one lane per record, 2 = masked store)
-#endif
+// Those duplicate and sink stores cost no HBM traffic: with one lane group
+// storing (the others into the sink) WRITE_SIZE stays 2.74 GB per C2 launch
+// (2.72 now) for 0.99 GB of visibilities, and a masked store (no sink) gives
+// 2.38 GB but 5.09 vs 4.85 ms (profiles/r06_degrid_store_ab.txt): the write
+// amplification is the scattered 8-byte visibility stores themselves.
 constexpr int kDegridSinkBlocks = 4096;  // sink slots (x 64 lanes)
 __device__ float4 g_zero16[1];            // 16 zero bytes (never written)
 template <int W, bool WS>
@@ -1832,15 +1741,8 @@ __global__ __launch_bounds__(64) void k_degrid_mfma(Geo g, const VisRec *__restr
             sr += __shfl_xor(sr, 32);
             si += __shfl_xor(si, 32);
             if constexpr (VD) {
-#if SDP_DG_STORE == 1
-                float2 *const dst = (valid && kg == 0) ? out + idx : dump;
-                *dst = make_float2(cre * sr - cim * si, cre * si + cim * sr);
-#elif SDP_DG_STORE == 2
-                if (valid && kg == 0) out[idx] = make_float2(cre * sr - cim * si, cre * si + cim * sr);
-#else
                 float2 *const dst = valid ? out + idx : dump;
                 *dst = make_float2(cre * sr - cim * si, cre * si + cim * sr);
-#endif
             } else {
                 float2 *const dst = valid ? out + ri : dump;
                 float2 v = *dst;
@@ -2147,34 +2049,6 @@ __device__ __forceinline__ double es_tap64(double f, int t, double ihw, double b
     return y > 0.0 ? exp(beta * (sqrt(y) - 1.0)) : 0.0;
 }
 
-template <class VT>
-__device__ __forceinline__ double2 eff_vis_d(const VT *vis, int64_t vrs, int64_t vcs,
-                                             const VisExtra &x, int64_t row, int chan) {
-    const VT *p = vis + row * vrs + chan * vcs;
-    if (!x.conv) {
-        if (!x.fbytes) return load_vis_d(p);
-        const double m = flag_mask(x, row, chan, x.fpol);
-        if (m == 0.0) return make_double2(0.0, 0.0);
-        const double2 v = load_vis_d(p);
-        return make_double2(v.x * m, v.y * m);
-    }
-    double re = 0.0, im = 0.0;
-    for (int k = 0; k < x.npv; ++k) {
-        if (x.cre[k] == 0.0 && x.cim[k] == 0.0) continue;
-        double m = 1.0;
-        if (x.fbytes) {
-            m = flag_mask(x, row, chan, k);
-            if (m == 0.0) continue;
-        }
-        double2 v = load_vis_d(p + k * x.vps);
-        v.x *= m;
-        v.y *= m;
-        re += x.cre[k] * v.x - x.cim[k] * v.y;
-        im += x.cre[k] * v.y + x.cim[k] * v.x;
-    }
-    return make_double2(re, im);
-}
-
 // value pass of the fp64 path (the count pass is k_bucket's): VisRec64 at
 // offs[key] + rank, value and phase factor in fp64
 template <class VT, bool kGrid>
@@ -2275,14 +2149,10 @@ constexpr int kTThreads = 1024;     // second-level kernels, bin scans
 constexpr int kT1Threads = 512;     // count and value passes (VGPR-limited occupancy)
 constexpr unsigned kTChunk = 131072;  // records per second-level chunk
 constexpr unsigned kTSeg = 16;       // chunks per segment of the cells' column prefix
-#ifndef SDP_TU
-#define SDP_TU 2
-#endif
-constexpr int kTU = SDP_TU;          // visibilities per lane in flight (value pass)
-#ifndef SDP_TUC
-#define SDP_TUC 2
-#endif
-constexpr int kTUc = SDP_TUC;        // the same for the count pass alone
+// visibilities per lane in flight in the value pass: 1 (C2: 1.10 ms, against
+// 1.21 for 2 and 1.10 for 4; profiles/r06_sort_tu_ab.txt)
+constexpr int kTU = 1;
+constexpr int kTUc = 2;  // the same for the count pass (C2: 0.66 ms, 0.69 for 4)
 constexpr int kTU2 = 4;              // records per lane in flight (cell count / final move)
 
 struct TChunk {
@@ -2312,81 +2182,11 @@ __device__ __forceinline__ unsigned lds_run_add(unsigned key, bool valid, unsign
     return hb + (unsigned)(lane - head);
 }
 
-// A visibility in two phases, so that a lane's kTU visibilities issue all
-// their loads before any of them is used: t_load (uvw of the row, frequency,
-// flag-masked weight) and t_classify (in-slab test, fp64 coordinates,
-// bucketed or not) -- bit-identical in the count and the value pass.
-// v < 2^32 (the plan refuses larger calls).
-struct TLoad {
-    uint32_t row, chan;
-    double um, vm, wm, s, wd;  // s = frequency / c (fsc[chan]: the same division as vis_coord)
-    double keep;               // 1 - flag of the weight's pol (1 without flags)
-    bool live;
-};
-
-// The weight and flag element types are compile-time in the two-level
-// passes -- WT: 4 = f32, 8 = f64 (no weights: a device 1.0f with zero
-// strides); FB: 0 = no flags, 1 = int8, 8 = int64 flags (int32 flags are
-// widened to int64 first, k_widen_flags) -- and a lane's visibilities load
-// from clamped, in-bounds
-// indices with no branch before their first use: all of a lane's kTU
-// visibilities' loads (uvw, frequency scale, weight, flag, and in the value
-// pass the visibility) are in flight together.  A runtime switch on the
-// types, with each load behind its own branch and a `live` test, had put a
-// wait for every load before the next one issued (C2 count pass: ~200
-// instructions and four serialised memory round trips per visibility).
-template <int WT, int FB>
-__device__ __forceinline__ TLoad t_load(const Geo &g, int64_t v, int64_t vend,
-                                        const double *__restrict__ uvw, int64_t rs,
-                                        const double *__restrict__ fsc,
-                                        const void *__restrict__ wgt, int64_t wrs, int64_t wcs,
-                                        const VisExtra &x) {
-    TLoad L;
-    L.live = v < vend;
-    const uint32_t v32 = (uint32_t)(L.live ? v : vend - 1), nc = (uint32_t)g.nchan;
-    // row = v / nchan through the fp64 reciprocal (exact to one step, then
-    // corrected), not an integer division
-    uint32_t r32 = (uint32_t)((double)v32 * g.inv_nchan);
-    if ((uint64_t)r32 * nc > v32) --r32;
-    else if ((uint64_t)(r32 + 1u) * nc <= v32) ++r32;
-    L.row = r32;
-    L.chan = v32 - r32 * nc;
-    const double *p = uvw + (int64_t)L.row * rs;
-    L.um = p[0];
-    L.vm = p[1];
-    L.wm = p[2];
-    L.s = fsc[L.chan];
-    double w;
-    const int64_t wi = (int64_t)L.row * wrs + (int64_t)L.chan * wcs;
-    if constexpr (WT == 8) w = static_cast<const double *>(wgt)[wi];
-    else w = (double)static_cast<const float *>(wgt)[wi];
-    L.keep = 1.0;
-    if constexpr (FB != 0) {
-        using FT = typename std::conditional<FB == 8, int64_t, int8_t>::type;
-        L.keep = 1.0 - (double)static_cast<const FT *>(
-                           x.flags)[(int64_t)L.row * x.frs + (int64_t)L.chan * x.fcs + x.fpol * x.fps];
-        // select, not multiply: a flagged sample's weight is an exact zero
-        // even when the stored weight is NaN or Inf
-        w = L.keep == 0.0 ? 0.0 : w * L.keep;
-    }
-    L.wd = L.live ? w : 0.0;
-    return L;
-}
-
-// int32 flags of a two-level pass as int64 (FB = 8): a contiguous
-// [nrow, nchan, npol] copy (one element for a zero-stride broadcast)
-__device__ float g_unit_weight = 1.0f;  // the weights of a call without weights
-template <class FT>
-__global__ void k_widen_flags(const FT *__restrict__ src, int64_t frs, int64_t fcs, int64_t fps,
-                              int64_t nrow, int nchan, int npol, int64_t *__restrict__ dst) {
-    const int64_t n = nrow * nchan * (int64_t)npol;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t rc = i / npol, row = rc / nchan;
-        const int pol = (int)(i - rc * npol), chan = (int)(rc - row * nchan);
-        dst[i] = (int64_t)src[row * frs + chan * fcs + pol * fps];
-    }
-}
+// A visibility of the two-level passes in two phases, so that a lane's kTU
+// visibilities issue all their loads before any of them is used: t_load
+// (above: uvw of the row, frequency, flag-masked weight) and t_classify
+// (in-slab test, fp64 coordinates, bucketed or not) -- bit-identical in the
+// count and the value pass.  v < 2^32 (the plan refuses larger calls).
 
 // frequency / c per channel (the division vis_coord performs per visibility)
 __global__ void k_fscale(const double *__restrict__ freq, int nchan, double *__restrict__ fsc) {
@@ -2542,48 +2342,6 @@ __global__ __launch_bounds__(kTThreads) void k_t_bins(int nb, const unsigned *__
         meta_ch[1] = nsg_t;
     }
 }
-
-// the visibility's value in two phases: `load` issues the loads (the
-// visibility from clamped indices, beside the lane's other loads), `value`
-// combines them after every load is in flight.  Without a pol conversion the
-// weight pol's flag (TLoad::keep) masks it; a pol conversion (x.conv, the
-// 4-pol frames) reads its pols and flags in `value`.
-template <class VT, int KIND, bool kGrid, int FB>
-struct TVal {
-    using type = typename std::conditional<KIND >= 2, double2, float2>::type;
-    __device__ static __forceinline__ VT load(const VT *vis, int64_t vrs, int64_t vcs,
-                                              const VisExtra &x, const TLoad &L) {
-        VT raw{};
-        if constexpr (kGrid)
-            if (vis && !x.conv) raw = vis[(int64_t)L.row * vrs + (int64_t)L.chan * vcs];
-        return raw;
-    }
-    __device__ static __forceinline__ type value(const VT *vis, int64_t vrs, int64_t vcs,
-                                                 const VisExtra &x, const TLoad &L, VT raw) {
-        type xv;
-        xv.x = 1;
-        xv.y = 0;
-        if constexpr (kGrid) {
-            if (!vis) return xv;  // (unit visibilities: the PSF)
-            if (x.conv) {
-                if constexpr (KIND >= 2) return eff_vis_d(vis, vrs, vcs, x, L.row, L.chan);
-                else return eff_vis(vis, vrs, vcs, x, L.row, L.chan);
-            }
-            const double2 v = make_double2((double)raw.x, (double)raw.y);
-            if constexpr (FB == 0) {
-                xv.x = v.x;
-                xv.y = v.y;
-            } else {
-                // select, not multiply: a NaN in a flagged visibility must not
-                // reach the image
-                const double m = L.keep;
-                xv.x = m == 0.0 ? 0.0 : v.x * m;
-                xv.y = m == 0.0 ? 0.0 : v.y * m;
-            }
-        }
-        return xv;
-    }
-};
 
 // KIND 0: RecC (4-padded invert), 1: VisRec (fp32 predict), 3: Rec64 (the
 // fp64 MFMA kernels)
@@ -3966,6 +3724,7 @@ struct Plan {
     bool pad64 = false;              // fp64 invert: VisRec64 cells padded to 4 (k_grid_f64_mfma)
     bool mfma64 = false;             // fp64 predict on k_degrid_f64_mfma (one-cell buckets)
     float2 *vdirect = nullptr;       // dirty2ms: the degridder writes c64 vis in place
+    float2 *zout = nullptr;          // ... and the rank pass zeroes the ones with no record
     int chunk_planes = 1;            // planes resident per pass
     int fft_planes = 1;              // planes per FFT / screen batch (spec, spec_in)
     int row_lo = 0, row_hi = 0;      // grid rows (x) the visibilities reach
@@ -4542,6 +4301,69 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     return P;
 }
 
+// The weights and flags of a call as the typed bucketing passes read them
+// (t_load<WT, FB>): no weights become a device 1.0f with zero strides, int32
+// flags a contiguous int64 copy (a zero-stride broadcast: one element);
+// dispatch() calls a kernel-launch template with the call's (WT, FB).
+struct TypedIn {
+    VisExtra x;
+    const void *wgt;
+    int64_t wrs, wcs;
+    int wt, fb;
+    template <class F>
+    void dispatch(F launch) const {
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I4 = std::integral_constant<int, 4>;
+        using I8 = std::integral_constant<int, 8>;
+        if (fb == 0) {
+            if (wt == 4) launch(I4{}, I0{});
+            else launch(I8{}, I0{});
+        } else if (fb == 1) {
+            if (wt == 4) launch(I4{}, I1{});
+            else launch(I8{}, I1{});
+        } else {
+            if (wt == 4) launch(I4{}, I8{});
+            else launch(I8{}, I8{});
+        }
+    }
+};
+
+static TypedIn typed_inputs(const Geo &g, const Inputs &in, hipStream_t st) {
+    TypedIn t;
+    t.x = in.x;
+    t.wgt = in.wgt;
+    t.wrs = in.wrs;
+    t.wcs = in.wcs;
+    if (!t.wgt) {
+        void *one = nullptr;
+        SDP_HIP_CHECK(hipGetSymbolAddress(&one, HIP_SYMBOL(g_unit_weight)));
+        t.wgt = one;
+        t.wrs = t.wcs = 0;
+        t.x.wgt_f64 = 0;
+    }
+    t.wt = t.x.wgt_f64 ? 8 : 4;
+    VisExtra &x = t.x;
+    if (x.fbytes == 4) {
+        const bool bc = x.frs == 0 && x.fcs == 0 && x.fps == 0;
+        const int np = bc ? 1 : x.npv;
+        const int64_t nr = bc ? 1 : g.nrow, nc = bc ? 1 : g.nchan;
+        int64_t *f64 = scratch<int64_t>("flags64", (size_t)std::max<int64_t>(nr * nc * np, 1));
+        const unsigned gw = (unsigned)std::max<int64_t>(
+            1, std::min<int64_t>(grid1d(nr * nc * np, 256), 65536));
+        if (g.nrow > 0)
+            k_widen_flags<int32_t><<<gw, 256, 0, st>>>(static_cast<const int32_t *>(x.flags), x.frs,
+                                                      x.fcs, x.fps, nr, (int)nc, np, f64);
+        x.flags = f64;
+        x.fbytes = 8;
+        x.frs = bc ? 0 : nc * np;
+        x.fcs = bc ? 0 : np;
+        x.fps = bc ? 0 : 1;
+    }
+    t.fb = x.fbytes;
+    return t;
+}
+
 // Bucketing (no host sync except the 4-padded record total): histogram with
 // ranks, scan, scatter of the records, work items, metadata.
 static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st,
@@ -4579,6 +4401,10 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
 
     const unsigned nb = grid1d(std::max<int64_t>(pt.nvis, 1), 256);
     double *slots = in.x.sumwt ? scratch<double>("sumwt_slots", kSumSlots) : nullptr;
+    // the typed passes' weights, flags and frequency scales (t_load)
+    const TypedIn ti = typed_inputs(g, in, st);
+    double *fsc = scratch<double>("t_fscale", g.nchan);
+    k_fscale<<<grid1d(g.nchan, 256), 256, 0, st>>>(in.freq, g.nchan, fsc);
     // weight sums: in the count pass, or in the value pass of a reused plan
     auto launch_bucket = [&](auto scatter_tag, unsigned *counter) {
         constexpr bool S = decltype(scatter_tag)::value;
@@ -4588,10 +4414,13 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
             using VT = typename decltype(vt_tag)::type;
             constexpr bool G = decltype(grid_tag)::value, C = decltype(compact_tag)::value;
             const VT *vp = static_cast<const VT *>(visp);
-            k_bucket<VT, S, G, C><<<nb, 256, 0, st>>>(g, pt.nvis, in.uvw, in.uvw_rs, in.freq, vp,
-                                                      in.vrs, in.vcs, in.wgt, in.wrs, in.wcs,
-                                                      in.x, sl, counter, kr, out, pt.nbad,
-                                                      S && P.subpad ? P.cls : nullptr);
+            ti.dispatch([&](auto wt_tag, auto fb_tag) {
+                k_bucket<VT, S, G, C, decltype(wt_tag)::value, decltype(fb_tag)::value>
+                    <<<nb, 256, 0, st>>>(g, pt.nvis, in.uvw, in.uvw_rs, fsc, vp, in.vrs, in.vcs,
+                                         ti.wgt, ti.wrs, ti.wcs, ti.x, sl, counter, kr, out,
+                                         pt.nbad, S && P.subpad ? P.cls : nullptr,
+                                         S ? nullptr : P.zout);
+            });
         };
         auto by_mode = [&](auto vt_tag) {
             using VT = typename decltype(vt_tag)::type;
@@ -4607,14 +4436,14 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
                         in.wcs, in.x, sl, counter, kr, o64);
                 return;
             }
-            if (grid_mode && S && (P.pad4 || P.subpad))  // 16-byte RecC records
-                go(vt_tag, std::true_type{}, std::true_type{}, in.vis);
-            else if (grid_mode)
-                go(vt_tag, std::true_type{}, std::false_type{}, in.vis);
-            else
-                go(vt_tag, std::false_type{}, std::false_type{}, nullptr);
+            // the value pass of an fp32 invert writes 16-byte RecC records
+            // (one-cell and large-grid plans are both 4-padded), a predict's
+            // 32-byte VisRec; the rank pass reads no visibilities (one
+            // instantiation)
+            if (S && grid_mode) go(vt_tag, std::true_type{}, std::true_type{}, in.vis);
+            else go(TypeTag<float2>{}, std::false_type{}, std::false_type{}, nullptr);
         };
-        if (in.vis_dtype == SDP_HIP_C128) by_mode(TypeTag<double2>{});
+        if (S && grid_mode && in.vis_dtype == SDP_HIP_C128) by_mode(TypeTag<double2>{});
         else by_mode(TypeTag<float2>{});
     };
     if (values_only) {  // SDP_HIP_REUSE_BUCKETS: keys, ranks, offsets, items kept
@@ -4727,7 +4556,6 @@ static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t 
     const auto r = chunk_items(P, p_lo, p_hi);
     const unsigned n = r.second - r.first;
     if (n == 0) return;
-    static const bool pc = env_int("SDP_HIP_GRID_PC", 0) != 0;
     if (P.subpad) {
         // units of 4 of a coarse item's 16 groups (2 x pairs x 2 y halves,
         // 4 x 16 cells, an 11 x 23-cell region).  C4 N = 1 gridding: 1 group
@@ -4735,18 +4563,9 @@ static void launch_grid_mfma_pad(const Plan &P, int p_lo, int p_hi, hipStream_t 
         // units flush fewer atomics (the small groups of C4's sparse cells,
         // ~120 records each, were bound by them) but hold more LDS per wave
         const unsigned nu = n * 4u;
-        if (pc)
-            k_grid_mfma_pc<W, WS, 4><<<nu, 128, grid_pc_lds<4>(), st>>>(
-                P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo,
-                p_hi, P.core);
-        else
-            k_grid_mfma_pad<W, WS, 4><<<nu, 64, grid_mfma_pad_lds<4>(), st>>>(
-                P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo,
-                p_hi, P.core);
-    } else if (pc) {
-        k_grid_mfma_pc<W, WS, 1><<<n, 128, grid_pc_lds<1>(), st>>>(
-            P.g, reinterpret_cast<const RecC *>(P.recs), P.pt.fitems + r.first, n, (float *)P.grid,
-            p_lo, p_hi, P.core);
+        k_grid_mfma_pad<W, WS, 4><<<nu, 64, grid_mfma_pad_lds<4>(), st>>>(
+            P.g, P.recs_pad, P.pt.fitems + 16 * (size_t)r.first, nu, (float *)P.grid, p_lo, p_hi,
+            P.core);
     } else
         k_grid_mfma_pad<W, WS, 1><<<n, 64, grid_mfma_pad_lds<1>(), st>>>(
             P.g, reinterpret_cast<const RecC *>(P.recs), P.pt.fitems + r.first, n, (float *)P.grid,
@@ -5206,54 +5025,10 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         if (after_clear) after_clear();
     }
     k_fscale<<<grid1d(g.nchan, 256), 256, 0, st>>>(in.freq, g.nchan, pt.t_fsc);
-    // the passes' weight and flag types (t_load): 1- and 4-byte flags are
-    // widened to a contiguous int64 copy first
-    VisExtra x = in.x;
-    const void *wgt = in.wgt;
-    int64_t wrs = in.wrs, wcs = in.wcs;
-    if (!wgt) {
-        void *one = nullptr;
-        SDP_HIP_CHECK(hipGetSymbolAddress(&one, HIP_SYMBOL(g_unit_weight)));
-        wgt = one;
-        wrs = wcs = 0;
-        x.wgt_f64 = 0;
-    }
-    const int wt = x.wgt_f64 ? 8 : 4;
-    if (x.fbytes == 4) {
-        // (a zero-stride broadcast flag widens to one element)
-        const bool bc = x.frs == 0 && x.fcs == 0 && x.fps == 0;
-        const int np = bc ? 1 : x.npv;
-        const int64_t nr = bc ? 1 : g.nrow, nc = bc ? 1 : g.nchan;
-        int64_t *f64 = scratch<int64_t>("flags64", (size_t)std::max<int64_t>(nr * nc * np, 1));
-        const unsigned gw = (unsigned)std::max<int64_t>(
-            1, std::min<int64_t>(grid1d(nr * nc * np, 256), 65536));
-        if (nvis > 0)
-            k_widen_flags<int32_t><<<gw, 256, 0, st>>>(static_cast<const int32_t *>(x.flags), x.frs,
-                                                      x.fcs, x.fps, nr, (int)nc, np, f64);
-        x.flags = f64;
-        x.fbytes = 8;
-        x.frs = bc ? 0 : nc * np;
-        x.fcs = bc ? 0 : np;
-        x.fps = bc ? 0 : 1;
-    }
-    const int fb = x.fbytes;
-    // calls the kernel template `launch` with the (WT, FB) of this call
-    auto with_types = [&](auto launch) {
-        using I0 = std::integral_constant<int, 0>;
-        using I1 = std::integral_constant<int, 1>;
-        using I4 = std::integral_constant<int, 4>;
-        using I8 = std::integral_constant<int, 8>;
-        if (fb == 0) {
-            if (wt == 4) launch(I4{}, I0{});
-            else launch(I8{}, I0{});
-        } else if (fb == 1) {
-            if (wt == 4) launch(I4{}, I1{});
-            else launch(I8{}, I1{});
-        } else {
-            if (wt == 4) launch(I4{}, I8{});
-            else launch(I8{}, I8{});
-        }
-    };
+    const TypedIn ti = typed_inputs(g, in, st);
+    const VisExtra &x = ti.x;
+    const void *wgt = ti.wgt;
+    const int64_t wrs = ti.wrs, wcs = ti.wcs;
     const int cus = cu_count();
     const unsigned gch = std::min<unsigned>(pt.t_maxch, 4u * (unsigned)cus);
     auto scatter = [&](double *sl) {
@@ -5261,7 +5036,7 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
             using VT = typename decltype(vt_tag)::type;
             constexpr int K = decltype(kind_tag)::value;
             constexpr bool G = decltype(grid_tag)::value;
-            with_types([&](auto wt_tag, auto fb_tag) {
+            ti.dispatch([&](auto wt_tag, auto fb_tag) {
                 k_t_scatter<VT, K, G, decltype(wt_tag)::value, decltype(fb_tag)::value>
                     <<<pt.t_g1, kT1Threads, lds_bins, st>>>(
                         g, nvis, pt.t_vpw, in.uvw, in.uvw_rs, pt.t_fsc,
@@ -5311,7 +5086,7 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
         return;
     }
     if (nvis > 0)
-        with_types([&](auto wt_tag, auto fb_tag) {
+        ti.dispatch([&](auto wt_tag, auto fb_tag) {
             k_t_count<decltype(wt_tag)::value, decltype(fb_tag)::value>
                 <<<pt.t_g1, kT1Threads, lds_bins, st>>>(g, nvis, pt.t_vpw, in.uvw, in.uvw_rs,
                                                         pt.t_fsc, wgt, wrs, wcs, x, slots, pt.t_binc,
@@ -5583,6 +5358,20 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
                                                                   in.vrs, in.vcs, oc);
         SDP_HIP_CHECK(hipGetLastError());
     };
+    // all planes in one pass into plain contiguous c64 visibilities: the
+    // degridder applies the record factor and writes each visibility once,
+    // and on the single-level bucketing the rank pass zeroes the
+    // visibilities no record reaches (no separate 1 GB zeroing pass on C2);
+    // otherwise the output is zeroed first
+    const bool trivial_oc = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
+    if (P.chunk_planes == g.nplanes && !accumulate && in.vis_dtype != SDP_HIP_C128 && trivial_oc &&
+        in.vcs == 1 && in.vrs == in.nchan && !P.f64) {
+        P.vdirect = static_cast<float2 *>(vis);
+        if (!g.tiled) P.zout = P.vdirect;
+    }
+    auto zero_vis_unless_fused = [&](hipStream_t s) {
+        if (!P.zout) zero_vis(s);
+    };
     // screens + FFTs of planes [p_lo, p_lo + np) into the grid
     std::vector<std::unique_ptr<StageTimer>> stage_t;
     auto plane_stage = [&](int p_lo, int np, hipStream_t s) {
@@ -5610,21 +5399,14 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         if (!overlap) return;
         hipStream_t aux = aux_stream();
         stream_after(aux, st);
-        zero_vis(aux);
+        zero_vis_unless_fused(aux);
         zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
         SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
         SDP_HIP_CHECK(hipEventRecord(zdone, aux));
     };
-    if (!overlap) zero_vis(st);
+    if (!overlap) zero_vis_unless_fused(st);
     bucket_all(P, in, false, st, start_aux);
     if (P.subsort) subsort_items(P, st);
-    // all planes in one pass into plain contiguous c64 visibilities: the
-    // degridder applies the record factor and writes each visibility once
-    // (the zeroing above covers the ones with no record)
-    const bool trivial_oc = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
-    if (P.chunk_planes == g.nplanes && !accumulate && in.vis_dtype != SDP_HIP_C128 && trivial_oc &&
-        in.vcs == 1 && in.vrs == in.nchan && !P.f64)
-        P.vdirect = static_cast<float2 *>(vis);
     // (the fp64 degridder writes each visibility itself, through the pol
     // conversion, adding into the zeroed output)
     float2 *acc = (P.vdirect || P.f64)
