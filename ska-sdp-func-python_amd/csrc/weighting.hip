@@ -44,7 +44,6 @@ struct Geom {
     int flag_bytes;  // 0: no flags, else 1 / 4 / 8 byte integers
     int zero_val;    // crval_u == crval_v == 0: one division gives cell and conjugate
     int win, win_u0, win_v0;  // LDS-privatised uv window (win x win cells), 0 = none
-    int dbg;                  // SDP_HIP_WEIGHT_DBG (measurement only): 1 no HBM atomics, 2 no LDS atomics
     int nt;                   // threads per block of k_grid_weights (256 or 1024)
     int mirror;               // conjugate cell == mirror of the cell about (cu2/2, cv2/2)
     long long cu2, cv2;       //   (crval 0, integral crpix): grid only the cell, fold later
@@ -210,12 +209,10 @@ __global__ __launch_bounds__(NT) void k_grid_weights(Geom g, int64_t ntiles,
         auto add_cell = [&](int plane0, long long pu, long long pv, const double *a) {
             const long long du = pu - g.win_u0, dv = pv - g.win_v0;
             if (g.win && du >= 0 && du < g.win && dv >= 0 && dv < g.win) {
-                if (g.dbg & 2) return;
 #pragma unroll
                 for (int p = 0; p < NP; ++p)
                     atomicAdd(&s_win[((plane0 + p) * g.win + dv) * g.win + du], a[p]);
             } else {
-                if (g.dbg & 1) return;
 #pragma unroll
                 for (int p = 0; p < NP; ++p)
                     atomicAdd(g1 + ((size_t)(plane0 + p) * g.ny + pv) * g.nx + pu, a[p]);
@@ -483,7 +480,7 @@ Geom make_geom(int64_t nrow, int nchan, int npol, int g_nchan, int ny, int nx, c
                 "flag element size must be 0, 1, 4 or 8 bytes");
     SDP_REQUIRE(wcs != nullptr && wcs[1] != 0.0 && wcs[4] != 0.0, "grid wcs cdelt must be non-zero");
     Geom g{nrow, nchan, npol, g_nchan, ny, nx, wcs[0], wcs[1], wcs[2], wcs[3], wcs[4], wcs[5],
-           flag_bytes, wcs[0] == 0.0 && wcs[3] == 0.0, 0, 0, 0, 0, 1024, 0, 0, 0};
+           flag_bytes, wcs[0] == 0.0 && wcs[3] == 0.0, 0, 0, 0, 1024, 0, 0, 0};
     if (const char *e = std::getenv("SDP_HIP_WEIGHT_NT")) g.nt = std::atoi(e) == 256 ? 256 : 1024;
     if (g.zero_val && wcs[2] == std::floor(wcs[2]) && wcs[5] == std::floor(wcs[5]) &&
         std::fabs(wcs[2]) < 1e9 && std::fabs(wcs[5]) < 1e9 && !std::getenv("SDP_HIP_WEIGHT_NOMIRROR")) {
@@ -491,7 +488,6 @@ Geom make_geom(int64_t nrow, int nchan, int npol, int g_nchan, int ny, int nx, c
         g.cu2 = 2 * ((long long)wcs[2] - 1);
         g.cv2 = 2 * ((long long)wcs[5] - 1);
     }
-    if (const char *e = std::getenv("SDP_HIP_WEIGHT_DBG")) g.dbg = std::atoi(e);
     return g;
 }
 

@@ -1860,6 +1860,79 @@ __global__ __launch_bounds__(256) void k_tr_t_to_grid(Geo g, const T *__restrict
     }
 }
 
+// c64 planes with ny % 4 == 0: the same transposes with 16-byte accesses (two
+// complex per lane; image rows come in even pairs, so a pair never straddles
+// the ky wrap) over tiles aligned to 64 grid rows.  grid -> T writes the
+// whole aligned tile: its rows below row_lo read as zeros, which T holds
+// there anyway.
+__global__ __launch_bounds__(256) void k_tr_grid_to_t16(Geo g, const float2 *__restrict__ grid,
+                                                        float2 *__restrict__ t, int row_lo,
+                                                        int row_hi) {
+    __shared__ float2 sm[kTr][kTr + 1];
+    const int x0 = (row_lo & ~(kTr - 1)) + blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
+    const int64_t plane = (int64_t)g.ngx * g.ngy, tplane = (int64_t)g.ny * g.ngx;
+    const int tid = threadIdx.y * kTr + threadIdx.x, c2 = tid & 31, rr = tid >> 5;
+    {
+        const int iy = i0 + 2 * c2;
+        const int Y = iy - g.ny / 2;
+        const int ky = Y < 0 ? Y + g.ngy : Y;
+#pragma unroll
+        for (int r = rr; r < kTr; r += 8) {
+            const int x = x0 + r;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (x >= row_lo && x < row_hi && iy < g.ny)
+                v = *reinterpret_cast<const float4 *>(grid + q * plane + (int64_t)x * g.ngy + ky);
+            sm[r][2 * c2] = make_float2(v.x, v.y);
+            sm[r][2 * c2 + 1] = make_float2(v.z, v.w);
+        }
+    }
+    __syncthreads();
+    const int x = x0 + 2 * c2;
+#pragma unroll
+    for (int r = rr; r < kTr; r += 8) {
+        const int iy = i0 + r;
+        if (iy < g.ny && x < g.ngx) {
+            const float2 a = sm[2 * c2][r], b = sm[2 * c2 + 1][r];
+            *reinterpret_cast<float4 *>(t + q * tplane + (int64_t)iy * g.ngx + x) =
+                make_float4(a.x, a.y, b.x, b.y);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tr_t_to_grid16(Geo g, const float2 *__restrict__ t,
+                                                        float2 *__restrict__ grid, int row_lo,
+                                                        int row_hi) {
+    __shared__ float2 sm[kTr][kTr + 1];
+    const int x0 = (row_lo & ~(kTr - 1)) + blockIdx.x * kTr, i0 = blockIdx.y * kTr, q = blockIdx.z;
+    const int64_t plane = (int64_t)g.ngx * g.ngy, tplane = (int64_t)g.ny * g.ngx;
+    const int tid = threadIdx.y * kTr + threadIdx.x, c2 = tid & 31, rr = tid >> 5;
+    {
+        const int x = x0 + 2 * c2;
+#pragma unroll
+        for (int r = rr; r < kTr; r += 8) {
+            const int iy = i0 + r;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (iy < g.ny && x < g.ngx)
+                v = *reinterpret_cast<const float4 *>(t + q * tplane + (int64_t)iy * g.ngx + x);
+            sm[2 * c2][r] = make_float2(v.x, v.y);
+            sm[2 * c2 + 1][r] = make_float2(v.z, v.w);
+        }
+    }
+    __syncthreads();
+    const int iy = i0 + 2 * c2;
+    const int Y = iy - g.ny / 2;
+    const int ky = Y < 0 ? Y + g.ngy : Y;
+#pragma unroll
+    for (int r = rr; r < kTr; r += 8) {
+        const int x = x0 + r;
+        if (x >= row_lo && x < row_hi && iy < g.ny) {
+            const float2 a = sm[r][2 * c2], b = sm[r][2 * c2 + 1];
+            *reinterpret_cast<float4 *>(grid + q * plane + (int64_t)x * g.ngy + ky) =
+                make_float4(a.x, a.y, b.x, b.y);
+        }
+    }
+}
+
 // w screens + grid correction reading the transposed spectrum (ix fastest:
 // coalesced T reads; RASCIL's transposed output (sx = 1) is coalesced too)
 template <class T>
@@ -3805,7 +3878,8 @@ static hipStream_t aux_stream() {
 }
 
 // The backward x-FFT input T_in holds the transposed band [row_lo, row_hi)
-// of every T row and zeros elsewhere.  The transpose writes only the band,
+// of every T row and zeros elsewhere.  The transposes write only the band
+// (the 16-byte one also the zeros around it in its 64-row aligned tiles),
 // so the zeros are kept across calls: the buffer is cleared only when it is
 // (re)allocated or the band / shape changes.
 struct BandState {
@@ -4900,6 +4974,17 @@ static dim3 tr_grid(const Geo &g, int xrows, int np) {
                 (unsigned)np);
 }
 
+// the 16-byte c64 transposes: image rows in even pairs (ny % 4 == 0), grid
+// rows and columns even (16-byte aligned pairs); tiles aligned to 64 rows
+static bool tr16(const Geo &g) {
+    return g.ny % 4 == 0 && g.ngy % 2 == 0 && g.ngx % 2 == 0;
+}
+static dim3 tr_grid16(const Geo &g, int row_lo, int row_hi, int np) {
+    const int xa = row_lo & ~(kTr - 1);
+    return dim3((unsigned)((row_hi - xa + kTr - 1) / kTr), (unsigned)((g.ny + kTr - 1) / kTr),
+                (unsigned)np);
+}
+
 // plane-stage kernels at the plan's precision (planes q0 .. q0 + nb - 1)
 static void tr_grid_to_t(const Plan &P, int q0, int nb, hipStream_t st) {
     const Geo &g = P.g;
@@ -4909,6 +4994,9 @@ static void tr_grid_to_t(const Plan &P, int q0, int nb, hipStream_t st) {
         k_tr_grid_to_t<double2><<<grd, blk, 0, st>>>(
             g, static_cast<const double2 *>(plane_ptr(P, q0, 0)),
             reinterpret_cast<double2 *>(P.spec_in), P.row_lo, P.row_hi);
+    else if (tr16(g))
+        k_tr_grid_to_t16<<<tr_grid16(g, P.row_lo, P.row_hi, nb), blk, 0, st>>>(
+            g, static_cast<const float2 *>(plane_ptr(P, q0, 0)), P.spec_in, P.row_lo, P.row_hi);
     else
         k_tr_grid_to_t<float2><<<grd, blk, 0, st>>>(
             g, static_cast<const float2 *>(plane_ptr(P, q0, 0)), P.spec_in, P.row_lo, P.row_hi);
@@ -4923,6 +5011,9 @@ static void tr_t_to_grid(const Plan &P, int q0, int nb, hipStream_t st) {
         k_tr_t_to_grid<double2><<<grd, blk, 0, st>>>(
             g, reinterpret_cast<const double2 *>(P.spec),
             static_cast<double2 *>(plane_ptr(P, q0, 0)), P.row_lo, P.row_hi);
+    else if (tr16(g))
+        k_tr_t_to_grid16<<<tr_grid16(g, P.row_lo, P.row_hi, nb), blk, 0, st>>>(
+            g, P.spec, static_cast<float2 *>(plane_ptr(P, q0, 0)), P.row_lo, P.row_hi);
     else
         k_tr_t_to_grid<float2><<<grd, blk, 0, st>>>(
             g, P.spec, static_cast<float2 *>(plane_ptr(P, q0, 0)), P.row_lo, P.row_hi);
