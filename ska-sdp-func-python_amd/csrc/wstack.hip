@@ -1966,23 +1966,20 @@ __global__ void k_screen_fwd_t(Geo g, const T *__restrict__ t, int p_begin, int 
     *o = accumulate ? *o + res : res;
 }
 
-// adjoint: T[q][iy][kx] = screen(q) * corr * dirty for kx in the image's
-// x-frequencies, 0 for the other kx (full rows are written)
+// adjoint: T[q][iy][kx] = screen(q) * corr * dirty for the kx of the image's
+// x-frequencies (thread ix: kx = (ix - nx/2) mod ngx); the other kx of the
+// forward x-FFT's input stay zero across calls (adj_input)
 template <class T>
 __global__ void k_screen_adj_t(Geo g, const double *__restrict__ dirty, int64_t sx, int64_t sy,
                                int p_begin, int np, T *__restrict__ t,
                                const double *__restrict__ tab) {
-    const int kx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ix = blockIdx.x * blockDim.x + threadIdx.x;
     const int iy = blockIdx.y;
-    if (kx >= g.ngx) return;
-    const int X = kx < g.ngx / 2 ? kx : kx - g.ngx;
-    const int ix = X + g.nx / 2;
+    if (ix >= g.nx) return;
+    const int X = ix - g.nx / 2;
+    const int kx = X < 0 ? X + g.ngx : X;
     const int64_t tplane = (int64_t)g.ny * g.ngx;
     T *dst = t + (int64_t)iy * g.ngx + kx;
-    if (ix < 0 || ix >= g.nx) {
-        for (int q = 0; q < np; ++q) dst[q * tplane] = cplx<T>(0.0, 0.0);
-        return;
-    }
     const PixelGeom p = pixel_geom(g, ix, iy, tab);
     const double val = p.inside ? dirty[ix * sx + iy * sy] * p.corr : 0.0;
     if (g.do_w) {
@@ -3805,6 +3802,7 @@ struct Plan {
     float2 *grid = nullptr;
     float2 *spec = nullptr;     // T[q][iy][kx]: transposed y-spectra (pruned FFT)
     float2 *spec_in = nullptr;  // band-only input of the backward x-FFT (zeros elsewhere)
+    float2 *spec_adj = nullptr;  // forward x-FFT input: the image's kx columns (zeros elsewhere)
     CoreAcc core{nullptr, 0, 0, 0, 0};  // fp32 invert: fp64 companion of the uv core
 };
 
@@ -3851,7 +3849,8 @@ static size_t grid_budget_bytes(size_t need_other) {
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b == 0) return (size_t)8 << 30;
     Workspace &ws = Workspace::get();
     const size_t held_planes =
-        ws.held(ws_name("grid")) + ws.held(ws_name("spec")) + ws.held(ws_name("spec_in"));
+        ws.held(ws_name("grid")) + ws.held(ws_name("spec")) + ws.held(ws_name("spec_in")) +
+        ws.held(ws_name("spec_adj"));
     const size_t held_other = ws.held(ws_name("recs")) + ws.held(ws_name("key_rank")) +
                               ws.held(ws_name("degrid_acc")) + ws.held(ws_name("recs_pad")) +
                               ws.held(ws_name("rec_cls")) + ws.held(ws_name("recs_a")) +
@@ -3886,6 +3885,7 @@ struct BandState {
     uint64_t epoch = 0;  // the allocation (Workspace epoch) the zeros were written to
     size_t elems = 0;
     int lo = -1, hi = -1, ny = 0, ngx = 0;
+    int cb = 0;  // element bytes (8: c64, 16: c128): a c128 band read as c64 is not zero
 };
 
 static float2 *band_input(const Plan &P, hipStream_t st) {
@@ -3902,9 +3902,38 @@ static float2 *band_input(const Plan &P, hipStream_t st) {
     std::lock_guard<std::mutex> lk(mu);
     BandState &b = states[2 * dev + ws_slot()];
     if (b.epoch != ep || b.elems < elems || b.lo != P.row_lo || b.hi != P.row_hi || b.ny != g.ny ||
-        b.ngx != g.ngx) {
+        b.ngx != g.ngx || b.cb != (int)cbytes(P)) {
         SDP_HIP_CHECK(hipMemsetAsync(buf, 0, elems * sizeof(float2), st));
-        b = BandState{ep, elems, P.row_lo, P.row_hi, g.ny, g.ngx};
+        b = BandState{ep, elems, P.row_lo, P.row_hi, g.ny, g.ngx, (int)cbytes(P)};
+    }
+    return buf;
+}
+
+// The forward x-FFT input of the predict holds the screened image in the
+// kx columns of the image's x-frequencies and zeros in the others; the
+// screens write only those columns, so the zeros are kept across calls (a
+// separate buffer: the invert's x-FFT output overwrites whole rows of spec)
+struct AdjState {
+    uint64_t epoch = 0;
+    size_t elems = 0;
+    int nx = 0, ny = 0, ngx = 0, cb = 0;  // (cb: element bytes, as BandState)
+};
+
+static float2 *adj_input(const Plan &P, hipStream_t st) {
+    static std::mutex mu;
+    static std::map<int, AdjState> states;
+    const Geo &g = P.g;
+    const size_t elems = (size_t)P.fft_planes * g.ny * g.ngx * (cbytes(P) / sizeof(float2));
+    float2 *buf = scratch<float2>("spec_adj", elems);
+    const uint64_t ep = Workspace::get().epoch(ws_name("spec_adj"));
+    int dev = 0;
+    SDP_HIP_CHECK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    AdjState &b = states[2 * dev + ws_slot()];
+    if (b.epoch != ep || b.elems < elems || b.nx != g.nx || b.ny != g.ny || b.ngx != g.ngx ||
+        b.cb != (int)cbytes(P)) {
+        SDP_HIP_CHECK(hipMemsetAsync(buf, 0, elems * sizeof(float2), st));
+        b = AdjState{ep, elems, g.nx, g.ny, g.ngx, (int)cbytes(P)};
     }
     return buf;
 }
@@ -4333,7 +4362,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
                 : (size_t)g.ntiles * g.nps * g.salt * 2 * sizeof(unsigned);
     const size_t need_other =
         (size_t)((double)nvis * (rec_bytes + sizeof(unsigned) + (grid_mode ? 0 : sizeof(float2)))) +
-        hist_bytes + (size_t)P.fft_planes * spec_plane;
+        hist_bytes + (size_t)P.fft_planes * spec_plane * (grid_mode ? 1 : 2);
     const int cp = (int)std::max<size_t>(1, grid_budget_bytes(need_other) / grid_plane);
     P.chunk_planes = std::min(cp, g.nplanes);
     P.fft_planes = std::min(P.fft_planes, P.chunk_planes);
@@ -4341,6 +4370,7 @@ static Plan plan_geometry(const Inputs &in, bool grid_mode, hipStream_t st) {
     P.grid = scratch<float2>("grid", (size_t)P.chunk_planes * g.ngx * g.ngy * cf);
     P.spec = scratch<float2>("spec", (size_t)P.fft_planes * g.ny * g.ngx * cf);
     if (grid_mode) P.spec_in = band_input(P, st);
+    else P.spec_adj = adj_input(P, st);
 
     // records per item: large enough to amortise the tile flush over dense
     // tiles, small enough that the uv core's heavy groups split into items
@@ -5036,12 +5066,12 @@ static void screen_fwd(const Plan &P, int p_begin, int nb, double *dirty, int64_
 static void screen_adj(const Plan &P, const double *dirty, int64_t sx, int64_t sy, int p_begin,
                        int nb, const double *tab, hipStream_t st) {
     const Geo &g = P.g;
-    const dim3 grd(grid1d(g.ngx, 256), g.ny);
+    const dim3 grd(grid1d(g.nx, 256), g.ny);
     if (P.f64)
         k_screen_adj_t<double2><<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_begin, nb,
-                                                     reinterpret_cast<double2 *>(P.spec), tab);
+                                                     reinterpret_cast<double2 *>(P.spec_adj), tab);
     else
-        k_screen_adj_t<float2><<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_begin, nb, P.spec, tab);
+        k_screen_adj_t<float2><<<grd, 256, 0, st>>>(g, dirty, sx, sy, p_begin, nb, P.spec_adj, tab);
     SDP_HIP_CHECK(hipGetLastError());
 }
 
@@ -5473,7 +5503,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
             t2.mark();
             screen_adj(P, dirty, sx, sy, p_lo + sb, nb, tab, s);
             t2.mark();
-            fft_rows_x(P, nb, HIPFFT_FORWARD, s);
+            fft_rows_x(P, nb, HIPFFT_FORWARD, s, P.spec_adj);
             tr_t_to_grid(P, sb, nb, s);
             fft_rows_y(P, sb, nb, HIPFFT_FORWARD, s);
             t2.mark();

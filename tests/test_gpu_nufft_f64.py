@@ -175,3 +175,28 @@ def test_invert_predict_ng_default_epsilon_is_fp64():
     ep64, ep32 = rel_rms(p64, exv), rel_rms(p32, exv)
     print(f"predict_ng: fp64 {ep64:.2e}, fp32 {ep32:.2e}")
     assert ep64 < 1e-10 and 1e-9 < ep32 < 5e-6
+
+
+def test_fp32_after_fp64_keeps_the_zeroed_fft_inputs():
+    """The x-FFT inputs keep their zeros across calls (the invert's band
+    input outside the band rows, the predict's input outside the image's
+    kx columns); a c128 call leaves them in c128 layout, so the next c64
+    call must clear them again: fp32 invert and predict after fp64 ones
+    equal fresh fp32 ones (the band here is a part of the grid rows)."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(78, frac=0.3)
+    img = np.random.default_rng(79).normal(size=(64, 64))
+
+    def run(eps, prec=None):
+        d, _ = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), 64, 64, cell, cell, eps, True,
+                                precision=prec)
+        v, _ = kernels.dirty2ms(T(uvw), T(freq), T(img), T(wgt), cell, cell, eps, True,
+                                precision=prec)
+        return d.cpu().numpy(), v.cpu().numpy()
+
+    kernels.release_workspace()
+    d0, v0 = run(1e-7)
+    run(1e-12)
+    d1, v1 = run(1e-7)
+    assert rel_rms(d1, d0) < 1e-6
+    assert rel_rms(v1, v0) < 1e-6
