@@ -5511,10 +5511,13 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     };
     // the output zeroing and the first plane chunk's band zeroing (HBM
     // writes) overlap the bucketing on the auxiliary stream, once the
-    // histogram clearing is queued.  (Running the whole plane stage there
-    // too measured slower on C2: 15.6 vs 15.4 ms -- the FFTs' HBM streaming
-    // and the bucketing's memory-side atomics slow each other down.)
+    // histogram clearing is queued.  With resident planes the whole plane
+    // stage (screens, FFTs into the grid: it depends only on the image)
+    // follows there too: C2 predict 13.01 -> 12.72 ms, at eps 1e-12 77.3 ->
+    // 75.8 ms (profiles/r06_predict_planes_aux_ab.txt; round 2, with the
+    // slower count pass of that time, it had measured 15.6 vs 15.4 ms)
     const bool overlap = env_int("SDP_HIP_ZERO_OVERLAP", 1) != 0;
+    const bool planes_aux = overlap && P.chunk_planes == g.nplanes;
     hipEvent_t zdone = nullptr;
     auto start_aux = [&] {
         if (!overlap) return;
@@ -5522,6 +5525,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         stream_after(aux, st);
         zero_vis_unless_fused(aux);
         zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
+        if (planes_aux) plane_stage(0, g.nplanes, aux);
         SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
         SDP_HIP_CHECK(hipEventRecord(zdone, aux));
     };
@@ -5543,10 +5547,11 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
             SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
             SDP_HIP_CHECK(hipEventDestroy(zdone));
             zdone = nullptr;
+            if (!planes_aux) plane_stage(p_lo, np, st);
         } else {
             zero_band(P, np, st);
+            plane_stage(p_lo, np, st);
         }
-        plane_stage(p_lo, np, st);
         StageTimer tg(st);
         tg.mark();
 #define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, acc, st)
