@@ -84,6 +84,21 @@ def test_dirty2ms_matches_exact(dow, bucket):
         assert rel_rms(v.cpu().numpy(), ex) < TOL
 
 
+def test_image_rows_not_a_multiple_of_4():
+    """ny % 4 != 0 takes the 8-byte plane transposes (the 16-byte ones pair
+    image rows across the ky wrap only when ny / 2 is even): invert and
+    predict against the exact sums."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(6)
+    ex = orc.ms2dirty_exact(uvw, freq, ms, wgt, 60, 50, cell, cell, True)
+    out, _ = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), 60, 50, cell, cell, 1e-7, True)
+    assert rel_rms(out.cpu().numpy(), ex) < TOL
+    img = np.random.default_rng(7).normal(size=(60, 50))
+    exv = orc.dirty2ms_exact(uvw, freq, img, wgt, cell, cell, True)
+    v, _ = kernels.dirty2ms(T(uvw), T(freq), T(img), T(wgt), cell, cell, 1e-7, True)
+    assert rel_rms(v.cpu().numpy(), exv) < TOL
+
+
 def test_unit_visibilities_weights_and_accumulate():
     """vis=None (PSF) and wgt=None are unit arrays; ACCUMULATE adds."""
     from ska_sdp_func_python_amd import kernels
