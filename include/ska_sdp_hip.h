@@ -257,6 +257,44 @@ int sdp_hip_ms2dirty_vis_batch(const double *uvw, int64_t uvw_row_stride,
                                size_t errbuf_len);
 
 /*
+ * sdp_hip_ms2dirty_vis_pols -- every image pol of one invert_ng image channel
+ * in one call (reference imaging/ng.py:240-289: one ducc0 ms2dirty per image
+ * pol over the same uvw).  The pols share one bucketing, and one value pass
+ * reads each visibility's pols, flags and weights once and writes every
+ * pol's records; then each pol is gridded, transformed and screened into its
+ * own image.  Results as npol_img sdp_hip_ms2dirty_vis calls, pol q with row
+ * q of the conversion matrix, the weights and flag mask of pol q.
+ * pol_coeff host array of 2*npol_img*npol_vis doubles: row q, vis pol k at
+ *           2*(q*npol_vis+k) (re, im); NULL = identity (image pol q = vis pol q)
+ * wgt       weights [nrow, nchan, >= npol_img] (f32 or f64), strides (row,
+ *           chan, pol); required
+ * dirty     image pol q at dirty + q*dirty_stride_pol, strides (x, y)
+ * sumwt     device doubles, pol q at sumwt + q*sumwt_stride (+= its masked
+ *           weight sum), or NULL
+ * npol_img  1..npol_vis.  flags may not hold KEEP / REUSE / BATCH bits.
+ * fp64 plans (epsilon < 1e-7 without SDP_HIP_FP32) and plans outside the
+ * one-cell single-level bucketing run the pols as separate calls.
+ * Other arguments as sdp_hip_ms2dirty_vis.
+ */
+int sdp_hip_ms2dirty_vis_pols(const double *uvw, int64_t uvw_row_stride,
+                              const double *freq, int nchan, int64_t nrow,
+                              const void *vis, int vis_dtype, int64_t vis_row_stride,
+                              int64_t vis_chan_stride, int64_t vis_pol_stride,
+                              int npol_vis, const double *pol_coeff, int npol_img,
+                              const void *wgt, int wgt_dtype, int64_t wgt_row_stride,
+                              int64_t wgt_chan_stride, int64_t wgt_pol_stride,
+                              const void *vis_flags, int flag_bytes,
+                              int64_t flag_row_stride, int64_t flag_chan_stride,
+                              int64_t flag_pol_stride, int npix_x, int npix_y,
+                              double pixsize_x, double pixsize_y, double epsilon,
+                              int do_wstacking, unsigned flags, double *dirty,
+                              int64_t dirty_stride_x, int64_t dirty_stride_y,
+                              int64_t dirty_stride_pol, double *sumwt,
+                              int64_t sumwt_stride, const double *shift_lmn,
+                              void *stream, sdp_hip_wgrid_info *info, char *errbuf,
+                              size_t errbuf_len);
+
+/*
  * sdp_hip_dirty2ms -- replaces ducc0.wgridder.dirty2ms as called by
  * predict_ng (reference src/ska_sdp_func_python/imaging/ng.py:99-112 MFS,
  * :117-129 per channel).  Exact adjoint of sdp_hip_ms2dirty:

@@ -601,6 +601,44 @@ __global__ void k_widen_flags(const FT *__restrict__ src, int64_t frs, int64_t f
     }
 }
 
+// A pol conversion's visibility (x.conv) for the typed passes: every used
+// pol's value and flag are loaded before any is combined.  The generic
+// eff_vis / eff_vis_d load a pol's flag, branch on it and only then load its
+// value, pol after pol -- serialised memory round trips (the 4-pol MFS value
+// pass ran at 1.5 TB/s).  Coefficients are uniform, flags selected, not
+// multiplied: a NaN in a flagged pol must not reach the image.
+template <class VT, int FB>
+__device__ __forceinline__ double2 conv_vis(const VT *vis, int64_t vrs, int64_t vcs,
+                                            const VisExtra &x, uint32_t row, uint32_t chan) {
+    using FT = typename std::conditional<FB == 8, int64_t, int8_t>::type;
+    const VT *p = vis + (int64_t)row * vrs + (int64_t)chan * vcs;
+    VT v[4];
+    FT f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = VT{};
+        f[k] = 0;
+        if (k < x.npv && (x.cre[k] != 0.0 || x.cim[k] != 0.0)) {
+            v[k] = p[k * x.vps];
+            if constexpr (FB != 0)
+                f[k] = static_cast<const FT *>(
+                    x.flags)[(int64_t)row * x.frs + (int64_t)chan * x.fcs + k * x.fps];
+        }
+    }
+    double re = 0.0, im = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k < x.npv && (x.cre[k] != 0.0 || x.cim[k] != 0.0)) {
+            const double m = 1.0 - (double)f[k];
+            const double vx = m == 0.0 ? 0.0 : (double)v[k].x * m;
+            const double vy = m == 0.0 ? 0.0 : (double)v[k].y * m;
+            re += x.cre[k] * vx - x.cim[k] * vy;
+            im += x.cre[k] * vy + x.cim[k] * vx;
+        }
+    }
+    return make_double2(re, im);
+}
+
 // the visibility's value in two phases: `load` issues the loads (the
 // visibility from clamped indices, beside the lane's other loads), `value`
 // combines them after every load is in flight.  Without a pol conversion the
@@ -624,8 +662,10 @@ struct TVal {
         if constexpr (kGrid) {
             if (!vis) return xv;  // (unit visibilities: the PSF)
             if (x.conv) {
-                if constexpr (KIND >= 2) return eff_vis_d(vis, vrs, vcs, x, L.row, L.chan);
-                else return eff_vis(vis, vrs, vcs, x, L.row, L.chan);
+                const double2 d = conv_vis<VT, FB>(vis, vrs, vcs, x, L.row, L.chan);
+                xv.x = d.x;
+                xv.y = d.y;
+                return xv;
             }
             const double2 v = make_double2((double)raw.x, (double)raw.y);
             if constexpr (FB == 0) {
@@ -771,6 +811,125 @@ __global__ void k_bucket(Geo g, int64_t nvis, const double *__restrict__ uvw, in
         wgt, wrs, wcs, x, sw_slots, counter, rk, recs, nbad, cls, zout);
 }
 
+// The image pols of one invert_ng call sharing one bucketing
+// (sdp_hip_ms2dirty_vis_pols): image pol q takes row q of the conversion
+// matrix over the visibility pols, the weights of pol q masked by the flags
+// of pol q, and its own record array.
+struct PolsSpec {
+    int npo = 0;                              // image pols (<= 4)
+    double cre[4][4] = {}, cim[4][4] = {};    // [image pol][vis pol]
+    const void *wgt = nullptr;                // weights [row, chan, pol]
+    int64_t wrs = 0, wcs = 0, wps = 0;
+    RecC *recs[4] = {};
+    double *slots[4] = {};                    // weight-sum slots per image pol, or null
+};
+
+// The value pass of all image pols at once (one-cell 4-padded plans): each
+// visibility's pols, flags and weights are read once and the npo records
+// written at the one position the shared bucketing gives it.  One pass per
+// image pol read the pol-interleaved visibilities, flags and weights whole
+// every time (their cache lines) -- the 4-pol MFS value passes ran 5.7 ms
+// each on C2.  The values are those of the per-pol pass bit for bit: the
+// conversion sum in fp64 rounded to fp32, times the fp32 masked weight, then
+// the record factor.
+template <class VT, int WT, int FB, int NPO>
+__global__ __launch_bounds__(256) void k_bucket_pols(Geo g, int64_t nvis,
+                                                     const double *__restrict__ uvw,
+                                                     int64_t uvw_rs,
+                                                     const double *__restrict__ fsc,
+                                                     const VT *__restrict__ vis, int64_t vrs,
+                                                     int64_t vcs, VisExtra x, PolsSpec ps,
+                                                     const unsigned *__restrict__ counter,
+                                                     const unsigned *__restrict__ rk) {
+    using FT = typename std::conditional<FB == 8, int64_t, int8_t>::type;
+    using WTT = typename std::conditional<WT == 8, double, float>::type;
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    // (t_load's weight and flag are pol 0's; the loop below reads every pol's)
+    const TLoad L = t_load<WT, FB>(g, v, nvis, uvw, uvw_rs, fsc, ps.wgt, ps.wrs, ps.wcs, x);
+    const int64_t vg = (int64_t)L.row * g.nchan + L.chan;
+    const bool outside = L.live && g.slab && slab_out_v(g, L.wm, L.s);
+    // every load of the visibility before any use
+    const unsigned mine = rk[vg];
+    const VT *pv = vis + (int64_t)L.row * vrs + (int64_t)L.chan * vcs;
+    VT vv[4];
+    FT ff[4];
+    WTT ww[NPO];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        vv[k] = VT{};
+        ff[k] = 0;
+        if (k < x.npv) {
+            vv[k] = pv[k * x.vps];
+            if constexpr (FB != 0)
+                ff[k] = static_cast<const FT *>(
+                    x.flags)[(int64_t)L.row * x.frs + (int64_t)L.chan * x.fcs + k * x.fps];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < NPO; ++q)
+        ww[q] = static_cast<const WTT *>(
+            ps.wgt)[(int64_t)L.row * ps.wrs + (int64_t)L.chan * ps.wcs + q * ps.wps];
+    // the masked weights (select: a flagged sample's weight is an exact zero
+    // even when the stored weight is NaN or Inf) and their sums
+    double wd[NPO];
+#pragma unroll
+    for (int q = 0; q < NPO; ++q) {
+        double w = (double)ww[q];
+        if constexpr (FB != 0) {
+            const double keep = 1.0 - (double)ff[q];
+            w = keep == 0.0 ? 0.0 : w * keep;
+        }
+        wd[q] = (L.live && !outside) ? w : 0.0;
+        if (ps.slots[q]) {
+            double ws = wd[q];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) ws += __shfl_xor(ws, o, 64);
+            if ((threadIdx.x & 63) == 0 && ws != 0.0)
+                atomicAdd(&ps.slots[q][(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) &
+                                       (kSumSlots - 1)],
+                          ws);
+        }
+    }
+    if (!L.live || outside || mine == 0xffffffffu) return;
+    const Coord c = vis_coord_v(g, L.um, L.vm, L.wm, L.s);
+    const unsigned pos = counter[coord_key(g, c, L.row)] + mine;
+    float sn = 0.0f, cs = 1.0f;
+    const bool rot = g.do_w || x.shift;
+    if (rot) {
+        double ph = g.do_w ? c.w * g.s0 : 0.0;
+        if (x.shift) ph += (L.um * x.sl + L.vm * x.sm + L.wm * x.sn) * L.s;
+        ph -= rint(ph);
+        sincospif((float)(2.0 * ph), &sn, &cs);
+    }
+    const double base = 1.0 - 0.5 * g.W;
+    const uint32_t qu = fix_frac(base - c.du, 21), qv = fix_frac(base - c.dv, 21);
+    const uint32_t qw = g.do_w ? fix_frac(base - c.dw, 22) : 0u;
+#pragma unroll
+    for (int q = 0; q < NPO; ++q) {
+        double re = 0.0, im = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < x.npv && (ps.cre[q][k] != 0.0 || ps.cim[q][k] != 0.0)) {
+                double m = 1.0;
+                if constexpr (FB != 0) m = 1.0 - (double)ff[k];
+                const double vx = m == 0.0 ? 0.0 : (double)vv[k].x * m;
+                const double vy = m == 0.0 ? 0.0 : (double)vv[k].y * m;
+                re += ps.cre[q][k] * vx - ps.cim[q][k] * vy;
+                im += ps.cre[q][k] * vy + ps.cim[q][k] * vx;
+            }
+        }
+        const float wt = (float)wd[q];
+        const float xr = (float)re, xi = (float)im;
+        const float cr = wt != 0.0f ? xr * wt : 0.0f, ci = wt != 0.0f ? xi * wt : 0.0f;
+        RecC rc;
+        rc.cre = rot ? cr * cs - ci * sn : cr;
+        rc.cim = rot ? cr * sn + ci * cs : ci;
+        rc.lo = qu | (qv << 21);
+        rc.hi = (qv >> 11) | (qw << 10);
+        ps.recs[q][pos] = rc;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_sum_slots(const double *__restrict__ slots, double *out) {
     double s = 0.0;
     for (int i = threadIdx.x; i < kSumSlots; i += 64) s += slots[i];
@@ -858,6 +1017,11 @@ __global__ __launch_bounds__(256) void k_group_sums(int64_t nunits, int ucells,
 // range, finite taps; they sit behind each cell's records, where the
 // scatter never writes), the units' item bases (ioffs) and their FineItem
 // work items.
+// the other image pols' record arrays of a pols call (k_bucket_pols): pads too
+struct PadMore {
+    RecC *r[3] = {nullptr, nullptr, nullptr};
+};
+
 template <bool PAD>
 __global__ __launch_bounds__(256) void k_group_fill(int64_t nunits, int units_per_plane,
                                                     int ucells,
@@ -865,7 +1029,8 @@ __global__ __launch_bounds__(256) void k_group_fill(int64_t nunits, int units_pe
                                                     const unsigned long long *__restrict__ gofs,
                                                     unsigned chunk, unsigned *__restrict__ offs,
                                                     unsigned *__restrict__ ioffs,
-                                                    RecC *__restrict__ recs, void *items) {
+                                                    RecC *__restrict__ recs, void *items,
+                                                    PadMore more = PadMore{}) {
     const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (k > nunits) return;
     const unsigned long long go = gofs[k];
@@ -891,7 +1056,12 @@ __global__ __launch_bounds__(256) void k_group_fill(int64_t nunits, int units_pe
                 RecC z;
                 z.cre = z.cim = 0.0f;
                 z.lo = z.hi = 0u;
-                for (unsigned i = run + n[j]; i < run + r; ++i) recs[i] = z;
+                for (unsigned i = run + n[j]; i < run + r; ++i) {
+                    recs[i] = z;
+#pragma unroll
+                    for (int m = 0; m < 3; ++m)
+                        if (more.r[m]) more.r[m][i] = z;
+                }
             }
             run += r;
             x.o[(q * 4 + j) & (kGroupCell - 1)] = run;
@@ -4472,7 +4642,8 @@ static TypedIn typed_inputs(const Geo &g, const Inputs &in, hipStream_t st) {
 // ranks, scan, scatter of the records, work items, metadata.
 static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t st,
                         bool values_only = false,
-                        const std::function<void()> &after_clear = nullptr) {
+                        const std::function<void()> &after_clear = nullptr,
+                        PolsSpec *pols = nullptr) {
     const Geo &g = P.g;
     Part &pt = P.pt;
     const size_t nkeys = (size_t)g.ntiles * g.nps * g.salt;
@@ -4588,18 +4759,53 @@ static void bucket_part(Plan &P, const Inputs &in, bool grid_mode, hipStream_t s
             SDP_HIP_CHECK(hipMemcpyAsync(htot, gofs + nunits, sizeof(unsigned long long),
                                          hipMemcpyDeviceToHost, st));
             SDP_HIP_CHECK(hipStreamSynchronize(st));
-            P.recs = scratch<VisRec>("recs", ((int64_t)(*htot >> 32) + 1) / 2 + 1);  // RecC
+            const int64_t nrc = ((int64_t)(*htot >> 32) + 1) / 2 + 1;  // RecC pairs
+            P.recs = scratch<VisRec>("recs", nrc);
+            if (pols) {  // the other image pols' records: same positions, same pads
+                static const char *names[4] = {"recs", "recs_pol1", "recs_pol2", "recs_pol3"};
+                pols->recs[0] = reinterpret_cast<RecC *>(P.recs);
+                for (int q = 1; q < pols->npo; ++q)
+                    pols->recs[q] = reinterpret_cast<RecC *>(scratch<VisRec>(names[q], nrc));
+            }
             k_sum_pads<<<1, 256, 0, st>>>(pslots, pt.npad);
         }
         const unsigned fb = grid1d(nunits + 1, 256);
+        PadMore more;
+        if (pols)
+            for (int q = 1; q < pols->npo; ++q) more.r[q - 1] = pols->recs[q];
         if (P.pad4)
             k_group_fill<true><<<fb, 256, 0, st>>>(nunits, upp, ucells, pt.hist, gofs, P.chunk,
                                                    pt.offs, pt.ioffs,
-                                                   reinterpret_cast<RecC *>(P.recs), pt.fitems);
+                                                   reinterpret_cast<RecC *>(P.recs), pt.fitems,
+                                                   more);
         else
             k_group_fill<false><<<fb, 256, 0, st>>>(nunits, upp, ucells, pt.hist, gofs, P.chunk,
                                                     pt.offs, pt.ioffs, nullptr, pt.fitems);
-        if (pt.nvis > 0) launch_bucket(std::true_type{}, pt.offs);
+        if (pt.nvis > 0 && pols) {
+            // every image pol's value pass at once (sdp_hip_ms2dirty_vis_pols)
+            SDP_REQUIRE(P.pad4 && grid_mode && !P.f64 && !P.subpad, "pols call: unsupported plan");
+            auto go = [&](auto vt_tag) {
+                using VT = typename decltype(vt_tag)::type;
+                ti.dispatch([&](auto wt_tag, auto fb_tag) {
+                    constexpr int WT = decltype(wt_tag)::value, FB = decltype(fb_tag)::value;
+                    const VT *vp = static_cast<const VT *>(in.vis);
+#define SDP_POLS(N)                                                                         \
+    k_bucket_pols<VT, WT, FB, N><<<nb, 256, 0, st>>>(g, pt.nvis, in.uvw, in.uvw_rs, fsc, vp, \
+                                                     in.vrs, in.vcs, ti.x, *pols, pt.offs, kr)
+                    switch (pols->npo) {
+                        case 1: SDP_POLS(1); break;
+                        case 2: SDP_POLS(2); break;
+                        case 3: SDP_POLS(3); break;
+                        default: SDP_POLS(4); break;
+                    }
+#undef SDP_POLS
+                });
+            };
+            if (in.vis_dtype == SDP_HIP_C128) go(TypeTag<double2>{});
+            else go(TypeTag<float2>{});
+        } else if (pt.nvis > 0) {
+            launch_bucket(std::true_type{}, pt.offs);
+        }
         k_part_meta<<<grid1d(g.nps + 1, 64), 64, 0, st>>>(pt.nbad, pt.offs + nkeys,
                                                           P.pad4 ? pt.npad : nullptr, pt.ioffs,
                                                           upp, g.nps, pt.meta);
@@ -5456,6 +5662,149 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
     }
 }
 
+// All image pols of one invert_ng call in one bucketing (sdp_hip_ms2dirty_vis_pols):
+// one rank pass, one value pass writing every pol's records (k_bucket_pols),
+// then each pol's gridding, FFT and screens into its own image.  `in` is
+// image pol 0's call (its conversion row, weights and flag pol); `ps` holds
+// every pol's rows and the weights' pol stride, `dirty[q]` / `sumwt[q]` the
+// outputs.  Plans the fused pass does not cover (fp64, two-level-only or
+// large-grid plans) run the pols one call each, sharing a kept bucketing.
+static void ms2dirty_pols(const Inputs &in, PolsSpec ps, double *const *dirty, int64_t sx,
+                          int64_t sy, double *const *sumwt, sdp_hip_wgrid_info *info,
+                          hipStream_t st) {
+    SDP_REQUIRE(ps.npo >= 1 && ps.npo <= 4, "npol_img must be 1..4");
+    SDP_REQUIRE(in.vis != nullptr && (in.vis_dtype == SDP_HIP_C64 || in.vis_dtype == SDP_HIP_C128),
+                "vis must be complex64 or complex128");
+    SDP_REQUIRE(ps.npo <= in.x.npv, "npol_img must not exceed npol_vis (pol q's flags mask its "
+                                    "weights)");
+    auto per_pol = [&] {
+        for (int q = 0; q < ps.npo; ++q) {
+            Inputs iq = in;
+            iq.x.conv = true;
+            for (int k = 0; k < 4; ++k) {
+                iq.x.cre[k] = ps.cre[q][k];
+                iq.x.cim[k] = ps.cim[q][k];
+            }
+            iq.x.fpol = q;
+            iq.wgt = static_cast<const char *>(ps.wgt) +
+                     q * ps.wps * (in.x.wgt_f64 ? sizeof(double) : sizeof(float));
+            iq.x.sumwt = sumwt[q];
+            iq.flags = (in.flags & ~(SDP_HIP_KEEP_BUCKETS | SDP_HIP_REUSE_BUCKETS)) |
+                       (ps.npo > 1 ? (q == 0 ? SDP_HIP_KEEP_BUCKETS : SDP_HIP_REUSE_BUCKETS) : 0);
+            ms2dirty(iq, dirty[q], sx, sy, q == ps.npo - 1 ? info : nullptr, st);
+        }
+    };
+    if (in.eps < 1.0e-7 && !(in.flags & SDP_HIP_FP32)) {
+        // (fp64: each pol its own two-level sort, as invert_ng runs them)
+        for (int q = 0; q < ps.npo; ++q) {
+            Inputs iq = in;
+            iq.x.conv = true;
+            for (int k = 0; k < 4; ++k) {
+                iq.x.cre[k] = ps.cre[q][k];
+                iq.x.cim[k] = ps.cim[q][k];
+            }
+            iq.x.fpol = q;
+            iq.wgt = static_cast<const char *>(ps.wgt) +
+                     q * ps.wps * (in.x.wgt_f64 ? sizeof(double) : sizeof(float));
+            iq.x.sumwt = sumwt[q];
+            iq.flags = in.flags & ~(SDP_HIP_KEEP_BUCKETS | SDP_HIP_REUSE_BUCKETS);
+            ms2dirty(iq, dirty[q], sx, sy, q == ps.npo - 1 ? info : nullptr, st);
+        }
+        return;
+    }
+    SlotGuard slot(in.flags);
+    StageTimer tm(st);
+    tm.mark();
+    Inputs inx = in;
+    inx.x.conv = true;
+    for (int k = 0; k < 4; ++k) {
+        inx.x.cre[k] = ps.cre[0][k];
+        inx.x.cim[k] = ps.cim[0][k];
+    }
+    inx.x.fpol = 0;
+    inx.x.all = true;         // every in-grid visibility: the bucketing holds for every pol
+    inx.x.sumwt = nullptr;    // (the value pass sums every pol's weights)
+    inx.flags = (in.flags & ~SDP_HIP_REUSE_BUCKETS) | SDP_HIP_KEEP_BUCKETS;  // single-level
+    Plan P = plan_geometry(inx, true, st);
+    if (P.f64 || P.g.tiled || P.g.sub != kTileCell || !P.pad4 || P.subpad) {
+        per_pol();
+        return;
+    }
+    setup_core(P);
+    const Geo &g = P.g;
+    const double *tab = phi_table(g.W, g.beta, st);
+    hipEvent_t zdone = nullptr;
+    auto start_zero = [&] {
+        if (env_int("SDP_HIP_ZERO_OVERLAP", 1) == 0) return;
+        hipStream_t aux = aux_stream();
+        stream_after(aux, st);
+        zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
+        SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
+        SDP_HIP_CHECK(hipEventRecord(zdone, aux));
+    };
+    double *slots = scratch<double>("sumwt_slots_pols", 4 * kSumSlots);
+    SDP_HIP_CHECK(hipMemsetAsync(slots, 0, 4 * kSumSlots * sizeof(double), st));
+    for (int q = 0; q < ps.npo; ++q) ps.slots[q] = sumwt[q] ? slots + q * kSumSlots : nullptr;
+    bucket_part(P, inx, true, st, false, start_zero, &ps);
+    for (int q = 0; q < ps.npo; ++q)
+        if (sumwt[q]) k_sum_slots<<<1, 64, 0, st>>>(ps.slots[q], sumwt[q]);
+    read_part_meta(P, st);
+    const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
+    float tgrid = 0, tfft = 0, tscr = 0;
+    for (int q = 0; q < ps.npo; ++q) {
+        P.recs = reinterpret_cast<VisRec *>(ps.recs[q]);
+        for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
+            const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
+            const int np = p_hi - p_lo;
+            if (zdone) {
+                SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
+                SDP_HIP_CHECK(hipEventDestroy(zdone));
+                zdone = nullptr;
+            } else {
+                zero_band(P, np, st);
+            }
+            {
+                StageTimer tg(st);
+                tg.mark();
+#define SDP_LAUNCH_GRID(WW) launch_grid<WW>(P, p_lo, p_hi, st)
+                SDP_W_DISPATCH(g.W, SDP_LAUNCH_GRID);
+#undef SDP_LAUNCH_GRID
+                SDP_HIP_CHECK(hipGetLastError());
+                tg.mark();
+                tgrid += tg.ms(0, 1);
+            }
+            core_merge(P, 0, np, st);
+            for (int sb = 0; sb < np; sb += P.fft_planes) {
+                const int nb = std::min(P.fft_planes, np - sb);
+                StageTimer t2(st);
+                t2.mark();
+                fft_rows_y(P, sb, nb, HIPFFT_BACKWARD, st);
+                tr_grid_to_t(P, sb, nb, st);
+                fft_rows_x(P, nb, HIPFFT_BACKWARD, st, P.spec_in);
+                t2.mark();
+                screen_fwd(P, p_lo + sb, nb, dirty[q], sx, sy,
+                           (accumulate || p_lo + sb > 0) ? 1 : 0, tab, st);
+                t2.mark();
+                tfft += t2.ms(0, 1);
+                tscr += t2.ms(1, 2);
+            }
+        }
+    }
+    if (zdone) {
+        SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
+        SDP_HIP_CHECK(hipEventDestroy(zdone));
+    }
+    P.recs = reinterpret_cast<VisRec *>(ps.recs[0]);
+    tm.mark();
+    fill_info(P, info);
+    if (info) {
+        info->ms_prep = tm.on ? tm.ms(0, 1) - tgrid - tfft - tscr : 0.0f;
+        info->ms_grid = tgrid;
+        info->ms_fft = tfft;
+        info->ms_screen = tscr;
+    }
+}
+
 static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t sy, void *vis,
                      sdp_hip_wgrid_info *info, hipStream_t st, const OutConv &oc = OutConv{}) {
     SDP_REQUIRE(in.vis_dtype == SDP_HIP_C64 || in.vis_dtype == SDP_HIP_C128,
@@ -5790,6 +6139,74 @@ int sdp_hip_ms2dirty_vis(const double *uvw, int64_t uvw_row_stride, const double
                               flags & ~(SDP_HIP_BATCH_FIRST | SDP_HIP_BATCH_LAST), nullptr, dirty,
                               dirty_stride_x, dirty_stride_y, sumwt, shift_lmn, stream, info,
                               errbuf, errbuf_len);
+}
+
+int sdp_hip_ms2dirty_vis_pols(const double *uvw, int64_t uvw_row_stride, const double *freq,
+                              int nchan, int64_t nrow, const void *vis, int vis_dtype,
+                              int64_t vis_row_stride, int64_t vis_chan_stride,
+                              int64_t vis_pol_stride, int npol_vis, const double *pol_coeff,
+                              int npol_img, const void *wgt, int wgt_dtype,
+                              int64_t wgt_row_stride, int64_t wgt_chan_stride,
+                              int64_t wgt_pol_stride, const void *vis_flags, int flag_bytes,
+                              int64_t flag_row_stride, int64_t flag_chan_stride,
+                              int64_t flag_pol_stride, int npix_x, int npix_y, double pixsize_x,
+                              double pixsize_y, double epsilon, int do_wstacking, unsigned flags,
+                              double *dirty, int64_t dirty_stride_x, int64_t dirty_stride_y,
+                              int64_t dirty_stride_pol, double *sumwt, int64_t sumwt_stride,
+                              const double *shift_lmn, void *stream, sdp_hip_wgrid_info *info,
+                              char *errbuf, size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(dirty != nullptr && freq != nullptr && vis != nullptr && wgt != nullptr &&
+                        (uvw != nullptr || nrow == 0),
+                    "null pointer argument");
+        SDP_REQUIRE(npol_vis >= 1 && npol_vis <= 4, "npol_vis must be 1..4");
+        SDP_REQUIRE(npol_img >= 1 && npol_img <= npol_vis, "npol_img must be 1..npol_vis");
+        SDP_REQUIRE(wgt_dtype == SDP_HIP_F32 || wgt_dtype == SDP_HIP_F64,
+                    "weights must be f32 or f64");
+        SDP_REQUIRE(vis_flags == nullptr || flag_bytes == 1 || flag_bytes == 4 || flag_bytes == 8,
+                    "flag element size must be 1, 4 or 8 bytes");
+        SDP_REQUIRE(!(flags & (SDP_HIP_KEEP_BUCKETS | SDP_HIP_REUSE_BUCKETS | SDP_HIP_BATCH_FIRST |
+                               SDP_HIP_BATCH_LAST)),
+                    "a pols call keeps, reuses or batches nothing");
+        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                          nrow,        vis,             vis_dtype,      vis_row_stride,
+                          vis_chan_stride, wgt,         wgt_row_stride, wgt_chan_stride,
+                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                          epsilon,     do_wstacking,    flags};
+        wstack::VisExtra &x = in.x;
+        x.vps = vis_pol_stride;
+        x.npv = npol_vis;
+        x.wgt_f64 = wgt_dtype == SDP_HIP_F64;
+        x.flags = vis_flags;
+        x.fbytes = vis_flags ? flag_bytes : 0;
+        x.frs = flag_row_stride;
+        x.fcs = flag_chan_stride;
+        x.fps = flag_pol_stride;
+        if (shift_lmn) {
+            x.shift = true;
+            x.sl = shift_lmn[0];
+            x.sm = shift_lmn[1];
+            x.sn = shift_lmn[2];
+        }
+        wstack::PolsSpec ps;
+        ps.npo = npol_img;
+        for (int q = 0; q < npol_img; ++q)
+            for (int k = 0; k < npol_vis; ++k) {
+                ps.cre[q][k] = pol_coeff ? pol_coeff[2 * (q * npol_vis + k)] : (q == k ? 1.0 : 0.0);
+                ps.cim[q][k] = pol_coeff ? pol_coeff[2 * (q * npol_vis + k) + 1] : 0.0;
+            }
+        ps.wgt = wgt;
+        ps.wrs = wgt_row_stride;
+        ps.wcs = wgt_chan_stride;
+        ps.wps = wgt_pol_stride;
+        double *outs[4] = {}, *sums[4] = {};
+        for (int q = 0; q < npol_img; ++q) {
+            outs[q] = dirty + q * dirty_stride_pol;
+            sums[q] = sumwt ? sumwt + q * sumwt_stride : nullptr;
+        }
+        wstack::ms2dirty_pols(in, ps, outs, dirty_stride_x, dirty_stride_y, sums, info,
+                              as_stream(stream));
+    });
 }
 
 int sdp_hip_ms2dirty_vis_batch(const double *uvw, int64_t uvw_row_stride, const double *freq,

@@ -106,6 +106,17 @@ SIGNATURES = {
         c_vp, c_i64, c_i64, c_vp,                 # dirty, strides, sumwt
         c_vp,                                     # shift_lmn (host doubles) or NULL
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
+    "sdp_hip_ms2dirty_vis_pols": [
+        c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
+        c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # vis, dtype, row/chan/pol strides, npol_vis
+        c_vp, c_int,                              # pol_coeff (host doubles) or NULL, npol_img
+        c_vp, c_int, c_i64, c_i64, c_i64,         # wgt, dtype, row/chan/pol strides
+        c_vp, c_int, c_i64, c_i64, c_i64,         # flags, bytes, strides
+        c_int, c_int, c_dbl, c_dbl, c_dbl, c_int, c_u32,
+        c_vp, c_i64, c_i64, c_i64,                # dirty, x / y / pol strides
+        c_vp, c_i64,                              # sumwt, its pol stride
+        c_vp,                                     # shift_lmn (host doubles) or NULL
+        c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_ms2dirty_vis_batch": [
         c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
         c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # vis, dtype, row/chan/pol strides, npol_vis

@@ -521,8 +521,32 @@ def invert_ng(bvis, model, dopsf=False, normalise=True, **kwargs):
                 if verbosity:
                     log.info("invert_ng: %s", info)
 
-    for pol, chans, ichan in calls:
-        grid_pol(pol, chans, ichan, pol == 0)
+    def grid_pols(chans, ichan):
+        """Every image pol of one image channel in one library call
+        (sdp_hip_ms2dirty_vis_pols): one bucketing and one value pass that
+        reads each visibility's pols, flags and weights once, then each
+        pol's gridding and FFT -- the results of one ms2dirty_vis call per
+        pol sharing a kept bucketing (C2 4 pols: 5.7 ms value pass per pol)."""
+        (part,) = batches(chans)
+        _, info = kernels.ms2dirty_vis_pols(
+            uvw, freq_t[part], ms[:, part, :], wgt[:, part, :npol], flags[:, part, :],
+            None if conv is None else [conv[p] for p in range(npol)], npixdirty, npixdirty,
+            pixsize, pixsize, epsilon, do_wstacking, flip_uw=True, out=image[ichan],
+            out_strides=(image.stride(1), 1, nx), accumulate=True, sumwt=sumwt_d[ichan, :npol],
+            shift_lmn=lmn, precision=precision)
+        if verbosity:
+            log.info("invert_ng: %s", info)
+
+    if share and tcuts is None and ms.shape[2] >= npol and wgt.shape[2] >= npol:
+        done = set()
+        for _, chans, ichan in calls:
+            key = (chans.start, chans.stop, ichan)
+            if key not in done:
+                done.add(key)
+                grid_pols(chans, ichan)
+    else:
+        for pol, chans, ichan in calls:
+            grid_pol(pol, chans, ichan, pol == 0)
     if overlap:
         main.wait_stream(side)
     if shard or loc:

@@ -363,6 +363,76 @@ def ms2dirty_vis(uvw, freq, vis, pol, wgt, flags, coef, npix_x, npix_y, pixsize_
     return out, info.as_dict()
 
 
+def ms2dirty_vis_pols(uvw, freq, vis, wgt, flags, coef, npix_x, npix_y, pixsize_x, pixsize_y,
+                      epsilon=1e-7, do_wstacking=True, flip_uw=False, out=None, out_strides=None,
+                      accumulate=False, sumwt=None, shift_lmn=None, precision=None):
+    """Every image pol of one invert_ng image channel in one call
+    (sdp_hip_ms2dirty_vis_pols): ``vis`` [nrow, nchan, npol_vis] complex and
+    ``flags`` (integer, or None) as ms2dirty_vis, ``wgt`` [nrow, nchan,
+    >= npol_img] f32/f64 (image pol q takes the weights and flags of pol q),
+    ``coef`` the conversion matrix [npol_img, npol_vis] (complex) or None for
+    the identity.  ``out`` [npol_img, ...] f64 with ``out_strides`` = (pol,
+    x, y) element strides; ``sumwt`` a [npol_img] f64 device view (+= each
+    pol's masked weight sum).  The pols share one bucketing and one value
+    pass; results as one ms2dirty_vis call per image pol."""
+    pbits = _prec_bits(epsilon, precision)
+    _check_uvw(uvw)
+    dev = uvw.device
+    freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
+    nrow, nchan = uvw.shape[0], freq.shape[0]
+    _on_gpu(vis, "vis")
+    if vis.dtype not in (torch.complex64, torch.complex128) or vis.dim() != 3 or \
+            tuple(vis.shape[:2]) != (nrow, nchan):
+        raise ValueError("vis must be complex [nrow, nchan, npol]")
+    npv = vis.shape[2]
+    if flags is not None:
+        _on_gpu(flags, "flags")
+        if flags.dtype not in _FLAG_DT or tuple(flags.shape) != tuple(vis.shape):
+            raise ValueError("flags must be an integer tensor shaped as vis")
+    _on_gpu(wgt, "wgt")
+    if wgt.dtype not in (torch.float32, torch.float64) or wgt.dim() != 3 or \
+            tuple(wgt.shape[:2]) != (nrow, nchan):
+        raise ValueError("wgt must be float32/float64 [nrow, nchan, npol]")
+    npo = npv if coef is None else len(coef)
+    if not 1 <= npo <= min(npv, wgt.shape[2]):
+        raise ValueError("npol_img must be 1..npol_vis (and have weights)")
+    cbuf = None
+    if coef is not None:
+        rows = [[complex(z) for z in r] for r in coef]
+        if any(len(r) != npv for r in rows):
+            raise ValueError("coef rows must have one entry per visibility pol")
+        cbuf = (ctypes.c_double * (2 * npo * npv))(
+            *[v for r in rows for z in r for v in (z.real, z.imag)])
+    if out is None:
+        out = _alloc((npo, npix_x, npix_y), torch.float64, dev)
+        out_strides = out.stride()
+    elif out_strides is None:
+        out_strides = out.stride()
+    _on_gpu(out, "out")
+    if out.dtype != torch.float64:
+        raise ValueError("dirty output must be float64")
+    if sumwt is not None and (sumwt.dtype != torch.float64 or not sumwt.is_cuda or
+                              sumwt.numel() < npo):
+        raise ValueError("sumwt must be a float64 device tensor with one entry per image pol")
+    bits = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+            | pbits)
+    info = _lib.WGridInfo()
+    _lib.call(
+        "sdp_hip_ms2dirty_vis_pols",
+        _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
+        _ptr(vis), _DT_CODE[vis.dtype], *vis.stride(), npv,
+        ctypes.cast(cbuf, ctypes.c_void_p) if cbuf is not None else None, npo,
+        _ptr(wgt), _DT_CODE[wgt.dtype], *wgt.stride(),
+        _ptr(flags), _FLAG_DT[flags.dtype] if flags is not None else 0,
+        *(flags.stride() if flags is not None else (0, 0, 0)),
+        int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
+        int(bool(do_wstacking)), bits,
+        _ptr(out), int(out_strides[1]), int(out_strides[2]), int(out_strides[0]),
+        _ptr(sumwt), int(sumwt.stride(0)) if sumwt is not None else 0, _host3(shift_lmn),
+        _stream(dev), ctypes.byref(info))
+    return out, info.as_dict()
+
+
 def dirty2ms_vis(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7,
                  do_wstacking=True, flip_uw=False, dirty_strides=None, npix=None,
                  accumulate=False, shift_lmn=None, precision=None):

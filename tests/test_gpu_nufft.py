@@ -605,6 +605,56 @@ def test_shared_bucketing_across_pols(bucket2, monkeypatch):
                              flip_uw=True, reuse_buckets=True)
 
 
+@pytest.mark.parametrize("path", ["fused", "coarse", "fp64"])
+@pytest.mark.parametrize("vdt", [torch.complex64, torch.complex128])
+def test_pols_call_matches_per_pol_calls(path, vdt, monkeypatch):
+    """sdp_hip_ms2dirty_vis_pols (invert_ng's image pols in one call: one
+    bucketing, one value pass writing every pol's records) against one
+    ms2dirty_vis call per image pol: a linear -> stokesIQUV conversion matrix,
+    int8 flags, f64 weights that differ per pol (pol 0 zero on a third of the
+    rows).  "coarse" (16x16-cell buckets) and "fp64" (epsilon 1e-12) are plans
+    the fused pass does not cover: the library runs them pol by pol.  Images
+    1e-6 relative RMS (fp32 sums inside a cell), weight sums 1e-12."""
+    from ska_sdp_func_python_amd import kernels
+    if path == "coarse":
+        monkeypatch.setenv("SDP_HIP_BUCKET", "16")
+    rng = np.random.default_rng(72)
+    nrow, nchan, npv, npix = 5000, 6, 4, 128
+    freq = np.linspace(1.0e9, 1.2e9, nchan)
+    umax = 3000.0
+    uvw_h = rng.uniform(-1, 1, (nrow, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw_h[:, 2] *= 0.3
+    dev = "cuda"
+    uvw = torch.as_tensor(uvw_h, device=dev)
+    freq_t = torch.as_tensor(freq, device=dev)
+    vis = torch.as_tensor(rng.normal(size=(nrow, nchan, npv)) +
+                          1j * rng.normal(size=(nrow, nchan, npv)), device=dev).to(vdt)
+    flags = torch.as_tensor(rng.uniform(size=(nrow, nchan, npv)) < 0.2, device=dev).to(torch.int8)
+    wgt = torch.as_tensor(rng.uniform(0.5, 2.0, (nrow, nchan, npv)), device=dev)
+    wgt[: nrow // 3, :, 0] = 0.0
+    conv = [[1, 0, 0, 1], [1, 0, 0, -1], [0, 1, 1, 0], [0, -1j, 1j, 0]]  # linear -> IQUV
+    cell = 0.35 / umax
+    eps = 1e-12 if path == "fp64" else 1e-5
+    args = (npix, npix, cell, cell, eps, True)
+    ind, sws = [], []
+    for q in range(4):
+        sw = torch.zeros(1, dtype=torch.float64, device=dev)
+        out, _ = kernels.ms2dirty_vis(uvw, freq_t, vis, q, wgt[:, :, q].contiguous(), flags,
+                                      conv[q], *args, flip_uw=True, sumwt=sw)
+        ind.append(out.cpu().numpy())
+        sws.append(float(sw.cpu()))
+    sw4 = torch.zeros(4, dtype=torch.float64, device=dev)
+    out4, info = kernels.ms2dirty_vis_pols(uvw, freq_t, vis, wgt, flags, conv, *args,
+                                           flip_uw=True, sumwt=sw4)
+    got, gsw = out4.cpu().numpy(), sw4.cpu().numpy()
+    tol = 1e-12 if path == "fp64" else 1e-6
+    for q in range(4):
+        assert rel_rms(got[q], ind[q]) < tol, q
+        assert abs(gsw[q] - sws[q]) <= 1e-12 * abs(sws[q])
+    if path == "fused":
+        assert info["nvis_used"] == nrow * nchan  # (every in-grid visibility bucketed)
+
+
 @pytest.mark.parametrize("ipf,pf", [("stokesI", "stokesI"), ("stokesIQUV", "linear"),
                                     ("stokesIQUV", "circular"), ("linear", "linear")])
 @pytest.mark.parametrize("mfs", [True, False])
