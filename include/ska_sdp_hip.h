@@ -339,6 +339,32 @@ int sdp_hip_dirty2ms_vis(const double *uvw, int64_t uvw_row_stride,
                          size_t errbuf_len);
 
 /*
+ * sdp_hip_dirty2ms_vis_pols -- every image pol of one predict_ng MFS call in
+ * one call (reference imaging/ng.py:99-112 per image pol, :131-136 the pol
+ * conversion): the pols share one bucketing; each image pol's planes are
+ * built and degridded, and one write-back combines all pols into every
+ * visibility pol.  Results as npol_img sdp_hip_dirty2ms_vis calls, the first
+ * without and the others with SDP_HIP_ACCUMULATE, pol q with column q of the
+ * conversion matrix.
+ * dirty     image pol q at dirty + q*dirty_stride_pol, strides (x, y)
+ * pol_coeff host array of 2*npol_img*npol_vis doubles: image pol q, vis pol k
+ *           at 2*(q*npol_vis+k) (re, im); NULL = identity
+ * Other arguments as sdp_hip_dirty2ms_vis.
+ */
+int sdp_hip_dirty2ms_vis_pols(const double *uvw, int64_t uvw_row_stride,
+                              const double *freq, int nchan, int64_t nrow,
+                              const double *dirty, int64_t dirty_stride_x,
+                              int64_t dirty_stride_y, int64_t dirty_stride_pol,
+                              int npol_img, int npix_x, int npix_y, double pixsize_x,
+                              double pixsize_y, double epsilon, int do_wstacking,
+                              unsigned flags, void *vis, int vis_dtype,
+                              int64_t vis_row_stride, int64_t vis_chan_stride,
+                              int64_t vis_pol_stride, int npol_vis,
+                              const double *pol_coeff, const double *shift_lmn,
+                              void *stream, sdp_hip_wgrid_info *info, char *errbuf,
+                              size_t errbuf_len);
+
+/*
  * sdp_hip_dft_point_v00 -- replaces ska_sdp_func.visibility.dft_point_v00
  * (reference src/ska_sdp_func_python/imaging/dft.py:173-178) and the cupy
  * dft_kernel (:185-262, :288-337).  Caller-allocated output, replaced (not

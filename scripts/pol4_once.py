@@ -1,6 +1,7 @@
 """The bench's 4-pol MFS invert_ng (linear c128 / f64 / int64 Visibility of
-the C2 layout -> stokesIQUV, eps 1e-7) run --reps times: the driver for a
-rocprofv3 kernel trace of the multi-pol path."""
+the C2 layout -> stokesIQUV, eps 1e-7) run --reps times, or with --predict
+predict_ng of a random stokesIQUV model into that Visibility: the driver for
+timings and rocprofv3 kernel traces of the multi-pol paths."""
 import argparse
 import math
 import os
@@ -15,10 +16,11 @@ sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func-python_amd"))
 import torch  # noqa: E402
 
 from ska_sdp_func_python_amd import datamodels as dm, simulation  # noqa: E402
-from ska_sdp_func_python_amd.imaging import invert_ng  # noqa: E402
+from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--predict", action="store_true")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 obs = simulation.device_observation(100, 64, 0.95e9, 1.76e9, config="MID", seed=0, device=dev)
@@ -39,9 +41,15 @@ b4 = dm.Visibility.constructor(
 m4 = dm.create_image(4096, cell, pc, polarisation_frame=dm.PolarisationFrame("stokesIQUV"),
                      frequency=float(freq.mean()),
                      channel_bandwidth=float(2 * (freq.max() - freq.min()) + 1e6), nchan=1)
+if a.predict:
+    m4["pixels"].data = torch.randn(1, 4, 4096, 4096, dtype=torch.float64, device=dev)
 for i in range(a.reps):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    invert_ng(b4, m4, epsilon=1e-7)
+    if a.predict:
+        predict_ng(b4, m4, epsilon=1e-7)
+    else:
+        invert_ng(b4, m4, epsilon=1e-7)
     torch.cuda.synchronize(dev)
-    print(f"4-pol invert_ng {1e3 * (time.perf_counter() - t0):.2f} ms", flush=True)
+    print(f"4-pol {'predict_ng' if a.predict else 'invert_ng'} "
+          f"{1e3 * (time.perf_counter() - t0):.2f} ms", flush=True)

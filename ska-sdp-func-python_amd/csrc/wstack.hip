@@ -2249,6 +2249,45 @@ __global__ void k_finalize(int64_t n, int nchan,
     }
 }
 
+// The image pols of one predict in one write-back (sdp_hip_dirty2ms_vis_pols):
+// each record's NPO degridded sums are combined into every visibility pol
+// through the conversion matrix's columns (fp64) and the visibility written
+// once, where one finalize per image pol read-modified-wrote every pol of it.
+struct PolAccs {
+    const float2 *a[4] = {};
+    OutConv oc[4];
+};
+template <class VT, int NPO>
+__global__ void k_finalize_pols(int64_t n, int nchan, const VisRec *__restrict__ recs,
+                                PolAccs pa, VT *vis, int64_t vrs, int64_t vcs, int accumulate) {
+    for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        const VisRec rc = recs[r];
+        float2 v[NPO];
+#pragma unroll
+        for (int q = 0; q < NPO; ++q) {
+            const float2 a = pa.a[q][r];
+            v[q] = make_float2(rc.cre * a.x - rc.cim * a.y, rc.cre * a.y + rc.cim * a.x);
+        }
+        const int64_t row = rc.idx / (uint32_t)nchan;
+        const int chan = (int)(rc.idx - row * nchan);
+        VT *p = vis + row * vrs + chan * vcs;
+        for (int k = 0; k < pa.oc[0].npv; ++k) {
+            double xr = 0.0, xi = 0.0;
+            bool any = false;
+#pragma unroll
+            for (int q = 0; q < NPO; ++q) {
+                const double cr = pa.oc[q].cre[k], ci = pa.oc[q].cim[k];
+                if (cr == 0.0 && ci == 0.0) continue;
+                any = true;
+                xr += cr * v[q].x - ci * v[q].y;
+                xi += cr * v[q].y + ci * v[q].x;
+            }
+            if (any) store_vis_d(p + k * pa.oc[0].vps, xr, xi, accumulate);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------
 // kernels: the fp64 NUFFT (epsilon < 1e-7, the reference's default 1e-12)
 // ------------------------------------------------------------------------
@@ -5806,7 +5845,14 @@ static void ms2dirty_pols(const Inputs &in, PolsSpec ps, double *const *dirty, i
 }
 
 static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t sy, void *vis,
-                     sdp_hip_wgrid_info *info, hipStream_t st, const OutConv &oc = OutConv{}) {
+                     sdp_hip_wgrid_info *info, hipStream_t st, const OutConv &oc = OutConv{},
+                     int npo = 1, const double *const *dirty_q = nullptr,
+                     const OutConv *oc_q = nullptr) {
+    // npo > 1 (sdp_hip_dirty2ms_vis_pols): image pol q is dirty_q[q] through
+    // the conversion column oc_q[q], into one output; the pols share the
+    // bucketing, each has its plane stage and degridding, and one write-back
+    // combines them (fp64: the degridder adds each pol itself)
+    auto img = [&](int q) { return npo > 1 ? dirty_q[q] : dirty; };
     SDP_REQUIRE(in.vis_dtype == SDP_HIP_C64 || in.vis_dtype == SDP_HIP_C128,
                 "vis must be complex64 or complex128");
     SlotGuard slot(in.flags);
@@ -5817,15 +5863,25 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     const double *tab = phi_table(g.W, g.beta, st);
     const int accumulate = (in.flags & SDP_HIP_ACCUMULATE) ? 1 : 0;
     const int64_t nvis = in.nrow * (int64_t)in.nchan;
+    OutConv ocz = oc;  // the visibility pols any image pol writes
+    if (npo > 1) {
+        ocz = oc_q[0];
+        for (int k = 0; k < ocz.npv; ++k) {
+            bool any = false;
+            for (int q = 0; q < npo; ++q) any |= oc_q[q].cre[k] != 0.0 || oc_q[q].cim[k] != 0.0;
+            ocz.cre[k] = any ? 1.0 : 0.0;
+            ocz.cim[k] = 0.0;
+        }
+    }
     auto zero_vis = [&](hipStream_t s) {
         if (accumulate || nvis <= 0) return;
         if (in.vis_dtype == SDP_HIP_C128)
             k_zero_vis<double2><<<grid1d(nvis, 256), 256, 0, s>>>(in.nrow, in.nchan,
                                                                    (double2 *)vis, in.vrs,
-                                                                   in.vcs, oc);
+                                                                   in.vcs, ocz);
         else
             k_zero_vis<float2><<<grid1d(nvis, 256), 256, 0, s>>>(in.nrow, in.nchan, (float2 *)vis,
-                                                                  in.vrs, in.vcs, oc);
+                                                                  in.vrs, in.vcs, ocz);
         SDP_HIP_CHECK(hipGetLastError());
     };
     // all planes in one pass into plain contiguous c64 visibilities: the
@@ -5834,8 +5890,8 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     // visibilities no record reaches (no separate 1 GB zeroing pass on C2);
     // otherwise the output is zeroed first
     const bool trivial_oc = oc.npv == 1 && oc.cre[0] == 1.0 && oc.cim[0] == 0.0;
-    if (P.chunk_planes == g.nplanes && !accumulate && in.vis_dtype != SDP_HIP_C128 && trivial_oc &&
-        in.vcs == 1 && in.vrs == in.nchan && !P.f64) {
+    if (npo == 1 && P.chunk_planes == g.nplanes && !accumulate && in.vis_dtype != SDP_HIP_C128 &&
+        trivial_oc && in.vcs == 1 && in.vrs == in.nchan && !P.f64) {
         P.vdirect = static_cast<float2 *>(vis);
         if (!g.tiled) P.zout = P.vdirect;
     }
@@ -5844,13 +5900,13 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     };
     // screens + FFTs of planes [p_lo, p_lo + np) into the grid
     std::vector<std::unique_ptr<StageTimer>> stage_t;
-    auto plane_stage = [&](int p_lo, int np, hipStream_t s) {
+    auto plane_stage = [&](int p_lo, int np, hipStream_t s, const double *image) {
         for (int sb = 0; sb < np; sb += P.fft_planes) {
             const int nb = std::min(P.fft_planes, np - sb);
             stage_t.emplace_back(new StageTimer(s));
             StageTimer &t2 = *stage_t.back();
             t2.mark();
-            screen_adj(P, dirty, sx, sy, p_lo + sb, nb, tab, s);
+            screen_adj(P, image, sx, sy, p_lo + sb, nb, tab, s);
             t2.mark();
             fft_rows_x(P, nb, HIPFFT_FORWARD, s, P.spec_adj);
             tr_t_to_grid(P, sb, nb, s);
@@ -5874,7 +5930,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         stream_after(aux, st);
         zero_vis_unless_fused(aux);
         zero_band(P, std::min(g.nplanes, P.chunk_planes), aux);
-        if (planes_aux) plane_stage(0, g.nplanes, aux);
+        if (planes_aux) plane_stage(0, g.nplanes, aux, img(0));
         SDP_HIP_CHECK(hipEventCreateWithFlags(&zdone, hipEventDisableTiming));
         SDP_HIP_CHECK(hipEventRecord(zdone, aux));
     };
@@ -5883,32 +5939,40 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
     if (P.subsort) subsort_items(P, st);
     // (the fp64 degridder writes each visibility itself, through the pol
     // conversion, adding into the zeroed output)
-    float2 *acc = (P.vdirect || P.f64)
-                      ? nullptr
-                      : scratch<float2>("degrid_acc", std::max<int64_t>(nvis, 1));
-    if (acc)
-        SDP_HIP_CHECK(hipMemsetAsync(acc, 0, std::max<int64_t>(nvis, 1) * sizeof(float2), st));
+    float2 *accs[4] = {};
+    if (!(P.vdirect || P.f64)) {
+        static const char *names[4] = {"degrid_acc", "degrid_acc1", "degrid_acc2", "degrid_acc3"};
+        for (int q = 0; q < npo; ++q) {
+            accs[q] = scratch<float2>(names[q], std::max<int64_t>(nvis, 1));
+            SDP_HIP_CHECK(
+                hipMemsetAsync(accs[q], 0, std::max<int64_t>(nvis, 1) * sizeof(float2), st));
+        }
+    }
+    float2 *const acc = accs[0];
     float tgrid = 0, tfft = 0, tscr = 0;
-    for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
+    for (int q = 0; q < npo; ++q) {
+      const OutConv &ocq = npo > 1 ? oc_q[q] : oc;
+      float2 *const accq = accs[q];
+      for (int p_lo = 0; p_lo < g.nplanes; p_lo += P.chunk_planes) {
         const int p_hi = std::min(g.nplanes, p_lo + P.chunk_planes);
         const int np = p_hi - p_lo;
         if (zdone) {
             SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
             SDP_HIP_CHECK(hipEventDestroy(zdone));
             zdone = nullptr;
-            if (!planes_aux) plane_stage(p_lo, np, st);
+            if (!planes_aux) plane_stage(p_lo, np, st, img(q));
         } else {
             zero_band(P, np, st);
-            plane_stage(p_lo, np, st);
+            plane_stage(p_lo, np, st, img(q));
         }
         StageTimer tg(st);
         tg.mark();
-#define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, acc, st)
+#define SDP_LAUNCH_DEGRID(WW) launch_degrid<WW>(P, p_lo, p_hi, accq, st)
         if (P.f64 && in.vis_dtype == SDP_HIP_C128)
-            degrid_f64<double2>(P, p_lo, p_hi, static_cast<double2 *>(vis), in.vrs, in.vcs, 1, oc,
+            degrid_f64<double2>(P, p_lo, p_hi, static_cast<double2 *>(vis), in.vrs, in.vcs, 1, ocq,
                                 st);
         else if (P.f64)
-            degrid_f64<float2>(P, p_lo, p_hi, static_cast<float2 *>(vis), in.vrs, in.vcs, 1, oc,
+            degrid_f64<float2>(P, p_lo, p_hi, static_cast<float2 *>(vis), in.vrs, in.vcs, 1, ocq,
                                st);
         else
             SDP_W_DISPATCH(g.W, SDP_LAUNCH_DEGRID);
@@ -5916,6 +5980,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         SDP_HIP_CHECK(hipGetLastError());
         tg.mark();
         tgrid += tg.ms(0, 1);
+      }
     }
     if (zdone) {  // (no plane pass ran)
         SDP_HIP_CHECK(hipStreamWaitEvent(st, zdone, 0));
@@ -5925,7 +5990,28 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
         tscr += t->ms(0, 1);
         tfft += t->ms(1, 2);
     }
-    if (!P.vdirect && !P.f64 && P.pt.nvis > 0) {
+    if (npo > 1 && !P.f64 && P.pt.nvis > 0) {
+        const unsigned nb = std::min<unsigned>(grid1d(P.pt.nvis, 256), 16384);
+        PolAccs pa;
+        for (int q = 0; q < npo; ++q) {
+            pa.a[q] = accs[q];
+            pa.oc[q] = oc_q[q];
+        }
+#define SDP_FIN(VT, N)                                                                     \
+    k_finalize_pols<VT, N><<<nb, 256, 0, st>>>(P.pt.nrec, in.nchan, P.recs, pa, (VT *)vis, \
+                                               in.vrs, in.vcs, accumulate)
+        if (in.vis_dtype == SDP_HIP_C128) {
+            if (npo == 2) SDP_FIN(double2, 2);
+            else if (npo == 3) SDP_FIN(double2, 3);
+            else SDP_FIN(double2, 4);
+        } else {
+            if (npo == 2) SDP_FIN(float2, 2);
+            else if (npo == 3) SDP_FIN(float2, 3);
+            else SDP_FIN(float2, 4);
+        }
+#undef SDP_FIN
+        SDP_HIP_CHECK(hipGetLastError());
+    } else if (!P.vdirect && !P.f64 && P.pt.nvis > 0) {
         const unsigned nb = std::min<unsigned>(grid1d(P.pt.nvis, 256), 16384);
         if (in.vis_dtype == SDP_HIP_C128)
             k_finalize<double2><<<nb, 256, 0, st>>>(P.pt.nrec, in.nchan, P.recs, acc,
@@ -6290,6 +6376,49 @@ int sdp_hip_dirty2ms_vis(const double *uvw, int64_t uvw_row_stride, const double
         }
         wstack::dirty2ms(in, dirty, dirty_stride_x, dirty_stride_y, vis, info, as_stream(stream),
                          oc);
+    });
+}
+
+int sdp_hip_dirty2ms_vis_pols(const double *uvw, int64_t uvw_row_stride, const double *freq,
+                              int nchan, int64_t nrow, const double *dirty,
+                              int64_t dirty_stride_x, int64_t dirty_stride_y,
+                              int64_t dirty_stride_pol, int npol_img, int npix_x, int npix_y,
+                              double pixsize_x, double pixsize_y, double epsilon,
+                              int do_wstacking, unsigned flags, void *vis, int vis_dtype,
+                              int64_t vis_row_stride, int64_t vis_chan_stride,
+                              int64_t vis_pol_stride, int npol_vis, const double *pol_coeff,
+                              const double *shift_lmn, void *stream, sdp_hip_wgrid_info *info,
+                              char *errbuf, size_t errbuf_len) {
+    return guarded(errbuf, errbuf_len, [&] {
+        SDP_REQUIRE(dirty != nullptr && freq != nullptr && vis != nullptr &&
+                        (uvw != nullptr || nrow == 0),
+                    "null pointer argument");
+        SDP_REQUIRE(npol_vis >= 1 && npol_vis <= 4, "npol_vis must be 1..4");
+        SDP_REQUIRE(npol_img >= 1 && npol_img <= 4, "npol_img must be 1..4");
+        wstack::Inputs in{uvw,         uvw_row_stride,  freq,           nchan,
+                          nrow,        nullptr,         vis_dtype,      vis_row_stride,
+                          vis_chan_stride, nullptr,     0,              0,
+                          npix_x,      npix_y,          pixsize_x,      pixsize_y,
+                          epsilon,     do_wstacking,    flags};
+        if (shift_lmn) {
+            in.x.shift = true;
+            in.x.sl = shift_lmn[0];
+            in.x.sm = shift_lmn[1];
+            in.x.sn = shift_lmn[2];
+        }
+        wstack::OutConv ocs[4];
+        const double *imgs[4] = {};
+        for (int q = 0; q < npol_img; ++q) {
+            ocs[q].npv = npol_vis;
+            ocs[q].vps = vis_pol_stride;
+            for (int k = 0; k < npol_vis; ++k) {
+                ocs[q].cre[k] = pol_coeff ? pol_coeff[2 * (q * npol_vis + k)] : (k == q ? 1.0 : 0.0);
+                ocs[q].cim[k] = pol_coeff ? pol_coeff[2 * (q * npol_vis + k) + 1] : 0.0;
+            }
+            imgs[q] = dirty + q * dirty_stride_pol;
+        }
+        wstack::dirty2ms(in, dirty, dirty_stride_x, dirty_stride_y, vis, info, as_stream(stream),
+                         ocs[0], npol_img, imgs, ocs);
     });
 }
 

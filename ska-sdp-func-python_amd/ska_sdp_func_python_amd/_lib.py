@@ -143,6 +143,15 @@ SIGNATURES = {
         c_vp,                                     # pol_coeff (host doubles) or NULL
         c_vp,                                     # shift_lmn (host doubles) or NULL
         c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
+    "sdp_hip_dirty2ms_vis_pols": [
+        c_vp, c_i64, c_vp, c_int, c_i64,          # uvw, stride, freq, nchan, nrow
+        c_vp, c_i64, c_i64, c_i64, c_int,         # dirty, x / y / pol strides, npol_img
+        c_int, c_int, c_dbl, c_dbl,
+        c_dbl, c_int, c_u32,
+        c_vp, c_int, c_i64, c_i64, c_i64, c_int,  # vis, dtype, strides, npol_vis
+        c_vp,                                     # pol_coeff [npol_img][npol_vis] or NULL
+        c_vp,                                     # shift_lmn (host doubles) or NULL
+        c_vp, ctypes.POINTER(WGridInfo)] + _ERR,
     "sdp_hip_dft_point_v00": [
         c_int, c_vp, c_vp, c_int, c_int, c_i64, c_int, c_vp, c_vp, c_int, c_vp] + _ERR,
     "sdp_hip_dft_point_metres": [

@@ -214,7 +214,14 @@ def predict_ng(bvis, model, **kwargs):
         return conv[:, p]
 
     info = None
-    for vpol in range(vnpol if hi > lo else 0):
+    if m_nchan == 1 and vnpol > 1 and hi > lo:
+        # every image pol in one call: one bucketing, one write-back
+        _, info = kernels.dirty2ms_vis_pols(uvw, freq_t, pixels[0], vist,
+                                            [coef(p) for p in range(vnpol)], pixsize, pixsize,
+                                            epsilon, do_wstacking, flip_uw=True,
+                                            dirty_strides=(pixels.stride(1), 1, nx),
+                                            npix=(nx, ny), shift_lmn=lmn, precision=precision)
+    for vpol in range(vnpol if hi > lo and not (m_nchan == 1 and vnpol > 1) else 0):
         if m_nchan == 1:
             _, info = kernels.dirty2ms_vis(uvw, freq_t, pixels[0, vpol], vist, coef(vpol), pixsize,
                                            pixsize, epsilon, do_wstacking, flip_uw=True,

@@ -473,6 +473,53 @@ def dirty2ms_vis(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7
     return out, info.as_dict()
 
 
+def dirty2ms_vis_pols(uvw, freq, dirty, out, coef, pixsize_x, pixsize_y, epsilon=1e-7,
+                      do_wstacking=True, flip_uw=False, dirty_strides=None, npix=None,
+                      accumulate=False, shift_lmn=None, precision=None):
+    """Every image pol of predict_ng in one call (sdp_hip_dirty2ms_vis_pols):
+    ``dirty`` [npol_img, ...] f64 with ``dirty_strides`` = (pol, x, y),
+    ``out`` [nrow, nchan, npol_vis] complex (any strides) gets
+    sum_q coef[q][k] * prediction_q in vis pol k (coef None: identity).  The
+    pols share one bucketing and one write-back; results as one dirty2ms_vis
+    call per image pol, accumulating after the first."""
+    pbits = _prec_bits(epsilon, precision)
+    _check_uvw(uvw)
+    dev = uvw.device
+    freq = _on_gpu(freq, "freq").to(torch.float64).contiguous()
+    nrow, nchan = uvw.shape[0], freq.shape[0]
+    _on_gpu(dirty, "dirty")
+    if dirty.dtype != torch.float64 or dirty.dim() != 3:
+        raise ValueError("dirty must be float64 [npol_img, nx, ny]")
+    npo = dirty.shape[0]
+    npix_x, npix_y = (dirty.shape[-2], dirty.shape[-1]) if npix is None else npix
+    if dirty_strides is None:
+        dirty_strides = dirty.stride()
+    _on_gpu(out, "out")
+    if out.dtype not in (torch.complex64, torch.complex128) or out.dim() != 3 or \
+            tuple(out.shape[:2]) != (nrow, nchan):
+        raise ValueError("out must be complex [nrow, nchan, npol]")
+    npv = out.shape[2]
+    if not 1 <= npo <= 4:
+        raise ValueError("npol_img must be 1..4")
+    cbuf = None
+    if coef is not None:
+        rows = [[complex(z) for z in r] for r in coef]
+        if len(rows) != npo or any(len(r) != npv for r in rows):
+            raise ValueError("coef must be [npol_img][npol_vis]")
+        cbuf = (ctypes.c_double * (2 * npo * npv))(
+            *[v for r in rows for z in r for v in (z.real, z.imag)])
+    bits = ((_lib.SDP_HIP_FLIP_UW if flip_uw else 0) | (_lib.SDP_HIP_ACCUMULATE if accumulate else 0)
+            | pbits)
+    info = _lib.WGridInfo()
+    _lib.call("sdp_hip_dirty2ms_vis_pols", _ptr(uvw), uvw.stride(0), _ptr(freq), nchan, nrow,
+              _ptr(dirty), int(dirty_strides[1]), int(dirty_strides[2]), int(dirty_strides[0]),
+              npo, int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
+              int(bool(do_wstacking)), bits, _ptr(out), _DT_CODE[out.dtype], *out.stride(), npv,
+              ctypes.cast(cbuf, ctypes.c_void_p) if cbuf is not None else None,
+              _host3(shift_lmn), _stream(dev), ctypes.byref(info))
+    return out, info.as_dict()
+
+
 def dirty2ms(uvw, freq, dirty, wgt, pixsize_x, pixsize_y, epsilon=1e-7,
              do_wstacking=True, flip_uw=False, out=None, dirty_strides=None,
              npix=None, accumulate=False, vis_dtype=torch.complex64, precision=None):

@@ -655,6 +655,47 @@ def test_pols_call_matches_per_pol_calls(path, vdt, monkeypatch):
         assert info["nvis_used"] == nrow * nchan  # (every in-grid visibility bucketed)
 
 
+@pytest.mark.parametrize("path", ["fine", "coarse", "fp64"])
+@pytest.mark.parametrize("vdt", [torch.complex64, torch.complex128])
+@pytest.mark.parametrize("acc", [False, True])
+def test_predict_pols_call_matches_per_pol_calls(path, vdt, acc, monkeypatch):
+    """sdp_hip_dirty2ms_vis_pols (predict_ng's image pols in one call: one
+    bucketing, each pol's planes and degridding, one write-back through the
+    conversion matrix) against one dirty2ms_vis call per image pol (the first
+    without, the others with accumulation): stokesIQUV -> linear, with and
+    without accumulation into the output; 16x16-cell buckets ("coarse") and
+    the fp64 path (epsilon 1e-12) too.  1e-6 relative RMS (fp32 sums of the
+    pols in the output dtype vs one fp64 sum)."""
+    from ska_sdp_func_python_amd import kernels
+    if path == "coarse":
+        monkeypatch.setenv("SDP_HIP_BUCKET", "16")
+    rng = np.random.default_rng(73)
+    nrow, nchan, npv, npix = 4000, 5, 4, 128
+    freq = np.linspace(1.0e9, 1.2e9, nchan)
+    umax = 3000.0
+    uvw_h = rng.uniform(-1, 1, (nrow, 3)) * umax * orc.C_LIGHT / freq.max()
+    uvw_h[:, 2] *= 0.3
+    dev = "cuda"
+    uvw = torch.as_tensor(uvw_h, device=dev)
+    freq_t = torch.as_tensor(freq, device=dev)
+    imgs = torch.as_tensor(rng.normal(size=(4, npix, npix)), device=dev)
+    # IQUV -> linear: column q of the conversion = image pol q's vis pols
+    cols = [[1, 0, 0, 1], [1, 0, 0, -1], [0, 1, 1, 0], [0, 1j, -1j, 0]]
+    cell = 0.35 / umax
+    eps = 1e-12 if path == "fp64" else 1e-5
+    base = torch.as_tensor(rng.normal(size=(nrow, nchan, npv)) +
+                           1j * rng.normal(size=(nrow, nchan, npv)), device=dev).to(vdt)
+    ref = base.clone() if acc else torch.zeros_like(base)
+    for q in range(4):
+        kernels.dirty2ms_vis(uvw, freq_t, imgs[q], ref, cols[q], cell, cell, eps, True,
+                             flip_uw=True, accumulate=acc or q > 0)
+    got = base.clone() if acc else torch.full_like(base, float("nan"))
+    kernels.dirty2ms_vis_pols(uvw, freq_t, imgs, got, cols, cell, cell, eps, True, flip_uw=True,
+                              accumulate=acc)
+    tol = 1e-12 if (path == "fp64" and vdt == torch.complex128) else 1e-6
+    assert rel_rms(got.cpu().numpy(), ref.cpu().numpy()) < tol
+
+
 @pytest.mark.parametrize("ipf,pf", [("stokesI", "stokesI"), ("stokesIQUV", "linear"),
                                     ("stokesIQUV", "circular"), ("linear", "linear")])
 @pytest.mark.parametrize("mfs", [True, False])
