@@ -186,7 +186,7 @@ def api_rates(args, obs, cell):
     bench workload: device-resident arrays, and host numpy arrays copied to
     the device inside the call (PCIe-inclusive; never the headline value)."""
     from ska_sdp_func_python_amd import datamodels as dm
-    from ska_sdp_func_python_amd.imaging import invert_ng
+    from ska_sdp_func_python_amd.imaging import invert_ng, predict_ng
     dev = obs["uvw"].device
     nrow, nchan = obs["nrow"], obs["vis"].shape[1]
     nb = 197 * 196 // 2
@@ -244,7 +244,7 @@ def api_rates(args, obs, cell):
         os.environ.pop("SDP_HIP_OVERLAP", None)
         return r
 
-    # a 4-pol MFS image (linear vis -> stokesIQUV, 4 NUFFT calls of 123.6 Mvis)
+    # a 4-pol MFS image (linear vis -> stokesIQUV: 4 pols of 123.6 Mvis in one library call)
     s4 = (nt, nb, nchan, 4)
     v4 = obs["vis"].to(torch.complex128).reshape(nt, nb, nchan, 1).expand(s4).contiguous()
     d4 = {"uvw": d["uvw"], "vis": v4, "w": torch.ones(s4, dtype=torch.float64, device=dev),
@@ -258,6 +258,20 @@ def api_rates(args, obs, cell):
                          frequency=float(freq.mean()),
                          channel_bandwidth=float(2 * (freq.max() - freq.min()) + 1e6), nchan=1)
     r4 = both(b4, m4)
+    # predict_ng of a 4-pol model into that Visibility (one call for every pol)
+    m4p = m4.copy(deep=True)
+    m4p["pixels"].data = torch.randn(tuple(m4["pixels"].data.shape), dtype=torch.float64,
+                                     device=dev)
+    predict_ng(b4, m4p, epsilon=EPS_REQUESTED)
+    ts = []
+    for _ in range(2):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        predict_ng(b4, m4p, epsilon=EPS_REQUESTED)
+        torch.cuda.synchronize(dev)
+        ts.append(time.perf_counter() - t0)
+    tp4 = min(ts)
+    del m4p
     # the same at the reference's default epsilon (fp64 NUFFT; each pol its
     # own two-level bucketing and MFMA gridder, pipelined)
     invert_ng(b4, m4, epsilon=EPS_REFERENCE)
@@ -279,6 +293,7 @@ def api_rates(args, obs, cell):
         "invert_ng_4pol_serial_ms": round(r4["serial"] * 1e3, 2),
         "invert_ng_4pol_Mvis_s": round(4 * nvis / r4["default"] / 1e6, 1),
         "invert_ng_4pol_eps1e-12_ms": round(t4_64 * 1e3, 2),
+        "predict_ng_4pol_ms": round(tp4 * 1e3, 2),
         "invert_ng_cube16_ms": round(rc["default"] * 1e3, 2),
         "invert_ng_cube16_serial_ms": round(rc["serial"] * 1e3, 2),
         "invert_ng_cube16_Mvis_s": round(nvis / rc["default"] / 1e6, 1)})
@@ -290,8 +305,9 @@ def api_rates(args, obs, cell):
                 "host_visibility_Mvis_s": round(nvis / t_host / 1e6, 1),
                 "note": "reference-shaped invert_ng on a c128/f64/int64 Visibility; the host "
                         "figure includes the H2D copies of ~5 GB (PCIe-inclusive) and the image "
-                        "D2H; 4pol: a linear-frame Visibility imaged to stokesIQUV (4 NUFFT "
-                        "calls sharing one bucketing); cube16: 64 vis channels onto a 16-channel "
+                        "D2H; 4pol: a linear-frame Visibility imaged to stokesIQUV (one library "
+                        "call: one bucketing and value pass for the 4 pols; predict_ng_4pol: a random stokesIQUV model into "
+                        "it, one library call for every pol); cube16: 64 vis channels onto a 16-channel "
                         "image (one call per image channel's run of 4 vis channels, 16 calls "
                         "pipelined over two streams); 'serial' = "
                         "SDP_HIP_OVERLAP=0 (one stream)"})
