@@ -50,8 +50,12 @@ __global__ __launch_bounds__(kThreads) void k_dft_mfma(int ncomp, const double *
                                                        const double *__restrict__ freq,
                                                        OT *__restrict__ vis) {
     __shared__ double s_b[kMfmaChunk * 4];  // (l, m, n - 1, 0) per component
-    __shared__ float2 s_fl[kMfmaChunk * NPOL];
-    using AT = typename std::conditional<std::is_same<OT, double2>::value, double, float>::type;
+    // c128 output: fp64 flux, sincos and sums (the reference's numpy fp64
+    // arithmetic for that dtype); c64: fp32 sincos of the fp64-reduced phase
+    constexpr bool kF64 = std::is_same<OT, double2>::value;
+    using FT2 = typename std::conditional<kF64, double2, float2>::type;
+    __shared__ FT2 s_fl[kMfmaChunk * NPOL];
+    using AT = typename std::conditional<kF64, double, float>::type;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int chan = blockIdx.y;
     const int k = lane >> 4, r16 = lane & 15;
@@ -85,14 +89,18 @@ __global__ __launch_bounds__(kThreads) void k_dft_mfma(int ncomp, const double *
         }
         for (int i = threadIdx.x; i < ncp * NPOL; i += kThreads) {
             const int c = i / NPOL, p = i - c * NPOL;
-            s_fl[i] = c < nc ? to_f2(flux[((int64_t)(c0 + c) * fnchan + fch) * NPOL + p])
-                             : make_float2(0.0f, 0.0f);
+            if constexpr (kF64)
+                s_fl[i] = c < nc ? flux[((int64_t)(c0 + c) * fnchan + fch) * NPOL + p]
+                                 : make_double2(0.0, 0.0);
+            else
+                s_fl[i] = c < nc ? to_f2(flux[((int64_t)(c0 + c) * fnchan + fch) * NPOL + p])
+                                 : make_float2(0.0f, 0.0f);
         }
         __syncthreads();
         for (int ct = 0; ct < ncp; ct += 16) {
             const int c = ct + r16;  // this lane's component
             const double bop = s_b[c * 4 + k];
-            float2 f[NPOL];
+            FT2 f[NPOL];
 #pragma unroll
             for (int p = 0; p < NPOL; ++p) f[p] = s_fl[c * NPOL + p];
             doublex4 ph[T];
@@ -105,19 +113,24 @@ __global__ __launch_bounds__(kThreads) void k_dft_mfma(int ncomp, const double *
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     // the phase in turns, reduced to [0, 1) in fp64
-                    const float x = (float)__builtin_amdgcn_fract(ph[t][i]);
-                    const float sn = __builtin_amdgcn_sinf(x);  // sin(2 pi x)
-                    const float cs = __builtin_amdgcn_cosf(x);
+                    if constexpr (kF64) {
+                        double sn, cs;
+                        sincospi(2.0 * __builtin_amdgcn_fract(ph[t][i]), &sn, &cs);
 #pragma unroll
-                    for (int p = 0; p < NPOL; ++p) {
-                        // f * exp(-2 pi i x) = f * (cs - i sn); fp32 sums as
-                        // two fused multiply-adds per part (packed pairs)
-                        if constexpr (std::is_same<AT, float>::value) {
+                        for (int p = 0; p < NPOL; ++p) {
+                            ar[t][i][p] = fma(f[p].y, sn, fma(f[p].x, cs, ar[t][i][p]));
+                            ai[t][i][p] = fma(-f[p].x, sn, fma(f[p].y, cs, ai[t][i][p]));
+                        }
+                    } else {
+                        const float x = (float)__builtin_amdgcn_fract(ph[t][i]);
+                        const float sn = __builtin_amdgcn_sinf(x);  // sin(2 pi x)
+                        const float cs = __builtin_amdgcn_cosf(x);
+#pragma unroll
+                        for (int p = 0; p < NPOL; ++p) {
+                            // f * exp(-2 pi i x) = f * (cs - i sn); fp32 sums
+                            // as two fused multiply-adds per part (packed pairs)
                             ar[t][i][p] = fmaf(f[p].y, sn, fmaf(f[p].x, cs, ar[t][i][p]));
                             ai[t][i][p] = fmaf(-f[p].x, sn, fmaf(f[p].y, cs, ai[t][i][p]));
-                        } else {
-                            ar[t][i][p] += (AT)(f[p].x * cs + f[p].y * sn);
-                            ai[t][i][p] += (AT)(f[p].y * cs - f[p].x * sn);
                         }
                     }
                 }
