@@ -2165,6 +2165,335 @@ __global__ void k_screen_adj_t(Geo g, const double *__restrict__ dirty, int64_t 
     }
 }
 
+// ---- fused x-FFT + w screens (fp32 planes, power-of-two ngx) ------------
+// One workgroup per image row iy.  Per plane of the batch the T row (c64,
+// N = ngx points) is transformed in LDS by a Stockham mixed-radix FFT: N / 16
+// threads hold 16 points each, radix-16 passes and at most one radix-2/4/8
+// pass (natural-order output, no bit reversal), LDS padded by one element
+// per 16 so the strided pass-0 writes are conflict-free.  The twiddles do not
+// depend on the plane: each thread's w, w^2, w^4, w^8 per pass are computed
+// once by sincospif (exact fractions) and the other powers by at most three
+// products.  The invert screens the FFT's image columns straight from LDS
+// into fp64 registers (the x-spectra are never written), the predict
+// screens the image into the FFT's input in LDS (the zero-filled x-FFT input
+// is never written or read).
+__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// e^{SG 2 pi i m / 16} (SG = +1: backward, -1: forward), m a constant
+template <int SG>
+__device__ __forceinline__ float2 root16(int m) {
+    constexpr float c16[16] = {1.0f,
+                               0.92387953251128673848f,
+                               0.70710678118654752440f,
+                               0.38268343236508978178f,
+                               0.0f,
+                               -0.38268343236508978178f,
+                               -0.70710678118654752440f,
+                               -0.92387953251128673848f,
+                               -1.0f,
+                               -0.92387953251128673848f,
+                               -0.70710678118654752440f,
+                               -0.38268343236508978178f,
+                               0.0f,
+                               0.38268343236508978178f,
+                               0.70710678118654752440f,
+                               0.92387953251128673848f};
+    m &= 15;
+    return make_float2(c16[m], SG * c16[(m + 12) & 15]);  // sin = cos(. - pi/2)
+}
+
+// R-point DFT (R = 2, 4, 8, 16) of v[0..R) in registers, radix-2
+// decimation in frequency: the result leaves bit-reversed (out[bitrev(r)] =
+// v[r]); the callers index it through fx_brev
+template <int R, int SG>
+__device__ __forceinline__ void fx_dft(float2 *v) {
+#pragma unroll
+    for (int L = R; L >= 2; L >>= 1) {
+        const int h = L >> 1;
+#pragma unroll
+        for (int s = 0; s < R; s += L) {
+#pragma unroll
+            for (int k = 0; k < h; ++k) {
+                const float2 a = v[s + k], b = v[s + k + h];
+                v[s + k] = make_float2(a.x + b.x, a.y + b.y);
+                const float2 d = make_float2(a.x - b.x, a.y - b.y);
+                v[s + k + h] = k == 0 ? d : cmulf(d, root16<SG>(k * (16 / L)));
+            }
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ constexpr int fx_brev(int r) {
+    int o = 0;
+    for (int b = 1, t = R >> 1; b < R; b <<= 1, t >>= 1)
+        if (r & b) o |= t;
+    return o;
+}
+
+__device__ __forceinline__ int fx_pad(int i) { return i + (i >> 4); }
+// fx_pad(t + c), pt = fx_pad(t), c a multiple of T: for T % 16 == 0 it is
+// pt + 17 c / 16 (an immediate offset from one base)
+template <int T>
+__device__ __forceinline__ int fx_padc(int t, int pt, int c) {
+    if constexpr (T % 16 == 0) return pt + (c / 16) * 17;
+    else return fx_pad(t + c);
+}
+
+// the 15 twiddles w^r, r = 1..15, from w, w^2, w^4, w^8
+__device__ __forceinline__ void fx_powers(const float2 (&b)[4], float2 *w) {
+    w[1] = b[0];
+    w[2] = b[1];
+    w[3] = cmulf(b[1], b[0]);
+    w[4] = b[2];
+    w[5] = cmulf(b[2], b[0]);
+    w[6] = cmulf(b[2], b[1]);
+    w[7] = cmulf(b[2], w[3]);
+#pragma unroll
+    for (int r = 1; r < 8; ++r) w[8 + r] = cmulf(b[3], w[r]);
+    w[8] = b[3];
+}
+
+template <int LOGN>
+struct FxShape {
+    static constexpr int N = 1 << LOGN;
+    static constexpr int T = N / 16;          // threads
+    static constexpr int P16 = LOGN / 4;      // radix-16 passes
+    static constexpr int RR = 1 << (LOGN % 4);  // last pass radix (1: none)
+    static constexpr int LDS = N + N / 16;    // padded float2 elements
+    // twiddle table (fx_twiddles), copied into LDS behind the data by each
+    // workgroup: radix-16 pass p >= 1 at tw_off(p), w and w^4 per k < 16^p;
+    // the last pass's e^{2 pi i t / N} at tw_off(P16)
+    static constexpr int tw_off(int p) { return p <= 1 ? 0 : tw_off(p - 1) + 2 * (1 << (4 * (p - 1))); }
+    static constexpr int TW = tw_off(P16) + T;
+    static constexpr size_t lds_bytes() { return (size_t)(LDS + TW) * 8; }
+};
+
+// the transform of the row held as v[r] = X[t + r T] (pass 0's inputs) into
+// buf (natural order, padded); ends with the workgroup synchronised
+template <int LOGN, int SG>
+__device__ __forceinline__ void fx_fft(float2 (&v)[16], float2 *buf, const float2 *__restrict__ twt,
+                                       int t) {
+    using S = FxShape<LOGN>;
+    // pass 0 (Ns = 1): no twiddles, outputs to 16 t + r
+    fx_dft<16, SG>(v);
+    {
+        float2 *const o = buf + 17 * t;  // fx_pad(16 t + r) = 17 t + r
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] = v[fx_brev<16>(r)];
+    }
+    __syncthreads();
+    const int pt = fx_pad(t);
+    int ns = 16;
+#pragma unroll
+    for (int p = 1; p < S::P16; ++p) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = buf[fx_padc<S::T>(t, pt, r * S::T)];
+        __syncthreads();
+        // twiddles w^r, w = e^{SG 2 pi i k / (16 Ns)}, k = t mod Ns
+        const int k = t % ns, d = (t / ns) * ns * 16 + k;
+        {
+            // (kk opaque: the twiddles are loaded and multiplied out per
+            // transform, not hoisted out of the caller's plane loop, where
+            // they held ~60 VGPRs)
+            int kk = k;
+            asm volatile("" : "+v"(kk));
+            float2 b[4], w[16];
+            const float4 q0 = *reinterpret_cast<const float4 *>(twt + S::tw_off(p) + 2 * kk);
+            b[0] = make_float2(q0.x, SG * q0.y);
+            b[2] = make_float2(q0.z, SG * q0.w);
+            b[1] = cmulf(b[0], b[0]);
+            b[3] = cmulf(b[2], b[2]);
+            fx_powers(b, w);
+#pragma unroll
+            for (int r = 1; r < 16; ++r) v[r] = cmulf(v[r], w[r]);
+        }
+        fx_dft<16, SG>(v);
+        const int pd = fx_pad(d);  // (ns >= 16: r ns is a multiple of 16)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) buf[pd + r * ns + ((r * ns) >> 4)] = v[fx_brev<16>(r)];
+        __syncthreads();
+        ns *= 16;
+    }
+    if constexpr (S::RR > 1) {
+        // last pass, Ns = N / RR: butterfly j = t + T m reads and writes
+        // X[j + r N / RR] in place (no hazard across threads)
+        constexpr int RR = S::RR, NB = 16 / RR, STR = S::N / RR;
+        int tt = t;
+        asm volatile("" : "+v"(tt));
+        const float2 l0 = twt[S::tw_off(S::P16) + tt], last = make_float2(l0.x, SG * l0.y);
+#pragma unroll
+        for (int m = 0; m < NB; ++m) {
+            float2 u[RR];
+            const int j = t + S::T * m;
+#pragma unroll
+            for (int r = 0; r < RR; ++r) u[r] = buf[fx_padc<S::T>(t, pt, S::T * m + r * STR)];
+            // twiddle w_j^r, w_j = e^{SG 2 pi i j / N} = last * e^{SG 2 pi i m / 16}
+            const float2 wj = m == 0 ? last : cmulf(last, root16<SG>(m));
+            float2 wr = wj;
+#pragma unroll
+            for (int r = 1; r < RR; ++r) {
+                u[r] = cmulf(u[r], wr);
+                if (r + 1 < RR) wr = cmulf(wr, wj);
+            }
+            fx_dft<RR, SG>(u);
+#pragma unroll
+            for (int r = 0; r < RR; ++r) buf[fx_padc<S::T>(t, pt, S::T * m + r * STR)] = u[fx_brev<RR>(r)];
+        }
+        __syncthreads();
+    }
+}
+
+// the workgroup's LDS copy of the twiddle table (behind the data buffer)
+template <int LOGN>
+__device__ __forceinline__ float2 *fx_twl(float2 *fbuf, const float2 *__restrict__ twg, int t) {
+    using S = FxShape<LOGN>;
+    float2 *const twl = fbuf + S::LDS;
+    for (int i = t; i < S::TW; i += S::T) twl[i] = twg[i];
+    __syncthreads();
+    return twl;
+}
+
+// pass 0's inputs v[r] = X[t + r T] of one T row; the columns outside the
+// band [lo, hi) are zeros in the buffer and are not read
+template <int LOGN>
+__device__ __forceinline__ void fx_load_row(float2 (&v)[16], const float2 *__restrict__ row, int t,
+                                            int lo, int hi) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int i = t + r * FxShape<LOGN>::T;
+        v[r] = (i >= lo && i < hi) ? row[i] : make_float2(0.0f, 0.0f);
+    }
+}
+
+// invert: dirty(ix, iy) (+)= corr * sum_q Re(FFT_x(T_in[q][iy])[gx] e^{2 pi i w_q s})
+template <int LOGN>
+__global__ __launch_bounds__(FxShape<LOGN>::T) __attribute__((amdgpu_waves_per_eu(4, 8))) void
+k_xfft_screen_fwd(
+    Geo g, const float2 *__restrict__ tin, int row_lo, int row_hi, int p_begin, int np,
+    double *dirty, int64_t sx, int64_t sy, int accumulate, const double *__restrict__ tab,
+    const float2 *__restrict__ twg) {
+    using S = FxShape<LOGN>;
+    constexpr int PX = 8;  // pixels per thread: nx <= N / 2 = 8 T
+    extern __shared__ float2 fbuf[];
+    const int t = threadIdx.x, iy = blockIdx.x;
+    float2 *const twl = fx_twl<LOGN>(fbuf, twg, t);
+    // (each pixel's s is recomputed per plane, as pixel_geom does: 16 VGPRs of
+    // stored s pushed the kernel past 128 VGPRs into scratch)
+    double acc[PX];
+#pragma unroll
+    for (int m = 0; m < PX; ++m) acc[m] = 0.0;
+    const double mm = (iy - g.ny / 2) * g.py, m2 = mm * mm;
+    const int64_t tplane = (int64_t)g.ny * g.ngx;
+    const float2 *row = tin + (int64_t)iy * g.ngx;
+    float2 v[16];
+    fx_load_row<LOGN>(v, row, t, row_lo, row_hi);
+    for (int q = 0; q < np; ++q) {
+        fx_fft<LOGN, 1>(v, fbuf, twl, t);
+        if (q + 1 < np) fx_load_row<LOGN>(v, row + (q + 1) * tplane, t, row_lo, row_hi);  // (in flight under the screens)
+        const double wq = g.w0 + (p_begin + q) * g.dw;
+        int tt = t;  // (opaque: the pixels' LDS addresses are not hoisted out of the plane loop)
+        asm volatile("" : "+v"(tt));
+#pragma unroll
+        for (int m = 0; m < PX; ++m) {
+            const int ix = tt + m * S::T;
+            if (ix < g.nx) {
+                const int X = ix - g.nx / 2;
+                const float2 h = fbuf[fx_pad(X < 0 ? X + g.ngx : X)];
+                if (g.do_w) {
+                    const double l = X * g.px, r2 = l * l + m2;
+                    const double sp = r2 < 1.0 ? r2 / (sqrt(1.0 - r2) + 1.0) - g.s0 : 0.0;
+                    double ph = wq * sp;
+                    ph -= rint(ph);
+                    double sn, cs;
+                    sincospi_t<float2>(2.0 * ph, &sn, &cs);
+                    acc[m] += (double)h.x * cs - (double)h.y * sn;
+                } else {
+                    acc[m] += (double)h.x;
+                }
+            }
+        }
+        __syncthreads();  // (the next plane's pass 0 overwrites the buffer)
+    }
+#pragma unroll
+    for (int m = 0; m < PX; ++m) {
+        const int ix = t + m * S::T;
+        if (ix < g.nx) {
+            const PixelGeom p = pixel_geom(g, ix, iy, tab);
+            const double res = p.inside ? acc[m] * p.corr : 0.0;
+            double *o = dirty + ix * sx + iy * sy;
+            *o = accumulate ? *o + res : res;
+        }
+    }
+}
+
+// predict: spec[q][iy][k] = FFT_x forward of the row whose image kx columns
+// hold corr * dirty(ix, iy) * e^{-2 pi i w_q s} (zeros elsewhere), the input
+// built in registers per thread (its 16 positions t + r T) -- the separate
+// screen pass and the zero-filled x-FFT input are not needed
+template <int LOGN>
+__global__ __launch_bounds__(FxShape<LOGN>::T) __attribute__((amdgpu_waves_per_eu(4, 8))) void
+k_screen_adj_xfft(Geo g, const double *__restrict__ dirty, int64_t sx, int64_t sy, int p_begin,
+                  int np, float2 *__restrict__ spec, const double *__restrict__ tab,
+                  const float2 *__restrict__ twg) {
+    using S = FxShape<LOGN>;
+    extern __shared__ float2 fbuf[];
+    const int t = threadIdx.x, iy = blockIdx.x;
+    float2 *const twl = fx_twl<LOGN>(fbuf, twg, t);
+    // the corrected image value at the thread's x positions t + r T that can
+    // hold a pixel (fp32, as the spectrum stores it; 0 where none maps): with
+    // nx <= N / 2 only r < 4 and r >= 12 can (|X| <= N / 4 = 4 T)
+    float val[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int r = e < 4 ? e : e + 8;
+        const int i = t + r * S::T;
+        const int X = i < g.ngx / 2 ? i : i - g.ngx, ix = X + g.nx / 2;
+        val[e] = 0.0f;
+        if (ix >= 0 && ix < g.nx) {
+            const PixelGeom p = pixel_geom(g, ix, iy, tab);
+            val[e] = p.inside ? (float)(dirty[ix * sx + iy * sy] * p.corr) : 0.0f;
+        }
+    }
+    const double mm = (iy - g.ny / 2) * g.py, m2 = mm * mm;
+    const int64_t tplane = (int64_t)g.ny * g.ngx;
+    const int pt = fx_pad(t);
+    for (int q = 0; q < np; ++q) {
+        const double wq = g.w0 + (p_begin + q) * g.dw;
+        int tt = t;  // (opaque, as in k_xfft_screen_fwd)
+        asm volatile("" : "+v"(tt));
+        float2 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = make_float2(0.0f, 0.0f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int r = e < 4 ? e : e + 8;
+            const int i = tt + r * S::T;
+            const int X = i < g.ngx / 2 ? i : i - g.ngx;
+            if (val[e] != 0.0f) {
+                if (g.do_w) {
+                    const double l = X * g.px, r2 = l * l + m2;
+                    const double sp = r2 / (sqrt(1.0 - r2) + 1.0) - g.s0;
+                    double ph = wq * sp;
+                    ph -= rint(ph);
+                    double sn, cs;
+                    sincospi_t<float2>(2.0 * ph, &sn, &cs);
+                    v[r] = make_float2((float)(val[e] * cs), (float)(-val[e] * sn));
+                } else {
+                    v[r] = make_float2(val[e], 0.0f);
+                }
+            }
+        }
+        fx_fft<LOGN, -1>(v, fbuf, twl, t);
+        float2 *o = spec + q * tplane + (int64_t)iy * g.ngx;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t + r * S::T] = fbuf[fx_padc<S::T>(t, pt, r * S::T)];
+        __syncthreads();  // (the next plane's pass 0 overwrites the buffer)
+    }
+}
+
 __device__ __forceinline__ void store_vis(float2 *p, float2 v, int accumulate) {
     if (accumulate) {
         const float2 o = *p;
@@ -5320,6 +5649,114 @@ static void screen_adj(const Plan &P, const double *dirty, int64_t sx, int64_t s
     SDP_HIP_CHECK(hipGetLastError());
 }
 
+// log2 of the x edge when the fused x-FFT + screen kernels serve the plan
+// (fp32 planes, ngx a power of two in [2^7, 2^14]), else 0: hipFFT x
+// transforms and the separate screens.  SDP_HIP_XFFT_FUSED=0 forces the latter.
+static int xfft_log2(const Plan &P) {
+    const int on = env_int("SDP_HIP_XFFT_FUSED", 1);
+    const int n = P.g.ngx;
+    if (P.f64 || !on || n <= 0 || (n & (n - 1)) || 2 * P.g.nx > n) return 0;
+    int l = 0;
+    while ((1 << l) < n) ++l;
+    return (l >= 7 && l <= 14) ? l : 0;
+}
+
+// the fused FFT's twiddle bases (FxShape::tw_off), e^{+2 pi i ...} in fp64
+// rounded to fp32 (the forward transforms conjugate them)
+template <int LOGN>
+static const float2 *fx_twiddles(hipStream_t st) {
+    using S = FxShape<LOGN>;
+    static const std::vector<float2> host = [] {
+        std::vector<float2> h(S::TW);
+        auto root = [](long num, long den) {
+            const long double a = 2.0L * 3.14159265358979323846264338327950288L * num / den;
+            return make_float2((float)std::cos(a), (float)std::sin(a));
+        };
+        for (int p = 1, ns = 16; p < S::P16; ++p, ns *= 16)
+            for (int k = 0; k < ns; ++k) {
+                h[S::tw_off(p) + 2 * k] = root(k, 16L * ns);
+                h[S::tw_off(p) + 2 * k + 1] = root(4L * k, 16L * ns);
+            }
+        for (int t = 0; t < S::T; ++t) h[S::tw_off(S::P16) + t] = root(t, S::N);
+        return h;
+    }();
+    float2 *d = scratch<float2>("fx_tw_" + std::to_string(LOGN), S::TW);
+    SDP_HIP_CHECK(hipMemcpyAsync(d, host.data(), S::TW * sizeof(float2), hipMemcpyHostToDevice, st));
+    return d;
+}
+
+template <int LOGN>
+static void launch_xfft_screen_fwd(const Plan &P, int p_begin, int nb, double *dirty, int64_t sx,
+                                   int64_t sy, int accumulate, const double *tab, hipStream_t st) {
+    using S = FxShape<LOGN>;
+    constexpr size_t lds = S::lds_bytes();
+    static const bool attr = [] {  // dynamic LDS above 64 KiB
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_xfft_screen_fwd<LOGN>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        return true;
+    }();
+    (void)attr;
+    k_xfft_screen_fwd<LOGN><<<P.g.ny, S::T, lds, st>>>(P.g, P.spec_in, P.row_lo, P.row_hi, p_begin,
+                                                       nb, dirty, sx, sy, accumulate, tab,
+                                                       fx_twiddles<LOGN>(st));
+    SDP_HIP_CHECK(hipGetLastError());
+}
+
+// the backward x transforms of planes [p_begin, p_begin + nb) (T rows in
+// spec_in) and their screens into the image: fused when xfft_log2 allows,
+// else hipFFT into spec + k_screen_fwd_t.  Times the two parts into *tfft and
+// *tscr (the fused kernel counts as the screen).
+static void xfft_screen_fwd(const Plan &P, int p_begin, int nb, double *dirty, int64_t sx,
+                            int64_t sy, int accumulate, const double *tab, hipStream_t st,
+                            StageTimer &t2) {
+    switch (xfft_log2(P)) {
+#define SDP_FX(L) \
+    case L: t2.mark(); launch_xfft_screen_fwd<L>(P, p_begin, nb, dirty, sx, sy, accumulate, tab, st); break;
+    SDP_FX(7) SDP_FX(8) SDP_FX(9) SDP_FX(10) SDP_FX(11) SDP_FX(12) SDP_FX(13) SDP_FX(14)
+#undef SDP_FX
+    default:
+        fft_rows_x(P, nb, HIPFFT_BACKWARD, st, P.spec_in);
+        t2.mark();
+        screen_fwd(P, p_begin, nb, dirty, sx, sy, accumulate, tab, st);
+    }
+    t2.mark();
+}
+
+template <int LOGN>
+static void launch_screen_adj_xfft(const Plan &P, const double *dirty, int64_t sx, int64_t sy,
+                                   int p_begin, int nb, const double *tab, hipStream_t st) {
+    using S = FxShape<LOGN>;
+    constexpr size_t lds = S::lds_bytes();
+    static const bool attr = [] {  // dynamic LDS above 64 KiB
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void *)k_screen_adj_xfft<LOGN>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        return true;
+    }();
+    (void)attr;
+    k_screen_adj_xfft<LOGN><<<P.g.ny, S::T, lds, st>>>(P.g, dirty, sx, sy, p_begin, nb, P.spec,
+                                                       tab, fx_twiddles<LOGN>(st));
+    SDP_HIP_CHECK(hipGetLastError());
+}
+
+// the predict's screens of planes [p_begin, p_begin + nb) and their forward
+// x transforms into spec: fused when xfft_log2 allows, else k_screen_adj_t
+// into the zero-kept input and hipFFT.  Marks t2 between the two parts (the
+// fused kernel counts as the screen).
+static void screen_adj_xfft(const Plan &P, const double *dirty, int64_t sx, int64_t sy,
+                            int p_begin, int nb, const double *tab, hipStream_t st,
+                            StageTimer &t2) {
+    switch (xfft_log2(P)) {
+#define SDP_FX(L) \
+    case L: launch_screen_adj_xfft<L>(P, dirty, sx, sy, p_begin, nb, tab, st); t2.mark(); break;
+    SDP_FX(7) SDP_FX(8) SDP_FX(9) SDP_FX(10) SDP_FX(11) SDP_FX(12) SDP_FX(13) SDP_FX(14)
+#undef SDP_FX
+    default:
+        screen_adj(P, dirty, sx, sy, p_begin, nb, tab, st);
+        t2.mark();
+        fft_rows_x(P, nb, HIPFFT_FORWARD, st, P.spec_adj);
+    }
+}
+
 static int cu_count() {
     static std::mutex mu;
     static std::map<int, int> cus;
@@ -5675,11 +6112,8 @@ static void ms2dirty(const Inputs &in, double *dirty, int64_t sx, int64_t sy,
             t2.mark();
             fft_rows_y(P, sb, nb, HIPFFT_BACKWARD, st);
             tr_grid_to_t(P, sb, nb, st);
-            fft_rows_x(P, nb, HIPFFT_BACKWARD, st, P.spec_in);
-            t2.mark();
-            screen_fwd(P, p_lo + sb, nb, dirty, sx, sy, (accumulate || p_lo + sb > 0) ? 1 : 0, tab,
-                       st);
-            t2.mark();
+            xfft_screen_fwd(P, p_lo + sb, nb, dirty, sx, sy,
+                            (accumulate || p_lo + sb > 0) ? 1 : 0, tab, st, t2);
             tfft += t2.ms(0, 1);
             tscr += t2.ms(1, 2);
         }
@@ -5819,11 +6253,8 @@ static void ms2dirty_pols(const Inputs &in, PolsSpec ps, double *const *dirty, i
                 t2.mark();
                 fft_rows_y(P, sb, nb, HIPFFT_BACKWARD, st);
                 tr_grid_to_t(P, sb, nb, st);
-                fft_rows_x(P, nb, HIPFFT_BACKWARD, st, P.spec_in);
-                t2.mark();
-                screen_fwd(P, p_lo + sb, nb, dirty[q], sx, sy,
-                           (accumulate || p_lo + sb > 0) ? 1 : 0, tab, st);
-                t2.mark();
+                xfft_screen_fwd(P, p_lo + sb, nb, dirty[q], sx, sy,
+                                (accumulate || p_lo + sb > 0) ? 1 : 0, tab, st, t2);
                 tfft += t2.ms(0, 1);
                 tscr += t2.ms(1, 2);
             }
@@ -5906,9 +6337,7 @@ static void dirty2ms(const Inputs &in, const double *dirty, int64_t sx, int64_t 
             stage_t.emplace_back(new StageTimer(s));
             StageTimer &t2 = *stage_t.back();
             t2.mark();
-            screen_adj(P, image, sx, sy, p_lo + sb, nb, tab, s);
-            t2.mark();
-            fft_rows_x(P, nb, HIPFFT_FORWARD, s, P.spec_adj);
+            screen_adj_xfft(P, image, sx, sy, p_lo + sb, nb, tab, s, t2);
             tr_t_to_grid(P, sb, nb, s);
             fft_rows_y(P, sb, nb, HIPFFT_FORWARD, s);
             t2.mark();

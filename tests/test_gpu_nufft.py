@@ -1089,3 +1089,27 @@ def test_invert_after_workspace_release_is_unchanged():
     b, _ = kernels.ms2dirty(*args)
     assert torch.isfinite(b).all()
     assert rel_rms(b.cpu().numpy(), a.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("npix,ny,dow", [(64, 48, True), (128, 128, False), (256, 200, True),
+                                         (1024, 1024, True), (2048, 1536, True),
+                                         (4096, 4096, True), (8192, 256, True)])
+def test_fused_xfft_screens_match_hipfft(npix, ny, dow, monkeypatch):
+    """The fused x-FFT + screen kernels (k_xfft_screen_fwd / k_screen_adj_xfft,
+    ngx = 2^7 .. 2^14) against hipFFT + the separate screens
+    (SDP_HIP_XFFT_FUSED=0), invert and predict: both are fp32 transforms of
+    the same planes, so they agree to fp32 rounding."""
+    from ska_sdp_func_python_amd import kernels
+    uvw, freq, ms, wgt, cell = _problem(11, nrow=4000, nchan=4, umax=2e4 * npix / 4096)
+    rng = np.random.default_rng(12)
+    img = rng.normal(size=(npix, ny))
+    outs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SDP_HIP_XFFT_FUSED", fused)
+        d, _ = kernels.ms2dirty(T(uvw), T(freq), T(ms), T(wgt), npix, ny, cell, cell * 0.9, 1e-7,
+                                dow, flip_uw=True)
+        v, _ = kernels.dirty2ms(T(uvw), T(freq), T(img), T(wgt), cell, cell * 0.9, 1e-7, dow,
+                                flip_uw=True)
+        outs[fused] = (d.cpu().numpy(), v.cpu().numpy())
+    assert rel_rms(outs["1"][0], outs["0"][0]) < 1e-6
+    assert rel_rms(outs["1"][1], outs["0"][1]) < 1e-6
