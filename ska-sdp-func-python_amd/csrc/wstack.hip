@@ -3324,7 +3324,7 @@ __global__ __launch_bounds__(kTThreads) void k_t_final_s(const TChunk *__restric
                                                          const unsigned *__restrict__ stot,
                                                          const unsigned *__restrict__ cbase,
                                                          const void *__restrict__ in,
-                                                         void *__restrict__ out) {
+                                                         void *__restrict__ out, int xmap) {
     using R = typename TRec<KIND>::type;
     constexpr int NW = (int)(sizeof(R) / sizeof(uint4));
     constexpr int U = NB / kTThreads;
@@ -3341,7 +3341,12 @@ __global__ __launch_bounds__(kTThreads) void k_t_final_s(const TChunk *__restric
     uint4 *dst = reinterpret_cast<uint4 *>(out);
     const int c0 = threadIdx.x * CPT;
     for (int j = 0; j < CPT; ++j) cnt[c0 + j] = 0u;
-    for (unsigned c = blockIdx.x; c < n; c += gridDim.x) {
+    // xmap: the workgroups resident on one XCD (blockIdx mod 8) take
+    // consecutive chunks -- of one bin, mostly -- whose writes to a cell's
+    // run fall into the same lines of that XCD's L2
+    const unsigned G = gridDim.x,
+                   off = xmap ? (blockIdx.x & 7u) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+    for (unsigned c = off; c < n; c += G) {
         const TChunk t = chunks[c];
         {
             const uint4 pv = reinterpret_cast<const uint4 *>(m2 + (size_t)c * kBinCells)[threadIdx.x];
@@ -5870,9 +5875,10 @@ static void bucket_tiled(Plan &P, const Inputs &in, bool grid_mode, hipStream_t 
             return true;
         }();
         (void)attr;
+        const int xmap = (gch % 8 == 0 && env_int("SDP_HIP_TFINAL_XCD", 1) != 0) ? 1 : 0;
         k_t_final_s<K, NB><<<gch, kTThreads, lds, st>>>(pt.t_chunks, pt.t_meta_ch, pt.t_lkey,
                                                          pt.t_m2, pt.t_stot, pt.t_cbase, pt.t_a,
-                                                         P.recs);
+                                                         P.recs, xmap);
     };
     auto final_move = [&] {
         // batches of 4096 (RecC), 2048 (VisRec, Rec64) records staged in LDS
