@@ -1184,9 +1184,18 @@ def main():
             args.cu_split = ""
     outs = [out] + ([torch.empty_like(out)] if pipe else [])
 
+    # the weight sum (ng.py:258) comes from the gridding call's count pass,
+    # which reads the weights anyway (kernels.ms2dirty_vis, invert_ng's entry
+    # point); SDP_BENCH_FUSED_SUMWT=0: bare ms2dirty + a separate torch sum
+    fused_sw = os.environ.get("SDP_BENCH_FUSED_SUMWT", "1") != "0"
+
     def grid_fn_slot(slot):
-        def fn(*a, **k):
-            r = kernels.ms2dirty(*a, slot=slot, **k)
+        def fn(uvw, freq, vis, wgt, *a, **k):
+            if fused_sw:
+                r = kernels.ms2dirty_vis(uvw, freq, vis.unsqueeze(2), 0, wgt, None, None, *a,
+                                         slot=slot, **k)
+            else:
+                r = kernels.ms2dirty(uvw, freq, vis, wgt, *a, slot=slot, **k)
             infos.append(r[1])
             return r
         return fn
@@ -1197,7 +1206,7 @@ def main():
         def run():
             parallel.invert_sharded(obs["uvw"], obs["freq"], obs["vis"], obs["wgt"], args.npix,
                                     cell, EPS_REQUESTED, True, flip_uw=True, normalise=True,
-                                    grid_fn=grid_fn_slot(j), out=outs[j])
+                                    grid_fn=grid_fn_slot(j), out=outs[j], fused_sumwt=fused_sw)
         if streams[j] is None or not pipelined:  # (serial: the whole GPU, default stream)
             run()
         else:

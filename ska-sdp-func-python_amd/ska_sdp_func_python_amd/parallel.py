@@ -527,12 +527,16 @@ def _gridder():
 
 
 def invert_sharded(uvw, freq, vis, wgt, npix, cell, epsilon=1e-7, do_wstacking=True,
-                   flip_uw=True, normalise=True, group=None, grid_fn=None, out=None):
+                   flip_uw=True, normalise=True, group=None, grid_fn=None, out=None,
+                   fused_sumwt=False):
     """Invert this rank's shard and all-reduce.
 
     uvw [nrow,3], freq [nchan_shard], vis/wgt [nrow, nchan_shard] are the
     rank-local arrays.  Returns (dirty [npix, npix] in RASCIL [y, x] order,
-    sumwt) identical on every rank.
+    sumwt) identical on every rank.  ``fused_sumwt``: the weight sum comes
+    from the gridding call itself (``grid_fn(..., sumwt=t)`` adds it to a
+    one-element f64 device tensor, as kernels.ms2dirty_vis's count pass does
+    while it reads the weights) instead of a separate reduction over them.
     """
     grid_fn = grid_fn or _gridder()
     dev = uvw.device
@@ -540,11 +544,17 @@ def invert_sharded(uvw, freq, vis, wgt, npix, cell, epsilon=1e-7, do_wstacking=T
         out = torch.zeros((npix, npix), dtype=torch.float64, device=dev)
     else:
         out.zero_()
+    extra = {}
+    if fused_sumwt:
+        extra["sumwt"] = torch.zeros(1, dtype=torch.float64, device=dev)
     if freq.numel() > 0 and uvw.shape[0] > 0:
         grid_fn(uvw, freq, vis, wgt, npix, npix, cell, cell, epsilon, do_wstacking,
-                flip_uw=flip_uw, out=out, out_strides=(1, npix), accumulate=True)
-    sumwt = (wgt.sum() if wgt is not None else torch.tensor(float(vis.numel()), device=dev))
-    sumwt = sumwt.to(torch.float64).reshape(1)
+                flip_uw=flip_uw, out=out, out_strides=(1, npix), accumulate=True, **extra)
+    if fused_sumwt:
+        sumwt = extra["sumwt"]
+    else:
+        sumwt = (wgt.sum() if wgt is not None else torch.tensor(float(vis.numel()), device=dev))
+        sumwt = sumwt.to(torch.float64).reshape(1)
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
         dist.all_reduce(sumwt, op=dist.ReduceOp.SUM, group=group)

@@ -30,6 +30,15 @@ def test_invert_and_predict_sharded_match_exact():
                                       1e-7, True)
     ex = orc.ms2dirty_exact(uvw * FLIP, freq, vis, wgt, npix, npix, cell, cell, True).T / wgt.sum()
     assert rel_rms(img.cpu().numpy(), ex) < 5e-6
+    # the weight sum fused into the gridding call (bench.py's step)
+    from ska_sdp_func_python_amd import kernels
+
+    def vis_fn(u, f, v, w, *a, **k):
+        return kernels.ms2dirty_vis(u, f, v.unsqueeze(2), 0, w, None, None, *a, **k)
+    img2, sw2 = parallel.invert_sharded(T(uvw), T(freq), T(vis).to(torch.complex64), T(wgt), npix,
+                                        cell, 1e-7, True, grid_fn=vis_fn, fused_sumwt=True)
+    assert abs(float(sw2) - float(wgt.astype(np.float64).sum())) < 1e-9 * float(wgt.sum())
+    assert rel_rms(img2.cpu().numpy(), img.cpu().numpy()) < 1e-6
     model = rng.normal(size=(npix, npix))  # [y, x]
     v = parallel.predict_sharded(T(uvw), T(freq), T(model), cell, 1e-7, True,
                                  vis_dtype=torch.complex128)
